@@ -1,0 +1,281 @@
+"""CPU oracle for the LE-coupling hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this module, and only as the checker (or the timed CPU
+baseline).  The product path (``ibamr_amd``) never imports it.
+
+Parity status: **parity unpinned** against the reference binary (the Fortran
+needs m4 + SAMRAI's ``pdat_m4arrdim*.i``, both absent).
+The arithmetic lives in ``le_oracle.c`` (a restatement of
+``ibtk/src/lagrangian/fortran/lagrangian_interaction{2,3}d.f.m4``); this module
+adds ctypes bindings and restates the C++ wrappers around it:
+
+* ``side_interp`` / ``side_spread`` -- ``LEInteractor.cpp:1017-1053`` and
+  ``:1876-1911`` (per-axis call, ``x_lower[axis] -= dx/2``,
+  ``SideGeometry::toSideBox``, AoS<->SoA of Q).
+* ``cell_*`` -- ``LEInteractor.cpp:708-755`` / ``1548-1613``.
+* ``node_*`` -- ``LEInteractor.cpp:838-967`` (``x_lower -= dx/2`` all dims,
+  ``toNodeBox``).
+* ``periodic_index_list`` -- ``LIndexSetData::cacheLocalIndices``
+  (``LIndexSetData.cpp:83-169``) for one patch covering a periodic domain,
+  with ``IndexUtilities::getCellIndex`` (``IndexUtilities-inl.h:66-89``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+_LIB_PATH = _HERE / "build" / "libleoracle.so"
+
+KERNELS = {
+    "PIECEWISE_CONSTANT": 0,
+    "DISCONTINUOUS_LINEAR": 1,
+    "PIECEWISE_LINEAR": 2,
+    "PIECEWISE_CUBIC": 3,
+    "IB_3": 4,
+    "IB_4": 5,
+    "IB_4_W8": 6,
+    "IB_6": 7,
+    "BSPLINE_4": 8,
+}
+STENCIL = {"PIECEWISE_CONSTANT": 1, "DISCONTINUOUS_LINEAR": 2, "PIECEWISE_LINEAR": 2, "PIECEWISE_CUBIC": 4,
+           "IB_3": 4, "IB_4": 4, "IB_4_W8": 8, "IB_6": 6, "BSPLINE_4": 4}
+
+_lib = None
+
+
+def build():
+    """Compile le_oracle.c with the committed Makefile (gcc, -ffp-contract=off)."""
+    import subprocess
+    subprocess.run(["make", "-s", "-C", str(_HERE)], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not _LIB_PATH.exists():
+            build()
+        L = ctypes.CDLL(str(_LIB_PATH))
+        dp = ctypes.POINTER(ctypes.c_double)
+        ip = ctypes.POINTER(ctypes.c_int)
+        c_int = ctypes.c_int
+        for name in ("ora_interp", "ora_spread"):
+            f = getattr(L, name)
+            f.restype = c_int
+            f.argtypes = [c_int, c_int, dp, dp, c_int, c_int, ip, ip, ip, dp, ip, dp, c_int, dp, dp]
+        L.ora_closed_form_weights.restype = c_int
+        L.ora_closed_form_weights.argtypes = [c_int, ctypes.c_double, c_int, dp]
+        L.ora_lagrangian_floor.restype = c_int
+        L.ora_lagrangian_floor.argtypes = [ctypes.c_double]
+        L.ora_ib_3_delta.restype = ctypes.c_double
+        L.ora_ib_3_delta.argtypes = [ctypes.c_double]
+        L.ora_piecewise_cubic_delta.restype = ctypes.c_double
+        L.ora_piecewise_cubic_delta.argtypes = [ctypes.c_double]
+        _lib = L
+    return _lib
+
+
+def _dp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _ip(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def kernel_id(kernel):
+    if kernel not in KERNELS:
+        raise ValueError(f"unknown kernel function {kernel}")
+    return KERNELS[kernel]
+
+
+def min_ghost_width(kernel):
+    """LEInteractor::getMinimumGhostWidth, LEInteractor.cpp:684-687."""
+    return STENCIL[kernel] // 2 + 1
+
+
+def weights_1d(kernel, X_o_dx, ilower=0):
+    """1-D weights of a closed-form kernel: (ic_lower, w[W])."""
+    W = STENCIL[kernel]
+    w = np.zeros(8)
+    icl = lib().ora_closed_form_weights(kernel_id(kernel), float(X_o_dx), int(ilower), _dp(w))
+    return icl, w[:W].copy()
+
+
+# --------------------------------------------------------------------------
+# raw Fortran-call equivalents
+# --------------------------------------------------------------------------
+def ghost_shape(ilower, iupper, nugc, depth=1):
+    """numpy shape (C order) of the Fortran array u(CELLdVECG, 0:depth-1)."""
+    n = [iupper[d] - ilower[d] + 1 + 2 * nugc[d] for d in range(len(ilower))]
+    return (depth,) + tuple(reversed(n))
+
+
+def interp(kernel, dx, x_lower, ilower, iupper, nugc, u, indices, Xshift, X, V, depth=1, axis=0):
+    """One call of lagrangian_<kernel>_interp{2,3}d_ (writes V in place)."""
+    ndim = len(ilower)
+    u = _f64(u)
+    assert u.size == int(np.prod(ghost_shape(ilower, iupper, nugc, depth)))
+    idx, xs, X = _i32(indices), _f64(Xshift), _f64(X)
+    assert V.dtype == np.float64 and V.flags.c_contiguous
+    rc = lib().ora_interp(kernel_id(kernel), ndim, _dp(_f64(dx)), _dp(_f64(x_lower)), int(depth), int(axis),
+                          _ip(_i32(ilower)), _ip(_i32(iupper)), _ip(_i32(nugc)), _dp(u), _ip(idx), _dp(xs),
+                          int(idx.size), _dp(X), _dp(V))
+    if rc != 0:
+        raise RuntimeError(f"ora_interp failed ({rc})")
+    return V
+
+
+def spread(kernel, dx, x_lower, ilower, iupper, nugc, u, indices, Xshift, X, V, depth=1, axis=0):
+    """One call of lagrangian_<kernel>_spread{2,3}d_ (accumulates into u)."""
+    ndim = len(ilower)
+    assert u.dtype == np.float64 and u.flags.c_contiguous
+    assert u.size == int(np.prod(ghost_shape(ilower, iupper, nugc, depth)))
+    idx, xs, X, V = _i32(indices), _f64(Xshift), _f64(X), _f64(V)
+    rc = lib().ora_spread(kernel_id(kernel), ndim, _dp(_f64(dx)), _dp(_f64(x_lower)), int(depth), int(axis),
+                          _ip(_i32(ilower)), _ip(_i32(iupper)), _ip(_i32(nugc)), _dp(u), _ip(idx), _dp(xs),
+                          int(idx.size), _dp(X), _dp(V))
+    if rc != 0:
+        raise RuntimeError(f"ora_spread failed ({rc})")
+    return u
+
+
+# --------------------------------------------------------------------------
+# C++ wrapper restatements
+# --------------------------------------------------------------------------
+def side_box(box_lo, box_hi, axis):
+    """SideGeometry::toSideBox: upper[axis] + 1."""
+    hi = list(box_hi)
+    hi[axis] += 1
+    return list(box_lo), hi
+
+
+def side_interp(kernel, dx, x_lower, box_lo, box_hi, gcw, u_axes, indices, Xshift, X, Q):
+    """LEInteractor::interpolate on SideData (LEInteractor.cpp:1017-1053).
+
+    u_axes[a] is the ghosted side array of axis a; Q is AoS (M, NDIM), written
+    at the listed markers only.
+    """
+    ndim = len(box_lo)
+    idx = _i32(indices)
+    if idx.size == 0:
+        return Q
+    local_sz = int(idx.max()) + 1
+    for axis in range(ndim):
+        xl = [float(v) for v in x_lower]
+        xl[axis] -= 0.5 * dx[axis]
+        lo, hi = side_box(box_lo, box_hi, axis)
+        Qa = np.zeros(local_sz)
+        interp(kernel, dx, xl, lo, hi, gcw, u_axes[axis], idx, Xshift, X, Qa, depth=1, axis=axis)
+        Q.reshape(-1, ndim)[idx, axis] = Qa[idx]
+    return Q
+
+
+def side_spread(kernel, dx, x_lower, box_lo, box_hi, gcw, u_axes, indices, Xshift, X, Q):
+    """LEInteractor::spread on SideData (LEInteractor.cpp:1876-1911)."""
+    ndim = len(box_lo)
+    idx = _i32(indices)
+    if idx.size == 0:
+        return u_axes
+    local_sz = int(idx.max()) + 1
+    Qr = np.asarray(Q).reshape(-1, ndim)
+    for axis in range(ndim):
+        xl = [float(v) for v in x_lower]
+        xl[axis] -= 0.5 * dx[axis]
+        lo, hi = side_box(box_lo, box_hi, axis)
+        Qa = np.zeros(local_sz)
+        Qa[idx] = Qr[idx, axis]
+        spread(kernel, dx, xl, lo, hi, gcw, u_axes[axis], idx, Xshift, X, Qa, depth=1, axis=axis)
+    return u_axes
+
+
+def cell_interp(kernel, dx, x_lower, box_lo, box_hi, gcw, u, indices, Xshift, X, Q, depth):
+    """LEInteractor::interpolate on CellData (LEInteractor.cpp:1058-1146 -> private :2399)."""
+    return interp(kernel, dx, x_lower, box_lo, box_hi, gcw, u, indices, Xshift, X, Q, depth=depth)
+
+
+def cell_spread(kernel, dx, x_lower, box_lo, box_hi, gcw, u, indices, Xshift, X, Q, depth):
+    return spread(kernel, dx, x_lower, box_lo, box_hi, gcw, u, indices, Xshift, X, Q, depth=depth)
+
+
+def node_interp(kernel, dx, x_lower, box_lo, box_hi, gcw, u, indices, Xshift, X, Q, depth):
+    """NodeData: x_lower -= dx/2 in every dim, NodeGeometry::toNodeBox (upper + 1)."""
+    xl = [x_lower[d] - 0.5 * dx[d] for d in range(len(box_lo))]
+    hi = [h + 1 for h in box_hi]
+    return interp(kernel, dx, xl, box_lo, hi, gcw, u, indices, Xshift, X, Q, depth=depth)
+
+
+def node_spread(kernel, dx, x_lower, box_lo, box_hi, gcw, u, indices, Xshift, X, Q, depth):
+    xl = [x_lower[d] - 0.5 * dx[d] for d in range(len(box_lo))]
+    hi = [h + 1 for h in box_hi]
+    return spread(kernel, dx, xl, box_lo, hi, gcw, u, indices, Xshift, X, Q, depth=depth)
+
+
+def get_cell_index(X, x_lower, x_upper, dx, ilower, iupper):
+    """IndexUtilities::getCellIndex (IndexUtilities-inl.h:66-89), vectorised."""
+    X = np.asarray(X, dtype=np.float64)
+    ndim = X.shape[1]
+    out = np.empty(X.shape, dtype=np.int64)
+    for d in range(ndim):
+        dl = X[:, d] - x_lower[d]
+        du = X[:, d] - x_upper[d]
+        lower = np.abs(dl) <= np.abs(du)
+        out[:, d] = np.where(lower, ilower[d] + np.floor(dl / dx[d]), iupper[d] + np.floor(du / dx[d]) + 1)
+    return out
+
+
+def periodic_index_list(X, x_lower, x_upper, dx, box_lo, box_hi, ghost, periodic=None):
+    """(indices, Xshift, cells) for one patch covering a periodic domain.
+
+    Every marker appears once at its own cell (interior) and once per periodic
+    image whose cell falls in the ghost box, with Xshift = +/-L in the
+    wrapped dims -- the lists LIndexSetData::cacheLocalIndices builds
+    (LIndexSetData.cpp:111-166: offset = -periodic_shift below the patch,
+    +periodic_shift above it).  Order: cell-major (x fastest), then marker.
+    """
+    X = np.asarray(X, dtype=np.float64)
+    M, ndim = X.shape
+    periodic = [True] * ndim if periodic is None else periodic
+    N = [box_hi[d] - box_lo[d] + 1 for d in range(ndim)]
+    cells = get_cell_index(X, x_lower, x_upper, dx, box_lo, box_hi)
+    ents_s, ents_off, ents_cell = [np.arange(M)], [np.zeros((M, ndim), np.int64)], [cells]
+    # images: shift the cell by -N (image below) or +N (image above) per dim
+    import itertools
+    for shifts in itertools.product(*[(-1, 0, 1) if periodic[d] else (0,) for d in range(ndim)]):
+        if all(s == 0 for s in shifts):
+            continue
+        c = cells.copy()
+        for d in range(ndim):
+            c[:, d] += shifts[d] * N[d]
+        inside = np.ones(M, dtype=bool)
+        for d in range(ndim):
+            inside &= (c[:, d] >= box_lo[d] - ghost) & (c[:, d] <= box_hi[d] + ghost)
+        if inside.any():
+            sel = np.nonzero(inside)[0]
+            ents_s.append(sel)
+            ents_off.append(np.tile(np.array(shifts, np.int64) * np.array(N), (sel.size, 1)))
+            ents_cell.append(c[sel])
+    s = np.concatenate(ents_s)
+    off = np.concatenate(ents_off)
+    cell = np.concatenate(ents_cell)
+    # cell-major order (x fastest) then marker index: the IndexData iteration order
+    key = np.zeros(s.size, dtype=np.int64)
+    stride = 1
+    for d in range(ndim):
+        key += (cell[:, d] - (box_lo[d] - ghost)) * stride
+        stride *= N[d] + 2 * ghost
+    order = np.lexsort((s, key))
+    Xshift = off[order].astype(np.float64) * np.asarray(dx)[None, :]
+    return s[order].astype(np.int32), Xshift, cell[order]

@@ -1,0 +1,208 @@
+"""CPU tests of the oracle (the restatement of the reference Fortran kernels).
+
+Pins the restatement with (1) known-answer weights computed in 60-digit decimal
+from the reference's own 1-D delta functions (tests/golden/kernel_weights.json,
+made by tests/golden/make_golden.py) and (2) the analytic identities the
+kernels are built to satisfy.  The reference has no test suite
+of its own for this path, and its Fortran cannot be built here, so the oracle
+is "parity unpinned" against the reference binary.
+"""
+import json
+from decimal import Decimal
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+GOLDEN = json.loads((Path(__file__).parent / "golden" / "kernel_weights.json").read_text())
+ALL = ["PIECEWISE_CONSTANT", "DISCONTINUOUS_LINEAR", "PIECEWISE_LINEAR", "PIECEWISE_CUBIC", "IB_3", "IB_4",
+       "IB_4_W8", "IB_6", "BSPLINE_4"]
+SMOOTH = ["PIECEWISE_LINEAR", "PIECEWISE_CUBIC", "IB_3", "IB_4", "IB_4_W8", "IB_6", "BSPLINE_4"]
+
+
+@pytest.mark.parametrize("case", [c for c in GOLDEN["cases"] if c["kernel"] in ("IB_4", "BSPLINE_4", "IB_4_W8")],
+                         ids=lambda c: f"{c['kernel']}@{c['X_o_dx']}")
+def test_closed_form_weights_known_answer(oracle, case):
+    icl, w = oracle.weights_1d(case["kernel"], float(case["X_o_dx"]))
+    assert icl == case["ic_lower"]
+    expect = np.array([float(Decimal(v)) for v in case["w"]])
+    np.testing.assert_allclose(w, expect, rtol=0, atol=2e-16 * 4)
+
+
+@pytest.mark.parametrize("case", [c for c in GOLDEN["cases"] if c["kernel"] in ("IB_3", "PIECEWISE_CUBIC")],
+                         ids=lambda c: f"{c['kernel']}@{c['X_o_dx']}")
+def test_pointwise_kernels_known_answer(oracle, case):
+    """IB_3 / PIECEWISE_CUBIC via a 1-cell-thick 2-D interpolation of unit vectors."""
+    k = case["kernel"]
+    x = float(case["X_o_dx"])
+    expect = [float(Decimal(v)) for v in case["w"]]
+    # 2-D grid wide enough in x; the y coordinate sits at a cell centre so the
+    # y weights are (0, 1, 0) for IB_3 and (phi(-1), phi(0), phi(1), ...) for pw-cubic
+    lo, hi, g = [-20, 0], [20, 0], [4, 4]
+    shape = oracle.ghost_shape(lo, hi, g)
+    X = np.array([[x, 0.5]])
+    got = []
+    for j in range(case["ic_lower"], case["ic_lower"] + len(expect)):
+        u = np.zeros(shape)
+        u[0, :, j - (lo[0] - g[0])] = 1.0  # whole y column at x-index j
+        V = np.zeros(1)
+        oracle.interp(k, [1.0, 1.0], [float(lo[0]), 0.0], lo, hi, g, u, [0], np.zeros((1, 2)), X, V)
+        got.append(V[0])
+    # the y-sum of weights is 1 (partition of unity) up to rounding
+    np.testing.assert_allclose(got, expect, rtol=0, atol=4e-15)
+
+
+def test_nint_half_away_from_zero(oracle):
+    # NINT(2.5) = 3, NINT(-2.5) = -3 (F7); IB_4 ic_lower = NINT(x) - 2
+    assert oracle.weights_1d("IB_4", 2.5)[0] == 1
+    assert oracle.weights_1d("IB_4", -2.5)[0] == -5
+    assert oracle.weights_1d("IB_4", 2.4999999999999996)[0] == 0
+
+
+def test_lagrangian_floor_quirk(oracle):
+    # int(x) - (x<0): -2.0 -> -3 (a6)
+    L = oracle.lib()
+    assert L.ora_lagrangian_floor(-2.0) == -3
+    assert L.ora_lagrangian_floor(-1.5) == -2
+    assert L.ora_lagrangian_floor(1.5) == 1
+    assert L.ora_lagrangian_floor(0.0) == 0
+
+
+def _moments(oracle, kernel, x):
+    icl, w = oracle.weights_1d(kernel, x)
+    d = x - (np.arange(icl, icl + w.size) + 0.5)
+    return w, d
+
+
+@pytest.mark.parametrize("kernel", ["IB_4", "IB_4_W8", "IB_6", "BSPLINE_4"])
+def test_closed_form_moments(oracle, kernel):
+    rng = np.random.default_rng(7)
+    for x in np.concatenate([rng.uniform(-50, 50, 200), [0.5, 1.0, 2.5, -2.5]]):
+        w, d = _moments(oracle, kernel, x)
+        assert abs(w.sum() - 1.0) < 4e-15
+        assert abs((w * d).sum()) < 4e-14
+        if kernel == "IB_4":
+            assert abs((w * w).sum() - 3.0 / 8.0) < 4e-15  # Peskin's sum-of-squares condition
+            assert abs(w[0::2].sum() - 0.5) < 4e-15  # even-odd condition
+        if kernel == "IB_6":
+            K = (59.0 / 60.0) * (1.0 - np.sqrt(1.0 - 3220.0 / 3481.0))
+            assert abs(w[0::2].sum() - 0.5) < 4e-15
+            assert abs((w * d * d).sum() - K) < 4e-14  # second moment = K
+            assert abs((w * d ** 3).sum()) < 4e-13
+        assert (w >= -1e-15).all() or kernel == "IB_6"
+
+
+# ---------------------------------------------------------------------------
+# whole-call identities
+# ---------------------------------------------------------------------------
+def _grid(ndim, N, g):
+    lo = [0] * ndim
+    hi = [N - 1] * ndim
+    return lo, hi, [g] * ndim
+
+
+@pytest.mark.parametrize("kernel", ALL)
+@pytest.mark.parametrize("ndim", [2, 3])
+def test_interp_constant_and_linear(oracle, kernel, ndim):
+    N = 12
+    g = oracle.min_ghost_width(kernel) + 1
+    lo, hi, gw = _grid(ndim, N, g)
+    dx = [1.0 / N] * ndim
+    xlo = [0.0] * ndim
+    rng = np.random.default_rng(1)
+    M = 50
+    X = rng.uniform(0.3, 0.7, (M, ndim))
+    idx = np.arange(M, dtype=np.int32)
+    xs = np.zeros((M, ndim))
+    shape = oracle.ghost_shape(lo, hi, gw)
+    V = np.zeros(M)
+    oracle.interp(kernel, dx, xlo, lo, hi, gw, np.full(shape, 2.5), idx, xs, X, V, axis=0)
+    np.testing.assert_allclose(V, 2.5, rtol=0, atol=1e-13)
+    if kernel in SMOOTH:
+        # u = cell-centre x coordinate -> interp reproduces X[:, 0]
+        n0 = shape[-1]
+        xc = (np.arange(n0) + (lo[0] - g) + 0.5) / N
+        u = np.broadcast_to(xc, shape).copy()
+        oracle.interp(kernel, dx, xlo, lo, hi, gw, u, idx, xs, X, V)
+        np.testing.assert_allclose(V, X[:, 0], rtol=0, atol=1e-13)
+
+
+@pytest.mark.parametrize("kernel", ALL)
+@pytest.mark.parametrize("ndim", [2, 3])
+def test_spread_conservation_and_adjointness(oracle, kernel, ndim):
+    N = 12
+    g = oracle.min_ghost_width(kernel) + 1
+    lo, hi, gw = _grid(ndim, N, g)
+    dx = [1.0 / N] * ndim
+    h = np.prod(dx)
+    xlo = [0.0] * ndim
+    rng = np.random.default_rng(2)
+    M = 40
+    X = rng.uniform(0.3, 0.7, (M, ndim))
+    idx = np.arange(M, dtype=np.int32)
+    xs = np.zeros((M, ndim))
+    shape = oracle.ghost_shape(lo, hi, gw)
+    F = rng.standard_normal(M)
+    f = np.zeros(shape)
+    oracle.spread(kernel, dx, xlo, lo, hi, gw, f, idx, xs, X, F)
+    assert abs(f.sum() * h - F.sum()) < 1e-12 * max(1.0, np.abs(F).sum())
+    u = rng.standard_normal(shape)
+    U = np.zeros(M)
+    oracle.interp(kernel, dx, xlo, lo, hi, gw, u, idx, xs, X, U)
+    lhs = (f * u).sum() * h
+    rhs = (F * U).sum()
+    assert abs(lhs - rhs) < 1e-12 * max(1.0, abs(rhs), np.abs(F).sum())
+
+
+@pytest.mark.parametrize("kernel", ["IB_4", "IB_6", "PIECEWISE_LINEAR", "PIECEWISE_CUBIC", "IB_3"])
+def test_clipping_at_ghost_box_edge(oracle, kernel):
+    """Markers near/outside the ghost box: stencils are clipped, never read/written out of range."""
+    N, g = 8, oracle.min_ghost_width(kernel)
+    lo, hi, gw = _grid(3, N, g)
+    dx = [1.0 / N] * 3
+    shape = oracle.ghost_shape(lo, hi, gw)
+    guard = 7
+    buf = np.full(np.prod(shape) + 2 * guard, 123.0)
+    u = buf[guard:-guard].reshape(shape)
+    u[...] = 0.0
+    X = np.array([[-(g + 0.9) / N, 0.5, 0.5], [(N + g + 0.9) / N, 0.5, 0.5], [-0.01, -0.01, 1.01], [0.5, 0.5, 0.5]])
+    F = np.ones(4)
+    oracle.spread(kernel, dx, [0, 0, 0], lo, hi, gw, u, np.arange(4), np.zeros((4, 3)), X, F)
+    assert (buf[:guard] == 123.0).all() and (buf[-guard:] == 123.0).all()
+    V = np.full(4, np.nan)
+    oracle.interp(kernel, dx, [0, 0, 0], lo, hi, gw, u, np.arange(4), np.zeros((4, 3)), X, V)
+    assert np.isfinite(V).all()
+
+
+def test_side_wrapper_periodic_images_match_unwrapped(oracle):
+    """Spreading the periodic index list on a ghosted periodic patch gives the
+    same interior values as spreading the unwrapped markers on a bigger grid."""
+    N, g, kernel = 10, 3, "IB_4"
+    lo, hi = [0, 0, 0], [N - 1] * 3
+    dx = [1.0 / N] * 3
+    rng = np.random.default_rng(3)
+    M = 30
+    X = rng.uniform(0, 1, (M, 3))
+    Fm = rng.standard_normal((M, 3))
+    idx, xs, _ = oracle.periodic_index_list(X, [0, 0, 0], [1, 1, 1], dx, lo, hi, g)
+    assert idx.size > M  # some images
+    f = [np.zeros(oracle.ghost_shape(*oracle.side_box(lo, hi, a), [g] * 3)) for a in range(3)]
+    oracle.side_spread(kernel, dx, [0, 0, 0], lo, hi, [g] * 3, f, idx, xs, X, Fm)
+    # brute force: sum the 27 images on an unghosted periodic grid
+    ref = [np.zeros((N, N, N)) for _ in range(3)]
+    import itertools
+    for a in range(3):
+        big_lo, big_hi = [-N] * 3, [2 * N - 1] * 3
+        fb = np.zeros(oracle.ghost_shape(*oracle.side_box(big_lo, big_hi, a), [g] * 3))
+        for sh in itertools.product((-1, 0, 1), repeat=3):
+            Xs = X + np.array(sh)[None, :]
+            xl = [0.0, 0.0, 0.0]
+            xl[a] -= 0.5 * dx[a]
+            blo, bhi = oracle.side_box(big_lo, big_hi, a)
+            # note: the big patch has x_lower at -1 (cell -N)
+            xl = [v - 1.0 for v in xl]
+            oracle.spread(kernel, dx, xl, blo, bhi, [g] * 3, fb, np.arange(M), np.zeros((M, 3)), Xs, Fm[:, a].copy())
+        off = g + N
+        ref[a] = fb[0, off:off + N, off:off + N, off:off + N]
+        got = f[a][0, g:g + N, g:g + N, g:g + N]
+        np.testing.assert_allclose(got, ref[a], rtol=0, atol=1e-9 * np.abs(ref[a]).max())
