@@ -1,0 +1,636 @@
+// le_abi.cpp -- the C-ABI of include/ibtk_le.h: contexts, marker binning and
+// the interp/spread entry points over device-resident data.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/ibtk_le.h"
+#include "le_internal.h"
+
+using namespace ibtk_le;
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+static thread_local std::string g_last_error;
+
+static int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                     \
+    do {                                                                                                  \
+        hipError_t _e = (expr);                                                                           \
+        if (_e != hipSuccess) return fail(IBTK_LE_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(_e));    \
+    } while (0)
+
+extern "C" const char* ibtk_le_last_error(void) { return g_last_error.c_str(); }
+extern "C" const char* ibtk_le_version(void) { return "ibtk_le 0.1 (gfx950)"; }
+
+// ---------------------------------------------------------------------------
+// kernel names (LEInteractor::getStencilSize, LEInteractor.cpp:668-682)
+// ---------------------------------------------------------------------------
+static const char* const kNames[K_COUNT] = {"PIECEWISE_CONSTANT", "DISCONTINUOUS_LINEAR", "PIECEWISE_LINEAR",
+                                            "PIECEWISE_CUBIC",    "IB_3",                 "IB_4",
+                                            "IB_4_W8",            "IB_6",                 "BSPLINE_4"};
+static const int kStencil[K_COUNT] = {1, 2, 2, 4, 4, 4, 8, 6, 4};
+
+extern "C" int ibtk_le_kernel_from_name(const char* name) {
+    if (!name) return -1;
+    for (int k = 0; k < K_COUNT; ++k)
+        if (std::strcmp(name, kNames[k]) == 0) return k;
+    return -1;
+}
+extern "C" const char* ibtk_le_kernel_name(int kernel) {
+    return (kernel >= 0 && kernel < K_COUNT) ? kNames[kernel] : nullptr;
+}
+extern "C" int ibtk_le_stencil_size(int kernel) {
+    return (kernel >= 0 && kernel < K_COUNT) ? kStencil[kernel] : -1;
+}
+extern "C" int ibtk_le_min_ghost_width(int kernel) {
+    // LEInteractor.cpp:684-687: floor(0.5*stencil) + 1
+    const int s = ibtk_le_stencil_size(kernel);
+    return s < 0 ? -1 : s / 2 + 1;
+}
+
+// ---------------------------------------------------------------------------
+// device buffers
+// ---------------------------------------------------------------------------
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return IBTK_LE_OK;
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes + bytes / 8 + 256;
+        if (hipMalloc(&p, want) != hipSuccess) {
+            p = nullptr;
+            return fail(IBTK_LE_ERR_NOMEM, "hipMalloc(%zu) failed", want);
+        }
+        cap = want;
+        return IBTK_LE_OK;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct ibtk_le_ctx_s {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevBuf keys_in, vals_in, temp, counts, offsets;
+    DevBuf err;  // one int
+    bool timing = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool ev_valid = false;
+};
+
+struct ibtk_le_markers_s {
+    ibtk_le_ctx ctx = nullptr;
+    int n = 0;
+    int kernel = -1;
+    int ndim = 0;
+    BinGeom bg{};
+    ibtk_le_patch_geom geom{};
+    DevBuf sorted_key, sorted_l, brick_start, indices, xshift;
+    bool has_indices = false, has_xshift = false;
+};
+
+static int set_device(ibtk_le_ctx ctx) {
+    HIP_TRY(hipSetDevice(ctx->device));
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_ctx_create(int device, void* stream, ibtk_le_ctx* out) {
+    if (!out) return fail(IBTK_LE_ERR_ARG, "ctx_create: null out");
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(IBTK_LE_ERR_ARG, "ctx_create: device %d of %d", device, ndev);
+    auto* c = new ibtk_le_ctx_s();
+    c->device = device;
+    c->stream = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipSetDevice(device));
+    int rc = c->err.ensure(sizeof(int));
+    if (rc) {
+        delete c;
+        return rc;
+    }
+    HIP_TRY(hipMemsetAsync(c->err.p, 0, sizeof(int), c->stream));
+    HIP_TRY(hipEventCreate(&c->ev0));
+    HIP_TRY(hipEventCreate(&c->ev1));
+    *out = c;
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_ctx_destroy(ibtk_le_ctx ctx) {
+    if (!ctx) return IBTK_LE_OK;
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    for (DevBuf* b : {&ctx->keys_in, &ctx->vals_in, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->err})
+        b->release();
+    if (ctx->ev0) hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) hipEventDestroy(ctx->ev1);
+    delete ctx;
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_ctx_set_stream(ibtk_le_ctx ctx, void* stream) {
+    if (!ctx) return fail(IBTK_LE_ERR_ARG, "null ctx");
+    ctx->stream = static_cast<hipStream_t>(stream);
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_ctx_synchronize(ibtk_le_ctx ctx) {
+    if (!ctx) return fail(IBTK_LE_ERR_ARG, "null ctx");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    int flag = 0;
+    HIP_TRY(hipMemcpy(&flag, ctx->err.p, sizeof(int), hipMemcpyDeviceToHost));
+    if (flag) {
+        HIP_TRY(hipMemset(ctx->err.p, 0, sizeof(int)));
+        return fail(IBTK_LE_ERR_INVARIANT,
+                    "device invariant failed (flag %d): a stencil left its staged region (1) or its bin bounds (2)",
+                    flag);
+    }
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_ctx_enable_timing(ibtk_le_ctx ctx, int enable) {
+    if (!ctx) return fail(IBTK_LE_ERR_ARG, "null ctx");
+    ctx->timing = enable != 0;
+    return IBTK_LE_OK;
+}
+
+extern "C" double ibtk_le_ctx_last_kernel_ms(ibtk_le_ctx ctx) {
+    if (!ctx || !ctx->ev_valid) return -1.0;
+    hipEventSynchronize(ctx->ev1);
+    float ms = -1.f;
+    if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) != hipSuccess) return -1.0;
+    return ms;
+}
+
+// ---------------------------------------------------------------------------
+// geometry helpers
+// ---------------------------------------------------------------------------
+static int check_geom(const ibtk_le_patch_geom* g) {
+    if (!g) return fail(IBTK_LE_ERR_ARG, "null geometry");
+    if (g->ndim != 2 && g->ndim != 3) return fail(IBTK_LE_ERR_ARG, "ndim must be 2 or 3 (got %d)", g->ndim);
+    for (int d = 0; d < g->ndim; ++d) {
+        if (g->iupper[d] < g->ilower[d]) return fail(IBTK_LE_ERR_ARG, "empty patch box in dim %d", d);
+        if (g->gcw[d] < 0) return fail(IBTK_LE_ERR_ARG, "negative ghost width");
+        if (!(g->dx[d] > 0.0)) return fail(IBTK_LE_ERR_ARG, "dx[%d] must be positive", d);
+    }
+    return IBTK_LE_OK;
+}
+
+// Brick grid over key cells: every key whose stencil can touch any array of the
+// patch (ghost box, + 1 for the shifted-frame extra face/node) gets a brick.
+static int make_bin_geom(const ibtk_le_patch_geom* g, int kernel, BinGeom& bg) {
+    const KernelInfo ki = kKernelInfo[kernel];
+    const int B = g->ndim == 3 ? BRICK3 : BRICK2;
+    std::memset(&bg, 0, sizeof(bg));
+    bg.ndim = g->ndim;
+    bg.shift = g->ndim == 3 ? 9 : 8;
+    long long nb = 1;
+    for (int d = 0; d < 3; ++d) {
+        if (d >= g->ndim) {
+            bg.nb[d] = 1;
+            continue;
+        }
+        const int lo = g->ilower[d] - g->gcw[d];
+        const int hi = g->iupper[d] + g->gcw[d] + 1;
+        bg.kmin[d] = lo - ki.HI;
+        const int kmax = hi - ki.LO;
+        const int E = kmax - bg.kmin[d] + 1;
+        bg.nb[d] = (E + B - 1) / B;
+        nb *= bg.nb[d];
+        bg.xlo[d] = g->x_lower[d];
+        bg.dx[d] = g->dx[d];
+        bg.ilower[d] = g->ilower[d];
+    }
+    const long long BV = 1LL << bg.shift;
+    if ((nb + 1) * BV >= (1LL << 32))
+        return fail(IBTK_LE_ERR_RANGE, "patch too large for 32-bit bin keys (%lld bricks)", nb);
+    bg.nbricks = (int)nb;
+    return IBTK_LE_OK;
+}
+
+static int end_bit_for(const BinGeom& bg) {
+    unsigned long long maxkey = ((unsigned long long)bg.nbricks << bg.shift);
+    int bits = 1;
+    while ((1ULL << bits) <= maxkey) ++bits;
+    return bits;
+}
+
+// Component descriptors of a centering (LEInteractor.cpp:1017-1053 for side:
+// x_lower[axis] -= dx/2 and SideGeometry::toSideBox; node: all dims shifted and
+// toNodeBox; edge: every dim but `axis` shifted and toEdgeBox).
+static int make_comps(const ibtk_le_patch_geom* g, int centering, int axis, double* const* q, int q_depth,
+                      int Q_depth, int first, int count, Params& p) {
+    const int nd = g->ndim;
+    p.ncomp = count;
+    for (int c = 0; c < count; ++c) {
+        CompDesc& cd = p.comp[c];
+        std::memset(&cd, 0, sizeof(cd));
+        const int comp = first + c;  // global component index
+        int shift_mask = 0, ext_mask = 0;
+        double* base = nullptr;
+        int depth_index = 0;
+        switch (centering) {
+        case IBTK_LE_CELL:
+            base = q[0];
+            depth_index = comp;
+            cd.qcomp = comp;
+            cd.axis = axis;
+            break;
+        case IBTK_LE_NODE:
+            base = q[0];
+            depth_index = comp;
+            shift_mask = ext_mask = (1 << nd) - 1;
+            cd.qcomp = comp;
+            cd.axis = axis;
+            break;
+        case IBTK_LE_SIDE:
+            base = q[comp];
+            shift_mask = ext_mask = 1 << comp;
+            cd.qcomp = comp;
+            cd.axis = comp;
+            break;
+        case IBTK_LE_EDGE:
+            base = q[comp];
+            shift_mask = ext_mask = ((1 << nd) - 1) & ~(1 << comp);
+            cd.qcomp = comp;
+            cd.axis = comp;
+            break;
+        default:
+            return fail(IBTK_LE_ERR_ARG, "unknown centering %d", centering);
+        }
+        if (!base) return fail(IBTK_LE_ERR_ARG, "null Eulerian array for component %d", comp);
+        int64_t n[3] = {1, 1, 1};
+        for (int d = 0; d < 3; ++d) {
+            if (d < nd) {
+                cd.lo[d] = g->ilower[d] - g->gcw[d];
+                cd.hi[d] = g->iupper[d] + g->gcw[d] + ((ext_mask >> d) & 1);
+                cd.ilower[d] = g->ilower[d];
+                cd.xlo[d] = g->x_lower[d];
+                if ((shift_mask >> d) & 1) cd.xlo[d] -= 0.5 * g->dx[d];
+                n[d] = cd.hi[d] - cd.lo[d] + 1;
+            } else {
+                cd.lo[d] = cd.hi[d] = 0;
+            }
+        }
+        cd.s1 = n[0];
+        cd.s2 = n[0] * n[1];
+        cd.u = base + (int64_t)depth_index * n[0] * n[1] * n[2];
+    }
+    (void)q_depth;
+    (void)Q_depth;
+    return IBTK_LE_OK;
+}
+
+static int ncomponents(const ibtk_le_patch_geom* g, int centering, int q_depth, int Q_depth) {
+    switch (centering) {
+    case IBTK_LE_CELL:
+    case IBTK_LE_NODE:
+        if (q_depth != Q_depth)
+            return -fail(IBTK_LE_ERR_DEPTH, "cell/node data: q depth %d != Q depth %d", q_depth, Q_depth);
+        return q_depth;
+    case IBTK_LE_SIDE:
+    case IBTK_LE_EDGE:
+        if (centering == IBTK_LE_EDGE && g->ndim != 3) return -fail(IBTK_LE_ERR_ARG, "edge data is 3-D only");
+        if (q_depth != 1 || Q_depth != g->ndim)
+            return -fail(IBTK_LE_ERR_DEPTH,
+                         "side/edge-centered data requires vector-valued data (q depth 1, Q depth NDIM; got %d, %d)",
+                         q_depth, Q_depth);
+        return g->ndim;
+    default:
+        return -fail(IBTK_LE_ERR_ARG, "unknown centering %d", centering);
+    }
+}
+
+static double ib6_K() { return (59.0 / 60.0) * (1.0 - std::sqrt(1.0 - (3220.0 / 3481.0))); }
+
+// ---------------------------------------------------------------------------
+// markers
+// ---------------------------------------------------------------------------
+extern "C" int ibtk_le_markers_create(ibtk_le_ctx ctx, ibtk_le_markers* out) {
+    if (!ctx || !out) return fail(IBTK_LE_ERR_ARG, "markers_create: null argument");
+    auto* m = new ibtk_le_markers_s();
+    m->ctx = ctx;
+    *out = m;
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_markers_destroy(ibtk_le_markers m) {
+    if (!m) return IBTK_LE_OK;
+    hipSetDevice(m->ctx->device);
+    hipStreamSynchronize(m->ctx->stream);
+    for (DevBuf* b : {&m->sorted_key, &m->sorted_l, &m->brick_start, &m->indices, &m->xshift}) b->release();
+    delete m;
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_markers_count(ibtk_le_markers m) { return m ? m->n : -1; }
+
+extern "C" int ibtk_le_markers_order(ibtk_le_markers m, const int** order_dev) {
+    if (!m || !order_dev) return fail(IBTK_LE_ERR_ARG, "markers_order: null argument");
+    *order_dev = m->sorted_l.as<int>();
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_patch_geom* geom, int kernel,
+                                   const double* X_dev, const int* indices_dev, const double* Xshift_dev,
+                                   int nindices) {
+    if (!ctx || !m) return fail(IBTK_LE_ERR_ARG, "markers_bin: null ctx/markers");
+    if (int rc = check_geom(geom)) return rc;
+    if (kernel < 0 || kernel >= K_COUNT) return fail(IBTK_LE_ERR_UNKNOWN_KERNEL, "Unknown kernel function %d", kernel);
+    if (nindices < 0) return fail(IBTK_LE_ERR_ARG, "negative list length");
+    if (nindices > 0 && !X_dev) return fail(IBTK_LE_ERR_ARG, "null X");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    BinGeom bg;
+    if (int rc = make_bin_geom(geom, kernel, bg)) return rc;
+    const hipStream_t s = ctx->stream;
+    const int n = nindices;
+    m->n = n;
+    m->kernel = kernel;
+    m->ndim = geom->ndim;
+    m->bg = bg;
+    m->geom = *geom;
+    m->has_indices = indices_dev != nullptr;
+    m->has_xshift = Xshift_dev != nullptr;
+    int rc = 0;
+    if ((rc = m->brick_start.ensure(sizeof(int) * (size_t)(bg.nbricks + 1)))) return rc;
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(m->brick_start.p, 0, sizeof(int) * (size_t)(bg.nbricks + 1), s));
+        return IBTK_LE_OK;
+    }
+    if ((rc = m->sorted_key.ensure(sizeof(unsigned) * (size_t)n))) return rc;
+    if ((rc = m->sorted_l.ensure(sizeof(int) * (size_t)n))) return rc;
+    if ((rc = ctx->keys_in.ensure(sizeof(unsigned) * (size_t)n))) return rc;
+    if ((rc = ctx->vals_in.ensure(sizeof(int) * (size_t)n))) return rc;
+    if (m->has_indices) {
+        if ((rc = m->indices.ensure(sizeof(int) * (size_t)n))) return rc;
+        HIP_TRY(hipMemcpyAsync(m->indices.p, indices_dev, sizeof(int) * (size_t)n, hipMemcpyDeviceToDevice, s));
+    }
+    if (m->has_xshift) {
+        const size_t xb = sizeof(double) * (size_t)n * geom->ndim;
+        if ((rc = m->xshift.ensure(xb))) return rc;
+        HIP_TRY(hipMemcpyAsync(m->xshift.p, Xshift_dev, xb, hipMemcpyDeviceToDevice, s));
+    }
+    Params p;
+    std::memset(&p, 0, sizeof(p));
+    p.bg = bg;
+    p.X = X_dev;
+    p.indices = m->has_indices ? m->indices.as<int>() : nullptr;
+    p.Xshift = m->has_xshift ? m->xshift.as<double>() : nullptr;
+    HIP_TRY(launch_bin(geom->ndim, kernel, p, n, ctx->keys_in.as<unsigned>(), ctx->vals_in.as<int>(), s));
+    const int end_bit = end_bit_for(bg);
+    size_t tb = 0;
+    HIP_TRY(launch_sort(nullptr, tb, ctx->keys_in.as<unsigned>(), m->sorted_key.as<unsigned>(),
+                        ctx->vals_in.as<int>(), m->sorted_l.as<int>(), n, end_bit, s));
+    if ((rc = ctx->temp.ensure(tb))) return rc;
+    tb = ctx->temp.cap;
+    HIP_TRY(launch_sort(ctx->temp.p, tb, ctx->keys_in.as<unsigned>(), m->sorted_key.as<unsigned>(),
+                        ctx->vals_in.as<int>(), m->sorted_l.as<int>(), n, end_bit, s));
+    HIP_TRY(launch_brick_start(m->sorted_key.as<unsigned>(), n, bg.nbricks, bg.shift, m->brick_start.as<int>(), s));
+    return IBTK_LE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// interp / spread
+// ---------------------------------------------------------------------------
+static bool same_geom(const ibtk_le_patch_geom& a, const ibtk_le_patch_geom& b) {
+    if (a.ndim != b.ndim) return false;
+    for (int d = 0; d < a.ndim; ++d) {
+        if (a.ilower[d] != b.ilower[d] || a.iupper[d] != b.iupper[d] || a.gcw[d] != b.gcw[d]) return false;
+        if (a.dx[d] != b.dx[d] || a.x_lower[d] != b.x_lower[d]) return false;
+    }
+    return true;
+}
+
+static int prepare(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const ibtk_le_patch_geom* geom, const double* X,
+                   Params& p) {
+    if (!ctx || !m) return fail(IBTK_LE_ERR_ARG, "null ctx/markers");
+    if (int rc = check_geom(geom)) return rc;
+    if (kernel < 0 || kernel >= K_COUNT) return fail(IBTK_LE_ERR_UNKNOWN_KERNEL, "Unknown kernel function %d", kernel);
+    if (m->kernel != kernel)
+        return fail(IBTK_LE_ERR_ARG, "markers were binned for kernel %s, not %s",
+                    m->kernel >= 0 ? kNames[m->kernel] : "(none)", kNames[kernel]);
+    if (!same_geom(m->geom, *geom)) return fail(IBTK_LE_ERR_ARG, "markers were binned for a different patch geometry");
+    if (m->n > 0 && !X) return fail(IBTK_LE_ERR_ARG, "null X");
+    std::memset(&p, 0, sizeof(p));
+    p.bg = m->bg;
+    p.X = X;
+    p.indices = m->has_indices ? m->indices.as<int>() : nullptr;
+    p.Xshift = m->has_xshift ? m->xshift.as<double>() : nullptr;
+    p.sorted_l = m->sorted_l.as<int>();
+    p.sorted_key = m->sorted_key.as<unsigned>();
+    p.brick_start = m->brick_start.as<int>();
+    p.err = ctx->err.as<int>();
+    p.K6 = ib6_K();
+    p.h3 = geom->ndim == 3 ? (geom->dx[0] * geom->dx[1]) * geom->dx[2] : geom->dx[0] * geom->dx[1];
+    return IBTK_LE_OK;
+}
+
+int ibtk_le::interp_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis, const void* geomv,
+                         const double* const* q_dev, int q_depth, double* Q_dev, int Q_depth, const double* X_dev,
+                         bool check_ghosts) {
+    const ibtk_le_patch_geom* geom = static_cast<const ibtk_le_patch_geom*>(geomv);
+    Params p;
+    if (int rc = prepare(ctx, m, kernel, geom, X_dev, p)) return rc;
+    // LEInteractor.cpp:2416-2426: interp needs min(gcw) >= floor(stencil/2)+1
+    int gmin = geom->gcw[0];
+    for (int d = 1; d < geom->ndim; ++d) gmin = std::min(gmin, geom->gcw[d]);
+    if (check_ghosts && gmin < ibtk_le_min_ghost_width(kernel))
+        return fail(IBTK_LE_ERR_GHOST_WIDTH,
+                    "LEInteractor::interpolate(): insufficient ghost cells: kernel %s needs %d, ghost width %d",
+                    kNames[kernel], ibtk_le_min_ghost_width(kernel), gmin);
+    const int nc = ncomponents(geom, centering, q_depth, Q_depth);
+    if (nc < 0) return -nc;
+    if (m->n == 0) return IBTK_LE_OK;  // LEInteractor.cpp:2427
+    if (!Q_dev || !q_dev) return fail(IBTK_LE_ERR_ARG, "null Q or q");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    p.Qout = Q_dev;
+    p.Q_depth = Q_depth;
+    ctx->ev_valid = false;
+    for (int first = 0; first < nc; first += MAXC) {
+        const int cnt = std::min(MAXC, nc - first);
+        if (int rc = make_comps(geom, centering, axis, const_cast<double* const*>(q_dev), q_depth, Q_depth, first,
+                                cnt, p))
+            return rc;
+        const bool t = ctx->timing && first == 0;
+        HIP_TRY(launch_interp(geom->ndim, kernel, p, m->n, ctx->stream, t ? ctx->ev0 : nullptr,
+                              t ? ctx->ev1 : nullptr));
+        if (t) ctx->ev_valid = true;
+    }
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                              const ibtk_le_patch_geom* geom, const double* const* q_dev, int q_depth, double* Q_dev,
+                              int Q_depth, const double* X_dev) {
+    return ibtk_le::interp_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, X_dev, true);
+}
+
+extern "C" int ibtk_le_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                              const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
+                              int Q_depth, const double* X_dev) {
+    Params p;
+    if (int rc = prepare(ctx, m, kernel, geom, X_dev, p)) return rc;
+    const int nc = ncomponents(geom, centering, q_depth, Q_depth);
+    if (nc < 0) return -nc;
+    if (m->n == 0) return IBTK_LE_OK;  // LEInteractor.cpp:2747
+    if (!Q_dev || !q_dev) return fail(IBTK_LE_ERR_ARG, "null Q or q");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    p.Qin = Q_dev;
+    p.Q_depth = Q_depth;
+    ctx->ev_valid = false;
+    for (int first = 0; first < nc; first += MAXC) {
+        const int cnt = std::min(MAXC, nc - first);
+        if (int rc = make_comps(geom, centering, axis, q_dev, q_depth, Q_depth, first, cnt, p)) return rc;
+        const bool t = ctx->timing && first == 0;
+        HIP_TRY(launch_spread(geom->ndim, kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
+        if (t) ctx->ev_valid = true;
+    }
+    return IBTK_LE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// periodic helpers
+// ---------------------------------------------------------------------------
+static int ghost_descs(const ibtk_le_patch_geom* g, int centering, double* const* q, int q_depth, GhostDesc* out,
+                       int* nout) {
+    const int nd = g->ndim;
+    int narr = 0;
+    for (int a = 0;; ++a) {
+        int ext_mask = 0;
+        double* base = nullptr;
+        int depth = 1;
+        if (centering == IBTK_LE_CELL || centering == IBTK_LE_NODE) {
+            if (a > 0) break;
+            base = q[0];
+            depth = q_depth;
+            ext_mask = centering == IBTK_LE_NODE ? (1 << nd) - 1 : 0;
+        } else if (centering == IBTK_LE_SIDE || centering == IBTK_LE_EDGE) {
+            if (a >= nd) break;
+            base = q[a];
+            ext_mask = centering == IBTK_LE_SIDE ? (1 << a) : (((1 << nd) - 1) & ~(1 << a));
+        } else {
+            return fail(IBTK_LE_ERR_ARG, "unknown centering %d", centering);
+        }
+        if (!base) return fail(IBTK_LE_ERR_ARG, "null Eulerian array");
+        int64_t n[3] = {1, 1, 1};
+        GhostDesc gd;
+        std::memset(&gd, 0, sizeof(gd));
+        for (int d = 0; d < nd; ++d) {
+            gd.lo[d] = g->ilower[d] - g->gcw[d];
+            gd.hi[d] = g->iupper[d] + g->gcw[d] + ((ext_mask >> d) & 1);
+            gd.ilo[d] = g->ilower[d];
+            gd.ihi[d] = g->iupper[d];
+            n[d] = gd.hi[d] - gd.lo[d] + 1;
+        }
+        gd.s1 = n[0];
+        gd.s2 = n[0] * n[1];
+        for (int k = 0; k < depth; ++k) {
+            if (narr >= 16) return fail(IBTK_LE_ERR_ARG, "too many arrays");
+            out[narr] = gd;
+            out[narr].u = base + (int64_t)k * n[0] * n[1] * n[2];
+            ++narr;
+        }
+    }
+    *nout = narr;
+    return IBTK_LE_OK;
+}
+
+static int ghost_op(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int centering, double* const* q, int q_depth,
+                    const int* periodic, int mode) {
+    if (!ctx || !q) return fail(IBTK_LE_ERR_ARG, "null argument");
+    if (int rc = check_geom(geom)) return rc;
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    GhostDesc gds[16];
+    int n = 0;
+    if (int rc = ghost_descs(geom, centering, q, q_depth, gds, &n)) return rc;
+    int per[3] = {1, 1, 1};
+    if (periodic)
+        for (int d = 0; d < geom->ndim; ++d) per[d] = periodic[d];
+    for (int d = 0; d < geom->ndim; ++d)
+        if (per[d] && geom->iupper[d] - geom->ilower[d] + 1 < 2 * geom->gcw[d] + 1)
+            return fail(IBTK_LE_ERR_ARG, "periodic dim %d narrower than 2*ghost+1", d);
+    for (int i = 0; i < n; ++i) {
+        if (mode == 0) HIP_TRY(launch_fill_periodic(geom->ndim, gds[i], per, ctx->stream));
+        else if (mode == 1) HIP_TRY(launch_fold_periodic(geom->ndim, gds[i], per, ctx->stream));
+        else HIP_TRY(launch_zero_ghosts(geom->ndim, gds[i], ctx->stream));
+    }
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_fill_periodic_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int centering,
+                                            double* const* q_dev, int q_depth, const int* periodic) {
+    return ghost_op(ctx, geom, centering, q_dev, q_depth, periodic, 0);
+}
+extern "C" int ibtk_le_fold_periodic_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int centering,
+                                            double* const* q_dev, int q_depth, const int* periodic) {
+    return ghost_op(ctx, geom, centering, q_dev, q_depth, periodic, 1);
+}
+extern "C" int ibtk_le_zero_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int centering,
+                                   double* const* q_dev, int q_depth) {
+    return ghost_op(ctx, geom, centering, q_dev, q_depth, nullptr, 2);
+}
+
+extern "C" int ibtk_le_periodic_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
+                                           int n_markers, int ghost, const int* periodic, int* indices_dev,
+                                           double* Xshift_dev, int capacity, int* count) {
+    if (!ctx || !count) return fail(IBTK_LE_ERR_ARG, "null argument");
+    if (int rc = check_geom(geom)) return rc;
+    if (n_markers < 0 || ghost < 0) return fail(IBTK_LE_ERR_ARG, "negative size");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    *count = 0;
+    if (n_markers == 0) return IBTK_LE_OK;
+    ImageDesc d;
+    std::memset(&d, 0, sizeof(d));
+    d.ndim = geom->ndim;
+    d.ghost = ghost;
+    for (int k = 0; k < geom->ndim; ++k) {
+        d.xlo[k] = geom->x_lower[k];
+        d.xup[k] = geom->x_upper[k];
+        d.dx[k] = geom->dx[k];
+        d.ilo[k] = geom->ilower[k];
+        d.ihi[k] = geom->iupper[k];
+        d.periodic[k] = periodic ? periodic[k] : 1;
+    }
+    int rc;
+    if ((rc = ctx->counts.ensure(sizeof(int) * (size_t)n_markers))) return rc;
+    if ((rc = ctx->offsets.ensure(sizeof(int) * (size_t)n_markers))) return rc;
+    const hipStream_t s = ctx->stream;
+    HIP_TRY(launch_image_count(d, X_dev, n_markers, ctx->counts.as<int>(), s));
+    size_t tb = 0;
+    HIP_TRY(launch_scan(nullptr, tb, ctx->counts.as<int>(), ctx->offsets.as<int>(), n_markers, s));
+    if ((rc = ctx->temp.ensure(tb))) return rc;
+    tb = ctx->temp.cap;
+    HIP_TRY(launch_scan(ctx->temp.p, tb, ctx->counts.as<int>(), ctx->offsets.as<int>(), n_markers, s));
+    int last[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&last[0], ctx->offsets.as<int>() + n_markers - 1, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&last[1], ctx->counts.as<int>() + n_markers - 1, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const int total = last[0] + last[1];
+    *count = total;
+    if (total > capacity || !indices_dev || !Xshift_dev)
+        return fail(IBTK_LE_ERR_ARG, "index list needs %d entries, capacity %d", total, capacity);
+    HIP_TRY(launch_image_write(d, X_dev, n_markers, ctx->offsets.as<int>(), indices_dev, Xshift_dev, capacity, s));
+    return IBTK_LE_OK;
+}

@@ -1,0 +1,134 @@
+// le_internal.h -- internal device-side descriptors of the LE coupling path.
+// Not part of the C-ABI (include/ibtk_le.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace ibtk_le {
+
+// Kernel ids (== ibtk_le_kernel).
+enum : int {
+    K_PIECEWISE_CONSTANT = 0,
+    K_DISCONTINUOUS_LINEAR = 1,
+    K_PIECEWISE_LINEAR = 2,
+    K_PIECEWISE_CUBIC = 3,
+    K_IB_3 = 4,
+    K_IB_4 = 5,
+    K_IB_4_W8 = 6,
+    K_IB_6 = 7,
+    K_BSPLINE_4 = 8,
+    K_COUNT = 9
+};
+
+// Host-visible copy of the kernel traits (le_stencil.h static_asserts agree):
+// W = stencil points per dim; every stencil index of every centering frame lies
+// in [key + LO, key + HI], key = the marker's cell-frame anchor.
+struct KernelInfo {
+    int W, LO, HI;
+};
+constexpr KernelInfo kKernelInfo[K_COUNT] = {
+    {1, 0, 1},   // PIECEWISE_CONSTANT
+    {2, -1, 2},  // DISCONTINUOUS_LINEAR
+    {2, -1, 2},  // PIECEWISE_LINEAR
+    {4, -2, 3},  // PIECEWISE_CUBIC
+    {3, -1, 2},  // IB_3
+    {4, -2, 2},  // IB_4
+    {8, -4, 4},  // IB_4_W8
+    {6, -3, 3},  // IB_6
+    {4, -2, 2},  // BSPLINE_4
+};
+
+constexpr int MAXC = 4;        // components processed by one launch
+constexpr int BRICK3 = 8;      // brick edge (cells) in 3-D: 8^3 = 512 cells
+constexpr int BRICK2 = 16;     // brick edge in 2-D: 16^2 = 256 cells
+constexpr int BLOCK = 256;     // threads per workgroup (4 waves)
+constexpr int SPREAD_CH = 64;  // candidate chunk of the spread kernel (one wave filters)
+
+// One Eulerian array (a component of side data, or a depth slice of cell /
+// node data) in SAMRAI's Fortran layout u(lo0:hi0, lo1:hi1, [lo2:hi2]).
+struct CompDesc {
+    double* u;       // device pointer to element (lo0, lo1, lo2)
+    int lo[3];       // ghost box lower
+    int hi[3];       // ghost box upper (inclusive)
+    int ilower[3];   // the "ilower" argument the Fortran receives (data box lower)
+    double xlo[3];   // the "x_lower" argument the Fortran receives (frame shift applied)
+    int qcomp;       // which AoS component of Q this array pairs with
+    int axis;        // `axis` argument (DISCONTINUOUS_LINEAR)
+    int64_t s1, s2;  // strides of dims 1 and 2 (elements)
+};
+
+// The brick grid over stencil-anchor ("key") cells.
+struct BinGeom {
+    int ndim;
+    int kmin[3];       // key cell of brick (0,0,0), cell (0,0,0)
+    int nb[3];         // bricks per dim
+    int nbricks;
+    int shift;         // log2(cells per brick)
+    double xlo[3];     // cell-frame x_lower of the patch
+    double dx[3];
+    int ilower[3];     // patch box lower
+};
+
+struct Params {
+    BinGeom bg;
+    int ncomp;
+    CompDesc comp[MAXC];
+    int Q_depth;
+    double h3;                 // dx0*dx1[*dx2], associated as the Fortran does
+    double K6;                 // IB_6 parameter K
+    const double* X;           // AoS positions
+    const int* indices;        // list entry -> marker (nullptr: identity)
+    const double* Xshift;      // list entry -> shift[NDIM] (nullptr: zero)
+    const int* sorted_l;       // sorted position -> list entry
+    const unsigned* sorted_key;
+    const int* brick_start;    // nbricks + 1 offsets into the sorted list
+    const int* nentries_dev;   // device copy of the list length
+    const double* Qin;         // spread: marker values
+    double* Qout;              // interp: marker values
+    int* err;                  // device error word (0 = fine)
+};
+
+// Host-side launchers (le_kernels.hip).
+hipError_t launch_bin(int ndim, int kernel, const Params& p, int n, unsigned* keys, int* vals, hipStream_t s);
+hipError_t launch_brick_start(const unsigned* keys, int n, int nbricks, int shift, int* bs, hipStream_t s);
+hipError_t launch_interp(int ndim, int kernel, const Params& p, int n, hipStream_t s, hipEvent_t ev0,
+                         hipEvent_t ev1);
+hipError_t launch_spread(int ndim, int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
+hipError_t launch_sort(void* temp, size_t& temp_bytes, const unsigned* kin, unsigned* kout, const int* vin,
+                       int* vout, int n, int end_bit, hipStream_t s);
+hipError_t launch_scan(void* temp, size_t& temp_bytes, const int* in, int* out, int n, hipStream_t s);
+
+// Periodic helpers
+struct GhostDesc {
+    double* u;
+    int lo[3], hi[3];     // ghost box
+    int ilo[3], ihi[3];   // unique (interior) index range per dim
+    int64_t s1, s2;
+};
+hipError_t launch_fill_periodic(int ndim, const GhostDesc& g, const int* periodic, hipStream_t s);
+hipError_t launch_fold_periodic(int ndim, const GhostDesc& g, const int* periodic, hipStream_t s);
+hipError_t launch_zero_ghosts(int ndim, const GhostDesc& g, hipStream_t s);
+
+struct ImageDesc {
+    int ndim;
+    double xlo[3], xup[3], dx[3];
+    int ilo[3], ihi[3];
+    int ghost;
+    int periodic[3];
+};
+hipError_t launch_image_count(const ImageDesc& d, const double* X, int n, int* counts, hipStream_t s);
+hipError_t launch_image_write(const ImageDesc& d, const double* X, int n, const int* offsets, int* idx,
+                              double* xshift, int capacity, hipStream_t s);
+
+}  // namespace ibtk_le
+
+// Internal entry used by the Fortran shims (skips the LEInteractor-level ghost check).
+struct ibtk_le_ctx_s;
+struct ibtk_le_markers_s;
+struct ibtk_le_patch_geom_s;
+namespace ibtk_le {
+int interp_impl(ibtk_le_ctx_s* ctx, ibtk_le_markers_s* m, int kernel, int centering, int axis, const void* geom,
+                const double* const* q_dev, int q_depth, double* Q_dev, int Q_depth, const double* X_dev,
+                bool check_ghosts);
+}  // namespace ibtk_le

@@ -1,0 +1,256 @@
+"""Python host API over the C-ABI (device-resident torch tensors).
+
+Thin, allocation-free wrappers: every array is a torch tensor on the GPU and is
+handed to libibtk_le.so by pointer.  Arrays follow SAMRAI's Fortran layout, so a
+3-D ghosted array of extents (n0, n1, n2) is a C-contiguous tensor of shape
+(n2, n1, n0) [x fastest], with an extra leading depth axis for cell/node data.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib
+from ._lib import PatchGeom, check, kernel_id
+
+CENTERING = _lib.CENTERING
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("ibtk_le works on device-resident tensors")
+    if not t.is_contiguous():
+        raise ValueError("tensor must be contiguous")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _ptr_array(ts: Sequence[torch.Tensor]):
+    arr = (ctypes.c_void_p * max(1, len(ts)))()
+    for i, t in enumerate(ts):
+        if t is None:
+            arr[i] = None
+            continue
+        if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("Eulerian arrays must be contiguous float64 device tensors")
+        arr[i] = t.data_ptr()
+    return arr
+
+
+@dataclass
+class Geometry:
+    """Patch box + ghost width + Cartesian geometry (one uniform patch)."""
+
+    ilower: Sequence[int]
+    iupper: Sequence[int]
+    gcw: int | Sequence[int]
+    dx: Sequence[float]
+    x_lower: Sequence[float]
+    x_upper: Optional[Sequence[float]] = None
+
+    def __post_init__(self):
+        self.ndim = len(self.ilower)
+        if isinstance(self.gcw, int):
+            self.gcw = [self.gcw] * self.ndim
+        if self.x_upper is None:
+            self.x_upper = [self.x_lower[d] + (self.iupper[d] - self.ilower[d] + 1) * self.dx[d]
+                            for d in range(self.ndim)]
+        self.c = PatchGeom.make(self.ilower, self.iupper, self.gcw, self.dx, self.x_lower, self.x_upper)
+
+    @staticmethod
+    def periodic_unit(N: Sequence[int], ghost: int, x_lower=None, x_upper=None):
+        nd = len(N)
+        xl = list(x_lower) if x_lower is not None else [0.0] * nd
+        xu = list(x_upper) if x_upper is not None else [1.0] * nd
+        dx = [(xu[d] - xl[d]) / N[d] for d in range(nd)]
+        return Geometry([0] * nd, [n - 1 for n in N], ghost, dx, xl, xu)
+
+    def array_shape(self, centering: str, comp: int = 0, depth: int = 1):
+        """torch shape of the ghosted array of component `comp`."""
+        ext = self.ext_mask(centering, comp)
+        n = [self.iupper[d] - self.ilower[d] + 1 + 2 * self.gcw[d] + ((ext >> d) & 1) for d in range(self.ndim)]
+        shape = tuple(reversed(n))
+        return ((depth,) + shape) if centering in ("cell", "node") else shape
+
+    def ext_mask(self, centering, comp=0):
+        full = (1 << self.ndim) - 1
+        return {"cell": 0, "node": full, "side": 1 << comp, "edge": full & ~(1 << comp)}[centering]
+
+    def ncomp(self, centering):
+        return self.ndim if centering in ("side", "edge") else 1
+
+    def alloc(self, centering: str, depth: int = 1, device="cuda", fill=0.0):
+        return [torch.full(self.array_shape(centering, c, depth), fill, dtype=torch.float64, device=device)
+                for c in range(self.ncomp(centering))]
+
+
+class Context:
+    """A library context bound to one device and a HIP stream (torch's current stream by default)."""
+
+    def __init__(self, device: int = 0, stream: Optional[torch.cuda.Stream] = None):
+        self.lib = _lib.load()
+        self.device = device
+        s = stream if stream is not None else torch.cuda.current_stream(device)
+        self.stream = s
+        h = ctypes.c_void_p()
+        check(self.lib.ibtk_le_ctx_create(device, ctypes.c_void_p(s.cuda_stream), ctypes.byref(h)))
+        self.h = h
+
+    def set_stream(self, stream: torch.cuda.Stream):
+        self.stream = stream
+        check(self.lib.ibtk_le_ctx_set_stream(self.h, ctypes.c_void_p(stream.cuda_stream)))
+
+    def synchronize(self):
+        check(self.lib.ibtk_le_ctx_synchronize(self.h))
+
+    def enable_timing(self, on=True):
+        check(self.lib.ibtk_le_ctx_enable_timing(self.h, int(on)))
+
+    def last_kernel_ms(self) -> float:
+        return float(self.lib.ibtk_le_ctx_last_kernel_ms(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.ibtk_le_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Markers:
+    """A binned marker list on the device (the device-side LIndexSetData)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        check(ctx.lib.ibtk_le_markers_create(ctx.h, ctypes.byref(h)))
+        self.h = h
+        self.kernel = None
+        self.geom = None
+
+    def bin(self, geom: Geometry, kernel: str, X: torch.Tensor, indices: Optional[torch.Tensor] = None,
+            Xshift: Optional[torch.Tensor] = None, n: Optional[int] = None):
+        if indices is not None:
+            assert indices.dtype == torch.int32
+            n = indices.numel()
+        elif n is None:
+            n = X.shape[0]
+        if Xshift is not None:
+            assert Xshift.dtype == torch.float64 and Xshift.numel() == n * geom.ndim
+        assert X.dtype == torch.float64
+        check(self.ctx.lib.ibtk_le_markers_bin(self.ctx.h, self.h, ctypes.byref(geom.c), kernel_id(kernel), _ptr(X),
+                                               _ptr(indices), _ptr(Xshift), int(n)))
+        self.kernel, self.geom, self.n = kernel, geom, n
+        return self
+
+    def count(self) -> int:
+        return int(self.ctx.lib.ibtk_le_markers_count(self.h))
+
+    def order(self) -> torch.Tensor:
+        """Canonical order (device int32 copy): order[i] = list position of the i-th sorted entry."""
+        p = ctypes.c_void_p()
+        check(self.ctx.lib.ibtk_le_markers_order(self.h, ctypes.byref(p)))
+        n = self.count()
+        out = torch.empty(n, dtype=torch.int32, device=f"cuda:{self.ctx.device}")
+        if n:
+            torch.cuda.current_stream(self.ctx.device).synchronize()
+            self.ctx.synchronize()
+            import ctypes as _c
+            hip = _hip()
+            check_hip(hip.hipMemcpy(_c.c_void_p(out.data_ptr()), p, _c.c_size_t(4 * n), 3))
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx.lib.ibtk_le_markers_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_hip_lib = None
+
+
+def _hip():
+    global _hip_lib
+    if _hip_lib is None:
+        _hip_lib = ctypes.CDLL("libamdhip64.so")
+        _hip_lib.hipMemcpy.restype = ctypes.c_int
+        _hip_lib.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    return _hip_lib
+
+
+def check_hip(rc):
+    if rc != 0:
+        raise RuntimeError(f"hip error {rc}")
+
+
+def interp(ctx: Context, markers: Markers, kernel: str, centering: str, geom: Geometry,
+           q: Sequence[torch.Tensor], Q: torch.Tensor, X: torch.Tensor, q_depth: int = 1, Q_depth: Optional[int] = None,
+           axis: int = 0):
+    """Q(d, s) = sum w q  (LEInteractor::interpolate)."""
+    if Q_depth is None:
+        Q_depth = geom.ndim if centering in ("side", "edge") else q_depth
+    arr = _ptr_array(q)
+    check(ctx.lib.ibtk_le_interp(ctx.h, markers.h, kernel_id(kernel), CENTERING[centering], axis,
+                                 ctypes.byref(geom.c), arr, q_depth, _ptr(Q), Q_depth, _ptr(X)))
+
+
+def spread(ctx: Context, markers: Markers, kernel: str, centering: str, geom: Geometry,
+           q: Sequence[torch.Tensor], Q: torch.Tensor, X: torch.Tensor, q_depth: int = 1, Q_depth: Optional[int] = None,
+           axis: int = 0):
+    """q += S Q  (LEInteractor::spread), deterministic marker-ordered sums."""
+    if Q_depth is None:
+        Q_depth = geom.ndim if centering in ("side", "edge") else q_depth
+    arr = _ptr_array(q)
+    check(ctx.lib.ibtk_le_spread(ctx.h, markers.h, kernel_id(kernel), CENTERING[centering], axis,
+                                 ctypes.byref(geom.c), arr, q_depth, _ptr(Q), Q_depth, _ptr(X)))
+
+
+def _periodic_arg(periodic, ndim):
+    if periodic is None:
+        return None
+    a = (ctypes.c_int * 3)(*([int(bool(p)) for p in periodic] + [1] * (3 - ndim)))
+    return ctypes.cast(a, ctypes.c_void_p), a
+
+
+def fill_periodic_ghosts(ctx: Context, geom: Geometry, centering: str, q, q_depth=1, periodic=None):
+    pa = _periodic_arg(periodic, geom.ndim)
+    check(ctx.lib.ibtk_le_fill_periodic_ghosts(ctx.h, ctypes.byref(geom.c), CENTERING[centering], _ptr_array(q),
+                                               q_depth, pa[0] if pa else None))
+
+
+def fold_periodic_ghosts(ctx: Context, geom: Geometry, centering: str, q, q_depth=1, periodic=None):
+    pa = _periodic_arg(periodic, geom.ndim)
+    check(ctx.lib.ibtk_le_fold_periodic_ghosts(ctx.h, ctypes.byref(geom.c), CENTERING[centering], _ptr_array(q),
+                                               q_depth, pa[0] if pa else None))
+
+
+def zero_ghosts(ctx: Context, geom: Geometry, centering: str, q, q_depth=1):
+    check(ctx.lib.ibtk_le_zero_ghosts(ctx.h, ctypes.byref(geom.c), CENTERING[centering], _ptr_array(q), q_depth))
+
+
+def periodic_index_list(ctx: Context, geom: Geometry, X: torch.Tensor, ghost: int, periodic=None):
+    """(indices int32, Xshift float64 [n, ndim]) device tensors, marker-major order."""
+    M = X.shape[0]
+    cnt = ctypes.c_int(0)
+    pa = _periodic_arg(periodic, geom.ndim)
+    cap = M * (3 ** geom.ndim) if ghost > 0 else M
+    idx = torch.empty(max(1, cap), dtype=torch.int32, device=X.device)
+    xs = torch.empty((max(1, cap), geom.ndim), dtype=torch.float64, device=X.device)
+    check(ctx.lib.ibtk_le_periodic_index_list(ctx.h, ctypes.byref(geom.c), _ptr(X), M, ghost,
+                                              pa[0] if pa else None, _ptr(idx), _ptr(xs), cap, ctypes.byref(cnt)))
+    n = cnt.value
+    return idx[:n].contiguous(), xs[:n].contiguous()

@@ -1,0 +1,172 @@
+/*
+ * ibtk_le.h -- C-ABI of the MI355X-native Lagrangian-Eulerian coupling path.
+ *
+ * This library replaces the Fortran kernels behind IBTK::LEInteractor
+ * (ibtk/src/lagrangian/LEInteractor.cpp, ibtk/src/lagrangian/fortran/
+ * lagrangian_interaction{2,3}d.f.m4) with hand-written CDNA4 (gfx950) HIP
+ * kernels.  Three levels are exported:
+ *
+ *  1. Device-resident API (ibtk_le_*): every array pointer is a device pointer;
+ *     work is stream-ordered on the context's HIP stream; nothing blocks unless
+ *     the function says so.  This is the level bench.py measures.
+ *  2. Fortran-symbol host shims (lagrangian_<kernel>_{interp,spread}{2,3}d_):
+ *     the exact symbols and by-reference signatures LEInteractor.cpp:68-619
+ *     declares (IBTK_FC_FUNC_ lowercase + trailing underscore), host memory in
+ *     and out (H2D -> kernel -> D2H).  Drop-in for the Fortran objects.
+ *  3. A C++ LEInteractor facade (include/ibtk_le/LEInteractor.h) over light
+ *     patch/data views, mirroring ibtk/include/ibtk/LEInteractor.h:100-993.
+ *
+ * Error convention (replaces TBOX_ERROR aborts, LEInteractor.cpp:679,2421,2740):
+ * every function returns an ibtk_le_status; ibtk_le_last_error() describes the
+ * most recent failure of the calling thread.
+ */
+#ifndef IBTK_LE_H
+#define IBTK_LE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes -------------------------------------------------------- */
+typedef enum {
+    IBTK_LE_OK = 0,
+    IBTK_LE_ERR_UNKNOWN_KERNEL = 1, /* LEInteractor.cpp:679 "Unknown kernel function"        */
+    IBTK_LE_ERR_GHOST_WIDTH = 2,    /* LEInteractor.cpp:2421, 2740 "insufficient ghost cells" */
+    IBTK_LE_ERR_DEPTH = 3,          /* LEInteractor.cpp:769, 1627 side/edge depth mismatch   */
+    IBTK_LE_ERR_ARG = 4,            /* invalid argument (null pointer, bad dim, bad box)     */
+    IBTK_LE_ERR_DEVICE = 5,         /* HIP runtime error                                     */
+    IBTK_LE_ERR_NOMEM = 6,          /* device allocation failed                              */
+    IBTK_LE_ERR_RANGE = 7,          /* index space too large for the 32-bit bin keys         */
+    IBTK_LE_ERR_INVARIANT = 8       /* a device-side consistency check failed                */
+} ibtk_le_status;
+
+/* ---- kernel functions (LEInteractor::getStencilSize, LEInteractor.cpp:668-682) */
+typedef enum {
+    IBTK_LE_KERNEL_PIECEWISE_CONSTANT = 0,
+    IBTK_LE_KERNEL_DISCONTINUOUS_LINEAR = 1,
+    IBTK_LE_KERNEL_PIECEWISE_LINEAR = 2,
+    IBTK_LE_KERNEL_PIECEWISE_CUBIC = 3,
+    IBTK_LE_KERNEL_IB_3 = 4,
+    IBTK_LE_KERNEL_IB_4 = 5,
+    IBTK_LE_KERNEL_IB_4_W8 = 6,
+    IBTK_LE_KERNEL_IB_6 = 7,
+    IBTK_LE_KERNEL_BSPLINE_4 = 8 /* not in the reference: cubic B-spline */
+} ibtk_le_kernel;
+
+/* ---- data centerings (SAMRAI pdat::{Cell,Side,Node,Edge}Data) ---------------- */
+typedef enum {
+    IBTK_LE_CELL = 0, /* one array, depth q_depth, unshifted frame                      */
+    IBTK_LE_SIDE = 1, /* NDIM arrays (one per axis), depth 1, x_lower[axis] -= dx/2     */
+    IBTK_LE_NODE = 2, /* one array, depth q_depth, x_lower -= dx/2 in every dim         */
+    IBTK_LE_EDGE = 3  /* 3D only: NDIM arrays, every dim but `axis` shifted             */
+} ibtk_le_centering;
+
+/* Patch geometry: the cell box, the ghost width of the Eulerian data and the
+ * Cartesian patch geometry (CartesianPatchGeometry::getDx/getXLower/getXUpper). */
+typedef struct {
+    int ndim;          /* 2 or 3 */
+    int ilower[3];     /* patch box lower (cell indices) */
+    int iupper[3];     /* patch box upper (inclusive)   */
+    int gcw[3];        /* ghost cell width of the Eulerian arrays */
+    double dx[3];
+    double x_lower[3];
+    double x_upper[3];
+} ibtk_le_patch_geom;
+
+typedef struct ibtk_le_ctx_s* ibtk_le_ctx;
+typedef struct ibtk_le_markers_s* ibtk_le_markers;
+
+/* ---- kernel-string helpers ---------------------------------------------------- */
+/* Returns the kernel id for "IB_4", "IB_6", ... or -1 (LEInteractor.cpp:668-682). */
+int ibtk_le_kernel_from_name(const char* name);
+const char* ibtk_le_kernel_name(int kernel);
+/* LEInteractor::getStencilSize / getMinimumGhostWidth (LEInteractor.cpp:668-687). */
+int ibtk_le_stencil_size(int kernel);
+int ibtk_le_min_ghost_width(int kernel);
+const char* ibtk_le_last_error(void);
+const char* ibtk_le_version(void);
+
+/* ---- context -------------------------------------------------------------------- */
+/* `stream` is a hipStream_t (NULL = the default stream).  The context caches the
+ * workspace the binning and sort steps need, so repeated calls allocate nothing. */
+int ibtk_le_ctx_create(int device, void* stream, ibtk_le_ctx* out);
+int ibtk_le_ctx_destroy(ibtk_le_ctx ctx);
+int ibtk_le_ctx_set_stream(ibtk_le_ctx ctx, void* stream);
+/* Waits for the context stream and reports device-side invariant failures
+ * latched by earlier calls (IBTK_LE_ERR_INVARIANT), then clears them. */
+int ibtk_le_ctx_synchronize(ibtk_le_ctx ctx);
+
+/* ---- marker binning (device LIndexSetData / LDataManager re-binning) --------------
+ * Replaces the per-patch index bookkeeping LEInteractor::buildLocalIndices
+ * (LEInteractor.cpp:3031-3108) hands to the Fortran: it takes the list of
+ * (local marker index, periodic shift) pairs -- `indices_dev`/`Xshift_dev`, or
+ * NULL/NULL for the identity list 0..n-1 with zero shifts -- and sorts it on the
+ * device by the stencil anchor cell of X(s)+Xshift (stable radix sort; bins of
+ * 8^3 cells in 3-D, 16^2 in 2-D).  The sorted order is the canonical order
+ * spreading sums in.  The handle keeps device copies of the sorted list. */
+int ibtk_le_markers_create(ibtk_le_ctx ctx, ibtk_le_markers* out);
+int ibtk_le_markers_destroy(ibtk_le_markers m);
+int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_patch_geom* geom, int kernel,
+                        const double* X_dev, const int* indices_dev, const double* Xshift_dev, int nindices);
+/* Number of list entries, and device pointers to the sorted list (entry -> marker
+ * index, and entry -> Xshift[NDIM]); valid until the next bin call. */
+int ibtk_le_markers_count(ibtk_le_markers m);
+/* Device pointer to the canonical order: order_dev[i] = position in the binned
+ * list (0..count-1) of the i-th entry in canonical order.  Valid until the next
+ * bin call; the caller may copy it to the host to feed the oracle the same list. */
+int ibtk_le_markers_order(ibtk_le_markers m, const int** order_dev);
+
+/* ---- interpolation / spreading on device-resident data --------------------------
+ * q_dev[c] points at the ghosted Fortran-ordered array of component c:
+ *   SIDE/EDGE: c = 0..NDIM-1, the array of axis c (SideData::getPointer(c)), depth 1
+ *   CELL/NODE: c = 0 only, an array of depth q_depth (depth slowest)
+ * Q_dev is the marker array in LData layout: AoS, Q_depth values per marker
+ * (SIDE/EDGE: Q_depth == NDIM).  X_dev: AoS NDIM positions per marker.
+ * The marker list is the one last binned into `m` (same kernel and geometry).
+ *
+ * interp:  Q(d, s) = sum_i w_i(X(s)+Xshift) q(i, d)   for every listed s
+ *          (LEInteractor.cpp:970-1055 / lagrangian_<k>_interp3d, f.m4:1258-1385)
+ * spread:  q(i, d) += sum_s w_i(X(s)+Xshift) Q(d, s) / (dx0 dx1 [dx2])
+ *          summed per grid point in the list's canonical (binned) order, without
+ *          atomics: deterministic and bit-stable run to run
+ *          (LEInteractor.cpp:1828-1913 / lagrangian_<k>_spread3d, f.m4:1395-1522) */
+int ibtk_le_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                   const ibtk_le_patch_geom* geom, const double* const* q_dev, int q_depth, double* Q_dev,
+                   int Q_depth, const double* X_dev);
+int ibtk_le_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                   const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
+                   int Q_depth, const double* X_dev);
+
+/* ---- helpers for a single periodic patch (uniform finest level) -----------------
+ * Fill the ghost layers of the arrays of `centering` from the periodic interior
+ * (the RefineSchedule::fillData the caller runs before interp, LDataManager.cpp:750). */
+int ibtk_le_fill_periodic_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int centering,
+                                 double* const* q_dev, int q_depth, const int* periodic);
+/* Spreading in ghost-region-sum mode: zero the ghost layers before spreading the
+ * interior markers, then fold every ghost value back onto its periodic interior
+ * image (dims folded slowest first, one source per destination per pass:
+ * deterministic).  The multi-GPU path uses the same fold along x/y and an RCCL
+ * exchange along z. */
+int ibtk_le_zero_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int centering, double* const* q_dev,
+                        int q_depth);
+int ibtk_le_fold_periodic_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int centering,
+                                 double* const* q_dev, int q_depth, const int* periodic);
+/* Build the list of interior markers and of their periodic images that fall in the
+ * ghost box (LIndexSetData::cacheLocalIndices, LIndexSetData.cpp:83-169, for one
+ * patch covering a periodic domain; getCellIndex, IndexUtilities-inl.h:66-89).
+ * Writes up to `capacity` entries into indices_dev / Xshift_dev (NDIM per entry)
+ * and the entry count into *count (host).  ghost = 0 gives the interior list. */
+int ibtk_le_periodic_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
+                                int n_markers, int ghost, const int* periodic, int* indices_dev,
+                                double* Xshift_dev, int capacity, int* count);
+
+/* Diagnostics: number of device kernel launches issued by the last interp/spread/bin
+ * call on this context, and the per-step timing of the last call's main kernel (ms,
+ * measured with HIP events on the context stream when enabled). */
+int ibtk_le_ctx_enable_timing(ibtk_le_ctx ctx, int enable);
+double ibtk_le_ctx_last_kernel_ms(ibtk_le_ctx ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IBTK_LE_H */

@@ -321,7 +321,16 @@ static void ora_piecewise_constant(int spread, const ora_box* b, const double* d
         for (int d = 0; d < ndim; ++d)
             ic[d] = ora_nint((X[(int64_t)ndim * s + d] + Xshift[(int64_t)ndim * l + d] - x_lower[d]) / dx[d] - 0.5) +
                     ilower[d];
+        /* The reference reads/writes u(ic) unchecked; a cell outside the ghost
+         * box is undefined there.  Here (and on the GPU) it is an empty
+         * stencil: interp gives 0, spread adds nothing. */
+        int inside = 1;
+        for (int d = 0; d < ndim; ++d) inside &= (ic[d] >= b->lo[d] && ic[d] <= b->hi[d]);
         for (int d = 0; d < depth; ++d) {
+            if (!inside) {
+                if (!spread) V[(int64_t)depth * s + d] = 0.0;
+                continue;
+            }
             const int64_t k = ora_idx(b, ic[0], ic[1], ic[2], d);
             if (!spread)
                 V[(int64_t)depth * s + d] = u[k];

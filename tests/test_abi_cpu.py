@@ -1,0 +1,68 @@
+"""CPU tests of the C-ABI library: it loads and exports every symbol include/*.h declares.
+
+No compute call is made here (no GPU in this container); the GPU tests exercise them.
+"""
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def declared_functions():
+    names = set()
+    for h in (ROOT / "include").rglob("*.h"):
+        text = h.read_text()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        text = re.sub(r"//[^\n]*", "", text)
+        for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(\w+)\s*\(", text, flags=re.M):
+            name = m.group(1)
+            if name in ("if", "while", "for", "return", "sizeof", "defined"):
+                continue
+            names.add(name)
+    return sorted(names)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from ibamr_amd import _lib
+    if not _lib.LIB_PATH.exists():
+        from ibamr_amd import build
+        build.build()
+    return _lib.load()
+
+
+def test_headers_declare_the_abi():
+    names = declared_functions()
+    assert "ibtk_le_interp" in names and "ibtk_le_spread" in names
+    assert "lagrangian_ib_4_interp3d_" in names and "lagrangian_ib_6_spread2d_" in names
+    assert len([n for n in names if n.startswith("lagrangian_")]) == 32
+
+
+def test_library_exports_every_declared_symbol(lib):
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, f"not exported: {missing}"
+
+
+def test_host_only_helpers(lib):
+    from ibamr_amd import _lib
+    assert _lib.kernel_id("IB_4") == 5
+    assert lib.ibtk_le_stencil_size(_lib.kernel_id("IB_6")) == 6
+    # LEInteractor::getMinimumGhostWidth: floor(stencil/2)+1
+    expect = {"PIECEWISE_CONSTANT": 1, "DISCONTINUOUS_LINEAR": 2, "PIECEWISE_LINEAR": 2, "PIECEWISE_CUBIC": 3,
+              "IB_3": 3, "IB_4": 3, "IB_4_W8": 5, "IB_6": 4, "BSPLINE_4": 3}
+    for k, g in expect.items():
+        assert lib.ibtk_le_min_ghost_width(_lib.kernel_id(k)) == g
+    assert lib.ibtk_le_kernel_from_name(b"USER_DEFINED") == -1
+    with pytest.raises(_lib.IBTKLEError):
+        _lib.kernel_id("NOPE")
+
+
+def test_no_oracle_in_product_path():
+    """The product package never imports the oracle (it is test infrastructure)."""
+    pat = re.compile(r"(import\s+oracle|from\s+oracle|le_oracle|libleoracle|ora_interp|ora_spread)")
+    for p in (ROOT / "ibamr_amd").rglob("*"):
+        if p.suffix in (".py", ".cpp", ".hip", ".h"):
+            assert not pat.search(p.read_text()), p
