@@ -1,0 +1,324 @@
+#!/usr/bin/env python3
+"""Benchmark of the LE coupling hot path: IB_4 3-D staggered interpolate + spread.
+
+One step = one IB coupling pass over the resident markers of every rank:
+  bin      re-bin the markers by stencil anchor (device radix sort)
+  fill     ghost fill of u (x/y periodic locally, z from the slab neighbours)
+  interp   U = J u   (LEInteractor::interpolate, side-centred, all 3 components)
+  spread   f += S F  (LEInteractor::spread into the ghosted slab, ghosts zeroed first)
+  sum      ghost-region sum of f (z over RCCL, x/y periodic locally)
+Marker-ops per step = 2 x markers (one interpolate and one spread per marker).
+
+Default workload = BASELINE.json configs[3] (cfg4): 1024^3 periodic staggered grid,
+1e8 uniformly scattered markers (seed 1234), IB_4, fp64.  It is the configuration
+the north-star target (>=1e10 marker-ops/s at >=50 % HBM roofline on one MI355X,
+>=6x at 8 GPUs) is quoted on, and it fits one GPU (~62 GB).  With --gpus N the same
+global problem is z-slab decomposed over N ranks (strong scaling).  --config cfg2/cfg3/
+cfg5 select the other BASELINE configs.
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "IB_4 3D spread+interp marker-ops/sec (fp64) + % HBM roofline, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+CONFIGS = {
+    "cfg2": dict(N=128, M=100_000, kernel="IB_4", markers="sphere",
+                 desc="cfg2: 128^3 periodic staggered grid, 1e5 markers on a sphere (r=0.35), IB_4"),
+    "cfg3": dict(N=512, M=10_000_000, kernel="IB_6", markers="uniform",
+                 desc="cfg3: 512^3 periodic staggered grid, 1e7 uniform markers, IB_6"),
+    "cfg4": dict(N=1024, M=100_000_000, kernel="IB_4", markers="uniform",
+                 desc="cfg4: 1024^3 periodic staggered grid, 1e8 uniform markers (seed 1234), IB_4, z-slabs"),
+    "cfg5": dict(N=512, M=10_000_000, kernel="IB_4", markers="clustered",
+                 desc="cfg5: 512^3 periodic staggered grid, 1e7 markers in ~2% of cells (4 sheets + 2 bundles), IB_4"),
+}
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def make_markers(kind, M, slab, seed, device):
+    """Markers of this rank: those whose z lies in the rank's slab [z0, z1)*dz."""
+    import torch
+    g = torch.Generator(device=device).manual_seed(seed + 7919 * slab.rank)
+    z_lo, z_hi = slab.z0 * slab.dx[2], slab.z1 * slab.dx[2]
+    if kind == "uniform":
+        m = M // slab.P + (1 if slab.rank < M % slab.P else 0)
+        X = torch.rand((m, 3), dtype=torch.float64, device=device, generator=g)
+        X[:, 2].mul_(z_hi - z_lo).add_(z_lo)
+        return X
+    if kind == "sphere":
+        # Fibonacci lattice on a sphere of radius 0.35 centred at 0.5
+        i = torch.arange(M, dtype=torch.float64, device=device) + 0.5
+        phi = torch.acos(1 - 2 * i / M)
+        theta = math.pi * (1 + 5 ** 0.5) * i
+        X = torch.stack([0.5 + 0.35 * torch.cos(theta) * torch.sin(phi),
+                         0.5 + 0.35 * torch.sin(theta) * torch.sin(phi),
+                         0.5 + 0.35 * torch.cos(phi)], dim=1)
+    elif kind == "clustered":
+        # 4 thin sheets (1 cell thick) + 2 fibre bundles, ~2% of cells
+        n_sheet = int(M * 0.8) // 4
+        n_fib = (M - 4 * n_sheet) // 2
+        h = 1.0 / slab.N[0]
+        parts = []
+        for k, z in enumerate((0.2, 0.4, 0.6, 0.8)):
+            s = torch.rand((n_sheet, 3), dtype=torch.float64, device=device, generator=g)
+            s[:, 2] = z + (s[:, 2] - 0.5) * h
+            parts.append(s)
+        for k, (cx, cy) in enumerate(((0.3, 0.3), (0.7, 0.6))):
+            f = torch.rand((n_fib, 3), dtype=torch.float64, device=device, generator=g)
+            r = 0.02 * torch.sqrt(f[:, 0])
+            t = 2 * math.pi * f[:, 1]
+            f[:, 0] = cx + r * torch.cos(t)
+            f[:, 1] = cy + r * torch.sin(t)
+            parts.append(f)
+        X = torch.cat(parts)
+    else:
+        raise ValueError(kind)
+    keep = (X[:, 2] >= z_lo) & (X[:, 2] < z_hi)
+    return X[keep].contiguous()
+
+
+def cpu_baseline(cfg, kernel, seconds_target=15.0):
+    """The oracle (single-thread C restatement) timed on a bounded, same-density sample.
+
+    Sample: a periodic N_s^3 grid with the workload's marker density (cell-sorted
+    order, as on the GPU), IB_4 side-centred interp + spread (periodic images in the
+    spread list, LIndexSetData semantics), repeated until ~seconds_target of CPU work.
+    """
+    import numpy as np
+    from oracle import oracle as ora
+    N = cfg["N"]
+    density = cfg["M"] / float(N ** 3)
+    Ns = min(N, 192)
+    Ms = max(1000, int(round(density * Ns ** 3)))
+    if cfg["markers"] == "sphere":
+        Ns, Ms = N, cfg["M"]
+    rng = np.random.default_rng(1234)
+    X = rng.uniform(0.0, 1.0, (Ms, 3))
+    if cfg["markers"] == "sphere":
+        i = np.arange(Ms) + 0.5
+        phi = np.arccos(1 - 2 * i / Ms)
+        th = math.pi * (1 + 5 ** 0.5) * i
+        X = np.stack([0.5 + 0.35 * np.cos(th) * np.sin(phi), 0.5 + 0.35 * np.sin(th) * np.sin(phi),
+                      0.5 + 0.35 * np.cos(phi)], 1)
+    c = np.floor(X * Ns).astype(np.int64)
+    X = X[np.lexsort((c[:, 0], c[:, 1], c[:, 2]))].copy()
+    F = rng.uniform(-1, 1, (Ms, 3))
+    g = ora.min_ghost_width(kernel)
+    lo, hi, dx = [0, 0, 0], [Ns - 1] * 3, [1.0 / Ns] * 3
+    u = [rng.uniform(-1, 1, ora.ghost_shape(*ora.side_box(lo, hi, a), [g] * 3)) for a in range(3)]
+    f = [np.zeros_like(a) for a in u]
+    idx_i = np.arange(Ms, dtype=np.int32)
+    xs_i = np.zeros((Ms, 3))
+    idx_s, xs_s, _ = ora.periodic_index_list(X, [0, 0, 0], [1, 1, 1], dx, lo, hi, g)
+    U = np.zeros((Ms, 3))
+    reps, elapsed = 0, 0.0
+    while elapsed < seconds_target or reps < 2:
+        t0 = time.perf_counter()
+        ora.side_interp(kernel, dx, [0, 0, 0], lo, hi, [g] * 3, u, idx_i, xs_i, X, U)
+        ora.side_spread(kernel, dx, [0, 0, 0], lo, hi, [g] * 3, f, idx_s, xs_s, X, F)
+        elapsed += time.perf_counter() - t0
+        reps += 1
+        if reps >= 50:
+            break
+    rate = 2.0 * Ms * reps / elapsed
+    return {"value": rate, "unit": "marker-ops/s", "cores": 1, "kind": "port",
+            "sample": f"{Ns}^3 periodic grid, {Ms} uniform markers (same density as the workload), "
+                      f"{kernel} side interp+spread, cell-sorted, {reps} reps, {elapsed:.1f} s, 1 thread (oracle C)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="cfg4", choices=sorted(CONFIGS))
+    ap.add_argument("--kernel", default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-rebin", action="store_true", help="bin once outside the timed loop")
+    args = ap.parse_args()
+
+    import torch
+    cfg = CONFIGS[args.config]
+    kernel = args.kernel or cfg["kernel"]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from ibamr_amd import le
+    from ibamr_amd.slab import Slab, SlabExchange
+
+    N = cfg["N"]
+    ghost = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
+    slab = Slab([N, N, N], world, rank, ghost)
+    geom = slab.geometry()
+    ctx = le.Context(local)
+
+    t_setup = time.perf_counter()
+    X = make_markers(cfg["markers"], cfg["M"], slab, 1234, dev)
+    M_local = X.shape[0]
+    gen = torch.Generator(device=dev).manual_seed(4321 + rank)
+    F = torch.rand((M_local, 3), dtype=torch.float64, device=dev, generator=gen).mul_(2).sub_(1)
+    U = torch.zeros((M_local, 3), dtype=torch.float64, device=dev)
+    u = geom.alloc("side", device=dev)
+    for a in u:
+        a.uniform_(-1.0, 1.0, generator=gen)
+    f = geom.alloc("side", device=dev)
+    ex_u = SlabExchange(slab, u, ctx)
+    ex_f = SlabExchange(slab, f, ctx)
+    bins = le.Markers(ctx)
+    bins.bin(geom, kernel, X)
+    # exact algorithmic bytes: distinct side points touched by the clipped stencils
+    masks = le.mark_stencils(ctx, bins, kernel, "side", geom, X)
+    S_touched = [int(m.sum(dtype=torch.int64).item()) for m in masks]
+    del masks
+    torch.cuda.synchronize()
+    M_total = M_local
+    if world > 1:
+        t = torch.tensor([M_local], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        M_total = int(t.item())
+    log(f"setup {time.perf_counter() - t_setup:.1f}s: rank {rank} markers {M_local} of {M_total}, "
+        f"slab z[{slab.z0},{slab.z1}), touched {S_touched}")
+
+    E = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    acc = {"bin": [], "interp": [], "spread": [], "exchange": []}
+
+    def step(record):
+        if record:
+            E[0].record()
+        if not args.no_rebin:
+            bins.bin(geom, kernel, X)
+        if record:
+            E[1].record()
+        ex_u.halo_fill()
+        le.interp(ctx, bins, kernel, "side", geom, u, U, X)
+        if record:
+            E[2].record()
+        le.zero_ghosts(ctx, geom, "side", f)
+        if record:
+            E[3].record()
+        le.spread(ctx, bins, kernel, "side", geom, f, F, X)
+        if record:
+            E[4].record()
+        ex_f.ghost_sum()
+        if record:
+            E[5].record()
+
+    def collect():
+        torch.cuda.synchronize()
+        acc["bin"].append(E[0].elapsed_time(E[1]))
+        acc["interp"].append(E[1].elapsed_time(E[2]))
+        acc["spread"].append(E[3].elapsed_time(E[4]))
+        acc["exchange"].append(E[2].elapsed_time(E[3]) + E[4].elapsed_time(E[5]))
+
+    for _ in range(args.warmup):
+        step(False)
+    ctx.synchronize()
+
+    # timed region: barrier + sync on both sides, exactly K steps
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ctx.synchronize()
+
+    # per-kernel breakdown on the context stream (separate instrumented steps)
+    for _ in range(max(3, min(args.steps, 10))):
+        step(True)
+        collect()
+
+    ms_per_step = 1e3 * elapsed / args.steps
+    value = 2.0 * M_total * args.steps / elapsed
+
+    def mean(v):
+        return sum(v) / len(v)
+
+    t_i, t_s = mean(acc["interp"]), mean(acc["spread"])
+    B_i = M_local * 48 + 8 * sum(S_touched)
+    B_s = M_local * 48 + 16 * sum(S_touched)
+    dominant = "spread" if t_s >= t_i else "interp"
+    achieved = (B_s / (t_s * 1e-3) if dominant == "spread" else B_i / (t_i * 1e-3)) / 1e9
+    pair = (B_i + B_s) / ((t_i + t_s) * 1e-3) / 1e9
+    traffic = None
+    pmc = ROOT / "profiles" / f"pmc_{args.config}_{kernel}_{world}gpu.json"
+    if pmc.exists():
+        try:
+            traffic = json.loads(pmc.read_text()).get("per_launch_bytes", {}).get(dominant)
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(cfg, kernel, args.cpu_seconds)
+        except Exception as e:  # the baseline must never hide the GPU result
+            cpu = {"value": None, "error": repr(e)}
+
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "marker-ops/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": cfg["desc"], "kernel": kernel, "grid": [N, N, N], "markers": M_total,
+                   "parallelism": f"z-slab x{world}", "ghost": ghost,
+                   "step": "bin + ghost fill + interp(3 comps) + zero ghosts + spread(3 comps) + ghost sum"},
+        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "algorithmic_bytes": {"interp": B_i, "spread": B_s},
+                     "pair_achieved": pair, "pair_frac": pair / HBM_PEAK_GBS},
+        "cpu_baseline": cpu,
+        "breakdown_ms": {k: mean(v) for k, v in acc.items()},
+        "touched_points": S_touched,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/ibtk_le.h"
 #include "le_internal.h"
@@ -632,5 +633,28 @@ extern "C" int ibtk_le_periodic_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_
     if (total > capacity || !indices_dev || !Xshift_dev)
         return fail(IBTK_LE_ERR_ARG, "index list needs %d entries, capacity %d", total, capacity);
     HIP_TRY(launch_image_write(d, X_dev, n_markers, ctx->offsets.as<int>(), indices_dev, Xshift_dev, capacity, s));
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_mark_stencils(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                                     const ibtk_le_patch_geom* geom, unsigned char* const* masks_dev, int q_depth,
+                                     const double* X_dev) {
+    Params p;
+    if (int rc = prepare(ctx, m, kernel, geom, X_dev, p)) return rc;
+    const int nc = ncomponents(geom, centering, q_depth, centering == IBTK_LE_SIDE || centering == IBTK_LE_EDGE
+                                                            ? geom->ndim
+                                                            : q_depth);
+    if (nc < 0) return -nc;
+    if (nc > MAXC) return fail(IBTK_LE_ERR_ARG, "mark_stencils: at most %d components", MAXC);
+    if (m->n == 0) return IBTK_LE_OK;
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    std::vector<double*> dummy(nc, reinterpret_cast<double*>(16));
+    if (int rc = make_comps(geom, centering, axis, dummy.data(), q_depth, q_depth, 0, nc, p)) return rc;
+    unsigned char* mk[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (int c = 0; c < nc; ++c) {
+        if (!masks_dev[c]) return fail(IBTK_LE_ERR_ARG, "null mask");
+        mk[c] = masks_dev[c];
+    }
+    HIP_TRY(launch_mark(geom->ndim, kernel, p, m->n, mk, ctx->stream));
     return IBTK_LE_OK;
 }

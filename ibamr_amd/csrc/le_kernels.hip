@@ -227,11 +227,11 @@ __global__ __launch_bounds__(BLOCK) void k_interp(Params p) {
 // Entries binned "outside" (no stencil point can reach any array): V = 0.
 __global__ __launch_bounds__(BLOCK) void k_interp_outside(Params p, int n) {
     const int first = p.brick_start[p.bg.nbricks];
-    const int e = first + blockIdx.x * BLOCK + threadIdx.x;
-    if (e >= n) return;
-    const int l = p.sorted_l[e];
-    const int s = p.indices ? p.indices[l] : l;
-    for (int c = 0; c < p.ncomp; ++c) p.Qout[(int64_t)p.Q_depth * s + p.comp[c].qcomp] = 0.0;
+    for (int e = first + blockIdx.x * BLOCK + threadIdx.x; e < n; e += gridDim.x * BLOCK) {
+        const int l = p.sorted_l[e];
+        const int s = p.indices ? p.indices[l] : l;
+        for (int c = 0; c < p.ncomp; ++c) p.Qout[(int64_t)p.Q_depth * s + p.comp[c].qcomp] = 0.0;
+    }
 }
 
 static int grid_for(int nbricks) {
@@ -257,7 +257,7 @@ hipError_t launch_interp_t(const Params& p, int n, hipStream_t s, hipEvent_t ev0
     if (ev1) hipEventRecord(ev1, s);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (n > 0) hipLaunchKernelGGL(k_interp_outside, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n);
+    if (n > 0) hipLaunchKernelGGL(k_interp_outside, dim3(64), dim3(BLOCK), 0, s, p, n);
     return hipGetLastError();
 }
 
@@ -504,6 +504,47 @@ hipError_t launch_spread_t(const Params& p, hipStream_t s, hipEvent_t ev0, hipEv
 }
 
 // ---------------------------------------------------------------------------
+// diagnostics: mark every array point some listed stencil touches (after
+// clipping), for the exact algorithmic-byte count |S_a| of the roofline.
+// ---------------------------------------------------------------------------
+template <int NDIM, int K>
+__global__ __launch_bounds__(BLOCK) void k_mark(Params p, int n, unsigned char* m0, unsigned char* m1,
+                                                unsigned char* m2, unsigned char* m3) {
+    constexpr int W = KT<K>::W;
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= n) return;
+    const int s = p.indices ? p.indices[e] : e;
+    unsigned char* masks[4] = {m0, m1, m2, m3};
+    for (int c = 0; c < p.ncomp; ++c) {
+        const CompDesc& cd = p.comp[c];
+        St<W> st[NDIM];
+        for (int d = 0; d < NDIM; ++d) {
+            const double Xraw = p.X[(int64_t)NDIM * s + d];
+            const double Xs = Xraw + (p.Xshift ? p.Xshift[(int64_t)NDIM * e + d] : 0.0);
+            stencil1d<K>(Xs, Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis, p.K6,
+                         st[d]);
+        }
+        for (int i2 = (NDIM == 3 ? st[NDIM - 1].ist : 0); i2 <= (NDIM == 3 ? st[NDIM - 1].isp : 0); ++i2)
+            for (int i1 = st[1].ist; i1 <= st[1].isp; ++i1)
+                for (int i0 = st[0].ist; i0 <= st[0].isp; ++i0) {
+                    const int g0 = st[0].icl + i0, g1 = st[1].icl + i1;
+                    const int g2 = NDIM == 3 ? st[NDIM - 1].icl + i2 : 0;
+                    const int64_t o = (int64_t)(g0 - cd.lo[0]) + (int64_t)(g1 - cd.lo[1]) * cd.s1 +
+                                      (NDIM == 3 ? (int64_t)(g2 - cd.lo[2]) * cd.s2 : 0);
+                    masks[c][o] = 1;  // idempotent, benign race
+                }
+    }
+}
+
+template <int NDIM, int K>
+hipError_t launch_mark_t(const Params& p, int n, unsigned char** masks, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL((k_mark<NDIM, K>), dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, masks[0], masks[1],
+                       masks[2], masks[3]);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------
 #define IBTK_LE_DISPATCH(NDIMV, KV, CALL)                                     \
@@ -527,6 +568,8 @@ using SpreadFn = hipError_t (*)(const Params&, hipStream_t, hipEvent_t, hipEvent
 template <int NDIM> static BinFn pick_bin(int k) { IBTK_LE_DISPATCH(NDIM, k, launch_bin_t) }
 template <int NDIM> static InterpFn pick_interp(int k) { IBTK_LE_DISPATCH(NDIM, k, launch_interp_t) }
 template <int NDIM> static SpreadFn pick_spread(int k) { IBTK_LE_DISPATCH(NDIM, k, launch_spread_t) }
+using MarkFn = hipError_t (*)(const Params&, int, unsigned char**, hipStream_t);
+template <int NDIM> static MarkFn pick_mark(int k) { IBTK_LE_DISPATCH(NDIM, k, launch_mark_t) }
 
 hipError_t launch_bin(int ndim, int kernel, const Params& p, int n, unsigned* keys, int* vals, hipStream_t s) {
     BinFn f = ndim == 3 ? pick_bin<3>(kernel) : pick_bin<2>(kernel);
@@ -545,6 +588,11 @@ hipError_t launch_interp(int ndim, int kernel, const Params& p, int n, hipStream
 hipError_t launch_spread(int ndim, int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     SpreadFn f = ndim == 3 ? pick_spread<3>(kernel) : pick_spread<2>(kernel);
     return f ? f(p, s, ev0, ev1) : hipErrorInvalidValue;
+}
+
+hipError_t launch_mark(int ndim, int kernel, const Params& p, int n, unsigned char** masks, hipStream_t s) {
+    MarkFn f = ndim == 3 ? pick_mark<3>(kernel) : pick_mark<2>(kernel);
+    return f ? f(p, n, masks, s) : hipErrorInvalidValue;
 }
 
 // ---------------------------------------------------------------------------

@@ -254,3 +254,14 @@ def periodic_index_list(ctx: Context, geom: Geometry, X: torch.Tensor, ghost: in
                                               pa[0] if pa else None, _ptr(idx), _ptr(xs), cap, ctypes.byref(cnt)))
     n = cnt.value
     return idx[:n].contiguous(), xs[:n].contiguous()
+
+
+def mark_stencils(ctx: Context, markers: Markers, kernel: str, centering: str, geom: Geometry, X: torch.Tensor,
+                  q_depth: int = 1, axis: int = 0):
+    """uint8 masks (one per component, shaped like the arrays) of the points some stencil touches."""
+    masks = [torch.zeros(geom.array_shape(centering, c, q_depth), dtype=torch.uint8, device=X.device)
+             for c in range(geom.ncomp(centering))]
+    arr = (ctypes.c_void_p * len(masks))(*[m.data_ptr() for m in masks])
+    check(ctx.lib.ibtk_le_mark_stencils(ctx.h, markers.h, kernel_id(kernel), CENTERING[centering], axis,
+                                        ctypes.byref(geom.c), arr, q_depth, _ptr(X)))
+    return masks

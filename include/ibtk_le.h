@@ -160,6 +160,13 @@ int ibtk_le_periodic_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom,
                                 int n_markers, int ghost, const int* periodic, int* indices_dev,
                                 double* Xshift_dev, int capacity, int* count);
 
+/* Diagnostics: masks_dev[c] (one byte per point of component c's ghosted array,
+ * same layout) gets 1 at every point some listed stencil touches after clipping.
+ * bench.py sums the masks for the exact algorithmic byte count |S_a|. */
+int ibtk_le_mark_stencils(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                          const ibtk_le_patch_geom* geom, unsigned char* const* masks_dev, int q_depth,
+                          const double* X_dev);
+
 /* Diagnostics: number of device kernel launches issued by the last interp/spread/bin
  * call on this context, and the per-step timing of the last call's main kernel (ms,
  * measured with HIP events on the context stream when enabled). */

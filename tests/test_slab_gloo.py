@@ -1,0 +1,160 @@
+"""Multi-rank slab decomposition on CPU (gloo, world size 2 and 4).
+
+Checks the z-halo fill and the ghost-region sum of ibamr_amd.slab against the
+global periodic answer.  The local x/y periodic pieces, which run as HIP kernels
+in the product, are replaced here by a numpy restatement of the same kernel
+semantics (ibamr_amd/csrc/le_kernels.hip, k_ghost): fill wraps all dims of a
+ghost point at once; fold walks dims slowest first, region d = (dims < d any,
+dim d ghost, dims > d interior), one source per destination per pass.
+Values are small integers so every sum is exact and the comparison is bitwise.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _interior(slab, comp):
+    """unique (interior) index ranges per dim in array coordinates, for dims x, y, z."""
+    g = slab.ghost
+    return [(g, g + slab.N[0]), (g, g + slab.N[1]), (g, g + slab.nz)]
+
+
+def _np_local(arrays, periodic, slab, mode):
+    for c, t in enumerate(arrays):
+        a = t.numpy()  # shares memory
+        rng = _interior(slab, c)
+        shape = a.shape[::-1]  # (nx, ny, nz)
+        nd = 3
+        if mode == "fill":
+            idx = np.indices(shape).reshape(3, -1).T  # (x, y, z)
+            for pt in idx:
+                inside = all(rng[d][0] <= pt[d] < rng[d][1] for d in range(nd))
+                if inside:
+                    continue
+                src = list(pt)
+                ok = True
+                for d in range(nd):
+                    if not (rng[d][0] <= pt[d] < rng[d][1]):
+                        if not periodic[d]:
+                            ok = False
+                            break
+                        n = rng[d][1] - rng[d][0]
+                        src[d] = rng[d][0] + (pt[d] - rng[d][0]) % n
+                if ok:
+                    a[pt[2], pt[1], pt[0]] = a[src[2], src[1], src[0]]
+        else:
+            for dreg in (2, 1, 0):
+                if not periodic[dreg]:
+                    continue
+                sl = [slice(None)] * 3  # in (x, y, z) order
+                for d in range(nd):
+                    if d > dreg:
+                        sl[d] = slice(*rng[d])
+                n = rng[dreg][1] - rng[dreg][0]
+                for j in list(range(0, rng[dreg][0])) + list(range(rng[dreg][1], shape[dreg])):
+                    dst = rng[dreg][0] + (j - rng[dreg][0]) % n
+                    s_src, s_dst = list(sl), list(sl)
+                    s_src[dreg], s_dst[dreg] = j, dst
+                    a[tuple(s_dst[::-1])] += a[tuple(s_src[::-1])]
+
+
+def _worker(rank, world, port, N, ghost, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ibamr_amd.slab import Slab, SlabExchange
+        slab = Slab([N, N, N], world, rank, ghost)
+        geom_shapes = []
+        for c in range(3):
+            n = [N + 2 * ghost + (1 if d == c else 0) for d in range(2)] + [slab.nz + 2 * ghost + (1 if c == 2 else 0)]
+            geom_shapes.append(tuple(reversed(n)))
+        rng = np.random.default_rng(100 + rank)
+        # ---- halo fill: interior = global field, ghosts garbage
+        Gs = [np.random.default_rng(7 + c).integers(-50, 50, (N, N, N)).astype(np.float64) for c in range(3)]
+        arrays = []
+        for c in range(3):
+            a = rng.integers(-1000, 1000, geom_shapes[c]).astype(np.float64)
+            zz = np.arange(a.shape[0]) - ghost + slab.z0
+            yy = np.arange(a.shape[1]) - ghost
+            xx = np.arange(a.shape[2]) - ghost
+            full = Gs[c][np.ix_(zz % N, yy % N, xx % N)]
+            inner = (slice(ghost, ghost + slab.nz), slice(ghost, ghost + N), slice(ghost, ghost + N))
+            a[inner] = full[inner]
+            arrays.append(torch.from_numpy(a))
+        ex = SlabExchange(slab, arrays, local_fill=lambda arr, per: _np_local(arr, per, slab, "fill"),
+                          local_fold=lambda arr, per: _np_local(arr, per, slab, "fold"))
+        ex.halo_fill()
+        for c in range(3):
+            a = arrays[c].numpy()
+            zz = np.arange(a.shape[0]) - ghost + slab.z0
+            yy = np.arange(a.shape[1]) - ghost
+            xx = np.arange(a.shape[2]) - ghost
+            expect = Gs[c][np.ix_(zz % N, yy % N, xx % N)]
+            assert np.array_equal(a, expect), f"halo_fill rank {rank} comp {c}"
+        # ---- ghost sum: every point (interior and ghost) carries a value; the
+        # result's interior must equal the sum of all values wrapping onto it
+        arrays = [torch.from_numpy(rng.integers(-20, 20, geom_shapes[c]).astype(np.float64)) for c in range(3)]
+        before = [a.numpy().copy() for a in arrays]
+        ex = SlabExchange(slab, arrays, local_fill=lambda arr, per: _np_local(arr, per, slab, "fill"),
+                          local_fold=lambda arr, per: _np_local(arr, per, slab, "fold"))
+        ex.ghost_sum()
+        # gather every rank's 'before' arrays to compute the global wrap-sum
+        objs = [None] * world
+        dist.all_gather_object(objs, (slab.z0, before))
+        for c in range(3):
+            tot = np.zeros((N, N, N))
+            for z0, bl in objs:
+                b = bl[c]
+                zz = (np.arange(b.shape[0]) - ghost + z0) % N
+                yy = (np.arange(b.shape[1]) - ghost) % N
+                xx = (np.arange(b.shape[2]) - ghost) % N
+                np.add.at(tot, np.ix_(zz, yy, xx), b)
+            a = arrays[c].numpy()
+            inner = a[ghost:ghost + slab.nz, ghost:ghost + N, ghost:ghost + N]
+            assert np.array_equal(inner, tot[slab.z0:slab.z1]), f"ghost_sum rank {rank} comp {c}"
+        out_q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        out_q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_slab_exchange_gloo(world):
+    N, ghost = 16, 3
+    if world > 1 and N // world < 2 * ghost + 2:
+        N = world * (2 * ghost + 2)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, ghost, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    for _ in range(world):
+        try:
+            results.append(q.get(timeout=120))
+        except Exception:
+            results.append((-1, "worker died: " + str([p.exitcode for p in procs])))
+            break
+    for p in procs:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    bad = [r for r in results if r[1] != "ok"]
+    assert not bad, bad[0][1]
