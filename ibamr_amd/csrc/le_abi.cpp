@@ -108,7 +108,7 @@ struct ibtk_le_markers_s {
     int ndim = 0;
     BinGeom bg{};
     ibtk_le_patch_geom geom{};
-    DevBuf sorted_key, sorted_l, brick_start, indices, xshift;
+    DevBuf sorted_key, sorted_l, sorted_s, sorted_X, brick_start, indices, xshift;
     bool has_indices = false, has_xshift = false;
 };
 
@@ -211,6 +211,7 @@ static int make_bin_geom(const ibtk_le_patch_geom* g, int kernel, BinGeom& bg) {
     for (int d = 0; d < 3; ++d) {
         if (d >= g->ndim) {
             bg.nb[d] = 1;
+            bg.nt[d] = 1;
             continue;
         }
         const int lo = g->ilower[d] - g->gcw[d];
@@ -218,7 +219,9 @@ static int make_bin_geom(const ibtk_le_patch_geom* g, int kernel, BinGeom& bg) {
         bg.kmin[d] = lo - ki.HI;
         const int kmax = hi - ki.LO;
         const int E = kmax - bg.kmin[d] + 1;
-        bg.nb[d] = (E + B - 1) / B;
+        const int nbd = (E + B - 1) / B;
+        bg.nt[d] = (nbd + TILE - 1) / TILE;  // bricks padded to whole tiles
+        bg.nb[d] = bg.nt[d] * TILE;
         nb *= bg.nb[d];
         bg.xlo[d] = g->x_lower[d];
         bg.dx[d] = g->dx[d];
@@ -341,7 +344,8 @@ extern "C" int ibtk_le_markers_destroy(ibtk_le_markers m) {
     if (!m) return IBTK_LE_OK;
     hipSetDevice(m->ctx->device);
     hipStreamSynchronize(m->ctx->stream);
-    for (DevBuf* b : {&m->sorted_key, &m->sorted_l, &m->brick_start, &m->indices, &m->xshift}) b->release();
+    for (DevBuf* b : {&m->sorted_key, &m->sorted_l, &m->sorted_s, &m->sorted_X, &m->brick_start, &m->indices, &m->xshift})
+        b->release();
     delete m;
     return IBTK_LE_OK;
 }
@@ -382,6 +386,8 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     }
     if ((rc = m->sorted_key.ensure(sizeof(unsigned) * (size_t)n))) return rc;
     if ((rc = m->sorted_l.ensure(sizeof(int) * (size_t)n))) return rc;
+    if ((rc = m->sorted_s.ensure(sizeof(int) * (size_t)n))) return rc;
+    if ((rc = m->sorted_X.ensure(sizeof(double) * (size_t)n * geom->ndim))) return rc;
     if ((rc = ctx->keys_in.ensure(sizeof(unsigned) * (size_t)n))) return rc;
     if ((rc = ctx->vals_in.ensure(sizeof(int) * (size_t)n))) return rc;
     if (m->has_indices) {
@@ -409,6 +415,8 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     HIP_TRY(launch_sort(ctx->temp.p, tb, ctx->keys_in.as<unsigned>(), m->sorted_key.as<unsigned>(),
                         ctx->vals_in.as<int>(), m->sorted_l.as<int>(), n, end_bit, s));
     HIP_TRY(launch_brick_start(m->sorted_key.as<unsigned>(), n, bg.nbricks, bg.shift, m->brick_start.as<int>(), s));
+    p.sorted_l = m->sorted_l.as<int>();
+    HIP_TRY(launch_gather_sorted(geom->ndim, p, n, m->sorted_s.as<int>(), m->sorted_X.as<double>(), s));
     return IBTK_LE_OK;
 }
 
@@ -440,6 +448,8 @@ static int prepare(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const ibtk_le
     p.indices = m->has_indices ? m->indices.as<int>() : nullptr;
     p.Xshift = m->has_xshift ? m->xshift.as<double>() : nullptr;
     p.sorted_l = m->sorted_l.as<int>();
+    p.sorted_s = m->sorted_s.as<int>();
+    p.sorted_X = m->sorted_X.as<double>();
     p.sorted_key = m->sorted_key.as<unsigned>();
     p.brick_start = m->brick_start.as<int>();
     p.err = ctx->err.as<int>();
@@ -593,9 +603,28 @@ extern "C" int ibtk_le_zero_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* ge
     return ghost_op(ctx, geom, centering, q_dev, q_depth, nullptr, 2);
 }
 
+static int index_list_impl(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev, int n_markers,
+                           int ghost, const int* periodic, const int* box_lo, const int* box_hi, int* indices_dev,
+                           double* Xshift_dev, int capacity, int* count);
+
 extern "C" int ibtk_le_periodic_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
                                            int n_markers, int ghost, const int* periodic, int* indices_dev,
                                            double* Xshift_dev, int capacity, int* count) {
+    return index_list_impl(ctx, geom, X_dev, n_markers, ghost, periodic, nullptr, nullptr, indices_dev, Xshift_dev,
+                           capacity, count);
+}
+
+extern "C" int ibtk_le_box_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
+                                      int n_markers, const int* box_lo, const int* box_hi, int* indices_dev,
+                                      int capacity, int* count) {
+    if (!box_lo || !box_hi) return fail(IBTK_LE_ERR_ARG, "null box");
+    return index_list_impl(ctx, geom, X_dev, n_markers, 0, nullptr, box_lo, box_hi, indices_dev, nullptr, capacity,
+                           count);
+}
+
+static int index_list_impl(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev, int n_markers,
+                           int ghost, const int* periodic, const int* box_lo, const int* box_hi, int* indices_dev,
+                           double* Xshift_dev, int capacity, int* count) {
     if (!ctx || !count) return fail(IBTK_LE_ERR_ARG, "null argument");
     if (int rc = check_geom(geom)) return rc;
     if (n_markers < 0 || ghost < 0) return fail(IBTK_LE_ERR_ARG, "negative size");
@@ -613,6 +642,11 @@ extern "C" int ibtk_le_periodic_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_
         d.ilo[k] = geom->ilower[k];
         d.ihi[k] = geom->iupper[k];
         d.periodic[k] = periodic ? periodic[k] : 1;
+        if (box_lo) {
+            d.filter = 1;
+            d.flo[k] = box_lo[k];
+            d.fhi[k] = box_hi[k];
+        }
     }
     int rc;
     if ((rc = ctx->counts.ensure(sizeof(int) * (size_t)n_markers))) return rc;
@@ -630,7 +664,7 @@ extern "C" int ibtk_le_periodic_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_
     HIP_TRY(hipStreamSynchronize(s));
     const int total = last[0] + last[1];
     *count = total;
-    if (total > capacity || !indices_dev || !Xshift_dev)
+    if (total > capacity || !indices_dev || (!Xshift_dev && !box_lo))
         return fail(IBTK_LE_ERR_ARG, "index list needs %d entries, capacity %d", total, capacity);
     HIP_TRY(launch_image_write(d, X_dev, n_markers, ctx->offsets.as<int>(), indices_dev, Xshift_dev, capacity, s));
     return IBTK_LE_OK;

@@ -1,0 +1,270 @@
+// le_aux.hip -- auxiliary device kernels of the LE coupling path: stencil
+// marking (roofline byte counts), periodic ghost fill / ghost-region fold, and
+// the periodic / box index lists (LIndexSetData::cacheLocalIndices,
+// LEInteractor::buildLocalIndices for one patch).  The hot path is le_hot.hip.
+#include <hip/hip_runtime.h>
+
+#include "le_internal.h"
+#include "le_stencil.h"
+
+namespace ibtk_le {
+
+#define IBTK_LE_DISPATCH(NDIMV, KV, CALL)                                     \
+    switch (KV) {                                                             \
+    case K_PIECEWISE_CONSTANT: return CALL<NDIMV, K_PIECEWISE_CONSTANT>;      \
+    case K_DISCONTINUOUS_LINEAR: return CALL<NDIMV, K_DISCONTINUOUS_LINEAR>;  \
+    case K_PIECEWISE_LINEAR: return CALL<NDIMV, K_PIECEWISE_LINEAR>;          \
+    case K_PIECEWISE_CUBIC: return CALL<NDIMV, K_PIECEWISE_CUBIC>;            \
+    case K_IB_3: return CALL<NDIMV, K_IB_3>;                                  \
+    case K_IB_4: return CALL<NDIMV, K_IB_4>;                                  \
+    case K_IB_4_W8: return CALL<NDIMV, K_IB_4_W8>;                            \
+    case K_IB_6: return CALL<NDIMV, K_IB_6>;                                  \
+    case K_BSPLINE_4: return CALL<NDIMV, K_BSPLINE_4>;                        \
+    default: return nullptr;                                                  \
+    }
+
+// ---------------------------------------------------------------------------
+// diagnostics: mark every array point some listed stencil touches (after
+// clipping), for the exact algorithmic-byte count |S_a| of the roofline.
+// ---------------------------------------------------------------------------
+template <int NDIM, int K>
+__global__ __launch_bounds__(BLOCK) void k_mark(Params p, int n, unsigned char* m0, unsigned char* m1,
+                                                unsigned char* m2, unsigned char* m3) {
+    constexpr int W = KT<K>::W;
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= n) return;
+    const int s = p.indices ? p.indices[e] : e;
+    unsigned char* masks[4] = {m0, m1, m2, m3};
+    for (int c = 0; c < p.ncomp; ++c) {
+        const CompDesc& cd = p.comp[c];
+        St<W> st[NDIM];
+        for (int d = 0; d < NDIM; ++d) {
+            const double Xraw = p.X[(int64_t)NDIM * s + d];
+            const double Xs = Xraw + (p.Xshift ? p.Xshift[(int64_t)NDIM * e + d] : 0.0);
+            stencil1d<K>(Xs, Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis, p.K6,
+                         st[d]);
+        }
+        for (int i2 = (NDIM == 3 ? st[NDIM - 1].ist : 0); i2 <= (NDIM == 3 ? st[NDIM - 1].isp : 0); ++i2)
+            for (int i1 = st[1].ist; i1 <= st[1].isp; ++i1)
+                for (int i0 = st[0].ist; i0 <= st[0].isp; ++i0) {
+                    const int g0 = st[0].icl + i0, g1 = st[1].icl + i1;
+                    const int g2 = NDIM == 3 ? st[NDIM - 1].icl + i2 : 0;
+                    const int64_t o = (int64_t)(g0 - cd.lo[0]) + (int64_t)(g1 - cd.lo[1]) * cd.s1 +
+                                      (NDIM == 3 ? (int64_t)(g2 - cd.lo[2]) * cd.s2 : 0);
+                    masks[c][o] = 1;  // idempotent, benign race
+                }
+    }
+}
+
+template <int NDIM, int K>
+hipError_t launch_mark_t(const Params& p, int n, unsigned char** masks, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL((k_mark<NDIM, K>), dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, masks[0], masks[1],
+                       masks[2], masks[3]);
+    return hipGetLastError();
+}
+
+using MarkFn = hipError_t (*)(const Params&, int, unsigned char**, hipStream_t);
+template <int NDIM> static MarkFn pick_mark(int k) { IBTK_LE_DISPATCH(NDIM, k, launch_mark_t) }
+
+hipError_t launch_mark(int ndim, int kernel, const Params& p, int n, unsigned char** masks, hipStream_t s) {
+    MarkFn f = ndim == 3 ? pick_mark<3>(kernel) : pick_mark<2>(kernel);
+    return f ? f(p, n, masks, s) : hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------------------
+// periodic ghost fill / ghost-region fold / ghost zeroing
+// ---------------------------------------------------------------------------
+// The ghost region of dim d (d = 0..NDIM-1): dims > d interior, dim d outside
+// the interior, dims < d anything in the ghost box.
+__device__ __forceinline__ bool ghost_point(const GhostDesc& g, int ndim, int dreg, int64_t t, int* pt) {
+    int64_t rem = t;
+    int ext[3];
+    for (int d = 0; d < ndim; ++d) {
+        if (d < dreg) ext[d] = g.hi[d] - g.lo[d] + 1;
+        else if (d == dreg) ext[d] = (g.ilo[d] - g.lo[d]) + (g.hi[d] - g.ihi[d]);
+        else ext[d] = g.ihi[d] - g.ilo[d] + 1;
+    }
+    for (int d = 0; d < ndim; ++d) {
+        const int q = (int)(rem % ext[d]);
+        rem /= ext[d];
+        if (d < dreg) pt[d] = g.lo[d] + q;
+        else if (d == dreg) {
+            const int nlo = g.ilo[d] - g.lo[d];
+            pt[d] = q < nlo ? g.lo[d] + q : g.ihi[d] + 1 + (q - nlo);
+        } else pt[d] = g.ilo[d] + q;
+    }
+    return rem == 0;
+}
+
+__device__ __forceinline__ int64_t goff(const GhostDesc& g, int ndim, const int* pt) {
+    int64_t o = pt[0] - g.lo[0];
+    if (ndim > 1) o += (int64_t)(pt[1] - g.lo[1]) * g.s1;
+    if (ndim > 2) o += (int64_t)(pt[2] - g.lo[2]) * g.s2;
+    return o;
+}
+
+__device__ __forceinline__ int wrap(int i, int lo, int n) {
+    int r = (i - lo) % n;
+    if (r < 0) r += n;
+    return lo + r;
+}
+
+// mode 0: fill (ghost <- periodic interior, all dims wrapped at once)
+// mode 1: fold dim dreg (interior-in-dreg point += ghost point), one source per destination
+// mode 2: zero
+__global__ __launch_bounds__(BLOCK) void k_ghost(GhostDesc g, int ndim, int dreg, int mode, int64_t count, int p0,
+                                                  int p1, int p2) {
+    const int64_t t = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= count) return;
+    int pt[3] = {0, 0, 0};
+    if (!ghost_point(g, ndim, dreg, t, pt)) return;
+    const int per[3] = {p0, p1, p2};
+    if (mode == 2) {
+        g.u[goff(g, ndim, pt)] = 0.0;
+        return;
+    }
+    if (mode == 0) {
+        int src[3] = {pt[0], pt[1], pt[2]};
+        for (int d = 0; d < ndim; ++d) {
+            if (src[d] < g.ilo[d] || src[d] > g.ihi[d]) {
+                if (!per[d]) return;
+                src[d] = wrap(src[d], g.ilo[d], g.ihi[d] - g.ilo[d] + 1);
+            }
+        }
+        g.u[goff(g, ndim, pt)] = g.u[goff(g, ndim, src)];
+        return;
+    }
+    // fold along dreg only
+    if (!per[dreg]) return;
+    int dst[3] = {pt[0], pt[1], pt[2]};
+    dst[dreg] = wrap(pt[dreg], g.ilo[dreg], g.ihi[dreg] - g.ilo[dreg] + 1);
+    const int64_t os = goff(g, ndim, pt), od = goff(g, ndim, dst);
+    g.u[od] = g.u[od] + g.u[os];
+}
+
+static int64_t ghost_count(const GhostDesc& g, int ndim, int dreg) {
+    int64_t c = 1;
+    for (int d = 0; d < ndim; ++d) {
+        if (d < dreg) c *= g.hi[d] - g.lo[d] + 1;
+        else if (d == dreg) c *= (g.ilo[d] - g.lo[d]) + (g.hi[d] - g.ihi[d]);
+        else c *= g.ihi[d] - g.ilo[d] + 1;
+    }
+    return c;
+}
+
+static hipError_t ghost_pass(const GhostDesc& g, int ndim, int dreg, int mode, const int* per, hipStream_t s) {
+    const int64_t cnt = ghost_count(g, ndim, dreg);
+    if (cnt <= 0) return hipSuccess;
+    const int64_t nb = (cnt + BLOCK - 1) / BLOCK;
+    hipLaunchKernelGGL(k_ghost, dim3((unsigned)nb), dim3(BLOCK), 0, s, g, ndim, dreg, mode, cnt, per[0], per[1],
+                       ndim > 2 ? per[2] : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_periodic(int ndim, const GhostDesc& g, const int* periodic, hipStream_t s) {
+    for (int d = 0; d < ndim; ++d) {
+        hipError_t e = ghost_pass(g, ndim, d, 0, periodic, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+hipError_t launch_fold_periodic(int ndim, const GhostDesc& g, const int* periodic, hipStream_t s) {
+    // slowest dim first: a point that is ghost in several dims is carried into
+    // the interior one dim at a time, each step with one source per destination
+    for (int d = ndim - 1; d >= 0; --d) {
+        hipError_t e = ghost_pass(g, ndim, d, 1, periodic, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+hipError_t launch_zero_ghosts(int ndim, const GhostDesc& g, hipStream_t s) {
+    const int per[3] = {1, 1, 1};
+    for (int d = 0; d < ndim; ++d) {
+        hipError_t e = ghost_pass(g, ndim, d, 2, per, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------
+// periodic index lists (LIndexSetData::cacheLocalIndices for one periodic patch)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void cell_index(const ImageDesc& d, const double* X, int* c) {
+    // IndexUtilities::getCellIndex, IndexUtilities-inl.h:66-89
+    for (int k = 0; k < d.ndim; ++k) {
+        const double dl = X[k] - d.xlo[k], du = X[k] - d.xup[k];
+        if (fabs(dl) <= fabs(du)) c[k] = d.ilo[k] + (int)floor(dl / d.dx[k]);
+        else c[k] = d.ihi[k] + (int)floor(du / d.dx[k]) + 1;
+    }
+}
+
+__device__ __forceinline__ int image_walk(const ImageDesc& d, const double* X, int* idx_out, double* xs_out,
+                                          int base, int capacity, int s) {
+    int c[3] = {0, 0, 0};
+    cell_index(d, X, c);
+    if (d.filter) {  // LEInteractor.cpp:3129-3137: keep markers whose cell is in the box
+        for (int k = 0; k < d.ndim; ++k)
+            if (c[k] < d.flo[k] || c[k] > d.fhi[k]) return 0;
+        if (idx_out && base < capacity) {
+            idx_out[base] = s;
+            if (xs_out)
+                for (int k = 0; k < d.ndim; ++k) xs_out[(int64_t)d.ndim * base + k] = 0.0;
+        }
+        return 1;
+    }
+    for (int k = 0; k < d.ndim; ++k)
+        if (c[k] < d.ilo[k] || c[k] > d.ihi[k]) return 0;  // not owned by this patch
+    int cnt = 0;
+    const int nimg = d.ndim == 3 ? 27 : 9;
+    for (int j = 0; j < nimg; ++j) {
+        // j = 13 (3-D) / 4 (2-D) is the unshifted entry; emit it first
+        const int jj = j == 0 ? (nimg / 2) : (j <= nimg / 2 ? j - 1 : j);
+        int sh[3] = {jj % 3 - 1, (jj / 3) % 3 - 1, d.ndim == 3 ? jj / 9 - 1 : 0};
+        bool ok = true;
+        for (int k = 0; k < d.ndim; ++k) {
+            if (sh[k] != 0 && !d.periodic[k]) ok = false;
+            const int n = d.ihi[k] - d.ilo[k] + 1;
+            const int ci = c[k] + sh[k] * n;
+            ok = ok && ci >= d.ilo[k] - d.ghost && ci <= d.ihi[k] + d.ghost;
+        }
+        if (!ok) continue;
+        if (idx_out && base + cnt < capacity) {
+            idx_out[base + cnt] = s;
+            for (int k = 0; k < d.ndim; ++k) {
+                const int n = d.ihi[k] - d.ilo[k] + 1;
+                // LIndexSetData.cpp:141: static_cast<double>(offset[d]) * dx[d]
+                xs_out[(int64_t)d.ndim * (base + cnt) + k] = (double)(sh[k] * n) * d.dx[k];
+            }
+        }
+        ++cnt;
+    }
+    return cnt;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_image_count(ImageDesc d, const double* X, int n, int* counts) {
+    const int s = blockIdx.x * BLOCK + threadIdx.x;
+    if (s >= n) return;
+    counts[s] = image_walk(d, X + (int64_t)d.ndim * s, nullptr, nullptr, 0, 0, s);
+}
+__global__ __launch_bounds__(BLOCK) void k_image_write(ImageDesc d, const double* X, int n, const int* offsets,
+                                                        int* idx, double* xs, int capacity) {
+    const int s = blockIdx.x * BLOCK + threadIdx.x;
+    if (s >= n) return;
+    image_walk(d, X + (int64_t)d.ndim * s, idx, xs, offsets[s], capacity, s);
+}
+
+hipError_t launch_image_count(const ImageDesc& d, const double* X, int n, int* counts, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_image_count, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, d, X, n, counts);
+    return hipGetLastError();
+}
+hipError_t launch_image_write(const ImageDesc& d, const double* X, int n, const int* offsets, int* idx,
+                              double* xshift, int capacity, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_image_write, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, d, X, n, offsets, idx,
+                       xshift, capacity);
+    return hipGetLastError();
+}
+
+}  // namespace ibtk_le

@@ -1,0 +1,650 @@
+// le_hot.hip -- the hot path on CDNA4 (gfx950): marker binning, interpolation
+// and spreading.  Replaces the l-loops of
+// ibtk/src/lagrangian/fortran/lagrangian_interaction{2,3}d.f.m4.
+//
+// Work decomposition:
+//  * bin: key = brick id (tiled, le_bricks.h) << 9 | cell-in-brick of the
+//    marker's cell-frame stencil anchor; stable device radix sort; brick CSR;
+//    then one coalescing pass writes the sorted marker index and the sorted
+//    shifted position X(s)+Xshift(l), so the interp/spread kernels read their
+//    markers contiguously.
+//  * interp: one workgroup item = (brick, component).  The union stencil region
+//    of the brick's markers, (8+HI-LO)^3 points of that component, is loaded
+//    from HBM with every load of a thread in flight at once and staged in LDS
+//    (13.8 KB for IB_4, so ~11 items are resident per CU); one thread per marker
+//    then sums its W^3 stencil from LDS in the Fortran loop order, so the result
+//    is bitwise the oracle's.
+//  * spread: one workgroup item = (super-brick of 16^3 cells, component).  The
+//    workgroup loads u_old of its 4096 points into LDS, walks the sorted entries
+//    of the 4x4x4 surrounding bricks in canonical (sorted) order, keeps those
+//    whose stencil can reach the super-brick (parallel filter + ordered block
+//    compaction), computes their 1-D weights in parallel, and one wave then adds
+//    candidate after candidate with lane = stencil point (ds_add_f64 into LDS).
+//    Each grid point therefore receives its contributions in list order exactly
+//    like the Fortran's sequential l-loop: no global atomics, deterministic,
+//    bitwise the oracle's on the same list.  16^3 super-bricks keep the halo
+//    over-processing at (20/16)^3 = 1.95x the owned markers for IB_4.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+
+#include "le_bricks.h"
+#include "le_internal.h"
+#include "le_stencil.h"
+
+namespace ibtk_le {
+
+constexpr int IBLOCK = 128;  // interp workgroup (2 waves)
+constexpr int SBLOCK = 256;  // spread workgroup (4 waves)
+
+static int num_cus() {
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+    }
+    return ncu;
+}
+
+static int grid_for(long items, int per_cu) {
+    long g = (long)num_cus() * per_cu;
+    if (g > items) g = items;
+    if (g >= 8) g &= ~7L;
+    return (int)(g > 0 ? g : 1);
+}
+
+// ---------------------------------------------------------------------------
+// binning
+// ---------------------------------------------------------------------------
+template <int NDIM, int K>
+__global__ __launch_bounds__(BLOCK) void k_bin(Params p, int n, unsigned* keys, int* vals) {
+    constexpr int B = BrickT<NDIM>::B;
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const int s = p.indices ? p.indices[i] : i;
+    bool out = false;
+    int rel[3] = {0, 0, 0};
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) {
+        const double Xs = p.X[(int64_t)NDIM * s + d] + (p.Xshift ? p.Xshift[(int64_t)NDIM * i + d] : 0.0);
+        const double xo = (Xs - p.bg.xlo[d]) / p.bg.dx[d];
+        if (!(fabs(xo) < 1.0e9)) {  // also catches NaN
+            out = true;
+            continue;
+        }
+        rel[d] = key_anchor<K>(xo) + p.bg.ilower[d] - p.bg.kmin[d];
+        if (rel[d] < 0 || rel[d] >= p.bg.nb[d] * B) out = true;
+    }
+    unsigned key;
+    if (out) {
+        key = (unsigned)p.bg.nbricks << BrickT<NDIM>::SHIFT;
+    } else {
+        int bc[3] = {0, 0, 0};
+        unsigned local = 0;
+        for (int d = NDIM - 1; d >= 0; --d) {
+            bc[d] = rel[d] / B;
+            local = local * (unsigned)B + (unsigned)(rel[d] - bc[d] * B);
+        }
+        key = ((unsigned)brick_id<NDIM>(p.bg, bc) << BrickT<NDIM>::SHIFT) | local;
+    }
+    keys[i] = key;
+    vals[i] = i;
+}
+
+// brick_start[b] = first sorted position whose bucket >= b, for b in [0, nbricks].
+__global__ __launch_bounds__(BLOCK) void k_brick_start(const unsigned* keys, int n, int nbricks, int shift, int* bs) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i > n) return;
+    const int bi = (i < n) ? (int)min(keys[i] >> shift, (unsigned)nbricks) : nbricks + 1;
+    const int bp = (i == 0) ? -1 : (int)min(keys[i - 1] >> shift, (unsigned)nbricks);
+    for (int b = bp + 1; b <= bi && b <= nbricks; ++b) bs[b] = i;
+}
+
+// sorted marker index and sorted X(s) + Xshift(l) (the Fortran's X(d,s)+Xshift(d,l))
+template <int NDIM>
+__global__ __launch_bounds__(BLOCK) void k_gather_sorted(Params p, int n, int* sorted_s, double* sorted_X) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= n) return;
+    const int l = p.sorted_l[e];
+    const int s = p.indices ? p.indices[l] : l;
+    sorted_s[e] = s;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d)
+        sorted_X[(int64_t)NDIM * e + d] =
+            p.X[(int64_t)NDIM * s + d] + (p.Xshift ? p.Xshift[(int64_t)NDIM * l + d] : 0.0);
+}
+
+template <int NDIM, int K>
+hipError_t launch_bin_t(const Params& p, int n, unsigned* keys, int* vals, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL((k_bin<NDIM, K>), dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, keys, vals);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// interpolation
+// ---------------------------------------------------------------------------
+template <int NDIM, int K> struct IShape {
+    using T = KT<K>;
+    static constexpr int B = BrickT<NDIM>::B;
+    static constexpr int R = B + T::HI - T::LO;  // region edge (points)
+    static constexpr int RV = NDIM == 3 ? R * R * R : R * R;
+    static constexpr int NL = (RV + IBLOCK - 1) / IBLOCK;  // staged values per thread
+};
+
+template <int NDIM, int K>
+__device__ __forceinline__ void marker_stencils(const Params& p, const CompDesc& cd, int e, int s,
+                                                St<KT<K>::W>* st) {
+    constexpr int FAM = KT<K>::FAM;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) {
+        const double Xs = p.sorted_X[(int64_t)NDIM * e + d];
+        const double Xraw = (FAM == 2) ? p.X[(int64_t)NDIM * s + d] : Xs;
+        stencil1d<K>(Xs, Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis, p.K6, st[d]);
+    }
+}
+
+template <int NDIM, int K>
+__global__ __launch_bounds__(IBLOCK) void k_interp(Params p) {
+    using T = KT<K>;
+    using S = IShape<NDIM, K>;
+    constexpr int W = T::W, FAM = T::FAM, B = S::B, R = S::R, RV = S::RV, NL = S::NL;
+    extern __shared__ __attribute__((aligned(16))) double reg[];
+    const int nc = p.ncomp;
+    const int nitems = p.bg.nbricks * nc;
+    const int G = gridDim.x;
+    for (int round = 0; round < nitems; round += G) {
+        const int it = xcd_item(round, G, blockIdx.x);
+        if (it >= nitems) continue;
+        const int b = it / nc, c = it - (it / nc) * nc;
+        const int beg = p.brick_start[b], end = p.brick_start[b + 1];
+        if (beg == end) continue;
+        int bc[3];
+        brick_coords<NDIM>(p.bg, b, bc);
+        int r0[3] = {0, 0, 0};
+        bool inside = true;
+        const CompDesc& cd = p.comp[c];
+#pragma unroll
+        for (int d = 0; d < NDIM; ++d) {
+            r0[d] = p.bg.kmin[d] + bc[d] * B + T::LO;
+            inside = inside && r0[d] >= cd.lo[d] && r0[d] + R - 1 <= cd.hi[d];
+        }
+        // issue every staging load of this thread before using any of them
+        double v[NL];
+        const int64_t o0 = (int64_t)(r0[0] - cd.lo[0]) + (int64_t)(r0[1] - cd.lo[1]) * cd.s1 +
+                           (NDIM == 3 ? (int64_t)(r0[2] - cd.lo[2]) * cd.s2 : 0);
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+            const int q = threadIdx.x + k * IBLOCK;
+            v[k] = 0.0;
+            if (q < RV) {
+                const int i0 = q % R, i1 = (q / R) % R, i2 = NDIM == 3 ? q / (R * R) : 0;
+                if (inside) {
+                    v[k] = cd.u[o0 + i0 + (int64_t)i1 * cd.s1 + (NDIM == 3 ? (int64_t)i2 * cd.s2 : 0)];
+                } else {
+                    const int g0 = r0[0] + i0, g1 = r0[1] + i1, g2 = r0[2] + i2;
+                    bool in = g0 >= cd.lo[0] && g0 <= cd.hi[0] && g1 >= cd.lo[1] && g1 <= cd.hi[1];
+                    if (NDIM == 3) in = in && g2 >= cd.lo[2] && g2 <= cd.hi[2];
+                    if (in)
+                        v[k] = cd.u[(int64_t)(g0 - cd.lo[0]) + (int64_t)(g1 - cd.lo[1]) * cd.s1 +
+                                    (NDIM == 3 ? (int64_t)(g2 - cd.lo[2]) * cd.s2 : 0)];
+                }
+            }
+        }
+        __syncthreads();  // the previous item's readers are done with reg
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+            const int q = threadIdx.x + k * IBLOCK;
+            if (q < RV) reg[q] = v[k];
+        }
+        __syncthreads();
+
+        for (int e = beg + threadIdx.x; e < end; e += IBLOCK) {
+            const int s = p.sorted_s[e];
+            St<W> st[NDIM];
+            marker_stencils<NDIM, K>(p, cd, e, s, st);
+            bool ok = true;
+#pragma unroll
+            for (int d = 0; d < NDIM; ++d)
+                if (st[d].ist <= st[d].isp)
+                    ok = ok && (st[d].icl + st[d].ist >= r0[d]) && (st[d].icl + st[d].isp < r0[d] + R);
+            if (!ok) {
+                atomicOr(p.err, 1);
+                continue;
+            }
+            double acc = 0.0;
+            if constexpr (FAM == 3) {
+                bool nonempty = true;
+#pragma unroll
+                for (int d = 0; d < NDIM; ++d) nonempty = nonempty && (st[d].ist <= st[d].isp);
+                if (nonempty) {
+                    int li = st[0].icl - r0[0] + R * (st[1].icl - r0[1]);
+                    if (NDIM == 3) li += R * R * (st[2].icl - r0[2]);
+                    acc = reg[li];
+                }
+            } else {
+                // Clipped stencil entries (outside [ist, isp]) get weight 0 and a
+                // clamped (in-region) LDS index: acc + 0 == acc, so the sum equals
+                // the Fortran's clipped sum bit for bit, without per-term branches.
+                double w[NDIM][W];
+                int o[NDIM][W];
+#pragma unroll
+                for (int d = 0; d < NDIM; ++d) {
+                    const int stride = d == 0 ? 1 : (d == 1 ? R : R * R);
+#pragma unroll
+                    for (int i = 0; i < W; ++i) {
+                        const bool in = i >= st[d].ist && i <= st[d].isp;
+                        w[d][i] = in ? st[d].w[i] : 0.0;
+                        o[d][i] = min(max(st[d].icl + i - r0[d], 0), R - 1) * stride;
+                    }
+                }
+                if constexpr (NDIM == 3) {
+#pragma unroll
+                    for (int i2 = 0; i2 < W; ++i2) {
+#pragma unroll
+                        for (int i1 = 0; i1 < W; ++i1) {
+                            const double* row = reg + o[1][i1] + o[2][i2];
+                            if constexpr (FAM == 0) {
+                                const double wyz = w[1][i1] * w[2][i2];  // f.m4:1349-1353
+#pragma unroll
+                                for (int i0 = 0; i0 < W; ++i0) {
+                                    const double wt = w[0][i0] * wyz;
+                                    acc = acc + wt * row[o[0][i0]];  // f.m4:1375
+                                }
+                            } else {
+#pragma unroll
+                                for (int i0 = 0; i0 < W; ++i0)
+                                    acc = acc + w[0][i0] * w[1][i1] * w[2][i2] * row[o[0][i0]];  // f.m4:545-548
+                            }
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int i1 = 0; i1 < W; ++i1) {
+                        const double* row = reg + o[1][i1];
+#pragma unroll
+                        for (int i0 = 0; i0 < W; ++i0) {
+                            if constexpr (FAM == 0) {
+                                const double wt = w[0][i0] * w[1][i1];
+                                acc = acc + wt * row[o[0][i0]];
+                            } else {
+                                acc = acc + w[0][i0] * w[1][i1] * row[o[0][i0]];
+                            }
+                        }
+                    }
+                }
+            }
+            p.Qout[(int64_t)p.Q_depth * s + cd.qcomp] = acc;
+        }
+    }
+}
+
+// Entries binned "outside" (no stencil point can reach any array): V = 0.
+__global__ __launch_bounds__(BLOCK) void k_interp_outside(Params p, int n) {
+    const int first = p.brick_start[p.bg.nbricks];
+    for (int e = first + blockIdx.x * BLOCK + threadIdx.x; e < n; e += gridDim.x * BLOCK) {
+        const int s = p.sorted_s[e];
+        for (int c = 0; c < p.ncomp; ++c) p.Qout[(int64_t)p.Q_depth * s + p.comp[c].qcomp] = 0.0;
+    }
+}
+
+template <int NDIM, int K>
+hipError_t launch_interp_t(const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    using S = IShape<NDIM, K>;
+    const size_t lds = (size_t)S::RV * sizeof(double);
+    if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute((const void*)k_interp<NDIM, K>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+    if (ev0) (void)hipEventRecord(ev0, s);
+    const long items = (long)p.bg.nbricks * p.ncomp;
+    hipLaunchKernelGGL((k_interp<NDIM, K>), dim3(grid_for(items, 16)), dim3(IBLOCK), lds, s, p);
+    if (ev1) (void)hipEventRecord(ev1, s);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (n > 0) hipLaunchKernelGGL(k_interp_outside, dim3(64), dim3(BLOCK), 0, s, p, n);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// spreading
+// ---------------------------------------------------------------------------
+template <int NDIM, int K> struct SShape {
+    using BT = BrickT<NDIM>;
+    static constexpr int B = BT::B, SB = BT::SB, SBV = BT::SBV, GROUP = BT::GROUP;
+    static constexpr int W = KT<K>::W;
+    static constexpr int P = NDIM == 3 ? W * W * W : W * W;  // stencil points
+    static constexpr int NPASS = (P + 63) / 64;
+    static constexpr int NBR = NDIM == 3 ? 64 : 16;  // neighbourhood bricks (4 per dim)
+    static constexpr int CH = W <= 4 ? 128 : 64;     // candidates per chunk
+    static constexpr int NACC = SBV / SBLOCK;        // acc values per thread
+    // LDS layout (byte offsets)
+    static constexpr size_t O_ACC = 0;
+    static constexpr size_t O_CW = O_ACC + sizeof(double) * SBV;
+    static constexpr size_t O_CF = O_CW + sizeof(double) * CH * NDIM * W;
+    static constexpr size_t O_CMASK = O_CF + sizeof(double) * CH;
+    static constexpr size_t O_CBASE = O_CMASK + sizeof(unsigned long long) * CH * NPASS;
+    static constexpr size_t O_NBR = O_CBASE + sizeof(int) * CH;
+    static constexpr size_t BYTES = O_NBR + sizeof(int) * (5 * NBR + 1 + 8);
+};
+
+template <int NDIM, int K>
+__global__ __launch_bounds__(SBLOCK) void k_spread(Params p) {
+    using T = KT<K>;
+    using S = SShape<NDIM, K>;
+    constexpr int W = T::W, FAM = T::FAM, LO = T::LO, HI = T::HI;
+    constexpr int B = S::B, SB = S::SB, SBV = S::SBV, P = S::P, NPASS = S::NPASS, NBR = S::NBR, CH = S::CH;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double* acc = reinterpret_cast<double*>(smem + S::O_ACC);
+    double* cw = reinterpret_cast<double*>(smem + S::O_CW);
+    double* cF = reinterpret_cast<double*>(smem + S::O_CF);
+    unsigned long long* cmask = reinterpret_cast<unsigned long long*>(smem + S::O_CMASK);
+    int* cbase = reinterpret_cast<int*>(smem + S::O_CBASE);
+    int* nid = reinterpret_cast<int*>(smem + S::O_NBR);
+    int* nst = nid + NBR;
+    int* nln = nst + NBR;
+    int* sst = nln + NBR;   // sorted starts
+    int* npre = sst + NBR;  // NBR+1 prefix offsets
+    int* misc = npre + NBR + 1;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // per-lane stencil point of each pass (wave 0 processes)
+    int loff[NPASS], li[NPASS][3];
+#pragma unroll
+    for (int ps = 0; ps < NPASS; ++ps) {
+        const int q = ps * 64 + lane;
+        li[ps][0] = q % W;
+        li[ps][1] = (q / W) % W;
+        li[ps][2] = NDIM == 3 ? q / (W * W) : 0;
+        loff[ps] = li[ps][0] + SB * (li[ps][1] + (NDIM == 3 ? SB * li[ps][2] : 0));
+    }
+    const int nc = p.ncomp;
+    const int nsb = p.bg.nbricks / S::GROUP;
+    const int nitems = nsb * nc;
+    const int G = gridDim.x;
+    for (int round = 0; round < nitems; round += G) {
+        const int it = xcd_item(round, G, blockIdx.x);
+        if (it >= nitems) continue;
+        const int sb = it / nc, c = it - (it / nc) * nc;
+        const CompDesc& cd = p.comp[c];
+        int bc0[3];
+        brick_coords<NDIM>(p.bg, sb * S::GROUP, bc0);
+        int kb0[3] = {0, 0, 0};
+        bool inside = true;
+#pragma unroll
+        for (int d = 0; d < NDIM; ++d) {
+            kb0[d] = p.bg.kmin[d] + bc0[d] * B;
+            inside = inside && kb0[d] >= cd.lo[d] && kb0[d] + SB - 1 <= cd.hi[d];
+        }
+
+        __syncthreads();  // the previous item is written back
+        if (tid < NBR) {
+            int q[3] = {bc0[0] + (tid & 3) - 1, bc0[1] + ((tid >> 2) & 3) - 1,
+                        NDIM == 3 ? bc0[2] + (tid >> 4) - 1 : 0};
+            bool valid = true;
+            for (int d = 0; d < NDIM; ++d) valid = valid && q[d] >= 0 && q[d] < p.bg.nb[d];
+            int id = INT_MAX, st = 0, ln = 0;
+            if (valid) {
+                id = brick_id<NDIM>(p.bg, q);
+                st = p.brick_start[id];
+                ln = p.brick_start[id + 1] - st;
+            }
+            nid[tid] = id;
+            nst[tid] = st;
+            nln[tid] = ln;
+        }
+        __syncthreads();
+        if (tid < NBR) {
+            // canonical order = increasing brick id: rank sort of the neighbourhood
+            const int my = nid[tid];
+            int rank = 0;
+            for (int k = 0; k < NBR; ++k) {
+                const int o = nid[k];
+                rank += (o < my) || (o == my && k < tid);
+            }
+            sst[rank] = nst[tid];
+            npre[rank + 1] = nln[tid];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            npre[0] = 0;
+            for (int k = 0; k < NBR; ++k) npre[k + 1] += npre[k];
+        }
+        __syncthreads();
+        const int total = npre[NBR];
+        if (total == 0) continue;
+
+        // u_old of the super-brick's points
+        {
+            double v[S::NACC];
+            const int64_t o0 = (int64_t)(kb0[0] - cd.lo[0]) + (int64_t)(kb0[1] - cd.lo[1]) * cd.s1 +
+                               (NDIM == 3 ? (int64_t)(kb0[2] - cd.lo[2]) * cd.s2 : 0);
+#pragma unroll
+            for (int k = 0; k < S::NACC; ++k) {
+                const int q = tid + k * SBLOCK;
+                const int i0 = q % SB, i1 = (q / SB) % SB, i2 = NDIM == 3 ? q / (SB * SB) : 0;
+                v[k] = 0.0;
+                if (inside) {
+                    v[k] = cd.u[o0 + i0 + (int64_t)i1 * cd.s1 + (NDIM == 3 ? (int64_t)i2 * cd.s2 : 0)];
+                } else {
+                    const int g0 = kb0[0] + i0, g1 = kb0[1] + i1, g2 = kb0[2] + i2;
+                    bool in = g0 >= cd.lo[0] && g0 <= cd.hi[0] && g1 >= cd.lo[1] && g1 <= cd.hi[1];
+                    if (NDIM == 3) in = in && g2 >= cd.lo[2] && g2 <= cd.hi[2];
+                    if (in)
+                        v[k] = cd.u[(int64_t)(g0 - cd.lo[0]) + (int64_t)(g1 - cd.lo[1]) * cd.s1 +
+                                    (NDIM == 3 ? (int64_t)(g2 - cd.lo[2]) * cd.s2 : 0)];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < S::NACC; ++k) acc[tid + k * SBLOCK] = v[k];
+        }
+
+        for (int base = 0; base < total; base += CH) {
+            __syncthreads();  // acc stored / previous chunk consumed
+            // ---- filter CH entries (threads 0..CH-1), ordered compaction
+            bool cand = false;
+            int idx = 0, kc[3] = {0, 0, 0};
+            if (tid < CH && base + tid < total) {
+                const int e = base + tid;
+                int lo = 0, hi = NBR - 1;  // largest j with npre[j] <= e
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (npre[mid] <= e) lo = mid;
+                    else hi = mid - 1;
+                }
+                idx = sst[lo] + (e - npre[lo]);
+                const unsigned key = p.sorted_key[idx];
+                int bq[3];
+                brick_coords<NDIM>(p.bg, (int)(key >> BrickT<NDIM>::SHIFT), bq);
+                unsigned loc = key & ((1u << BrickT<NDIM>::SHIFT) - 1u);
+                cand = true;
+#pragma unroll
+                for (int d = 0; d < NDIM; ++d) {
+                    kc[d] = p.bg.kmin[d] + bq[d] * B + (int)(loc % (unsigned)B);
+                    loc /= (unsigned)B;
+                    cand = cand && kc[d] >= kb0[d] - HI && kc[d] <= kb0[d] + SB - 1 - LO;
+                }
+            }
+            const unsigned long long bal = __ballot(cand);
+            if (lane == 0 && wave < CH / 64) misc[wave] = __popcll(bal);
+            __syncthreads();
+            int off = 0, ncand = 0;
+            for (int w = 0; w < CH / 64; ++w) {
+                off += (w < wave) ? misc[w] : 0;
+                ncand += misc[w];
+            }
+            if (cand) {
+                // ---- prep: this candidate's stencil in component c's frame
+                const int pos = off + __popcll(bal & ((1ull << lane) - 1ull));
+                const int s = p.sorted_s[idx];
+                St<W> st[NDIM];
+                marker_stencils<NDIM, K>(p, cd, idx, s, st);
+                cF[pos] = p.Qin[(int64_t)p.Q_depth * s + cd.qcomp];
+                unsigned vm[3] = {0u, 0u, 0u};  // valid stencil indices per dim
+                int cb = 0, mul = 1;
+#pragma unroll
+                for (int d = 0; d < NDIM; ++d) {
+                    // binning invariant: the stencil lies in [key + LO, key + HI]
+                    if (st[d].ist <= st[d].isp &&
+                        (st[d].icl + st[d].ist < kc[d] + LO || st[d].icl + st[d].isp > kc[d] + HI))
+                        atomicOr(p.err, 2);
+#pragma unroll
+                    for (int i = 0; i < W; ++i) {
+                        const int lc = st[d].icl + i - kb0[d];
+                        if (i >= st[d].ist && i <= st[d].isp && lc >= 0 && lc < SB) vm[d] |= 1u << i;
+                        // closed form: wz = w2/(dx0*dx1*dx2) (f.m4:1486); 2-D wy = w1/(dx0*dx1)
+                        cw[(pos * NDIM + d) * W + i] = (FAM == 0 && d == NDIM - 1) ? st[d].w[i] / p.h3 : st[d].w[i];
+                    }
+                    cb += (st[d].icl - kb0[d]) * mul;
+                    mul *= SB;
+                }
+                cbase[pos] = cb;
+                unsigned long long m[NPASS];
+#pragma unroll
+                for (int ps = 0; ps < NPASS; ++ps) m[ps] = 0ull;
+                const int n2 = NDIM == 3 ? W : 1;
+                for (int i2 = 0; i2 < n2; ++i2) {
+                    if (NDIM == 3 && !((vm[2] >> i2) & 1u)) continue;
+                    for (int i1 = 0; i1 < W; ++i1) {
+                        if (!((vm[1] >> i1) & 1u)) continue;
+                        const int q0 = W * i1 + W * W * i2;
+                        const unsigned long long row = (unsigned long long)vm[0];
+#pragma unroll
+                        for (int ps = 0; ps < NPASS; ++ps) {
+                            const int sh = q0 - 64 * ps;
+                            if (sh >= 0 && sh < 64) m[ps] |= row << sh;
+                            else if (sh < 0 && sh > -W) m[ps] |= row >> (-sh);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int ps = 0; ps < NPASS; ++ps) cmask[pos * NPASS + ps] = m[ps];
+            }
+            __syncthreads();
+            // ---- one wave adds the candidates in canonical order, lane = stencil point
+            if (wave == 0) {
+                for (int ci = 0; ci < ncand; ++ci) {
+                    const double* w = cw + ci * NDIM * W;
+                    const double F = cF[ci];
+                    const int cb = cbase[ci];
+#pragma unroll
+                    for (int ps = 0; ps < NPASS; ++ps) {
+                        const unsigned long long m = cmask[ci * NPASS + ps];
+                        if (!((m >> lane) & 1ull)) continue;
+                        double contrib;
+                        if constexpr (FAM == 3) {
+                            contrib = F / p.h3;  // f.m4:170-171
+                        } else if constexpr (FAM == 0) {
+                            double wt;
+                            if constexpr (NDIM == 3)
+                                wt = w[li[ps][0]] * (w[W + li[ps][1]] * w[2 * W + li[ps][2]]);  // f.m4:1485-1492
+                            else
+                                wt = w[li[ps][0]] * w[W + li[ps][1]];
+                            contrib = wt * F;  // f.m4:1512-1513
+                        } else {
+                            if constexpr (NDIM == 3)
+                                contrib = w[li[ps][0]] * w[W + li[ps][1]] * w[2 * W + li[ps][2]] * F / p.h3;
+                            else
+                                contrib = w[li[ps][0]] * w[W + li[ps][1]] * F / p.h3;  // f.m4:668-672
+                        }
+                        __hip_atomic_fetch_add(&acc[cb + loff[ps]], contrib, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // write back the super-brick's points
+        {
+            const int64_t o0 = (int64_t)(kb0[0] - cd.lo[0]) + (int64_t)(kb0[1] - cd.lo[1]) * cd.s1 +
+                               (NDIM == 3 ? (int64_t)(kb0[2] - cd.lo[2]) * cd.s2 : 0);
+#pragma unroll
+            for (int k = 0; k < S::NACC; ++k) {
+                const int q = tid + k * SBLOCK;
+                const int i0 = q % SB, i1 = (q / SB) % SB, i2 = NDIM == 3 ? q / (SB * SB) : 0;
+                if (inside) {
+                    cd.u[o0 + i0 + (int64_t)i1 * cd.s1 + (NDIM == 3 ? (int64_t)i2 * cd.s2 : 0)] = acc[q];
+                } else {
+                    const int g0 = kb0[0] + i0, g1 = kb0[1] + i1, g2 = kb0[2] + i2;
+                    bool in = g0 >= cd.lo[0] && g0 <= cd.hi[0] && g1 >= cd.lo[1] && g1 <= cd.hi[1];
+                    if (NDIM == 3) in = in && g2 >= cd.lo[2] && g2 <= cd.hi[2];
+                    if (in)
+                        cd.u[(int64_t)(g0 - cd.lo[0]) + (int64_t)(g1 - cd.lo[1]) * cd.s1 +
+                             (NDIM == 3 ? (int64_t)(g2 - cd.lo[2]) * cd.s2 : 0)] = acc[q];
+                }
+            }
+        }
+    }
+}
+
+template <int NDIM, int K>
+hipError_t launch_spread_t(const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    using S = SShape<NDIM, K>;
+    const size_t lds = S::BYTES;
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute((const void*)k_spread<NDIM, K>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+    if (ev0) (void)hipEventRecord(ev0, s);
+    const long items = (long)(p.bg.nbricks / S::GROUP) * p.ncomp;
+    hipLaunchKernelGGL((k_spread<NDIM, K>), dim3(grid_for(items, 8)), dim3(SBLOCK), lds, s, p);
+    if (ev1) (void)hipEventRecord(ev1, s);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// dispatch
+// ---------------------------------------------------------------------------
+#define IBTK_LE_DISPATCH(NDIMV, KV, CALL)                                     \
+    switch (KV) {                                                             \
+    case K_PIECEWISE_CONSTANT: return CALL<NDIMV, K_PIECEWISE_CONSTANT>;      \
+    case K_DISCONTINUOUS_LINEAR: return CALL<NDIMV, K_DISCONTINUOUS_LINEAR>;  \
+    case K_PIECEWISE_LINEAR: return CALL<NDIMV, K_PIECEWISE_LINEAR>;          \
+    case K_PIECEWISE_CUBIC: return CALL<NDIMV, K_PIECEWISE_CUBIC>;            \
+    case K_IB_3: return CALL<NDIMV, K_IB_3>;                                  \
+    case K_IB_4: return CALL<NDIMV, K_IB_4>;                                  \
+    case K_IB_4_W8: return CALL<NDIMV, K_IB_4_W8>;                            \
+    case K_IB_6: return CALL<NDIMV, K_IB_6>;                                  \
+    case K_BSPLINE_4: return CALL<NDIMV, K_BSPLINE_4>;                        \
+    default: return nullptr;                                                  \
+    }
+
+using BinFn = hipError_t (*)(const Params&, int, unsigned*, int*, hipStream_t);
+using InterpFn = hipError_t (*)(const Params&, int, hipStream_t, hipEvent_t, hipEvent_t);
+using SpreadFn = hipError_t (*)(const Params&, hipStream_t, hipEvent_t, hipEvent_t);
+
+template <int NDIM> static BinFn pick_bin(int k) { IBTK_LE_DISPATCH(NDIM, k, launch_bin_t) }
+template <int NDIM> static InterpFn pick_interp(int k) { IBTK_LE_DISPATCH(NDIM, k, launch_interp_t) }
+template <int NDIM> static SpreadFn pick_spread(int k) { IBTK_LE_DISPATCH(NDIM, k, launch_spread_t) }
+
+hipError_t launch_bin(int ndim, int kernel, const Params& p, int n, unsigned* keys, int* vals, hipStream_t s) {
+    BinFn f = ndim == 3 ? pick_bin<3>(kernel) : pick_bin<2>(kernel);
+    return f ? f(p, n, keys, vals, s) : hipErrorInvalidValue;
+}
+hipError_t launch_brick_start(const unsigned* keys, int n, int nbricks, int shift, int* bs, hipStream_t s) {
+    hipLaunchKernelGGL(k_brick_start, dim3((n + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, keys, n, nbricks, shift,
+                       bs);
+    return hipGetLastError();
+}
+hipError_t launch_gather_sorted(int ndim, const Params& p, int n, int* sorted_s, double* sorted_X, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (ndim == 3)
+        hipLaunchKernelGGL(k_gather_sorted<3>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, sorted_s,
+                           sorted_X);
+    else
+        hipLaunchKernelGGL(k_gather_sorted<2>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, sorted_s,
+                           sorted_X);
+    return hipGetLastError();
+}
+hipError_t launch_interp(int ndim, int kernel, const Params& p, int n, hipStream_t s, hipEvent_t ev0,
+                         hipEvent_t ev1) {
+    InterpFn f = ndim == 3 ? pick_interp<3>(kernel) : pick_interp<2>(kernel);
+    return f ? f(p, n, s, ev0, ev1) : hipErrorInvalidValue;
+}
+hipError_t launch_spread(int ndim, int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    SpreadFn f = ndim == 3 ? pick_spread<3>(kernel) : pick_spread<2>(kernel);
+    return f ? f(p, s, ev0, ev1) : hipErrorInvalidValue;
+}
+
+}  // namespace ibtk_le

@@ -43,7 +43,7 @@ constexpr int MAXC = 4;        // components processed by one launch
 constexpr int BRICK3 = 8;      // brick edge (cells) in 3-D: 8^3 = 512 cells
 constexpr int BRICK2 = 16;     // brick edge in 2-D: 16^2 = 256 cells
 constexpr int BLOCK = 256;     // threads per workgroup (4 waves)
-constexpr int SPREAD_CH = 64;  // candidate chunk of the spread kernel (one wave filters)
+constexpr int TILE = 4;        // bricks per tile edge
 
 // One Eulerian array (a component of side data, or a depth slice of cell /
 // node data) in SAMRAI's Fortran layout u(lo0:hi0, lo1:hi1, [lo2:hi2]).
@@ -58,11 +58,15 @@ struct CompDesc {
     int64_t s1, s2;  // strides of dims 1 and 2 (elements)
 };
 
-// The brick grid over stencil-anchor ("key") cells.
+// The brick grid over stencil-anchor ("key") cells.  Bricks (8^3 cells in 3-D,
+// 16^2 in 2-D) are numbered tile by tile (tiles of 4^NDIM bricks, tiles in
+// linear order), Morton order inside a tile; an aligned 2^NDIM group of bricks
+// (a spread "super-brick") therefore has 2^NDIM consecutive ids.
 struct BinGeom {
     int ndim;
     int kmin[3];       // key cell of brick (0,0,0), cell (0,0,0)
-    int nb[3];         // bricks per dim
+    int nb[3];         // bricks per dim (multiple of 4)
+    int nt[3];         // tiles per dim
     int nbricks;
     int shift;         // log2(cells per brick)
     double xlo[3];     // cell-frame x_lower of the patch
@@ -81,6 +85,8 @@ struct Params {
     const int* indices;        // list entry -> marker (nullptr: identity)
     const double* Xshift;      // list entry -> shift[NDIM] (nullptr: zero)
     const int* sorted_l;       // sorted position -> list entry
+    const int* sorted_s;       // sorted position -> marker index
+    const double* sorted_X;    // sorted position -> X(s) + Xshift(l) [NDIM]
     const unsigned* sorted_key;
     const int* brick_start;    // nbricks + 1 offsets into the sorted list
     const int* nentries_dev;   // device copy of the list length
@@ -92,6 +98,7 @@ struct Params {
 // Host-side launchers (le_kernels.hip).
 hipError_t launch_bin(int ndim, int kernel, const Params& p, int n, unsigned* keys, int* vals, hipStream_t s);
 hipError_t launch_brick_start(const unsigned* keys, int n, int nbricks, int shift, int* bs, hipStream_t s);
+hipError_t launch_gather_sorted(int ndim, const Params& p, int n, int* sorted_s, double* sorted_X, hipStream_t s);
 hipError_t launch_interp(int ndim, int kernel, const Params& p, int n, hipStream_t s, hipEvent_t ev0,
                          hipEvent_t ev1);
 hipError_t launch_spread(int ndim, int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
@@ -117,6 +124,8 @@ struct ImageDesc {
     int ilo[3], ihi[3];
     int ghost;
     int periodic[3];
+    int filter;           // 1: emit (s, 0) iff the cell lies in [flo, fhi] (no images)
+    int flo[3], fhi[3];
 };
 hipError_t launch_image_count(const ImageDesc& d, const double* X, int n, int* counts, hipStream_t s);
 hipError_t launch_image_write(const ImageDesc& d, const double* X, int n, const int* offsets, int* idx,

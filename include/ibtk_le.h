@@ -155,10 +155,18 @@ int ibtk_le_fold_periodic_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom
  * ghost box (LIndexSetData::cacheLocalIndices, LIndexSetData.cpp:83-169, for one
  * patch covering a periodic domain; getCellIndex, IndexUtilities-inl.h:66-89).
  * Writes up to `capacity` entries into indices_dev / Xshift_dev (NDIM per entry)
- * and the entry count into *count (host).  ghost = 0 gives the interior list. */
+ * and the entry count into *count (host).  ghost = 0 gives the interior list.
+ * If the list needs more than `capacity` entries, nothing is written, *count
+ * holds the required size and IBTK_LE_ERR_ARG is returned. */
 int ibtk_le_periodic_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
                                 int n_markers, int ghost, const int* periodic, int* indices_dev,
                                 double* Xshift_dev, int capacity, int* count);
+
+/* Markers whose cell (IndexUtilities::getCellIndex against the patch box) lies in
+ * [box_lo, box_hi], no periodic shifts: the list LEInteractor's X-only overloads
+ * build (LEInteractor.cpp:3110-3139).  Marker-major order. */
+int ibtk_le_box_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev, int n_markers,
+                           const int* box_lo, const int* box_hi, int* indices_dev, int capacity, int* count);
 
 /* Diagnostics: masks_dev[c] (one byte per point of component c's ghosted array,
  * same layout) gets 1 at every point some listed stencil touches after clipping.

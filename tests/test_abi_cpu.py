@@ -13,7 +13,7 @@ ROOT = Path(__file__).resolve().parents[1]
 
 def declared_functions():
     names = set()
-    for h in (ROOT / "include").rglob("*.h"):
+    for h in (ROOT / "include").glob("*.h"):  # the C-ABI headers (the C++ facade is checked below)
         text = h.read_text()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         text = re.sub(r"//[^\n]*", "", text)
@@ -66,3 +66,19 @@ def test_no_oracle_in_product_path():
     for p in (ROOT / "ibamr_amd").rglob("*"):
         if p.suffix in (".py", ".cpp", ".hip", ".h"):
             assert not pat.search(p.read_text()), p
+
+
+def test_cpp_facade_methods_exported(lib):
+    """The C++ LEInteractor facade (include/ibtk_le/LEInteractor.h) is compiled into the library."""
+    import shutil
+    import subprocess
+    nm = shutil.which("nm")
+    if nm is None:
+        pytest.skip("nm not available")
+    from ibamr_amd import _lib
+    out = subprocess.run([nm, "-DC", str(_lib.LIB_PATH)], capture_output=True, text=True).stdout
+    hdr = (ROOT / "include" / "ibtk_le" / "LEInteractor.h").read_text()
+    methods = sorted(set(re.findall(r"static\s+\w+\s+(\w+)\(", hdr)))
+    assert {"interpolate", "spread", "getStencilSize", "getMinimumGhostWidth"} <= set(methods)
+    for m in methods:
+        assert f"IBTK::LEInteractor::{m}(" in out, m
