@@ -135,15 +135,24 @@ template <int NDIM, int K> struct IShape {
 };
 
 template <int NDIM, int K>
-__device__ __forceinline__ void marker_stencils(const Params& p, const CompDesc& cd, int e, int s,
-                                                St<KT<K>::W>* st) {
+__device__ __forceinline__ void marker_stencils_x(const Params& p, const CompDesc& cd, const double* Xs, int s,
+                                                  St<KT<K>::W>* st) {
     constexpr int FAM = KT<K>::FAM;
 #pragma unroll
     for (int d = 0; d < NDIM; ++d) {
-        const double Xs = p.sorted_X[(int64_t)NDIM * e + d];
-        const double Xraw = (FAM == 2) ? p.X[(int64_t)NDIM * s + d] : Xs;
-        stencil1d<K>(Xs, Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis, p.K6, st[d]);
+        const double Xraw = (FAM == 2) ? p.X[(int64_t)NDIM * s + d] : Xs[d];
+        stencil1d<K>(Xs[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis, p.K6,
+                     st[d]);
     }
+}
+
+template <int NDIM, int K>
+__device__ __forceinline__ void marker_stencils(const Params& p, const CompDesc& cd, int e, int s,
+                                                St<KT<K>::W>* st) {
+    double Xs[NDIM];
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) Xs[d] = p.sorted_X[(int64_t)NDIM * e + d];
+    marker_stencils_x<NDIM, K>(p, cd, Xs, s, st);
 }
 
 template <int NDIM, int K>
@@ -170,6 +179,15 @@ __global__ __launch_bounds__(IBLOCK) void k_interp(Params p) {
         for (int d = 0; d < NDIM; ++d) {
             r0[d] = p.bg.kmin[d] + bc[d] * B + T::LO;
             inside = inside && r0[d] >= cd.lo[d] && r0[d] + R - 1 <= cd.hi[d];
+        }
+        // this thread's first marker, loaded together with the staging loads
+        const int e0 = beg + threadIdx.x;
+        int s0 = 0;
+        double x0[NDIM];
+        if (e0 < end) {
+            s0 = p.sorted_s[e0];
+#pragma unroll
+            for (int d = 0; d < NDIM; ++d) x0[d] = p.sorted_X[(int64_t)NDIM * e0 + d];
         }
         // issue every staging load of this thread before using any of them
         double v[NL];
@@ -201,10 +219,15 @@ __global__ __launch_bounds__(IBLOCK) void k_interp(Params p) {
         }
         __syncthreads();
 
-        for (int e = beg + threadIdx.x; e < end; e += IBLOCK) {
-            const int s = p.sorted_s[e];
+        for (int e = e0; e < end; e += IBLOCK) {
+            int s = s0;
+            if (e != e0) {
+                s = p.sorted_s[e];
+#pragma unroll
+                for (int d = 0; d < NDIM; ++d) x0[d] = p.sorted_X[(int64_t)NDIM * e + d];
+            }
             St<W> st[NDIM];
-            marker_stencils<NDIM, K>(p, cd, e, s, st);
+            marker_stencils_x<NDIM, K>(p, cd, x0, s, st);
             bool ok = true;
 #pragma unroll
             for (int d = 0; d < NDIM; ++d)
@@ -315,18 +338,23 @@ template <int NDIM, int K> struct SShape {
     static constexpr int B = BT::B, SB = BT::SB, SBV = BT::SBV, GROUP = BT::GROUP;
     static constexpr int W = KT<K>::W;
     static constexpr int P = NDIM == 3 ? W * W * W : W * W;  // stencil points
-    static constexpr int NPASS = (P + 63) / 64;
-    static constexpr int NBR = NDIM == 3 ? 64 : 16;  // neighbourhood bricks (4 per dim)
-    static constexpr int CH = W <= 4 ? 128 : 64;     // candidates per chunk
-    static constexpr int NACC = SBV / SBLOCK;        // acc values per thread
+    static constexpr int NPASS = (P + 63) / 64;              // 64-lane passes per stencil
+    static constexpr int NQ = SBLOCK / 64;                   // waves = quarters of the super-brick
+    static constexpr int QW = SB / NQ;                       // planes (3-D z) / rows (2-D y) per quarter
+    static constexpr int NBR = NDIM == 3 ? 64 : 16;          // neighbourhood bricks (4 per dim)
+    static constexpr int CH = 64;                            // candidates per prep/process chunk
+    static constexpr int KMAX = 4;                           // entries per thread per filter pass
+    static constexpr int CAP = KMAX * SBLOCK;                // candidate list capacity per filter pass
+    static constexpr int NACC = SBV / SBLOCK;                // acc values per thread
     // LDS layout (byte offsets)
     static constexpr size_t O_ACC = 0;
     static constexpr size_t O_CW = O_ACC + sizeof(double) * SBV;
     static constexpr size_t O_CF = O_CW + sizeof(double) * CH * NDIM * W;
     static constexpr size_t O_CMASK = O_CF + sizeof(double) * CH;
-    static constexpr size_t O_CBASE = O_CMASK + sizeof(unsigned long long) * CH * NPASS;
-    static constexpr size_t O_NBR = O_CBASE + sizeof(int) * CH;
-    static constexpr size_t BYTES = O_NBR + sizeof(int) * (5 * NBR + 1 + 8);
+    static constexpr size_t O_CBASE = O_CMASK + sizeof(unsigned long long) * CH * NQ * NPASS;
+    static constexpr size_t O_CIDX = O_CBASE + sizeof(int) * CH;
+    static constexpr size_t O_NBR = O_CIDX + sizeof(int) * CAP;
+    static constexpr size_t BYTES = O_NBR + sizeof(int) * (5 * NBR + 1 + KMAX * NQ + 8);
 };
 
 template <int NDIM, int K>
@@ -334,22 +362,26 @@ __global__ __launch_bounds__(SBLOCK) void k_spread(Params p) {
     using T = KT<K>;
     using S = SShape<NDIM, K>;
     constexpr int W = T::W, FAM = T::FAM, LO = T::LO, HI = T::HI;
-    constexpr int B = S::B, SB = S::SB, SBV = S::SBV, P = S::P, NPASS = S::NPASS, NBR = S::NBR, CH = S::CH;
+    constexpr int B = S::B, SB = S::SB, SBV = S::SBV, NPASS = S::NPASS, NBR = S::NBR, CH = S::CH, NQ = S::NQ;
+    constexpr int QW = S::QW, KMAX = S::KMAX, CAP = S::CAP;
+    constexpr int QD = NDIM - 1;  // the quartered dim
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double* acc = reinterpret_cast<double*>(smem + S::O_ACC);
     double* cw = reinterpret_cast<double*>(smem + S::O_CW);
     double* cF = reinterpret_cast<double*>(smem + S::O_CF);
     unsigned long long* cmask = reinterpret_cast<unsigned long long*>(smem + S::O_CMASK);
     int* cbase = reinterpret_cast<int*>(smem + S::O_CBASE);
+    int* cidx = reinterpret_cast<int*>(smem + S::O_CIDX);
     int* nid = reinterpret_cast<int*>(smem + S::O_NBR);
     int* nst = nid + NBR;
     int* nln = nst + NBR;
     int* sst = nln + NBR;   // sorted starts
     int* npre = sst + NBR;  // NBR+1 prefix offsets
-    int* misc = npre + NBR + 1;
+    int* cnt = npre + NBR + 1;  // [KMAX][NQ] filter counts
+    int* misc = cnt + KMAX * NQ;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // per-lane stencil point of each pass (wave 0 processes)
+    // per-lane stencil point of each pass
     int loff[NPASS], li[NPASS][3];
 #pragma unroll
     for (int ps = 0; ps < NPASS; ++ps) {
@@ -415,11 +447,11 @@ __global__ __launch_bounds__(SBLOCK) void k_spread(Params p) {
         const int total = npre[NBR];
         if (total == 0) continue;
 
-        // u_old of the super-brick's points
+        // u_old of the super-brick's points (loads issued now, stored below)
+        const int64_t o0 = (int64_t)(kb0[0] - cd.lo[0]) + (int64_t)(kb0[1] - cd.lo[1]) * cd.s1 +
+                           (NDIM == 3 ? (int64_t)(kb0[2] - cd.lo[2]) * cd.s2 : 0);
         {
             double v[S::NACC];
-            const int64_t o0 = (int64_t)(kb0[0] - cd.lo[0]) + (int64_t)(kb0[1] - cd.lo[1]) * cd.s1 +
-                               (NDIM == 3 ? (int64_t)(kb0[2] - cd.lo[2]) * cd.s2 : 0);
 #pragma unroll
             for (int k = 0; k < S::NACC; ++k) {
                 const int q = tid + k * SBLOCK;
@@ -440,98 +472,146 @@ __global__ __launch_bounds__(SBLOCK) void k_spread(Params p) {
             for (int k = 0; k < S::NACC; ++k) acc[tid + k * SBLOCK] = v[k];
         }
 
-        for (int base = 0; base < total; base += CH) {
-            __syncthreads();  // acc stored / previous chunk consumed
-            // ---- filter CH entries (threads 0..CH-1), ordered compaction
-            bool cand = false;
-            int idx = 0, kc[3] = {0, 0, 0};
-            if (tid < CH && base + tid < total) {
-                const int e = base + tid;
-                int lo = 0, hi = NBR - 1;  // largest j with npre[j] <= e
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (npre[mid] <= e) lo = mid;
-                    else hi = mid - 1;
-                }
-                idx = sst[lo] + (e - npre[lo]);
-                const unsigned key = p.sorted_key[idx];
-                int bq[3];
-                brick_coords<NDIM>(p.bg, (int)(key >> BrickT<NDIM>::SHIFT), bq);
-                unsigned loc = key & ((1u << BrickT<NDIM>::SHIFT) - 1u);
-                cand = true;
+        for (int fbase = 0; fbase < total; fbase += CAP) {
+            // ---- filter up to CAP entries: every key load in flight at once
+            unsigned key[KMAX];
+            int eidx[KMAX];
 #pragma unroll
-                for (int d = 0; d < NDIM; ++d) {
-                    kc[d] = p.bg.kmin[d] + bq[d] * B + (int)(loc % (unsigned)B);
-                    loc /= (unsigned)B;
-                    cand = cand && kc[d] >= kb0[d] - HI && kc[d] <= kb0[d] + SB - 1 - LO;
-                }
-            }
-            const unsigned long long bal = __ballot(cand);
-            if (lane == 0 && wave < CH / 64) misc[wave] = __popcll(bal);
-            __syncthreads();
-            int off = 0, ncand = 0;
-            for (int w = 0; w < CH / 64; ++w) {
-                off += (w < wave) ? misc[w] : 0;
-                ncand += misc[w];
-            }
-            if (cand) {
-                // ---- prep: this candidate's stencil in component c's frame
-                const int pos = off + __popcll(bal & ((1ull << lane) - 1ull));
-                const int s = p.sorted_s[idx];
-                St<W> st[NDIM];
-                marker_stencils<NDIM, K>(p, cd, idx, s, st);
-                cF[pos] = p.Qin[(int64_t)p.Q_depth * s + cd.qcomp];
-                unsigned vm[3] = {0u, 0u, 0u};  // valid stencil indices per dim
-                int cb = 0, mul = 1;
-#pragma unroll
-                for (int d = 0; d < NDIM; ++d) {
-                    // binning invariant: the stencil lies in [key + LO, key + HI]
-                    if (st[d].ist <= st[d].isp &&
-                        (st[d].icl + st[d].ist < kc[d] + LO || st[d].icl + st[d].isp > kc[d] + HI))
-                        atomicOr(p.err, 2);
-#pragma unroll
-                    for (int i = 0; i < W; ++i) {
-                        const int lc = st[d].icl + i - kb0[d];
-                        if (i >= st[d].ist && i <= st[d].isp && lc >= 0 && lc < SB) vm[d] |= 1u << i;
-                        // closed form: wz = w2/(dx0*dx1*dx2) (f.m4:1486); 2-D wy = w1/(dx0*dx1)
-                        cw[(pos * NDIM + d) * W + i] = (FAM == 0 && d == NDIM - 1) ? st[d].w[i] / p.h3 : st[d].w[i];
+            for (int k = 0; k < KMAX; ++k) {
+                const int e = fbase + k * SBLOCK + tid;
+                key[k] = 0xffffffffu;
+                eidx[k] = -1;
+                if (e < total) {
+                    int lo = 0, hi = NBR - 1;  // largest j with npre[j] <= e
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (npre[mid] <= e) lo = mid;
+                        else hi = mid - 1;
                     }
-                    cb += (st[d].icl - kb0[d]) * mul;
-                    mul *= SB;
+                    eidx[k] = sst[lo] + (e - npre[lo]);
+                    key[k] = p.sorted_key[eidx[k]];
                 }
-                cbase[pos] = cb;
-                unsigned long long m[NPASS];
+            }
+            unsigned long long bal[KMAX];
 #pragma unroll
-                for (int ps = 0; ps < NPASS; ++ps) m[ps] = 0ull;
-                const int n2 = NDIM == 3 ? W : 1;
-                for (int i2 = 0; i2 < n2; ++i2) {
-                    if (NDIM == 3 && !((vm[2] >> i2) & 1u)) continue;
-                    for (int i1 = 0; i1 < W; ++i1) {
-                        if (!((vm[1] >> i1) & 1u)) continue;
-                        const int q0 = W * i1 + W * W * i2;
-                        const unsigned long long row = (unsigned long long)vm[0];
+            for (int k = 0; k < KMAX; ++k) {
+                bool cand = eidx[k] >= 0;
+                if (cand) {
+                    int bq[3];
+                    brick_coords<NDIM>(p.bg, (int)(key[k] >> BrickT<NDIM>::SHIFT), bq);
+                    unsigned loc = key[k] & ((1u << BrickT<NDIM>::SHIFT) - 1u);
 #pragma unroll
-                        for (int ps = 0; ps < NPASS; ++ps) {
-                            const int sh = q0 - 64 * ps;
-                            if (sh >= 0 && sh < 64) m[ps] |= row << sh;
-                            else if (sh < 0 && sh > -W) m[ps] |= row >> (-sh);
+                    for (int d = 0; d < NDIM; ++d) {
+                        const int kc = p.bg.kmin[d] + bq[d] * B + (int)(loc % (unsigned)B);
+                        loc /= (unsigned)B;
+                        cand = cand && kc >= kb0[d] - HI && kc <= kb0[d] + SB - 1 - LO;
+                    }
+                }
+                bal[k] = __ballot(cand);
+                if (!cand) eidx[k] = -1;
+                if (lane == 0) cnt[k * NQ + wave] = __popcll(bal[k]);
+            }
+            __syncthreads();
+            // ordered compaction: entry order is (k, wave, lane)
+            int before = 0, ncand = 0;
+            for (int k = 0; k < KMAX; ++k)
+                for (int w = 0; w < NQ; ++w) {
+                    const int n = cnt[k * NQ + w];
+                    ncand += n;
+                }
+#pragma unroll
+            for (int k = 0; k < KMAX; ++k) {
+                if (eidx[k] >= 0) {
+                    int pos = 0;
+                    for (int kk = 0; kk < KMAX; ++kk)
+                        for (int w = 0; w < NQ; ++w)
+                            if (kk < k || (kk == k && w < wave)) pos += cnt[kk * NQ + w];
+                    pos += __popcll(bal[k] & ((1ull << lane) - 1ull));
+                    cidx[pos] = eidx[k];
+                }
+            }
+            (void)before;
+
+            for (int cb0 = 0; cb0 < ncand; cb0 += CH) {
+                __syncthreads();  // cidx written / previous chunk consumed
+                const int nch = min(CH, ncand - cb0);
+                if (tid < nch) {
+                    // ---- prep: this candidate's stencil in component c's frame
+                    const int pos = tid;
+                    const int idx = cidx[cb0 + tid];
+                    const int s = p.sorted_s[idx];
+                    const unsigned kk = p.sorted_key[idx];
+                    St<W> st[NDIM];
+                    marker_stencils<NDIM, K>(p, cd, idx, s, st);
+                    cF[pos] = p.Qin[(int64_t)p.Q_depth * s + cd.qcomp];
+                    int bq[3];
+                    brick_coords<NDIM>(p.bg, (int)(kk >> BrickT<NDIM>::SHIFT), bq);
+                    unsigned loc = kk & ((1u << BrickT<NDIM>::SHIFT) - 1u);
+                    unsigned vm[3] = {0u, 0u, 0u};  // valid stencil indices per dim
+                    int cbv = 0, mul = 1;
+#pragma unroll
+                    for (int d = 0; d < NDIM; ++d) {
+                        const int kc = p.bg.kmin[d] + bq[d] * B + (int)(loc % (unsigned)B);
+                        loc /= (unsigned)B;
+                        // binning invariant: the stencil lies in [key + LO, key + HI]
+                        if (st[d].ist <= st[d].isp &&
+                            (st[d].icl + st[d].ist < kc + LO || st[d].icl + st[d].isp > kc + HI))
+                            atomicOr(p.err, 2);
+#pragma unroll
+                        for (int i = 0; i < W; ++i) {
+                            const int lc = st[d].icl + i - kb0[d];
+                            if (i >= st[d].ist && i <= st[d].isp && lc >= 0 && lc < SB) vm[d] |= 1u << i;
+                            // closed form: wz = w2/(dx0*dx1*dx2) (f.m4:1486); 2-D wy = w1/(dx0*dx1)
+                            cw[(pos * NDIM + d) * W + i] =
+                                (FAM == 0 && d == NDIM - 1) ? st[d].w[i] / p.h3 : st[d].w[i];
+                        }
+                        cbv += (st[d].icl - kb0[d]) * mul;
+                        mul *= SB;
+                    }
+                    cbase[pos] = cbv;
+                    // per-quarter, per-pass lane masks (quarter = wave owning the plane)
+                    unsigned long long m[NQ][NPASS];
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+                        for (int ps = 0; ps < NPASS; ++ps) m[q][ps] = 0ull;
+                    const int n2 = NDIM == 3 ? W : 1;
+                    for (int i2 = 0; i2 < n2; ++i2) {
+                        if (NDIM == 3 && !((vm[2] >> i2) & 1u)) continue;
+                        for (int i1 = 0; i1 < W; ++i1) {
+                            if (!((vm[1] >> i1) & 1u)) continue;
+                            const int lq = (QD == 2 ? st[2 % NDIM].icl + i2 : st[1].icl + i1) - kb0[QD];
+                            const int qq = lq / QW;
+                            const int q0 = W * i1 + W * W * i2;
+                            const unsigned long long row = (unsigned long long)vm[0];
+#pragma unroll
+                            for (int q = 0; q < NQ; ++q) {
+                                if (q != qq) continue;
+#pragma unroll
+                                for (int ps = 0; ps < NPASS; ++ps) {
+                                    const int sh = q0 - 64 * ps;
+                                    if (sh >= 0 && sh < 64) m[q][ps] |= row << sh;
+                                    else if (sh < 0 && sh > -W) m[q][ps] |= row >> (-sh);
+                                }
+                            }
                         }
                     }
-                }
 #pragma unroll
-                for (int ps = 0; ps < NPASS; ++ps) cmask[pos * NPASS + ps] = m[ps];
-            }
-            __syncthreads();
-            // ---- one wave adds the candidates in canonical order, lane = stencil point
-            if (wave == 0) {
-                for (int ci = 0; ci < ncand; ++ci) {
+                    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+                        for (int ps = 0; ps < NPASS; ++ps) cmask[(pos * NQ + q) * NPASS + ps] = m[q][ps];
+                }
+                __syncthreads();
+                // ---- each wave adds, in canonical order, the stencil points of the
+                // candidates that fall in its quarter (lane = stencil point)
+                for (int ci = 0; ci < nch; ++ci) {
                     const double* w = cw + ci * NDIM * W;
-                    const double F = cF[ci];
-                    const int cb = cbase[ci];
 #pragma unroll
                     for (int ps = 0; ps < NPASS; ++ps) {
-                        const unsigned long long m = cmask[ci * NPASS + ps];
+                        const unsigned long long m = cmask[(ci * NQ + wave) * NPASS + ps];
+                        if (m == 0ull) continue;  // wave-uniform
                         if (!((m >> lane) & 1ull)) continue;
+                        const double F = cF[ci];
                         double contrib;
                         if constexpr (FAM == 3) {
                             contrib = F / p.h3;  // f.m4:170-171
@@ -548,31 +628,28 @@ __global__ __launch_bounds__(SBLOCK) void k_spread(Params p) {
                             else
                                 contrib = w[li[ps][0]] * w[W + li[ps][1]] * F / p.h3;  // f.m4:668-672
                         }
-                        __hip_atomic_fetch_add(&acc[cb + loff[ps]], contrib, __ATOMIC_RELAXED,
+                        __hip_atomic_fetch_add(&acc[cbase[ci] + loff[ps]], contrib, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
             }
+            __syncthreads();  // cidx / cnt reuse by the next filter pass
         }
         __syncthreads();
         // write back the super-brick's points
-        {
-            const int64_t o0 = (int64_t)(kb0[0] - cd.lo[0]) + (int64_t)(kb0[1] - cd.lo[1]) * cd.s1 +
-                               (NDIM == 3 ? (int64_t)(kb0[2] - cd.lo[2]) * cd.s2 : 0);
 #pragma unroll
-            for (int k = 0; k < S::NACC; ++k) {
-                const int q = tid + k * SBLOCK;
-                const int i0 = q % SB, i1 = (q / SB) % SB, i2 = NDIM == 3 ? q / (SB * SB) : 0;
-                if (inside) {
-                    cd.u[o0 + i0 + (int64_t)i1 * cd.s1 + (NDIM == 3 ? (int64_t)i2 * cd.s2 : 0)] = acc[q];
-                } else {
-                    const int g0 = kb0[0] + i0, g1 = kb0[1] + i1, g2 = kb0[2] + i2;
-                    bool in = g0 >= cd.lo[0] && g0 <= cd.hi[0] && g1 >= cd.lo[1] && g1 <= cd.hi[1];
-                    if (NDIM == 3) in = in && g2 >= cd.lo[2] && g2 <= cd.hi[2];
-                    if (in)
-                        cd.u[(int64_t)(g0 - cd.lo[0]) + (int64_t)(g1 - cd.lo[1]) * cd.s1 +
-                             (NDIM == 3 ? (int64_t)(g2 - cd.lo[2]) * cd.s2 : 0)] = acc[q];
-                }
+        for (int k = 0; k < S::NACC; ++k) {
+            const int q = tid + k * SBLOCK;
+            const int i0 = q % SB, i1 = (q / SB) % SB, i2 = NDIM == 3 ? q / (SB * SB) : 0;
+            if (inside) {
+                cd.u[o0 + i0 + (int64_t)i1 * cd.s1 + (NDIM == 3 ? (int64_t)i2 * cd.s2 : 0)] = acc[q];
+            } else {
+                const int g0 = kb0[0] + i0, g1 = kb0[1] + i1, g2 = kb0[2] + i2;
+                bool in = g0 >= cd.lo[0] && g0 <= cd.hi[0] && g1 >= cd.lo[1] && g1 <= cd.hi[1];
+                if (NDIM == 3) in = in && g2 >= cd.lo[2] && g2 <= cd.hi[2];
+                if (in)
+                    cd.u[(int64_t)(g0 - cd.lo[0]) + (int64_t)(g1 - cd.lo[1]) * cd.s1 +
+                         (NDIM == 3 ? (int64_t)(g2 - cd.lo[2]) * cd.s2 : 0)] = acc[q];
             }
         }
     }

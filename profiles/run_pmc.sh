@@ -1,0 +1,15 @@
+#!/bin/bash
+# Counter passes over a short bench run (one rocprofv3 pass per counter group,
+# --kernel-trace only; no sys/runtime tracing, per the pool rules).
+# Usage: profiles/run_pmc.sh <outdir> <bench args...>
+set -o pipefail
+out=$1; shift
+export TMPDIR=/tmp
+mkdir -p "$out"
+rocprofv3 -L > "$out/counters_available.txt" 2>&1 || true
+i=0
+for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES" \
+           "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAIT_INST_LDS"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -T -d "$out/pass$i" -o pmc -- python3 bench.py "$@" --no-cpu-baseline > "$out/pass$i.log" 2>&1 || { echo "pass $i ($grp) failed rc=$?"; tail -5 "$out/pass$i.log"; }
+done
