@@ -94,7 +94,7 @@ struct DevBuf {
 struct ibtk_le_ctx_s {
     int device = 0;
     hipStream_t stream = nullptr;
-    DevBuf keys_in, vals_in, temp, counts, offsets;
+    DevBuf keys_in, vals_in, temp, counts, offsets, fbuf;
     DevBuf err;  // one int
     bool timing = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -142,7 +142,7 @@ extern "C" int ibtk_le_ctx_destroy(ibtk_le_ctx ctx) {
     if (!ctx) return IBTK_LE_OK;
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
-    for (DevBuf* b : {&ctx->keys_in, &ctx->vals_in, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->err})
+    for (DevBuf* b : {&ctx->keys_in, &ctx->vals_in, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->fbuf, &ctx->err})
         b->release();
     if (ctx->ev0) hipEventDestroy(ctx->ev0);
     if (ctx->ev1) hipEventDestroy(ctx->ev1);
@@ -510,6 +510,9 @@ extern "C" int ibtk_le_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, in
     if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
     p.Qin = Q_dev;
     p.Q_depth = Q_depth;
+    p.nsorted = m->n;
+    if (int rc = ctx->fbuf.ensure(sizeof(double) * (size_t)m->n * (size_t)std::min(nc, MAXC))) return rc;
+    p.sorted_F = ctx->fbuf.as<double>();
     ctx->ev_valid = false;
     for (int first = 0; first < nc; first += MAXC) {
         const int cnt = std::min(MAXC, nc - first);

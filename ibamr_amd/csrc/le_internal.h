@@ -91,6 +91,8 @@ struct Params {
     const int* brick_start;    // nbricks + 1 offsets into the sorted list
     const int* nentries_dev;   // device copy of the list length
     const double* Qin;         // spread: marker values
+    const double* sorted_F;    // spread: Qin gathered in sorted order, [comp][sorted position]
+    int nsorted;               // list length
     double* Qout;              // interp: marker values
     int* err;                  // device error word (0 = fine)
 };
