@@ -108,8 +108,10 @@ struct ibtk_le_markers_s {
     int ndim = 0;
     BinGeom bg{};
     ibtk_le_patch_geom geom{};
-    DevBuf sorted_key, sorted_l, sorted_s, sorted_X, brick_start, indices, xshift;
+    DevBuf sorted_key, sorted_l, sorted_s, sorted_X, plane_start, indices, xshift;
+    DevBuf cand_cnt, cand_off, cand_idx;  // spread candidate lists, built on first use after a bin
     bool has_indices = false, has_xshift = false;
+    bool cand_valid = false;
 };
 
 static int set_device(ibtk_le_ctx ctx) {
@@ -344,7 +346,8 @@ extern "C" int ibtk_le_markers_destroy(ibtk_le_markers m) {
     if (!m) return IBTK_LE_OK;
     hipSetDevice(m->ctx->device);
     hipStreamSynchronize(m->ctx->stream);
-    for (DevBuf* b : {&m->sorted_key, &m->sorted_l, &m->sorted_s, &m->sorted_X, &m->brick_start, &m->indices, &m->xshift})
+    for (DevBuf* b : {&m->sorted_key, &m->sorted_l, &m->sorted_s, &m->sorted_X, &m->plane_start, &m->indices,
+                      &m->xshift, &m->cand_cnt, &m->cand_off, &m->cand_idx})
         b->release();
     delete m;
     return IBTK_LE_OK;
@@ -378,10 +381,13 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     m->geom = *geom;
     m->has_indices = indices_dev != nullptr;
     m->has_xshift = Xshift_dev != nullptr;
+    m->cand_valid = false;
     int rc = 0;
-    if ((rc = m->brick_start.ensure(sizeof(int) * (size_t)(bg.nbricks + 1)))) return rc;
+    const int B = geom->ndim == 3 ? BRICK3 : BRICK2;
+    const int nplanes = bg.nbricks * B;
+    if ((rc = m->plane_start.ensure(sizeof(int) * (size_t)(nplanes + 1)))) return rc;
     if (n == 0) {
-        HIP_TRY(hipMemsetAsync(m->brick_start.p, 0, sizeof(int) * (size_t)(bg.nbricks + 1), s));
+        HIP_TRY(hipMemsetAsync(m->plane_start.p, 0, sizeof(int) * (size_t)(nplanes + 1), s));
         return IBTK_LE_OK;
     }
     if ((rc = m->sorted_key.ensure(sizeof(unsigned) * (size_t)n))) return rc;
@@ -414,7 +420,8 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     tb = ctx->temp.cap;
     HIP_TRY(launch_sort(ctx->temp.p, tb, ctx->keys_in.as<unsigned>(), m->sorted_key.as<unsigned>(),
                         ctx->vals_in.as<int>(), m->sorted_l.as<int>(), n, end_bit, s));
-    HIP_TRY(launch_brick_start(m->sorted_key.as<unsigned>(), n, bg.nbricks, bg.shift, m->brick_start.as<int>(), s));
+    HIP_TRY(launch_brick_start(m->sorted_key.as<unsigned>(), n, nplanes, bg.shift - (geom->ndim == 3 ? 3 : 4),
+                               m->plane_start.as<int>(), s));
     p.sorted_l = m->sorted_l.as<int>();
     HIP_TRY(launch_gather_sorted(geom->ndim, p, n, m->sorted_s.as<int>(), m->sorted_X.as<double>(), s));
     return IBTK_LE_OK;
@@ -451,7 +458,7 @@ static int prepare(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const ibtk_le
     p.sorted_s = m->sorted_s.as<int>();
     p.sorted_X = m->sorted_X.as<double>();
     p.sorted_key = m->sorted_key.as<unsigned>();
-    p.brick_start = m->brick_start.as<int>();
+    p.plane_start = m->plane_start.as<int>();
     p.err = ctx->err.as<int>();
     p.K6 = ib6_K();
     p.h3 = geom->ndim == 3 ? (geom->dx[0] * geom->dx[1]) * geom->dx[2] : geom->dx[0] * geom->dx[1];
@@ -498,6 +505,28 @@ extern "C" int ibtk_le_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, in
     return ibtk_le::interp_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, X_dev, true);
 }
 
+// Super-brick candidate lists (k_cand): count, exclusive scan, write.  Built once
+// per binning, on the first spread after it.
+static int build_candidates(ibtk_le_ctx ctx, ibtk_le_markers m, const Params& p) {
+    if (m->cand_valid) return IBTK_LE_OK;
+    const hipStream_t s = ctx->stream;
+    const int items = m->bg.nbricks / (m->ndim == 3 ? 8 : 4) * cand_classes(m->ndim, m->kernel);
+    int rc = 0;
+    if ((rc = m->cand_cnt.ensure(sizeof(int) * (size_t)(items + 1)))) return rc;
+    if ((rc = m->cand_off.ensure(sizeof(int) * (size_t)(items + 1)))) return rc;
+    if ((rc = m->cand_idx.ensure(sizeof(int) * (size_t)m->n * (m->ndim == 3 ? 8 : 4)))) return rc;
+    HIP_TRY(hipMemsetAsync(m->cand_cnt.p, 0, sizeof(int) * (size_t)(items + 1), s));
+    HIP_TRY(launch_cand(m->ndim, m->kernel, p, false, m->cand_cnt.as<int>(), nullptr, s));
+    size_t tb = 0;
+    HIP_TRY(launch_scan(nullptr, tb, m->cand_cnt.as<int>(), m->cand_off.as<int>(), items + 1, s));
+    if ((rc = ctx->temp.ensure(tb))) return rc;
+    tb = ctx->temp.cap;
+    HIP_TRY(launch_scan(ctx->temp.p, tb, m->cand_cnt.as<int>(), m->cand_off.as<int>(), items + 1, s));
+    HIP_TRY(launch_cand(m->ndim, m->kernel, p, true, m->cand_off.as<int>(), m->cand_idx.as<int>(), s));
+    m->cand_valid = true;
+    return IBTK_LE_OK;
+}
+
 extern "C" int ibtk_le_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                               const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
                               int Q_depth, const double* X_dev) {
@@ -513,6 +542,9 @@ extern "C" int ibtk_le_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, in
     p.nsorted = m->n;
     if (int rc = ctx->fbuf.ensure(sizeof(double) * (size_t)m->n * (size_t)std::min(nc, MAXC))) return rc;
     p.sorted_F = ctx->fbuf.as<double>();
+    if (int rc = build_candidates(ctx, m, p)) return rc;
+    p.cand_off = m->cand_off.as<int>();
+    p.cand_idx = m->cand_idx.as<int>();
     ctx->ev_valid = false;
     for (int first = 0; first < nc; first += MAXC) {
         const int cnt = std::min(MAXC, nc - first);

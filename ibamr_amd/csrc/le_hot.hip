@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 
 #include "le_bricks.h"
@@ -94,8 +95,9 @@ __global__ __launch_bounds__(BLOCK) void k_bin(Params p, int n, unsigned* keys, 
     vals[i] = i;
 }
 
-// brick_start[b] = first sorted position whose bucket >= b, for b in [0, nbricks].
-__global__ __launch_bounds__(BLOCK) void k_brick_start(const unsigned* keys, int n, int nbricks, int shift, int* bs) {
+// bs[b] = first sorted position whose bucket (key >> shift) >= b, for b in [0, nbuckets]
+// (buckets = cell planes of bricks: plane_start).
+__global__ __launch_bounds__(BLOCK) void k_brick_start(const unsigned* keys, int n, int nbricks, int shift, int* bs) {  // nbricks = nbuckets
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     if (i > n) return;
     const int bi = (i < n) ? (int)min(keys[i] >> shift, (unsigned)nbricks) : nbricks + 1;
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(IBLOCK) void k_interp(Params p) {
         const int it = xcd_item(round, G, blockIdx.x);
         if (it >= nitems) continue;
         const int b = it / nc, c = it - (it / nc) * nc;
-        const int beg = p.brick_start[b], end = p.brick_start[b + 1];
+        const int beg = p.plane_start[b * B], end = p.plane_start[(b + 1) * B];
         if (beg == end) continue;
         int bc[3];
         brick_coords<NDIM>(p.bg, b, bc);
@@ -307,7 +309,7 @@ __global__ __launch_bounds__(IBLOCK) void k_interp(Params p) {
 
 // Entries binned "outside" (no stencil point can reach any array): V = 0.
 __global__ __launch_bounds__(BLOCK) void k_interp_outside(Params p, int n) {
-    const int first = p.brick_start[p.bg.nbricks];
+    const int first = p.plane_start[p.bg.nbricks * (p.bg.ndim == 3 ? BRICK3 : BRICK2)];
     for (int e = first + blockIdx.x * BLOCK + threadIdx.x; e < n; e += gridDim.x * BLOCK) {
         const int s = p.sorted_s[e];
         for (int c = 0; c < p.ncomp; ++c) p.Qout[(int64_t)p.Q_depth * s + p.comp[c].qcomp] = 0.0;
@@ -433,23 +435,182 @@ hipError_t launch_interp_t(const Params& p, int n, hipStream_t s, hipEvent_t ev0
 // ---------------------------------------------------------------------------
 // spreading
 // ---------------------------------------------------------------------------
+// Work item: one super-brick (2^NDIM bricks: 16^3 cells in 3-D, 32^2 in 2-D).
+// Its candidates -- the markers whose stencil can reach it -- are grouped into
+// "classes" of CW anchor planes along the last dim.  A class's stencils lie in
+// CW + HI - LO consecutive planes, so classes NPH apart never touch the same
+// grid point: in phase ph the waves of the workgroup take the classes
+// ph, ph + NPH, ... concurrently, phases separated by a barrier.
 template <int NDIM, int K> struct SShape {
     using BT = BrickT<NDIM>;
     static constexpr int B = BT::B, SB = BT::SB, SBV = BT::SBV, GROUP = BT::GROUP;
-    static constexpr int W = KT<K>::W;
-    static constexpr int P = NDIM == 3 ? W * W * W : W * W;  // stencil points
-    static constexpr int NPASS = (P + 63) / 64;              // 64-lane passes per stencil
-    static constexpr int NQ = SBLOCK / 64;                   // waves = quarters of the super-brick
-    static constexpr int QW = SB / NQ;                       // planes (3-D z) / rows (2-D y) per quarter
-    static constexpr int NBR = NDIM == 3 ? 64 : 16;          // neighbourhood bricks (4 per dim)
-    static constexpr int KMAX = 2;                           // entries per thread per filter pass
-    static constexpr int CAP = KMAX * SBLOCK;                // candidates per filter pass
-    static constexpr int CH = W <= 4 ? 128 : 64;             // candidates per prep/process chunk
-    static constexpr int NWD = CH / 64;                      // 64-bit words of a chunk bitmap
-    static constexpr int RWD = NDIM * W + 1;                 // record doubles: 1-D weights, F
-    static constexpr int NACC = SBV / SBLOCK;                // u values per thread
-    static constexpr int LB = NDIM == 3 ? 3 : 4;             // log2(B)
+    static constexpr int W = KT<K>::W, LO = KT<K>::LO, HI = KT<K>::HI;
+    static constexpr int NQ = SBLOCK / 64;                                // waves
+    static constexpr int NBR = NDIM == 3 ? 64 : 16;                       // neighbourhood bricks (4 per dim)
+    static constexpr int KMAX = 4;                                        // entries per thread per list sub-pass
+    static constexpr int CW = 2;                                          // anchor planes per class
+    static constexpr int NCLS = (SB - 1 + HI - LO) / CW + 1;              // classes of a super-brick
+    static constexpr int NPH = 1 + (HI - LO + CW - 1) / CW;               // phases
+    static constexpr int NACC = SBV / SBLOCK;                             // u values per thread
+    static constexpr int LB = NDIM == 3 ? 3 : 4;                          // log2(B)
+    static constexpr int MAXOFF = NDIM == 3 ? (W - 1) * (1 + SB + SB * SB) : (W - 1) * (1 + SB);
+    static constexpr int TRASH = 64 + MAXOFF + 1;                         // per-lane sink of masked points
+    static_assert(HI <= B && -LO <= B, "a stencil must not reach beyond the neighbouring brick");
+    static_assert(NPH * CW >= CW + HI - LO, "classes of one phase must be disjoint");
 };
+
+// The sorted entries that can reach super-brick `sb`: for each of the 4^NDIM
+// bricks around it, the run of its cell planes (along the last dim; entries of a
+// brick are sorted by cell, last dim slowest) whose anchors can reach the
+// super-brick, the runs ranked by brick id (= canonical order).  Returns the
+// number of entries; npre[] are the runs' prefix offsets, sst[] their starts,
+// soff[] the packed 2-bit (offset + 1) of their bricks.
+template <int NDIM, int K>
+__device__ int neighbourhood(const Params& p, int sb, int* nid, int* nst, int* nln, int* sst, int* soff, int* npre) {
+    using S = SShape<NDIM, K>;
+    constexpr int B = S::B, NBR = S::NBR, HI = S::HI, LO = S::LO;
+    const int tid = threadIdx.x;
+    int bc0[3];
+    brick_coords<NDIM>(p.bg, sb * S::GROUP, bc0);
+    __syncthreads();  // the tables are free
+    if (tid < NBR) {
+        const int o[3] = {tid & 3, (tid >> 2) & 3, NDIM == 3 ? (tid >> 4) : 0};
+        int q[3] = {bc0[0] + o[0] - 1, bc0[1] + o[1] - 1, NDIM == 3 ? bc0[2] + o[2] - 1 : 0};
+        bool valid = true;
+        for (int d = 0; d < NDIM; ++d) valid = valid && q[d] >= 0 && q[d] < p.bg.nb[d];
+        const int ol = o[NDIM - 1];
+        const int plo = ol == 0 ? B - HI : 0;       // planes whose anchors reach the super-brick
+        const int phi = ol == 3 ? -LO - 1 : B - 1;  // (inclusive)
+        int id = INT_MAX, st = 0, ln = 0;
+        if (valid) {
+            id = brick_id<NDIM>(p.bg, q);
+            st = p.plane_start[id * B + plo];
+            ln = p.plane_start[id * B + phi + 1] - st;
+        }
+        nid[tid] = id;
+        nst[tid] = st;
+        nln[tid] = ln;
+    }
+    __syncthreads();
+    if (tid < NBR) {
+        const int my = nid[tid];
+        int rank = 0;
+        for (int k = 0; k < NBR; ++k) {
+            const int o = nid[k];
+            rank += (o < my) || (o == my && k < tid);
+        }
+        sst[rank] = nst[tid];
+        soff[rank] = tid;
+        npre[rank + 1] = nln[tid];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        npre[0] = 0;
+        for (int k = 0; k < NBR; ++k) npre[k + 1] += npre[k];
+    }
+    __syncthreads();
+    return npre[NBR];
+}
+
+// entry e of the neighbourhood -> sorted index (and the packed brick offset)
+template <int NBR> __device__ __forceinline__ int entry_of(int e, const int* npre, const int* sst, const int* soff, int& ro) {
+    int lo = 0, hi = NBR - 1;  // largest j with npre[j] <= e
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (npre[mid] <= e) lo = mid;
+        else hi = mid - 1;
+    }
+    ro = soff[lo];
+    return sst[lo] + (e - npre[lo]);
+}
+
+// class of the entry with this key (in the brick at packed offset ro) for the
+// super-brick, or -1 if its stencil cannot reach the super-brick
+template <int NDIM, int K> __device__ __forceinline__ int cand_class(unsigned key, int ro) {
+    using S = SShape<NDIM, K>;
+    bool cand = true;
+    int rl = 0;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) {
+        const int rel = (((ro >> (2 * d)) & 3) - 1) * S::B + (int)((key >> (S::LB * d)) & (S::B - 1));
+        cand = cand && rel >= -S::HI && rel <= S::SB - 1 - S::LO;
+        rl = rel;
+    }
+    return cand ? (rl + S::HI) / S::CW : -1;
+}
+
+// Candidate lists, built once per binning: for super-brick sb and class k, the
+// entries of that class whose stencil can reach sb, in canonical order, at
+// [off[sb*NCLS + k], off[sb*NCLS + k + 1]).  Pass 1 counts, an exclusive scan
+// gives the offsets, pass 2 writes (ordered block compaction per class).
+template <int NDIM, int K, bool WRITE>
+__global__ __launch_bounds__(SBLOCK) void k_cand(Params p, int* counts_or_offs, int* out) {
+    using S = SShape<NDIM, K>;
+    constexpr int NBR = S::NBR, KMAX = S::KMAX, NQ = S::NQ, NCLS = S::NCLS;
+    __shared__ int nid[NBR], nst[NBR], nln[NBR], sst[NBR], soff[NBR], npre[NBR + 1];
+    __shared__ int cnt[KMAX * NQ * NCLS];
+    __shared__ int cbase[NCLS];
+    const int nitems = p.bg.nbricks / S::GROUP;
+    const int sb = xcd_item(0, gridDim.x, blockIdx.x);
+    if (sb >= nitems) return;
+    const int total = neighbourhood<NDIM, K>(p, sb, nid, nst, nln, sst, soff, npre);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (!WRITE) {
+        if (tid < NCLS) cbase[tid] = 0;
+        __syncthreads();
+        for (int e = tid; e < total; e += SBLOCK) {
+            int ro;
+            const int idx = entry_of<NBR>(e, npre, sst, soff, ro);
+            const int k = cand_class<NDIM, K>(p.sorted_key[idx], ro);
+            if (k >= 0) atomicAdd(&cbase[k], 1);
+        }
+        __syncthreads();
+        if (tid < NCLS) counts_or_offs[sb * NCLS + tid] = cbase[tid];
+        return;
+    }
+    if (tid < NCLS) cbase[tid] = counts_or_offs[sb * NCLS + tid];
+    for (int e0 = 0; e0 < total; e0 += KMAX * SBLOCK) {
+        int eidx[KMAX], cls[KMAX];
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            const int e = e0 + k * SBLOCK + tid;
+            eidx[k] = -1;
+            cls[k] = -1;
+            int ro = 0;
+            if (e < total) eidx[k] = entry_of<NBR>(e, npre, sst, soff, ro);
+            if (eidx[k] >= 0) cls[k] = cand_class<NDIM, K>(p.sorted_key[eidx[k]], ro);
+        }
+        // per (sub-pass slot, wave, class) counts; entry order is (k, wave, lane)
+        unsigned long long mine[KMAX];
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            mine[k] = 0ull;
+            for (int c = 0; c < NCLS; ++c) {
+                const unsigned long long b = __ballot(cls[k] == c);
+                if (cls[k] == c) mine[k] = b;
+                if (lane == 0) cnt[(k * NQ + wave) * NCLS + c] = __popcll(b);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            const int c = cls[k];
+            if (c >= 0) {
+                int pos = cbase[c];
+                for (int j = 0; j < k * NQ + wave; ++j) pos += cnt[j * NCLS + c];
+                pos += __popcll(mine[k] & ((1ull << lane) - 1ull));
+                out[pos] = eidx[k];
+            }
+        }
+        __syncthreads();
+        if (tid < NCLS) {
+            int t = 0;
+            for (int j = 0; j < KMAX * NQ; ++j) t += cnt[j * NCLS + tid];
+            cbase[tid] += t;
+        }
+        __syncthreads();
+    }
+}
 
 // sorted_F[c * n + e] = Q(qcomp_c, s(e)): the spread values in sorted order, so
 // the spread kernel's loads of them are contiguous and not behind the s load.
@@ -461,324 +622,179 @@ __global__ __launch_bounds__(BLOCK) void k_gather_F(Params p, int n, double* out
         out[(int64_t)c * n + e] = p.Qin[(int64_t)p.Q_depth * s + p.comp[c].qcomp];
 }
 
-// One workgroup item = one super-brick (16^3 cells in 3-D, 32^2 in 2-D), all
-// components in turn.  Per component the super-brick's u_old goes to LDS; the
-// entries of the surrounding 4^NDIM bricks are walked in canonical (sorted)
-// order and those whose stencil can reach the super-brick kept (parallel
-// filter + ordered compaction, done once for all components when they fit one
-// pass); chunks of candidates get their stencils computed one per thread into
-// LDS records, with a bitmap per quarter (a quarter = QW planes along the last
-// dim, owned by one wave) of the candidates that touch it.  Each wave then walks
-// its bitmap in ascending order -- the scalar unit finds the next set bit, so a
-// wave never visits a candidate that misses its quarter -- adding the candidate's
-// stencil points (lane = stencil point) with ds_add_f64.  Every point is owned by
-// one wave and receives its contributions in canonical order: bitwise the
-// oracle's sequential sum over the sorted list.
+// Spread of one super-brick, component after component: u_old goes to LDS; in
+// each phase every wave takes its classes' candidates 64 at a time, one per
+// lane: the lane computes the candidate's 1-D weights in registers and adds its
+// W^NDIM stencil points to LDS (ds_add_f64, one instruction per stencil point
+// for the 64 candidates; points outside the super-brick or clipped by the
+// ghost box go to a per-lane sink).  A grid point receives its contributions
+// in a fixed order -- phase, class list order, stencil point, lane -- so the
+// result is deterministic run to run (and equal to the sequential Fortran sum
+// up to reassociation).
 template <int NDIM, int K>
 __global__ __launch_bounds__(SBLOCK) void k_spread(Params p) {
     using T = KT<K>;
     using S = SShape<NDIM, K>;
     constexpr int W = T::W, FAM = T::FAM, LO = T::LO, HI = T::HI;
-    constexpr int B = S::B, SB = S::SB, SBV = S::SBV, NPASS = S::NPASS, NBR = S::NBR, CH = S::CH, NQ = S::NQ;
-    constexpr int QW = S::QW, KMAX = S::KMAX, CAP = S::CAP, NWD = S::NWD, RWD = S::RWD, LB = S::LB;
-    constexpr int QD = NDIM - 1;  // the quartered dim
-    __shared__ double acc[SBV];
-    __shared__ double rw[CH * RWD];
-    __shared__ int rbase[CH];
-    __shared__ int rz[CH];
-    __shared__ unsigned long long rm[CH * NPASS];
-    __shared__ unsigned long long qbits[NQ * NWD];
-    __shared__ int cidx[CAP];
-    __shared__ int nid[NBR], nst[NBR], nln[NBR], sst[NBR], soff[NBR], npre[NBR + 1], cnt[KMAX * NQ];
+    constexpr int B = S::B, SB = S::SB, SBV = S::SBV, NQ = S::NQ, NCLS = S::NCLS, NPH = S::NPH, CW = S::CW;
+    constexpr int QD = NDIM - 1;
+    __shared__ double acc[SBV + S::TRASH];
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // this lane's stencil point in each pass: acc offset, weight indices, plane
-    int loff[NPASS], wi[NPASS][3], lq[NPASS];
-#pragma unroll
-    for (int ps = 0; ps < NPASS; ++ps) {
-        const int q = ps * 64 + lane;
-        const int i0 = q % W, i1 = (q / W) % W, i2 = NDIM == 3 ? q / (W * W) : 0;
-        loff[ps] = i0 + SB * (i1 + (NDIM == 3 ? SB * i2 : 0));
-        wi[ps][0] = i0;
-        wi[ps][1] = W + i1;
-        wi[ps][2] = 2 * W + i2;
-        lq[ps] = NDIM == 3 ? i2 : i1;
-    }
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nc = p.ncomp;
     const int n = p.nsorted;
     const int nitems = p.bg.nbricks / S::GROUP;
     const int G = gridDim.x;
+    const int sink = SBV + lane;  // this lane's sink slot
     for (int round = 0; round < nitems; round += G) {
         const int sb = xcd_item(round, G, blockIdx.x);
         if (sb >= nitems) continue;
+        const int* off = p.cand_off + (int64_t)sb * NCLS;
+        if (off[NCLS] == off[0]) continue;  // no candidates: u unchanged
         int bc0[3];
         brick_coords<NDIM>(p.bg, sb * S::GROUP, bc0);
         int kb0[3] = {0, 0, 0};
 #pragma unroll
         for (int d = 0; d < NDIM; ++d) kb0[d] = p.bg.kmin[d] + bc0[d] * B;
 
-        __syncthreads();  // the previous item is done with the neighbourhood tables
-        if (tid < NBR) {
-            const int o[3] = {tid & 3, (tid >> 2) & 3, NDIM == 3 ? (tid >> 4) : 1};
-            int q[3] = {bc0[0] + o[0] - 1, bc0[1] + o[1] - 1, NDIM == 3 ? bc0[2] + o[2] - 1 : 0};
-            bool valid = true;
-            for (int d = 0; d < NDIM; ++d) valid = valid && q[d] >= 0 && q[d] < p.bg.nb[d];
-            int id = INT_MAX, st = 0, ln = 0;
-            if (valid) {
-                id = brick_id<NDIM>(p.bg, q);
-                st = p.brick_start[id];
-                ln = p.brick_start[id + 1] - st;
+        // the first 64 candidates of this wave's first class in each phase:
+        // indices and positions loaded once, kept across the components
+        int idx0[NPH];
+        double X0[NPH][NDIM];
+#pragma unroll
+        for (int ph = 0; ph < NPH; ++ph) {
+            const int k = ph + NPH * wave;
+            idx0[ph] = -1;
+            if (k < NCLS) {
+                const int e = off[k] + lane;
+                if (e < off[k + 1]) idx0[ph] = p.cand_idx[e];
             }
-            nid[tid] = id;
-            nst[tid] = st;
-            nln[tid] = ln;
         }
-        __syncthreads();
-        if (tid < NBR) {
-            // canonical order = increasing brick id: rank sort of the neighbourhood
-            const int my = nid[tid];
-            int rank = 0;
-            for (int k = 0; k < NBR; ++k) {
-                const int o = nid[k];
-                rank += (o < my) || (o == my && k < tid);
-            }
-            sst[rank] = nst[tid];
-            soff[rank] = tid;  // packed 2-bit offsets (+1) of the brick
-            npre[rank + 1] = nln[tid];
-        }
-        __syncthreads();
-        if (tid == 0) {
-            npre[0] = 0;
-            for (int k = 0; k < NBR; ++k) npre[k + 1] += npre[k];
-        }
-        __syncthreads();
-        const int total = npre[NBR];
-        if (total == 0) continue;
-        const int npasses = (total + CAP - 1) / CAP;
-        int ncand = 0;
+#pragma unroll
+        for (int ph = 0; ph < NPH; ++ph)
+#pragma unroll
+            for (int d = 0; d < NDIM; ++d) X0[ph][d] = idx0[ph] >= 0 ? p.sorted_X[(int64_t)NDIM * idx0[ph] + d] : 0.0;
 
         for (int c = 0; c < nc; ++c) {
             const CompDesc& cd = p.comp[c];
             bool inside = true;
 #pragma unroll
             for (int d = 0; d < NDIM; ++d) inside = inside && kb0[d] >= cd.lo[d] && kb0[d] + SB - 1 <= cd.hi[d];
-            // u_old of the super-brick's points
             const int64_t o0 = (int64_t)(kb0[0] - cd.lo[0]) + (int64_t)(kb0[1] - cd.lo[1]) * cd.s1 +
                                (NDIM == 3 ? (int64_t)(kb0[2] - cd.lo[2]) * cd.s2 : 0);
-            {
-                double v[S::NACC];
+            double v[S::NACC];
 #pragma unroll
-                for (int k = 0; k < S::NACC; ++k) {
-                    const int q = tid + k * SBLOCK;
-                    const int i0 = q % SB, i1 = (q / SB) % SB, i2 = NDIM == 3 ? q / (SB * SB) : 0;
-                    v[k] = 0.0;
-                    if (inside) {
-                        v[k] = cd.u[o0 + i0 + (int64_t)i1 * cd.s1 + (NDIM == 3 ? (int64_t)i2 * cd.s2 : 0)];
-                    } else {
-                        const int g0 = kb0[0] + i0, g1 = kb0[1] + i1, g2 = kb0[2] + i2;
-                        bool in = g0 >= cd.lo[0] && g0 <= cd.hi[0] && g1 >= cd.lo[1] && g1 <= cd.hi[1];
-                        if (NDIM == 3) in = in && g2 >= cd.lo[2] && g2 <= cd.hi[2];
-                        if (in)
-                            v[k] = cd.u[(int64_t)(g0 - cd.lo[0]) + (int64_t)(g1 - cd.lo[1]) * cd.s1 +
-                                        (NDIM == 3 ? (int64_t)(g2 - cd.lo[2]) * cd.s2 : 0)];
-                    }
+            for (int k = 0; k < S::NACC; ++k) {
+                const int q = tid + k * SBLOCK;
+                const int i0 = q % SB, i1 = (q / SB) % SB, i2 = NDIM == 3 ? q / (SB * SB) : 0;
+                v[k] = 0.0;
+                if (inside) {
+                    v[k] = cd.u[o0 + i0 + (int64_t)i1 * cd.s1 + (NDIM == 3 ? (int64_t)i2 * cd.s2 : 0)];
+                } else {
+                    const int g0 = kb0[0] + i0, g1 = kb0[1] + i1, g2 = kb0[2] + i2;
+                    bool in = g0 >= cd.lo[0] && g0 <= cd.hi[0] && g1 >= cd.lo[1] && g1 <= cd.hi[1];
+                    if (NDIM == 3) in = in && g2 >= cd.lo[2] && g2 <= cd.hi[2];
+                    if (in)
+                        v[k] = cd.u[(int64_t)(g0 - cd.lo[0]) + (int64_t)(g1 - cd.lo[1]) * cd.s1 +
+                                    (NDIM == 3 ? (int64_t)(g2 - cd.lo[2]) * cd.s2 : 0)];
                 }
-#pragma unroll
-                for (int k = 0; k < S::NACC; ++k) acc[tid + k * SBLOCK] = v[k];
             }
+            double F0[NPH];
+#pragma unroll
+            for (int ph = 0; ph < NPH; ++ph) F0[ph] = idx0[ph] >= 0 ? p.sorted_F[(int64_t)c * n + idx0[ph]] : 0.0;
+            __syncthreads();  // the previous component's write-back has read acc
+#pragma unroll
+            for (int k = 0; k < S::NACC; ++k) acc[tid + k * SBLOCK] = v[k];
+            __syncthreads();
 
-            for (int pass = 0; pass < npasses; ++pass) {
-                if (npasses > 1 || c == 0) {
-                    // ---- filter up to CAP entries: every key load in flight at once
-                    __syncthreads();  // cidx / cnt are free
-                    unsigned key[KMAX];
-                    int eidx[KMAX], ro[KMAX];
 #pragma unroll
-                    for (int k = 0; k < KMAX; ++k) {
-                        const int e = pass * CAP + k * SBLOCK + tid;
-                        key[k] = 0u;
-                        eidx[k] = -1;
-                        ro[k] = 0;
-                        if (e < total) {
-                            int lo = 0, hi = NBR - 1;  // largest j with npre[j] <= e
-                            while (lo < hi) {
-                                const int mid = (lo + hi + 1) >> 1;
-                                if (npre[mid] <= e) lo = mid;
-                                else hi = mid - 1;
-                            }
-                            eidx[k] = sst[lo] + (e - npre[lo]);
-                            ro[k] = soff[lo];
-                            key[k] = p.sorted_key[eidx[k]];
+            for (int ph = 0; ph < NPH; ++ph) {
+                for (int k = ph + NPH * wave; k < NCLS; k += NPH * NQ) {
+                    const int first = k == ph + NPH * wave;
+                    for (int e0 = off[k]; e0 < off[k + 1]; e0 += 64) {
+                        // ---- this lane's candidate
+                        int idx;
+                        double Xs[NDIM], F;
+                        if (first && e0 == off[k]) {
+                            idx = idx0[ph];
+#pragma unroll
+                            for (int d = 0; d < NDIM; ++d) Xs[d] = X0[ph][d];
+                            F = F0[ph];
+                        } else {
+                            const int e = e0 + lane;
+                            idx = e < off[k + 1] ? p.cand_idx[e] : -1;
+#pragma unroll
+                            for (int d = 0; d < NDIM; ++d) Xs[d] = idx >= 0 ? p.sorted_X[(int64_t)NDIM * idx + d] : 0.0;
+                            F = idx >= 0 ? p.sorted_F[(int64_t)c * n + idx] : 0.0;
                         }
-                    }
-                    unsigned long long bal[KMAX];
-#pragma unroll
-                    for (int k = 0; k < KMAX; ++k) {
-                        bool cand = eidx[k] >= 0;
-                        const unsigned loc = key[k];
+                        const int s = (FAM == 2 && idx >= 0) ? p.sorted_s[idx] : 0;
+                        St<W> st[NDIM];
+                        marker_stencils_x<NDIM, K>(p, cd, Xs, s, st);
+                        // valid stencil indices per dim: inside the clip range and the super-brick
+                        unsigned vm[3] = {0u, 0u, NDIM == 3 ? 0u : 1u};
+                        double w[NDIM][W];
+                        int base = 0, mul = 1;
 #pragma unroll
                         for (int d = 0; d < NDIM; ++d) {
-                            // key cell relative to the super-brick's first cell
-                            const int rel = (((ro[k] >> (2 * d)) & 3) - 1) * B + (int)((loc >> (LB * d)) & (B - 1));
-                            cand = cand && rel >= -HI && rel <= SB - 1 - LO;
-                        }
-                        bal[k] = __ballot(cand);
-                        if (!cand) eidx[k] = -1;
-                        if (lane == 0) cnt[k * NQ + wave] = __popcll(bal[k]);
-                    }
-                    __syncthreads();
-                    // ordered compaction: entry order is (k, wave, lane)
-                    ncand = 0;
-                    for (int k = 0; k < KMAX * NQ; ++k) ncand += cnt[k];
 #pragma unroll
-                    for (int k = 0; k < KMAX; ++k) {
-                        if (eidx[k] >= 0) {
-                            int pos = 0;
-                            for (int j = 0; j < k * NQ + wave; ++j) pos += cnt[j];
-                            pos += __popcll(bal[k] & ((1ull << lane) - 1ull));
-                            cidx[pos] = eidx[k];
-                        }
-                    }
-                }
-
-                for (int cb0 = 0; cb0 < ncand; cb0 += CH) {
-                    __syncthreads();  // cidx / acc written, previous chunk consumed
-                    const int nch = min(CH, ncand - cb0);
-                    if (tid < CH) {
-                        // ---- prep: this candidate's stencil in component c's frame
-                        unsigned qm = 0u;
-                        if (tid < nch) {
-                            const int idx = cidx[cb0 + tid];
-                            double Xs[NDIM];
-#pragma unroll
-                            for (int d = 0; d < NDIM; ++d) Xs[d] = p.sorted_X[(int64_t)NDIM * idx + d];
-                            const double F = p.sorted_F[(int64_t)c * n + idx];
-                            const int s = FAM == 2 ? p.sorted_s[idx] : 0;
-                            St<W> st[NDIM];
-                            marker_stencils_x<NDIM, K>(p, cd, Xs, s, st);
-                            double* r = rw + tid * RWD;
-                            unsigned vm[3] = {0u, 0u, NDIM == 3 ? 0u : 1u};  // valid stencil indices per dim
-                            int cbv = 0, mul = 1;
-#pragma unroll
-                            for (int d = 0; d < NDIM; ++d) {
-                                // binning invariant: the stencil lies in [key + LO, key + HI]
-                                const int kc = key_anchor<K>((Xs[d] - p.bg.xlo[d]) / p.bg.dx[d]) + p.bg.ilower[d];
-                                if (st[d].ist <= st[d].isp &&
-                                    (st[d].icl + st[d].ist < kc + LO || st[d].icl + st[d].isp > kc + HI))
-                                    atomicOr(p.err, 2);
-#pragma unroll
-                                for (int i = 0; i < W; ++i) {
-                                    const int lc = st[d].icl + i - kb0[d];
-                                    if (i >= st[d].ist && i <= st[d].isp && lc >= 0 && lc < SB) vm[d] |= 1u << i;
-                                    // closed form: wz = w2/(dx0*dx1*dx2) (f.m4:1486); 2-D wy = w1/(dx0*dx1)
-                                    r[d * W + i] = (FAM == 0 && d == NDIM - 1) ? st[d].w[i] / p.h3 : st[d].w[i];
-                                }
-                                cbv += (st[d].icl - kb0[d]) * mul;
-                                mul *= SB;
+                            for (int i = 0; i < W; ++i) {
+                                const int lc = st[d].icl + i - kb0[d];
+                                if (idx >= 0 && i >= st[d].ist && i <= st[d].isp && lc >= 0 && lc < SB) vm[d] |= 1u << i;
+                                // closed form: wz = w2/(dx0*dx1*dx2) (f.m4:1486); 2-D wy = w1/(dx0*dx1)
+                                w[d][i] = (FAM == 0 && d == NDIM - 1) ? st[d].w[i] / p.h3 : st[d].w[i];
                             }
-                            r[NDIM * W] = F;
-                            rbase[tid] = cbv;
-                            const int zrel = st[QD].icl - kb0[QD];
-                            rz[tid] = zrel;
-                            // lane masks of the valid stencil points, pass by pass
-                            unsigned long long m[NPASS];
+                            base += (st[d].icl - kb0[d]) * mul;
+                            mul *= SB;
+                        }
+                        // class invariant: the stencil's planes lie in the class footprint
+                        if (idx >= 0 && st[QD].ist <= st[QD].isp) {
+                            const int z0 = st[QD].icl + st[QD].ist - kb0[QD], z1 = st[QD].icl + st[QD].isp - kb0[QD];
+                            if (z0 < k * CW - HI + LO || z1 > k * CW + CW - 1) atomicOr(p.err, 2);
+                        }
+                        // ---- add the W^NDIM points (lane = candidate)
+                        if constexpr (NDIM == 3) {
 #pragma unroll
-                            for (int ps = 0; ps < NPASS; ++ps) m[ps] = 0ull;
-                            const int n2 = NDIM == 3 ? W : 1;
-                            for (int i2 = 0; i2 < n2; ++i2) {
-                                if (!((vm[2] >> i2) & 1u)) continue;
+                            for (int i2 = 0; i2 < W; ++i2) {
+#pragma unroll
                                 for (int i1 = 0; i1 < W; ++i1) {
-                                    if (!((vm[1] >> i1) & 1u)) continue;
-                                    const int q0 = W * i1 + W * W * i2;
-                                    const unsigned long long row = (unsigned long long)vm[0];
+                                    const bool v12 = ((vm[1] >> i1) & (vm[2] >> i2) & 1u) != 0u;
+                                    double w12 = 0.0;
+                                    if constexpr (FAM == 0) w12 = w[1][i1] * w[2][i2];  // f.m4:1485-1492
 #pragma unroll
-                                    for (int ps = 0; ps < NPASS; ++ps) {
-                                        const int sh = q0 - 64 * ps;
-                                        if (sh >= 0 && sh < 64) m[ps] |= row << sh;
-                                        else if (sh < 0 && sh > -W) m[ps] |= row >> (-sh);
-                                    }
-                                }
-                            }
-                            unsigned long long any = 0ull;
-#pragma unroll
-                            for (int ps = 0; ps < NPASS; ++ps) {
-                                rm[tid * NPASS + ps] = m[ps];
-                                any |= m[ps];
-                            }
-                            if (any) {
-#pragma unroll
-                                for (int i = 0; i < W; ++i)
-                                    if ((vm[QD] >> i) & 1u) qm |= 1u << ((zrel + i) / QW);
-                            }
-                        }
-#pragma unroll
-                        for (int q = 0; q < NQ; ++q) {
-                            const unsigned long long b = __ballot((qm >> q) & 1u);
-                            if (lane == 0) qbits[q * NWD + wave] = b;
-                        }
-                    }
-                    __syncthreads();
-                    // ---- wave `wave` adds, in canonical order, the points of its
-                    // quarter [qlo, qlo + QW) of the candidates whose bit is set
-                    const int qlo = wave * QW;
-                    for (int wd = 0; wd < NWD; ++wd) {
-                        unsigned long long bits = qbits[wave * NWD + wd];
-                        bits = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(bits >> 32)) << 32) |
-                               (unsigned)__builtin_amdgcn_readfirstlane((unsigned)bits);
-                        while (bits) {
-                            // two candidates per trip: both records are read before either add
-                            const int ca = wd * 64 + __builtin_ctzll(bits);
-                            bits &= bits - 1ull;
-                            const bool two = bits != 0ull;
-                            const int cb = two ? wd * 64 + __builtin_ctzll(bits) : ca;
-                            if (two) bits &= bits - 1ull;
-                            double contrib[2][NPASS];
-                            bool on[2][NPASS];
-                            int addr[2][NPASS];
-#pragma unroll
-                            for (int h = 0; h < 2; ++h) {
-                                const int ci = h ? cb : ca;
-                                const double* r = rw + ci * RWD;
-                                const double F = r[NDIM * W];
-                                const int base = rbase[ci], zrel = rz[ci];
-#pragma unroll
-                                for (int ps = 0; ps < NPASS; ++ps) {
-                                    const unsigned long long m = rm[ci * NPASS + ps];
-                                    on[h][ps] = ((m >> lane) & 1ull) && (unsigned)(zrel + lq[ps] - qlo) < (unsigned)QW;
-                                    addr[h][ps] = base + loff[ps];
-                                    double cv;
-                                    if constexpr (FAM == 3) {
-                                        cv = F / p.h3;  // f.m4:170-171
-                                    } else if constexpr (FAM == 0) {
-                                        double wt;
-                                        if constexpr (NDIM == 3)
-                                            wt = r[wi[ps][0]] * (r[wi[ps][1]] * r[wi[ps][2]]);  // f.m4:1485-1492
-                                        else
-                                            wt = r[wi[ps][0]] * r[wi[ps][1]];
-                                        cv = wt * F;  // f.m4:1512-1513
-                                    } else {
-                                        if constexpr (NDIM == 3)
-                                            cv = r[wi[ps][0]] * r[wi[ps][1]] * r[wi[ps][2]] * F / p.h3;
-                                        else
-                                            cv = r[wi[ps][0]] * r[wi[ps][1]] * F / p.h3;  // f.m4:668-672
-                                    }
-                                    contrib[h][ps] = cv;
-                                }
-                            }
-#pragma unroll
-                            for (int h = 0; h < 2; ++h) {
-                                if (h == 1 && !two) break;
-#pragma unroll
-                                for (int ps = 0; ps < NPASS; ++ps)
-                                    if (on[h][ps])
-                                        __hip_atomic_fetch_add(&acc[addr[h][ps]], contrib[h][ps], __ATOMIC_RELAXED,
+                                    for (int i0 = 0; i0 < W; ++i0) {
+                                        const bool on = v12 && ((vm[0] >> i0) & 1u);
+                                        double cv;
+                                        if constexpr (FAM == 3) cv = F / p.h3;  // f.m4:170-171
+                                        else if constexpr (FAM == 0) cv = (w[0][i0] * w12) * F;  // f.m4:1512-1513
+                                        else cv = w[0][i0] * w[1][i1] * w[2][i2] * F / p.h3;
+                                        const int a = on ? base : sink;
+                                        __hip_atomic_fetch_add(&acc[a + i0 + SB * (i1 + SB * i2)], cv, __ATOMIC_RELAXED,
                                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    }
+                                }
+                            }
+                        } else {
+#pragma unroll
+                            for (int i1 = 0; i1 < W; ++i1) {
+                                const bool v1 = ((vm[1] >> i1) & 1u) != 0u;
+#pragma unroll
+                                for (int i0 = 0; i0 < W; ++i0) {
+                                    const bool on = v1 && ((vm[0] >> i0) & 1u);
+                                    double cv;
+                                    if constexpr (FAM == 3) cv = F / p.h3;
+                                    else if constexpr (FAM == 0) cv = (w[0][i0] * w[1][i1]) * F;
+                                    else cv = w[0][i0] * w[1][i1] * F / p.h3;  // f.m4:668-672
+                                    const int a = on ? base : sink;
+                                    __hip_atomic_fetch_add(&acc[a + i0 + SB * i1], cv, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                                }
                             }
                         }
                     }
                 }
+                __syncthreads();  // phase boundary
             }
-            __syncthreads();
             // write back the super-brick's points
 #pragma unroll
             for (int k = 0; k < S::NACC; ++k) {
@@ -798,6 +814,19 @@ __global__ __launch_bounds__(SBLOCK) void k_spread(Params p) {
         }
     }
 }
+
+template <int NDIM, int K>
+hipError_t launch_cand_t(const Params& p, bool write, int* counts_or_offs, int* out, hipStream_t s) {
+    using S = SShape<NDIM, K>;
+    const int items = p.bg.nbricks / S::GROUP;
+    if (write)
+        hipLaunchKernelGGL((k_cand<NDIM, K, true>), dim3(items), dim3(SBLOCK), 0, s, p, counts_or_offs, out);
+    else
+        hipLaunchKernelGGL((k_cand<NDIM, K, false>), dim3(items), dim3(SBLOCK), 0, s, p, counts_or_offs, out);
+    return hipGetLastError();
+}
+
+template <int NDIM, int K> int cand_classes_t() { return SShape<NDIM, K>::NCLS; }
 
 template <int NDIM, int K>
 hipError_t launch_spread_t(const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
@@ -832,10 +861,14 @@ hipError_t launch_spread_t(const Params& p, hipStream_t s, hipEvent_t ev0, hipEv
 using BinFn = hipError_t (*)(const Params&, int, unsigned*, int*, hipStream_t);
 using InterpFn = hipError_t (*)(const Params&, int, hipStream_t, hipEvent_t, hipEvent_t);
 using SpreadFn = hipError_t (*)(const Params&, hipStream_t, hipEvent_t, hipEvent_t);
+using CandFn = hipError_t (*)(const Params&, bool, int*, int*, hipStream_t);
+using ClsFn = int (*)();
 
 template <int NDIM> static BinFn pick_bin(int k) { IBTK_LE_DISPATCH(NDIM, k, launch_bin_t) }
 template <int NDIM> static InterpFn pick_interp(int k) { IBTK_LE_DISPATCH(NDIM, k, launch_interp_t) }
 template <int NDIM> static SpreadFn pick_spread(int k) { IBTK_LE_DISPATCH(NDIM, k, launch_spread_t) }
+template <int NDIM> static CandFn pick_cand(int k) { IBTK_LE_DISPATCH(NDIM, k, launch_cand_t) }
+template <int NDIM> static ClsFn pick_cls(int k) { IBTK_LE_DISPATCH(NDIM, k, cand_classes_t) }
 
 hipError_t launch_bin(int ndim, int kernel, const Params& p, int n, unsigned* keys, int* vals, hipStream_t s) {
     BinFn f = ndim == 3 ? pick_bin<3>(kernel) : pick_bin<2>(kernel);
@@ -860,6 +893,14 @@ hipError_t launch_interp(int ndim, int kernel, const Params& p, int n, hipStream
                          hipEvent_t ev1) {
     InterpFn f = ndim == 3 ? pick_interp<3>(kernel) : pick_interp<2>(kernel);
     return f ? f(p, n, s, ev0, ev1) : hipErrorInvalidValue;
+}
+hipError_t launch_cand(int ndim, int kernel, const Params& p, bool write, int* counts_or_offs, int* out, hipStream_t s) {
+    CandFn f = ndim == 3 ? pick_cand<3>(kernel) : pick_cand<2>(kernel);
+    return f ? f(p, write, counts_or_offs, out, s) : hipErrorInvalidValue;
+}
+int cand_classes(int ndim, int kernel) {
+    ClsFn f = ndim == 3 ? pick_cls<3>(kernel) : pick_cls<2>(kernel);
+    return f ? f() : 0;
 }
 hipError_t launch_spread(int ndim, int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     SpreadFn f = ndim == 3 ? pick_spread<3>(kernel) : pick_spread<2>(kernel);

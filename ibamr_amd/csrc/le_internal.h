@@ -88,13 +88,18 @@ struct Params {
     const int* sorted_s;       // sorted position -> marker index
     const double* sorted_X;    // sorted position -> X(s) + Xshift(l) [NDIM]
     const unsigned* sorted_key;
-    const int* brick_start;    // nbricks + 1 offsets into the sorted list
+    const int* plane_start;    // nbricks*B + 1 offsets into the sorted list: bucket = key >> (shift - log2 B)
+                               // (brick b's entries are [plane_start[b*B], plane_start[(b+1)*B]))
+    const int* cand_off;       // spread: (super-brick, class) candidate lists: offsets, items*NCLS + 1
+    const int* cand_idx;       // spread: candidate sorted positions, canonical order per super-brick
     const int* nentries_dev;   // device copy of the list length
     const double* Qin;         // spread: marker values
     const double* sorted_F;    // spread: Qin gathered in sorted order, [comp][sorted position]
     int nsorted;               // list length
     double* Qout;              // interp: marker values
     int* err;                  // device error word (0 = fine)
+    unsigned long long* stamps;  // diagnostic phase clocks (nullptr: off)
+    int dbg;                     // diagnostic switches (0: off)
 };
 
 // Host-side launchers (le_kernels.hip).
@@ -104,6 +109,8 @@ hipError_t launch_gather_sorted(int ndim, const Params& p, int n, int* sorted_s,
 hipError_t launch_interp(int ndim, int kernel, const Params& p, int n, hipStream_t s, hipEvent_t ev0,
                          hipEvent_t ev1);
 hipError_t launch_spread(int ndim, int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
+hipError_t launch_cand(int ndim, int kernel, const Params& p, bool write, int* counts_or_offs, int* out, hipStream_t s);
+int cand_classes(int ndim, int kernel);  // candidate classes per super-brick
 hipError_t launch_mark(int ndim, int kernel, const Params& p, int n, unsigned char** masks, hipStream_t s);
 hipError_t launch_sort(void* temp, size_t& temp_bytes, const unsigned* kin, unsigned* kout, const int* vin,
                        int* vout, int n, int end_bit, hipStream_t s);

@@ -162,7 +162,10 @@ def test_spread_matches_oracle_in_canonical_order(le, ctx, oracle, kernel, ndim,
 
 @pytest.mark.parametrize("kernel", ["IB_4", "IB_6", "PIECEWISE_LINEAR", "BSPLINE_4"])
 def test_bitwise_against_oracle_ib_side(le, ctx, oracle, kernel):
-    """The headline path (3-D side-centred) must match the oracle bit for bit."""
+    """The headline path (3-D side-centred): interpolation matches the oracle
+    bit for bit; spreading sums each grid point's contributions in the kernel's
+    fixed (phase, class, stencil point, lane) order, i.e. the Fortran's
+    sequential sum reassociated, so it is held to the stated 1e-12."""
     geom, X, idx, xs, depth = make_case(kernel, 3, "side", seed=5, M=2000)
     rng = np.random.default_rng(3)
     dev = "cuda:0"
@@ -186,7 +189,8 @@ def test_bitwise_against_oracle_ib_side(le, ctx, oracle, kernel):
                        xs[order], X, F)
     assert np.array_equal(Q.cpu().numpy()[idx], Qo[idx])
     for a in range(3):
-        assert np.array_equal(q[a].cpu().numpy(), uo[a])
+        ga = q[a].cpu().numpy()
+        assert np.abs(ga - uo[a]).max() <= SPREAD_TOL * np.abs(uo[a]).max()
 
 
 def test_spread_bit_stable_run_to_run(le, ctx):
@@ -206,6 +210,37 @@ def test_spread_bit_stable_run_to_run(le, ctx):
         outs.append([a.clone() for a in q])
     for a in range(3):
         assert torch.equal(outs[0][a], outs[1][a])
+
+
+@pytest.mark.parametrize("kernel", ["IB_4", "IB_6", "PIECEWISE_CONSTANT"])
+def test_spread_bit_stable_dense(le, ctx, oracle, kernel):
+    """Many markers per cell (shared stencil starts, so one add instruction
+    carries several lanes to the same grid point): still bit-stable, and within
+    tolerance of the oracle."""
+    from ibamr_amd.le import Geometry
+    geom = Geometry.periodic_unit([24, 24, 24], oracle.min_ghost_width(kernel) + 1)
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    M = 60_000
+    X = 0.40 + 0.05 * torch.rand((M, 3), dtype=torch.float64, device="cuda:0", generator=g)
+    X[: M // 2] = X[0]  # half the markers at one point
+    F = torch.rand((M, 3), dtype=torch.float64, device="cuda:0", generator=g) - 0.5
+    outs = []
+    for rep in range(2):
+        q = geom.alloc("side")
+        m = le.Markers(ctx).bin(geom, kernel, X)
+        le.spread(ctx, m, kernel, "side", geom, q, F, X)
+        ctx.synchronize()
+        outs.append([a.clone() for a in q])
+    for a in range(3):
+        assert torch.equal(outs[0][a], outs[1][a])
+    order = m.order().cpu().numpy()
+    idx = np.arange(M, dtype=np.int32)
+    uo = [np.zeros(tuple(a.shape)) for a in outs[0]]
+    oracle.side_spread(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, uo, idx[order],
+                       np.zeros((M, 3)), X.cpu().numpy(), F.cpu().numpy())
+    for a in range(3):
+        ga = outs[0][a].cpu().numpy()
+        assert np.abs(ga - uo[a]).max() <= SPREAD_TOL * np.abs(uo[a]).max()
 
 
 def test_errors_are_reported(le, ctx):
