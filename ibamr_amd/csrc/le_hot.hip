@@ -129,12 +129,18 @@ hipError_t launch_bin_t(const Params& p, int n, unsigned* keys, int* vals, hipSt
 // ---------------------------------------------------------------------------
 // interpolation
 // ---------------------------------------------------------------------------
+// Interpolation work item: a group of GB consecutive bricks (2x2[x1] bricks, or
+// one brick for the wide kernels) and all its markers; per component the union
+// stencil region of the group, R0 x R1 [x R2] points, is staged in LDS.
 template <int NDIM, int K> struct IShape {
     using T = KT<K>;
     static constexpr int B = BrickT<NDIM>::B;
-    static constexpr int R = B + T::HI - T::LO;  // region edge (points)
-    static constexpr int RV = NDIM == 3 ? R * R * R : R * R;
-    static constexpr int NL = (RV + IBLOCK - 1) / IBLOCK;  // staged values per thread
+    static constexpr int GB = T::W <= 4 ? 4 : 1;   // bricks per item (ids b..b+GB-1: 2x2[x1] in Morton order)
+    static constexpr int E0 = GB == 4 ? 2 * B : B;  // anchor extent of the item in dims 0 and 1
+    static constexpr int R0 = E0 + T::HI - T::LO, R1 = R0;
+    static constexpr int R2 = NDIM == 3 ? B + T::HI - T::LO : 1;
+    static constexpr int RV = R0 * R1 * R2;
+    static constexpr int NL = (RV + BLOCK - 1) / BLOCK;  // staged values per thread
 };
 
 template <int NDIM, int K>
@@ -158,33 +164,70 @@ __device__ __forceinline__ void marker_stencils(const Params& p, const CompDesc&
     marker_stencils_x<NDIM, K>(p, cd, Xs, s, st);
 }
 
+// region value loads of component cd for the item whose region starts at r0
 template <int NDIM, int K>
-__global__ __launch_bounds__(IBLOCK) void k_interp(Params p) {
+__device__ __forceinline__ void stage_load(const CompDesc& cd, const int* r0, double* v) {
+    using S = IShape<NDIM, K>;
+    constexpr int R0 = S::R0, R1 = S::R1, R2 = S::R2, RV = S::RV;
+    bool inside = true;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) {
+        const int R = d == 0 ? R0 : (d == 1 ? R1 : R2);
+        inside = inside && r0[d] >= cd.lo[d] && r0[d] + R - 1 <= cd.hi[d];
+    }
+    const int64_t o0 = (int64_t)(r0[0] - cd.lo[0]) + (int64_t)(r0[1] - cd.lo[1]) * cd.s1 +
+                       (NDIM == 3 ? (int64_t)(r0[2] - cd.lo[2]) * cd.s2 : 0);
+    // (recomputed per item on purpose: hoisted out of the item loop, the 3*NL
+    // index registers would stay live through the stencil sums)
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+#pragma unroll
+    for (int k = 0; k < S::NL; ++k) {
+        const int q = t + k * BLOCK;
+        v[k] = 0.0;
+        if (q < RV) {
+            const int i0 = q % R0, i1 = (q / R0) % R1, i2 = NDIM == 3 ? q / (R0 * R1) : 0;
+            if (inside) {
+                v[k] = cd.u[o0 + i0 + (int64_t)i1 * cd.s1 + (NDIM == 3 ? (int64_t)i2 * cd.s2 : 0)];
+            } else {
+                const int g0 = r0[0] + i0, g1 = r0[1] + i1, g2 = r0[2] + i2;
+                bool in = g0 >= cd.lo[0] && g0 <= cd.hi[0] && g1 >= cd.lo[1] && g1 <= cd.hi[1];
+                if (NDIM == 3) in = in && g2 >= cd.lo[2] && g2 <= cd.hi[2];
+                if (in)
+                    v[k] = cd.u[(int64_t)(g0 - cd.lo[0]) + (int64_t)(g1 - cd.lo[1]) * cd.s1 +
+                                (NDIM == 3 ? (int64_t)(g2 - cd.lo[2]) * cd.s2 : 0)];
+            }
+        }
+    }
+}
+
+// One workgroup item = GB bricks, every component: the component's region is
+// staged in LDS (the next component's loads are in flight while this one is
+// summed), then one thread per marker sums its W^NDIM stencil from LDS in the
+// Fortran loop order -- bitwise the oracle's value.
+template <int NDIM, int K>
+__global__ __launch_bounds__(BLOCK) void k_interp(Params p) {
     using T = KT<K>;
     using S = IShape<NDIM, K>;
-    constexpr int W = T::W, FAM = T::FAM, B = S::B, R = S::R, RV = S::RV, NL = S::NL;
-    extern __shared__ __attribute__((aligned(16))) double reg[];
+    constexpr int W = T::W, FAM = T::FAM, B = S::B, R0 = S::R0, R1 = S::R1, R2 = S::R2, NL = S::NL;
+    __shared__ double reg[S::RV];
     const int nc = p.ncomp;
-    const int nitems = p.bg.nbricks * nc;
+    const int nitems = p.bg.nbricks / S::GB;
     const int G = gridDim.x;
+    const int tid = threadIdx.x;
     for (int round = 0; round < nitems; round += G) {
         const int it = xcd_item(round, G, blockIdx.x);
         if (it >= nitems) continue;
-        const int b = it / nc, c = it - (it / nc) * nc;
-        const int beg = p.plane_start[b * B], end = p.plane_start[(b + 1) * B];
+        const int b0 = it * S::GB;
+        const int beg = p.plane_start[b0 * B], end = p.plane_start[(b0 + S::GB) * B];
         if (beg == end) continue;
         int bc[3];
-        brick_coords<NDIM>(p.bg, b, bc);
+        brick_coords<NDIM>(p.bg, b0, bc);
         int r0[3] = {0, 0, 0};
-        bool inside = true;
-        const CompDesc& cd = p.comp[c];
 #pragma unroll
-        for (int d = 0; d < NDIM; ++d) {
-            r0[d] = p.bg.kmin[d] + bc[d] * B + T::LO;
-            inside = inside && r0[d] >= cd.lo[d] && r0[d] + R - 1 <= cd.hi[d];
-        }
-        // this thread's first marker, loaded together with the staging loads
-        const int e0 = beg + threadIdx.x;
+        for (int d = 0; d < NDIM; ++d) r0[d] = p.bg.kmin[d] + bc[d] * B + T::LO;
+        // this thread's first marker, kept across the components
+        const int e0 = beg + tid;
         int s0 = 0;
         double x0[NDIM];
         if (e0 < end) {
@@ -192,117 +235,108 @@ __global__ __launch_bounds__(IBLOCK) void k_interp(Params p) {
 #pragma unroll
             for (int d = 0; d < NDIM; ++d) x0[d] = p.sorted_X[(int64_t)NDIM * e0 + d];
         }
-        // issue every staging load of this thread before using any of them
-        double v[NL];
-        const int64_t o0 = (int64_t)(r0[0] - cd.lo[0]) + (int64_t)(r0[1] - cd.lo[1]) * cd.s1 +
-                           (NDIM == 3 ? (int64_t)(r0[2] - cd.lo[2]) * cd.s2 : 0);
+        for (int c = 0; c < nc; ++c) {
+            const CompDesc& cd = p.comp[c];
+            {
+                double v[NL];
+                stage_load<NDIM, K>(cd, r0, v);
+                __syncthreads();  // the previous readers of reg are done
 #pragma unroll
-        for (int k = 0; k < NL; ++k) {
-            const int q = threadIdx.x + k * IBLOCK;
-            v[k] = 0.0;
-            if (q < RV) {
-                const int i0 = q % R, i1 = (q / R) % R, i2 = NDIM == 3 ? q / (R * R) : 0;
-                if (inside) {
-                    v[k] = cd.u[o0 + i0 + (int64_t)i1 * cd.s1 + (NDIM == 3 ? (int64_t)i2 * cd.s2 : 0)];
-                } else {
-                    const int g0 = r0[0] + i0, g1 = r0[1] + i1, g2 = r0[2] + i2;
-                    bool in = g0 >= cd.lo[0] && g0 <= cd.hi[0] && g1 >= cd.lo[1] && g1 <= cd.hi[1];
-                    if (NDIM == 3) in = in && g2 >= cd.lo[2] && g2 <= cd.hi[2];
-                    if (in)
-                        v[k] = cd.u[(int64_t)(g0 - cd.lo[0]) + (int64_t)(g1 - cd.lo[1]) * cd.s1 +
-                                    (NDIM == 3 ? (int64_t)(g2 - cd.lo[2]) * cd.s2 : 0)];
+                for (int k = 0; k < NL; ++k) {
+                    const int q = tid + k * BLOCK;
+                    if (q < S::RV) reg[q] = v[k];
                 }
+                __syncthreads();
             }
-        }
-        __syncthreads();  // the previous item's readers are done with reg
-#pragma unroll
-        for (int k = 0; k < NL; ++k) {
-            const int q = threadIdx.x + k * IBLOCK;
-            if (q < RV) reg[q] = v[k];
-        }
-        __syncthreads();
 
-        for (int e = e0; e < end; e += IBLOCK) {
-            int s = s0;
-            if (e != e0) {
-                s = p.sorted_s[e];
+            for (int e = e0; e < end; e += BLOCK) {
+                int s = s0;
+                double xs[NDIM];
 #pragma unroll
-                for (int d = 0; d < NDIM; ++d) x0[d] = p.sorted_X[(int64_t)NDIM * e + d];
-            }
-            St<W> st[NDIM];
-            marker_stencils_x<NDIM, K>(p, cd, x0, s, st);
-            bool ok = true;
+                for (int d = 0; d < NDIM; ++d) xs[d] = x0[d];
+                if (e != e0) {
+                    s = p.sorted_s[e];
 #pragma unroll
-            for (int d = 0; d < NDIM; ++d)
-                if (st[d].ist <= st[d].isp)
-                    ok = ok && (st[d].icl + st[d].ist >= r0[d]) && (st[d].icl + st[d].isp < r0[d] + R);
-            if (!ok) {
-                atomicOr(p.err, 1);
-                continue;
-            }
-            double acc = 0.0;
-            if constexpr (FAM == 3) {
-                bool nonempty = true;
-#pragma unroll
-                for (int d = 0; d < NDIM; ++d) nonempty = nonempty && (st[d].ist <= st[d].isp);
-                if (nonempty) {
-                    int li = st[0].icl - r0[0] + R * (st[1].icl - r0[1]);
-                    if (NDIM == 3) li += R * R * (st[2].icl - r0[2]);
-                    acc = reg[li];
+                    for (int d = 0; d < NDIM; ++d) xs[d] = p.sorted_X[(int64_t)NDIM * e + d];
                 }
-            } else {
-                // Clipped stencil entries (outside [ist, isp]) get weight 0 and a
-                // clamped (in-region) LDS index: acc + 0 == acc, so the sum equals
-                // the Fortran's clipped sum bit for bit, without per-term branches.
-                double w[NDIM][W];
-                int o[NDIM][W];
+                St<W> st[NDIM];
+                marker_stencils_x<NDIM, K>(p, cd, xs, s, st);
+                bool ok = true;
 #pragma unroll
                 for (int d = 0; d < NDIM; ++d) {
-                    const int stride = d == 0 ? 1 : (d == 1 ? R : R * R);
-#pragma unroll
-                    for (int i = 0; i < W; ++i) {
-                        const bool in = i >= st[d].ist && i <= st[d].isp;
-                        w[d][i] = in ? st[d].w[i] : 0.0;
-                        o[d][i] = min(max(st[d].icl + i - r0[d], 0), R - 1) * stride;
-                    }
+                    const int R = d == 0 ? R0 : (d == 1 ? R1 : R2);
+                    if (st[d].ist <= st[d].isp)
+                        ok = ok && (st[d].icl + st[d].ist >= r0[d]) && (st[d].icl + st[d].isp < r0[d] + R);
                 }
-                if constexpr (NDIM == 3) {
+                if (!ok) {
+                    atomicOr(p.err, 1);
+                    continue;
+                }
+                double acc = 0.0;
+                if constexpr (FAM == 3) {
+                    bool nonempty = true;
 #pragma unroll
-                    for (int i2 = 0; i2 < W; ++i2) {
-#pragma unroll
-                        for (int i1 = 0; i1 < W; ++i1) {
-                            const double* row = reg + o[1][i1] + o[2][i2];
-                            if constexpr (FAM == 0) {
-                                const double wyz = w[1][i1] * w[2][i2];  // f.m4:1349-1353
-#pragma unroll
-                                for (int i0 = 0; i0 < W; ++i0) {
-                                    const double wt = w[0][i0] * wyz;
-                                    acc = acc + wt * row[o[0][i0]];  // f.m4:1375
-                                }
-                            } else {
-#pragma unroll
-                                for (int i0 = 0; i0 < W; ++i0)
-                                    acc = acc + w[0][i0] * w[1][i1] * w[2][i2] * row[o[0][i0]];  // f.m4:545-548
-                            }
-                        }
+                    for (int d = 0; d < NDIM; ++d) nonempty = nonempty && (st[d].ist <= st[d].isp);
+                    if (nonempty) {
+                        int li = st[0].icl - r0[0] + R0 * (st[1].icl - r0[1]);
+                        if (NDIM == 3) li += R0 * R1 * (st[2 % NDIM].icl - r0[2]);
+                        acc = reg[li];
                     }
                 } else {
+                    // Clipped stencil entries (outside [ist, isp]) get weight 0 and a
+                    // clamped (in-region) LDS index: acc + 0 == acc, so the sum equals
+                    // the Fortran's clipped sum bit for bit, without per-term branches.
+                    double w[NDIM][W];
+                    int o[NDIM][W];
 #pragma unroll
-                    for (int i1 = 0; i1 < W; ++i1) {
-                        const double* row = reg + o[1][i1];
+                    for (int d = 0; d < NDIM; ++d) {
+                        const int R = d == 0 ? R0 : (d == 1 ? R1 : R2);
+                        const int stride = d == 0 ? 1 : (d == 1 ? R0 : R0 * R1);
 #pragma unroll
-                        for (int i0 = 0; i0 < W; ++i0) {
-                            if constexpr (FAM == 0) {
-                                const double wt = w[0][i0] * w[1][i1];
-                                acc = acc + wt * row[o[0][i0]];
-                            } else {
-                                acc = acc + w[0][i0] * w[1][i1] * row[o[0][i0]];
+                        for (int i = 0; i < W; ++i) {
+                            const bool in = i >= st[d].ist && i <= st[d].isp;
+                            w[d][i] = in ? st[d].w[i] : 0.0;
+                            o[d][i] = min(max(st[d].icl + i - r0[d], 0), R - 1) * stride;
+                        }
+                    }
+                    if constexpr (NDIM == 3) {
+#pragma unroll
+                        for (int i2 = 0; i2 < W; ++i2) {
+#pragma unroll
+                            for (int i1 = 0; i1 < W; ++i1) {
+                                const double* row = reg + o[1][i1] + o[2][i2];
+                                if constexpr (FAM == 0) {
+                                    const double wyz = w[1][i1] * w[2][i2];  // f.m4:1349-1353
+#pragma unroll
+                                    for (int i0 = 0; i0 < W; ++i0) {
+                                        const double wt = w[0][i0] * wyz;
+                                        acc = acc + wt * row[o[0][i0]];  // f.m4:1375
+                                    }
+                                } else {
+#pragma unroll
+                                    for (int i0 = 0; i0 < W; ++i0)
+                                        acc = acc + w[0][i0] * w[1][i1] * w[2][i2] * row[o[0][i0]];  // f.m4:545-548
+                                }
+                            }
+                        }
+                    } else {
+#pragma unroll
+                        for (int i1 = 0; i1 < W; ++i1) {
+                            const double* row = reg + o[1][i1];
+#pragma unroll
+                            for (int i0 = 0; i0 < W; ++i0) {
+                                if constexpr (FAM == 0) {
+                                    const double wt = w[0][i0] * w[1][i1];
+                                    acc = acc + wt * row[o[0][i0]];
+                                } else {
+                                    acc = acc + w[0][i0] * w[1][i1] * row[o[0][i0]];
+                                }
                             }
                         }
                     }
                 }
+                p.Qout[(int64_t)p.Q_depth * s + cd.qcomp] = acc;
             }
-            p.Qout[(int64_t)p.Q_depth * s + cd.qcomp] = acc;
         }
     }
 }
@@ -405,7 +439,7 @@ static int interp_mode() {
     static int mode = -1;
     if (mode < 0) {
         const char* v = getenv("IBTK_LE_INTERP");
-        mode = (v && v[0] == 's') ? 0 : 1;  // 0 staged, 1 direct
+        mode = (v && v[0] == 'd') ? 1 : 0;  // 0 staged, 1 direct
     }
     return mode;
 }
@@ -413,18 +447,14 @@ static int interp_mode() {
 template <int NDIM, int K>
 hipError_t launch_interp_t(const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     using S = IShape<NDIM, K>;
-    const size_t lds = (size_t)S::RV * sizeof(double);
-    if (lds > 64 * 1024)
-        (void)hipFuncSetAttribute((const void*)k_interp<NDIM, K>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
     if (ev0) (void)hipEventRecord(ev0, s);
     if (interp_mode() == 1) {
         if (n > 0) hipLaunchKernelGGL((k_interp_direct<NDIM, K>), dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n);
         if (ev1) (void)hipEventRecord(ev1, s);
         return hipGetLastError();
     }
-    const long items = (long)p.bg.nbricks * p.ncomp;
-    hipLaunchKernelGGL((k_interp<NDIM, K>), dim3(grid_for(items, 16)), dim3(IBLOCK), lds, s, p);
+    const long items = (long)(p.bg.nbricks / S::GB);
+    hipLaunchKernelGGL((k_interp<NDIM, K>), dim3(grid_for(items, 64)), dim3(BLOCK), 0, s, p);
     if (ev1) (void)hipEventRecord(ev1, s);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
