@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -95,7 +96,9 @@ struct ibtk_le_ctx_s {
     int device = 0;
     hipStream_t stream = nullptr;
     DevBuf keys_in, vals_in, temp, counts, offsets, fbuf;
-    DevBuf err;  // one int
+    DevBuf err;   // one int
+    DevBuf sink;  // 64 doubles (Params::sink)
+    DevBuf stamps;  // diagnostic phase clocks (IBTK_LE_STAMPS=1)
     bool timing = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool ev_valid = false;
@@ -107,8 +110,10 @@ struct ibtk_le_markers_s {
     int kernel = -1;
     int ndim = 0;
     BinGeom bg{};
+    ColGeom cg{};        // 3-D: column binning (le_sweep.hip)
+    int S = 0, nseg = 0;  // 3-D: sweep segments
     ibtk_le_patch_geom geom{};
-    DevBuf sorted_key, sorted_l, sorted_s, sorted_X, plane_start, indices, xshift;
+    DevBuf sorted_key, sorted_l, sorted_s, sorted_X, sorted_a, plane_start, indices, xshift;
     DevBuf cand_cnt, cand_off, cand_idx;  // spread candidate lists, built on first use after a bin
     bool has_indices = false, has_xshift = false;
     bool cand_valid = false;
@@ -129,6 +134,7 @@ extern "C" int ibtk_le_ctx_create(int device, void* stream, ibtk_le_ctx* out) {
     c->stream = static_cast<hipStream_t>(stream);
     HIP_TRY(hipSetDevice(device));
     int rc = c->err.ensure(sizeof(int));
+    if (!rc) rc = c->sink.ensure(64 * sizeof(double));
     if (rc) {
         delete c;
         return rc;
@@ -144,7 +150,7 @@ extern "C" int ibtk_le_ctx_destroy(ibtk_le_ctx ctx) {
     if (!ctx) return IBTK_LE_OK;
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
-    for (DevBuf* b : {&ctx->keys_in, &ctx->vals_in, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->fbuf, &ctx->err})
+    for (DevBuf* b : {&ctx->keys_in, &ctx->vals_in, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->fbuf, &ctx->err, &ctx->sink})
         b->release();
     if (ctx->ev0) hipEventDestroy(ctx->ev0);
     if (ctx->ev1) hipEventDestroy(ctx->ev1);
@@ -233,6 +239,39 @@ static int make_bin_geom(const ibtk_le_patch_geom* g, int kernel, BinGeom& bg) {
     if ((nb + 1) * BV >= (1LL << 32))
         return fail(IBTK_LE_ERR_RANGE, "patch too large for 32-bit bin keys (%lld bricks)", nb);
     bg.nbricks = (int)nb;
+    return IBTK_LE_OK;
+}
+
+// 3-D column grid over key cells: every key whose stencil can touch any array
+// of the patch, for every centering (ghost box, + 1 for the extra face/node).
+static int make_col_geom(const ibtk_le_patch_geom* g, int kernel, BinGeom& bg, ColGeom& cg) {
+    const KernelInfo ki = kKernelInfo[kernel];
+    std::memset(&bg, 0, sizeof(bg));
+    std::memset(&cg, 0, sizeof(cg));
+    bg.ndim = 3;
+    for (int d = 0; d < 3; ++d) {
+        bg.xlo[d] = g->x_lower[d];
+        bg.dx[d] = g->dx[d];
+        bg.ilower[d] = g->ilower[d];
+        const int lo = g->ilower[d] - g->gcw[d];
+        const int hi = g->iupper[d] + g->gcw[d] + 1;
+        cg.org[d] = lo - ki.HI;
+        cg.ext[d] = hi - ki.LO - cg.org[d] + 1;
+    }
+    // one empty guard column / row on each side in x and y
+    cg.ncx = (cg.ext[0] + COLX - 1) / COLX + 2;
+    cg.ncy = (cg.ext[1] + COLY - 1) / COLY + 2;
+    cg.org[0] -= COLX;
+    cg.org[1] -= COLY;
+    cg.ext[0] = cg.ncx * COLX;
+    cg.ext[1] = cg.ncy * COLY;
+    cg.nz = cg.ext[2];
+    cg.ncol = cg.ncx * cg.ncy;
+    if (cg.ext[0] > 65535 || cg.ext[1] > 65535)
+        return fail(IBTK_LE_ERR_RANGE, "patch too wide for 16-bit packed key cells");
+    const long long nb = (long long)cg.nz * cg.ncol * NBAND;
+    if (nb + 1 >= (1LL << 31)) return fail(IBTK_LE_ERR_RANGE, "patch too large for 31-bit bucket keys");
+    cg.nbuckets = (int)nb;
     return IBTK_LE_OK;
 }
 
@@ -346,7 +385,7 @@ extern "C" int ibtk_le_markers_destroy(ibtk_le_markers m) {
     if (!m) return IBTK_LE_OK;
     hipSetDevice(m->ctx->device);
     hipStreamSynchronize(m->ctx->stream);
-    for (DevBuf* b : {&m->sorted_key, &m->sorted_l, &m->sorted_s, &m->sorted_X, &m->plane_start, &m->indices,
+    for (DevBuf* b : {&m->sorted_key, &m->sorted_l, &m->sorted_s, &m->sorted_X, &m->sorted_a, &m->plane_start, &m->indices,
                       &m->xshift, &m->cand_cnt, &m->cand_off, &m->cand_idx})
         b->release();
     delete m;
@@ -371,20 +410,28 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     if (nindices > 0 && !X_dev) return fail(IBTK_LE_ERR_ARG, "null X");
     if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
     BinGeom bg;
-    if (int rc = make_bin_geom(geom, kernel, bg)) return rc;
+    ColGeom cg{};
+    const bool cols = geom->ndim == 3;
+    if (cols) {
+        if (int rc = make_col_geom(geom, kernel, bg, cg)) return rc;
+    } else {
+        if (int rc = make_bin_geom(geom, kernel, bg)) return rc;
+    }
     const hipStream_t s = ctx->stream;
     const int n = nindices;
     m->n = n;
     m->kernel = kernel;
     m->ndim = geom->ndim;
     m->bg = bg;
+    m->cg = cg;
+    if (cols) sweep_segments(cg, m->S, m->nseg);
     m->geom = *geom;
     m->has_indices = indices_dev != nullptr;
     m->has_xshift = Xshift_dev != nullptr;
     m->cand_valid = false;
     int rc = 0;
     const int B = geom->ndim == 3 ? BRICK3 : BRICK2;
-    const int nplanes = bg.nbricks * B;
+    const int nplanes = cols ? cg.nbuckets : bg.nbricks * B;  // bucket starts: nplanes + 1
     if ((rc = m->plane_start.ensure(sizeof(int) * (size_t)(nplanes + 1)))) return rc;
     if (n == 0) {
         HIP_TRY(hipMemsetAsync(m->plane_start.p, 0, sizeof(int) * (size_t)(nplanes + 1), s));
@@ -408,11 +455,18 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     Params p;
     std::memset(&p, 0, sizeof(p));
     p.bg = bg;
+    p.cg = cg;
     p.X = X_dev;
     p.indices = m->has_indices ? m->indices.as<int>() : nullptr;
     p.Xshift = m->has_xshift ? m->xshift.as<double>() : nullptr;
-    HIP_TRY(launch_bin(geom->ndim, kernel, p, n, ctx->keys_in.as<unsigned>(), ctx->vals_in.as<int>(), s));
-    const int end_bit = end_bit_for(bg);
+    if (cols) HIP_TRY(launch_bin_col(kernel, p, n, ctx->keys_in.as<unsigned>(), ctx->vals_in.as<int>(), s));
+    else HIP_TRY(launch_bin(geom->ndim, kernel, p, n, ctx->keys_in.as<unsigned>(), ctx->vals_in.as<int>(), s));
+    int end_bit = 1;
+    if (cols) {
+        while ((1ULL << end_bit) <= (unsigned long long)cg.nbuckets) ++end_bit;
+    } else {
+        end_bit = end_bit_for(bg);
+    }
     size_t tb = 0;
     HIP_TRY(launch_sort(nullptr, tb, ctx->keys_in.as<unsigned>(), m->sorted_key.as<unsigned>(),
                         ctx->vals_in.as<int>(), m->sorted_l.as<int>(), n, end_bit, s));
@@ -420,10 +474,13 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     tb = ctx->temp.cap;
     HIP_TRY(launch_sort(ctx->temp.p, tb, ctx->keys_in.as<unsigned>(), m->sorted_key.as<unsigned>(),
                         ctx->vals_in.as<int>(), m->sorted_l.as<int>(), n, end_bit, s));
-    HIP_TRY(launch_brick_start(m->sorted_key.as<unsigned>(), n, nplanes, bg.shift - (geom->ndim == 3 ? 3 : 4),
-                               m->plane_start.as<int>(), s));
+    HIP_TRY(launch_brick_start(m->sorted_key.as<unsigned>(), n, nplanes,
+                               cols ? 0 : bg.shift - (geom->ndim == 3 ? 3 : 4), m->plane_start.as<int>(), s));
     p.sorted_l = m->sorted_l.as<int>();
-    HIP_TRY(launch_gather_sorted(geom->ndim, p, n, m->sorted_s.as<int>(), m->sorted_X.as<double>(), s));
+    if (cols)
+        HIP_TRY(launch_gather_col(kernel, p, n, m->sorted_s.as<int>(), m->sorted_X.as<double>(), nullptr, s));
+    else
+        HIP_TRY(launch_gather_sorted(geom->ndim, p, n, m->sorted_s.as<int>(), m->sorted_X.as<double>(), s));
     return IBTK_LE_OK;
 }
 
@@ -451,6 +508,11 @@ static int prepare(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const ibtk_le
     if (m->n > 0 && !X) return fail(IBTK_LE_ERR_ARG, "null X");
     std::memset(&p, 0, sizeof(p));
     p.bg = m->bg;
+    p.cg = m->cg;
+    p.S = m->S;
+    p.nseg = m->nseg;
+    p.sorted_a = m->sorted_a.as<unsigned>();
+    p.nsorted = m->n;
     p.X = X;
     p.indices = m->has_indices ? m->indices.as<int>() : nullptr;
     p.Xshift = m->has_xshift ? m->xshift.as<double>() : nullptr;
@@ -460,6 +522,7 @@ static int prepare(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const ibtk_le
     p.sorted_key = m->sorted_key.as<unsigned>();
     p.plane_start = m->plane_start.as<int>();
     p.err = ctx->err.as<int>();
+    p.sink = ctx->sink.as<double>();
     p.K6 = ib6_K();
     p.h3 = geom->ndim == 3 ? (geom->dx[0] * geom->dx[1]) * geom->dx[2] : geom->dx[0] * geom->dx[1];
     return IBTK_LE_OK;
@@ -492,8 +555,11 @@ int ibtk_le::interp_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cen
                                 cnt, p))
             return rc;
         const bool t = ctx->timing && first == 0;
-        HIP_TRY(launch_interp(geom->ndim, kernel, p, m->n, ctx->stream, t ? ctx->ev0 : nullptr,
-                              t ? ctx->ev1 : nullptr));
+        if (geom->ndim == 3)
+            HIP_TRY(launch_interp_sweep(kernel, p, m->n, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
+        else
+            HIP_TRY(launch_interp(geom->ndim, kernel, p, m->n, ctx->stream, t ? ctx->ev0 : nullptr,
+                                  t ? ctx->ev1 : nullptr));
         if (t) ctx->ev_valid = true;
     }
     return IBTK_LE_OK;
@@ -542,15 +608,45 @@ extern "C" int ibtk_le_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, in
     p.nsorted = m->n;
     if (int rc = ctx->fbuf.ensure(sizeof(double) * (size_t)m->n * (size_t)std::min(nc, MAXC))) return rc;
     p.sorted_F = ctx->fbuf.as<double>();
-    if (int rc = build_candidates(ctx, m, p)) return rc;
-    p.cand_off = m->cand_off.as<int>();
-    p.cand_idx = m->cand_idx.as<int>();
+    if (geom->ndim == 2) {
+        if (int rc = build_candidates(ctx, m, p)) return rc;
+        p.cand_off = m->cand_off.as<int>();
+        p.cand_idx = m->cand_idx.as<int>();
+    }
     ctx->ev_valid = false;
     for (int first = 0; first < nc; first += MAXC) {
         const int cnt = std::min(MAXC, nc - first);
         if (int rc = make_comps(geom, centering, axis, q_dev, q_depth, Q_depth, first, cnt, p)) return rc;
         const bool t = ctx->timing && first == 0;
-        HIP_TRY(launch_spread(geom->ndim, kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
+        const char* dbg = getenv("IBTK_LE_STAMPS");
+        const size_t nst = (size_t)m->cg.ncol * m->nseg * cnt * 8;
+        if (geom->ndim == 3 && dbg && dbg[0] == '1') {
+            if (int rc = ctx->stamps.ensure(nst * sizeof(unsigned long long))) return rc;
+            HIP_TRY(hipMemsetAsync(ctx->stamps.p, 0, nst * sizeof(unsigned long long), ctx->stream));
+            p.stamps = ctx->stamps.as<unsigned long long>();
+        }
+        if (geom->ndim == 3)
+            HIP_TRY(launch_spread_sweep(kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
+        else
+            HIP_TRY(launch_spread(geom->ndim, kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
+        if (p.stamps) {  // per-phase cycle totals over the work items (diagnostics only)
+            std::vector<unsigned long long> h(nst);
+            HIP_TRY(hipMemcpyAsync(h.data(), p.stamps, nst * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                   ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            double tot[6] = {0, 0, 0, 0, 0, 0};
+            long items = 0;
+            for (size_t i = 0; i < nst / 8; ++i) {
+                unsigned long long sum = 0;
+                for (int k = 0; k < 6; ++k) sum += h[i * 8 + k];
+                if (!sum) continue;
+                ++items;
+                for (int k = 0; k < 6; ++k) tot[k] += (double)h[i * 8 + k];
+            }
+            fprintf(stderr, "spread stamps: %ld items; mean cycles/item: prologue %.0f wait %.0f chunk0 %.0f dense %.0f tail %.0f drain %.0f\n",
+                    items, tot[0] / items, tot[1] / items, tot[2] / items, tot[3] / items, tot[4] / items, tot[5] / items);
+            p.stamps = nullptr;
+        }
         if (t) ctx->ev_valid = true;
     }
     return IBTK_LE_OK;

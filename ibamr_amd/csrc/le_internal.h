@@ -74,8 +74,31 @@ struct BinGeom {
     int ilower[3];     // patch box lower
 };
 
+// 3-D column binning (le_sweep.hip).  Stencil-anchor ("key") cells are grouped
+// into columns of COLX x COLY cells in (x, y); z is swept plane by plane.  Each
+// (anchor plane, column) is split into NBAND bands by where the key cell sits
+// in the column: xb = 0 / 2 if the stencil reaches the x-1 / x+1 column (1
+// otherwise), yb likewise, band = 3*xb + yb.  Bucket = (z*ncol + col)*NBAND +
+// band, col = cy*ncx + cx: the sorted list is z-major (every grid point sees its
+// contributions in list order when the columns are swept in z), and the markers
+// of a neighbouring column that reach a given column are a few contiguous bucket
+// ranges.  Columns 0 and ncx-1 (rows 0 and ncy-1) are empty guards, so every
+// real column has all eight neighbours.  nbuckets marks "outside".
+constexpr int COLX = 32;
+constexpr int COLY = 16;
+constexpr int NBAND = 9;
+struct ColGeom {
+    int org[3];     // absolute key cell of column (0,0) (a guard), plane 0
+    int ext[3];     // key-cell extent covered: ncx*COLX, ncy*COLY, nz
+    int ncx, ncy, nz, ncol;
+    int nbuckets;   // nz * ncol * NBAND
+};
+
 struct Params {
     BinGeom bg;
+    ColGeom cg;                // 3-D column binning
+    const unsigned* sorted_a;  // sorted position -> packed key cell (x | y << 16), relative to cg.org
+    int S, nseg;               // sweep segment length (planes) and segments per column
     int ncomp;
     CompDesc comp[MAXC];
     int Q_depth;
@@ -98,6 +121,7 @@ struct Params {
     int nsorted;               // list length
     double* Qout;              // interp: marker values
     int* err;                  // device error word (0 = fine)
+    double* sink;              // 64 doubles: the store target of masked-off lanes (branch-free stores)
     unsigned long long* stamps;  // diagnostic phase clocks (nullptr: off)
     int dbg;                     // diagnostic switches (0: off)
 };
@@ -115,6 +139,14 @@ hipError_t launch_mark(int ndim, int kernel, const Params& p, int n, unsigned ch
 hipError_t launch_sort(void* temp, size_t& temp_bytes, const unsigned* kin, unsigned* kout, const int* vin,
                        int* vout, int n, int end_bit, hipStream_t s);
 hipError_t launch_scan(void* temp, size_t& temp_bytes, const int* in, int* out, int n, hipStream_t s);
+
+// 3-D column sweep (le_sweep.hip)
+hipError_t launch_bin_col(int kernel, const Params& p, int n, unsigned* keys, int* vals, hipStream_t s);
+hipError_t launch_gather_col(int kernel, const Params& p, int n, int* sorted_s, double* sorted_X,
+                             unsigned* sorted_a, hipStream_t s);
+hipError_t launch_interp_sweep(int kernel, const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
+hipError_t launch_spread_sweep(int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
+void sweep_segments(const ColGeom& cg, int& S, int& nseg);
 
 // Periodic helpers
 struct GhostDesc {

@@ -1,0 +1,882 @@
+// le_sweep.hip -- the 3-D hot path on CDNA4 (gfx950): column binning, and
+// interpolation / spreading as z-sweeps over (x,y) columns.  Replaces the
+// l-loops of ibtk/src/lagrangian/fortran/lagrangian_interaction3d.f.m4 for every
+// kernel function (IB_4 :1258-1522, IB_6 :1851-2255, IB_4_W8 :1532-1850, the
+// piecewise kernels :49-971).
+//
+// Decomposition:
+//  * bin: key = (anchor plane z, column) with columns of COLX x COLY key cells;
+//    stable device radix sort; bucket starts; a coalescing pass writes the
+//    sorted marker index, the sorted shifted position X(s)+Xshift(l) and the
+//    packed key cell.  The sorted list is z-major.
+//  * one wavefront = one work item (column, z-segment, component); no
+//    barriers, the waves of a CU are independent workers.
+//  * interp: the item streams the z-planes of its column's staged region
+//    (column + stencil halo) through an LDS ring of HI-LO+1 planes (the next
+//    two planes prefetched in registers).  For anchor plane a, one lane per
+//    marker sums its W^3 stencil from the ring in the Fortran loop order (i2,
+//    i1, i0), so the value is bitwise the oracle's.
+//  * spread: the item owns the column's points in its z-segment.  Planes are
+//    loaded (u_old) when the first anchor plane that reaches them comes up and
+//    written back when the last one has passed.  Per anchor plane, the markers
+//    of the 3x3 neighbouring buckets whose stencil reaches the column (11
+//    contiguous ranges of the sorted list, by band) are staged 64 at a time,
+//    one lane per candidate; each lane computes its 1-D weights in registers
+//    and issues its W^3 adds as LDS f64 atomics (ds_add_f64) into the ring.
+//    Every grid point receives its contributions in a fixed order (staging
+//    order, lane order within an instruction): bit-stable from run to run,
+//    within rounding of the oracle's sequential l-loop.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdio>
+#include <cstdlib>
+
+#include "le_internal.h"
+#include "le_stencil.h"
+
+namespace ibtk_le {
+
+constexpr int SW = 64;  // one wavefront per work item
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// ---------------------------------------------------------------------------
+// binning
+// ---------------------------------------------------------------------------
+// Key cell of a marker relative to the column grid (cell-frame anchor, the same
+// rule the stencils use); false if it lies outside the grid (no stencil point
+// of it can reach any array).
+template <int K> __device__ __forceinline__ bool col_key_cell(const Params& p, const double* Xs, int* ka) {
+    bool in = true;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const double xo = (Xs[d] - p.bg.xlo[d]) / p.bg.dx[d];
+        if (!(fabs(xo) < 1.0e9)) {  // also catches NaN
+            in = false;
+            ka[d] = 0;
+            continue;
+        }
+        ka[d] = key_anchor<K>(xo) + p.bg.ilower[d] - p.cg.org[d];
+        if (ka[d] < 0 || ka[d] >= p.cg.ext[d]) in = false;
+    }
+    return in;
+}
+
+// band of a key cell in its column: xb = 0 if its stencil reaches the x-1
+// column, 2 if it reaches x+1, else 1; yb likewise; band = 3*xb + yb
+template <int K> __device__ __forceinline__ int key_band(int kx, int ky) {
+    constexpr int LO = KT<K>::LO, HI = KT<K>::HI;
+    static_assert(-1 - LO < COLY - HI, "a stencil must not reach both neighbouring columns");
+    const int xl = kx & (COLX - 1), yl = ky & (COLY - 1);
+    const int xb = xl <= -1 - LO ? 0 : (xl >= COLX - HI ? 2 : 1);
+    const int yb = yl <= -1 - LO ? 0 : (yl >= COLY - HI ? 2 : 1);
+    return 3 * xb + yb;
+}
+
+template <int K>
+__global__ __launch_bounds__(BLOCK) void k_bin_col(Params p, int n, unsigned* keys, int* vals) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const int s = p.indices ? p.indices[i] : i;
+    double Xs[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) Xs[d] = p.X[(int64_t)3 * s + d] + (p.Xshift ? p.Xshift[(int64_t)3 * i + d] : 0.0);
+    int ka[3];
+    unsigned key = (unsigned)p.cg.nbuckets;
+    if (col_key_cell<K>(p, Xs, ka)) {
+        const int col = (ka[1] / COLY) * p.cg.ncx + ka[0] / COLX;
+        key = (unsigned)((ka[2] * p.cg.ncol + col) * NBAND + key_band<K>(ka[0], ka[1]));
+    }
+    keys[i] = key;
+    vals[i] = i;
+}
+
+template <int K>
+__global__ __launch_bounds__(BLOCK) void k_gather_col(Params p, int n, int* sorted_s, double* sorted_X,
+                                                      unsigned* sorted_a) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= n) return;
+    const int l = p.sorted_l[e];
+    const int s = p.indices ? p.indices[l] : l;
+    sorted_s[e] = s;
+    double Xs[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        Xs[d] = p.X[(int64_t)3 * s + d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
+        sorted_X[(int64_t)3 * e + d] = Xs[d];
+    }
+    if (sorted_a) {
+        int ka[3];
+        col_key_cell<K>(p, Xs, ka);
+        sorted_a[e] = ((unsigned)ka[0] & 0xffffu) | ((unsigned)ka[1] << 16);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// work items
+// ---------------------------------------------------------------------------
+// Items are (segment, column, component), component fastest; blocks are dealt
+// round-robin over the 8 XCDs, so give XCD x a contiguous range of items: the
+// three components of a column and its x-neighbours run on one XCD at about the
+// same time and share marker data and halo planes through its L2.
+__device__ __forceinline__ int sweep_item(int nitems) {
+    const int G = gridDim.x;  // multiple of 8
+    const int per = G >> 3;
+    const int b = blockIdx.x;
+    const int it = (b & 7) * per + (b >> 3);
+    return it < nitems ? it : -1;
+}
+
+// bucket index of (anchor plane a, column col, band)
+__device__ __forceinline__ int bucket(const Params& p, int a, int col, int band) {
+    return (a * p.cg.ncol + col) * NBAND + band;
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA and counted waits
+// ---------------------------------------------------------------------------
+// Everything the sweeps read inside their z loop (planes, marker data, bucket
+// starts) arrives by LDS-DMA (global_load_lds, per-lane source addresses, no
+// VGPR destination), issued one step ahead.  The loop then holds no ordinary
+// global load, so the compiler inserts no vmcnt waits of its own; each step
+// opens with one counted wait, vmcnt(N) with N = the memory operations the
+// previous step issued after the data this step needs (their order and number
+// per step are fixed: masked lanes load clamped addresses and store to
+// Params::sink).
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+// global_load_lds_dword in inline asm rather than the builtin: the compiler then
+// does not track the LDS write and inserts no vmcnt(0) before every LDS read
+// that might alias it (it cannot tell ring slots apart) -- the counted waits
+// below are the synchronisation.  M0 = the wave-uniform LDS byte address.
+__device__ __forceinline__ void glds4(const void* g, void* l) {
+    const unsigned m = (unsigned)(uintptr_t)(lds_void_t*)l;
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(m) : "memory", "m0");
+}
+template <int N> __device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void mem_fence_compiler() { asm volatile("" ::: "memory"); }
+
+// diagnostic phase clocks (Params::stamps != nullptr): per work item, cycles
+// spent per phase, accumulated in registers and written once at the end
+struct Clk {
+    unsigned long long t = 0, acc[6] = {0, 0, 0, 0, 0, 0};
+    bool on = false;
+    __device__ __forceinline__ void start(bool enable) {
+        on = enable;
+        if (on) t = __builtin_amdgcn_s_memtime();
+    }
+    __device__ __forceinline__ void lap(int ph) {
+        if (on) {
+            const unsigned long long u = __builtin_amdgcn_s_memtime();
+            acc[ph] += u - t;
+            t = u;
+        }
+    }
+    __device__ __forceinline__ void flush(const Params& p, int it) {
+        if (on && lane_id() == 0)
+            for (int k = 0; k < 6; ++k) p.stamps[(int64_t)it * 8 + k] = acc[k];
+    }
+};
+
+// ---------------------------------------------------------------------------
+// interpolation
+// ---------------------------------------------------------------------------
+template <int K> struct ISh {
+    using T = KT<K>;
+    static constexpr int W = T::W, LO = T::LO, HI = T::HI, FAM = T::FAM;
+    static constexpr int RX = COLX + HI - LO, RY = COLY + HI - LO;  // staged plane: column + stencil halo
+    static constexpr int NS = HI - LO + 1;                          // planes an anchor plane reads (a+LO .. a+HI)
+    static constexpr int NSL = NS + 1;                              // ring slots (+1 in flight)
+    static constexpr int PV = RX * RY;
+    static constexpr int PDW = 2 * PV;                              // dwords per plane
+    static constexpr int PD = (PDW + SW - 1) / SW;                  // DMA instructions per plane
+    static constexpr int PVP = PD * SW / 2;                         // ring slot stride (doubles): whole DMA rows
+    static constexpr int NMD = 7;                                   // marker dwords staged: s, X[3]
+    static constexpr int PT = 64;                                   // planes per bucket-start table
+    static constexpr int WAIT = PD;                                 // step-start vmcnt: the plane DMA
+};
+
+template <int K> __device__ __forceinline__ int islot(int prel) {
+    using S = ISh<K>;
+    return (int)((unsigned)(prel - S::LO) % (unsigned)S::NSL);  // prel >= LO
+}
+
+// DMA of staged plane z (absolute, clamped into the array) into ring slot
+// `slot`; doff[i] = the lane's array offset (clamped) of dword 64 i + lane.
+template <int K>
+__device__ __forceinline__ void iplane_dma(const CompDesc& cd, double* ring, int slot, int z, const int* doff) {
+    using S = ISh<K>;
+    const int zc = min(max(z, cd.lo[2]), cd.hi[2]);
+    const char* pb = (const char*)(cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2) + 4 * (lane_id() & 1);
+    char* lb = (char*)(ring + slot * S::PVP);
+#pragma unroll
+    for (int i = 0; i < S::PD; ++i) glds4(pb + 8 * (int64_t)doff[i], lb + 256 * i);
+}
+
+// zero the ring entries of plane z (slot) that lie outside the component array
+// (clamped loads brought in neighbours' values): staged zeros keep acc + w*0 ==
+// acc for the clipped stencil points.  okm bit i: dword 64 i + lane in the array.
+template <int K>
+__device__ __forceinline__ void iplane_fix(const CompDesc& cd, double* ring, int slot, int z, unsigned okm) {
+    using S = ISh<K>;
+    const bool zin = z >= cd.lo[2] && z <= cd.hi[2];
+    unsigned* lb = (unsigned*)(ring + slot * S::PVP);
+    const int lane = lane_id();
+#pragma unroll
+    for (int i = 0; i < S::PD; ++i) {
+        const int d = lane + SW * i;
+        if ((S::PDW % SW == 0 || d < S::PDW) && !(zin && ((okm >> i) & 1u))) lb[d] = 0u;
+    }
+}
+
+template <int K>
+__device__ __forceinline__ double interp_marker(const Params& p, const CompDesc& cd, const double* ring, int gx0,
+                                                int gy0, int a, const double* Xs, int s) {
+    using S = ISh<K>;
+    constexpr int W = S::W, FAM = S::FAM, RX = S::RX, PV = S::PVP;  // PV: ring slot stride
+    St<W> st[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const double Xraw = (FAM == 2) ? p.X[(int64_t)3 * s + d] : Xs[d];
+        stencil1d<K>(Xs[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis, p.K6, st[d]);
+    }
+    const int ox = st[0].icl - gx0, oy = st[1].icl - gy0, oz = st[2].icl - p.cg.org[2];
+    // binning invariant: the points read lie in the staged column region and
+    // ring (FAM 0 reads all W per dim, clipped ones as staged zeros)
+    bool ok;
+    if constexpr (FAM == 0) {
+        ok = ox >= 0 && ox + W <= RX && oy >= 0 && oy + W <= S::RY && oz >= a + S::LO && oz + W - 1 <= a + S::HI;
+    } else {
+        bool empty = false;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) empty = empty || st[d].ist > st[d].isp;
+        if (empty) return 0.0;
+        ok = ox + st[0].ist >= 0 && ox + st[0].isp < RX && oy + st[1].ist >= 0 && oy + st[1].isp < S::RY &&
+             oz + st[2].ist >= a + S::LO && oz + st[2].isp <= a + S::HI;
+    }
+    if (!ok) {
+        atomicOr(p.err, 1);
+        return 0.0;
+    }
+    double acc = 0.0;
+    if constexpr (FAM == 3) {
+        acc = ring[islot<K>(oz) * PV + oy * RX + ox];
+    } else if constexpr (FAM == 0) {
+        // Clipped points (outside the ghost box) are staged as 0: acc + (w*wyz)*0
+        // == acc bit for bit (acc is never -0), so the clipped sum of
+        // f.m4:1366-1382 needs no per-point branch.
+        const double* base = ring + oy * RX + ox;
+#pragma unroll
+        for (int i2 = 0; i2 < W; ++i2) {
+            const double* pl = base + islot<K>(oz + i2) * PV;
+#pragma unroll
+            for (int i1 = 0; i1 < W; ++i1) {
+                const double wyz = st[1].w[i1] * st[2].w[i2];  // f.m4:1349-1353
+#pragma unroll
+                for (int i0 = 0; i0 < W; ++i0) {
+                    const double wt = st[0].w[i0] * wyz;
+                    acc = acc + wt * pl[i1 * RX + i0];  // f.m4:1375
+                }
+            }
+        }
+    } else {
+        // piecewise kernels: weights outside [ist, isp] are 0 and the index is
+        // clamped into the stencil's valid range, acc + 0*u == acc.
+        double w[3][W];
+        int o[3][W];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+#pragma unroll
+            for (int i = 0; i < W; ++i) {
+                const bool in = i >= st[d].ist && i <= st[d].isp;
+                w[d][i] = in ? st[d].w[i] : 0.0;
+                o[d][i] = min(max(i, st[d].ist), st[d].isp);
+            }
+        }
+#pragma unroll
+        for (int i2 = 0; i2 < W; ++i2) {
+            const double* pl = ring + islot<K>(oz + o[2][i2]) * PV + oy * RX + ox;
+#pragma unroll
+            for (int i1 = 0; i1 < W; ++i1) {
+#pragma unroll
+                for (int i0 = 0; i0 < W; ++i0)
+                    acc = acc + w[0][i0] * w[1][i1] * w[2][i2] * pl[o[1][i1] * RX + o[0][i0]];  // f.m4:545-548
+            }
+        }
+    }
+    return acc;
+}
+
+
+// Interpolation work item = (segment, column, component).  The item sweeps its
+// anchor planes [a0, a1); the ring holds staged planes a+LO..a+HI plus plane
+// a+HI+1 in flight; the markers of anchor plane a+1 are staged while plane a is
+// summed.  One lane per marker sums its W^3 stencil from the ring (Fortran loop
+// order, bitwise the oracle's).
+template <int K>
+__global__ __launch_bounds__(SW) void k_interp_sweep(Params p) {
+    using S = ISh<K>;
+    constexpr int LO = S::LO, HI = S::HI, RX = S::RX, PD = S::PD, PT = S::PT, NMD = S::NMD;
+    __shared__ double ring[S::NSL * S::PVP];
+    __shared__ unsigned stg[NMD * SW];   // staged markers: [dword][lane]
+    __shared__ int tab[2][PT][2];        // [beg, end) of the column's markers per anchor plane
+    const int nitems = p.cg.ncol * p.nseg * p.ncomp;
+    const int it = sweep_item(nitems);
+    if (it < 0) return;
+    const int c = it % p.ncomp;
+    const int cs = it / p.ncomp;
+    const int col = cs % p.cg.ncol, seg = cs / p.cg.ncol;
+    const int a0 = seg * p.S, a1 = min(a0 + p.S, p.cg.nz);
+    const int lane = lane_id();
+    const int* bs = p.plane_start;
+    {
+        bool any = false;
+        for (int a = a0 + lane; a < a1; a += SW) any = any || bs[bucket(p, a, col, NBAND)] > bs[bucket(p, a, col, 0)];
+        if (!__any(any)) return;
+    }
+    const CompDesc cd = p.comp[c];
+    const int cx = col % p.cg.ncx, cy = col / p.cg.ncx;
+    const int gx0 = p.cg.org[0] + cx * COLX + LO, gy0 = p.cg.org[1] + cy * COLY + LO;
+    const int zorg = p.cg.org[2];
+    const int nlast = p.nsorted - 1;
+    const bool fringe = !(gx0 >= cd.lo[0] && gx0 + RX - 1 <= cd.hi[0] && gy0 >= cd.lo[1] && gy0 + S::RY - 1 <= cd.hi[1]);
+    // per-lane DMA source offsets and in-array bits of the plane's dwords
+    int doff[PD];
+    unsigned okm = 0;
+#pragma unroll
+    for (int i = 0; i < PD; ++i) {
+        const int q = min((lane + SW * i) >> 1, S::PV - 1);
+        const int gxu = gx0 + q % RX, gyu = gy0 + q / RX;
+        const int gx = min(max(gxu, cd.lo[0]), cd.hi[0]), gy = min(max(gyu, cd.lo[1]), cd.hi[1]);
+        doff[i] = (gx - cd.lo[0]) + (gy - cd.lo[1]) * (int)cd.s1;
+        if (gx == gxu && gy == gyu) okm |= 1u << i;
+    }
+    // bucket-start tables: buffer b holds anchor planes [a0 + t PT, a0 + (t+1) PT), b = t & 1
+    auto tab_dma = [&](int t) {
+        const int from = a0 + t * PT;
+        char* lb = (char*)&tab[t & 1][0][0];
+#pragma unroll
+        for (int i = 0; i < (2 * PT + SW - 1) / SW; ++i) {
+            const int d = min(lane + SW * i, 2 * PT - 1);
+            const int a = min(from + (d >> 1), p.cg.nz - 1);
+            glds4(bs + bucket(p, a, col, (d & 1) ? NBAND : 0), lb + 256 * i);
+        }
+    };
+    auto tab_at = [&](int a, int k) { const int r = a - a0; return tab[(r / PT) & 1][r % PT][k]; };
+    // marker staging: sorted position e -> s, X (7 dwords)
+    auto mk_dma = [&](int beg, int cnt) {
+        const int e = min(beg + min(lane, max(cnt - 1, 0)), nlast);
+        glds4(p.sorted_s + e, (char*)stg);
+        const char* xs = (const char*)(p.sorted_X + (int64_t)3 * e);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) glds4(xs + 4 * k, (char*)stg + 256 * (k + 1));
+    };
+    auto mk_get = [&](int j, int& s, double* X) {
+        s = (int)stg[j];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            X[k] = __hiloint2double((int)stg[SW * (2 + 2 * k) + j], (int)stg[SW * (1 + 2 * k) + j]);
+    };
+
+    // prologue, in the steady-state issue order: tables, ring planes, markers of
+    // a0, plane a0+HI+1
+    tab_dma(0);
+    tab_dma(1);
+    wait_vm<0>();
+    for (int k = LO; k <= HI; ++k) iplane_dma<K>(cd, ring, islot<K>(a0 + k), zorg + a0 + k, doff);
+    int cur_n;
+    {
+        const int b = tab_at(a0, 0), e = tab_at(a0, 1);
+        cur_n = min(e - b, SW);
+        mk_dma(b, cur_n);
+    }
+    mem_fence_compiler();
+    const int plast = a1 - 1 + HI;  // last plane the item reads
+    iplane_dma<K>(cd, ring, islot<K>(a0 + HI + 1), zorg + min(a0 + HI + 1, plast), doff);
+    wait_vm<S::WAIT>();
+    if (fringe)
+        for (int k = LO; k <= HI; ++k) iplane_fix<K>(cd, ring, islot<K>(a0 + k), zorg + a0 + k, okm);
+    else
+        for (int k = LO; k <= HI; ++k)
+            if (zorg + a0 + k < cd.lo[2] || zorg + a0 + k > cd.hi[2]) iplane_fix<K>(cd, ring, islot<K>(a0 + k), zorg + a0 + k, okm);
+
+    for (int a = a0; a < a1; ++a) {
+        // step start: markers of a and plane a+HI have landed
+        if (a > a0) {
+            wait_vm<S::WAIT>();
+            const int zn = zorg + a + HI;
+            if (fringe || zn < cd.lo[2] || zn > cd.hi[2]) iplane_fix<K>(cd, ring, islot<K>(a + HI), zn, okm);
+        }
+        const int beg = tab_at(a, 0), end = tab_at(a, 1);
+        // chunk 0 from the staged markers; the value is stored at the end of the step
+        double acc0 = 0.0;
+        int s0 = 0;
+        if (lane < cur_n) {
+            double X[3];
+            mk_get(lane, s0, X);
+            acc0 = interp_marker<K>(p, cd, ring, gx0, gy0, a, X, s0);
+        }
+        // further chunks of a dense plane: staged, waited for and stored here
+        for (int e0 = beg + SW; e0 < end; e0 += SW) {
+            const int n = min(end - e0, SW);
+            mem_fence_compiler();
+            mk_dma(e0, n);
+            wait_vm<0>();
+            if (lane < n) {
+                int s;
+                double X[3];
+                mk_get(lane, s, X);
+                p.Qout[(int64_t)p.Q_depth * s + cd.qcomp] = interp_marker<K>(p, cd, ring, gx0, gy0, a, X, s);
+            }
+            mem_fence_compiler();
+        }
+        // next: this chunk's store, bucket-start table (every PT planes),
+        // markers of a+1, plane a+HI+2 (into the slot plane a+LO leaves).
+        // Stores may complete out of order with loads, so none is issued
+        // between a DMA and the counted wait that relies on it.
+        mem_fence_compiler();
+        {
+            double* dst = lane < cur_n ? p.Qout + ((int64_t)p.Q_depth * s0 + cd.qcomp) : p.sink + lane;
+            *dst = acc0;
+        }
+        mem_fence_compiler();
+        if (a + 1 < a1 && ((a + 1 - a0) % PT) == 0 && a + 1 + PT < a1) tab_dma((a + 1 - a0) / PT + 1);
+        const int nb = a + 1 < a1 ? tab_at(a + 1, 0) : 0;
+        const int nn = a + 1 < a1 ? min(tab_at(a + 1, 1) - nb, SW) : 0;
+        mk_dma(nb, nn);
+        mem_fence_compiler();
+        iplane_dma<K>(cd, ring, islot<K>(a + HI + 2), zorg + min(a + HI + 2, plast), doff);
+        mem_fence_compiler();
+        cur_n = nn;
+    }
+    wait_vm<0>();  // drain the dummy DMAs before the wave's LDS is released
+}
+
+// Entries binned "outside" (no stencil point can reach any array): V = 0.
+__global__ __launch_bounds__(BLOCK) void k_interp_outside_col(Params p, int n) {
+    const int first = p.plane_start[p.cg.nbuckets];
+    for (int e = first + blockIdx.x * BLOCK + threadIdx.x; e < n; e += gridDim.x * BLOCK) {
+        const int s = p.sorted_s[e];
+        for (int c = 0; c < p.ncomp; ++c) p.Qout[(int64_t)p.Q_depth * s + p.comp[c].qcomp] = 0.0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// spreading
+// ---------------------------------------------------------------------------
+template <int K> struct SSh {
+    using T = KT<K>;
+    static constexpr int W = T::W, LO = T::LO, HI = T::HI, FAM = T::FAM;
+    static constexpr int NS = HI - LO + 1;              // planes an anchor plane reaches
+    static constexpr int NSL = NS + 1;                  // ring slots (+1 in flight)
+    static constexpr int PV = COLX * COLY;              // owned points per plane
+    static constexpr int NPL = PV / SW;
+    static constexpr int PD = 2 * PV / SW;              // DMA instructions per plane (one row each)
+    static constexpr int NCD = FAM == 2 ? 9 : 8;        // candidate dwords staged: X[3], V (, s)
+    static constexpr int PT = 8;                        // planes per bucket-start table
+    static constexpr int TW = 3 * 28;                   // table ints per plane
+    static constexpr int TD = (PT * TW + SW - 1) / SW;  // DMA instructions per table
+    static constexpr int NR = 11;                       // candidate ranges per anchor plane
+    static constexpr int WAIT = PD;                     // step-start vmcnt: the plane DMA
+    static constexpr int TRASH = NSL * PV;              // ring offset of the per-lane trash slots
+    static_assert(NS <= 16, "plane field");
+    static_assert(COLX == 32 && COLY >= 8, "32-point rows; bands need COLY >= 8");
+};
+
+// ring plane layout: row-major 32 x COLY (the bank of a point is x mod 32)
+__device__ __forceinline__ int swz(int x, int y) { return y * COLX + x; }
+
+template <int K> __device__ __forceinline__ int sslot(int prel) {
+    using S = SSh<K>;
+    return (int)((unsigned)(prel + 16 * S::NSL) % (unsigned)S::NSL);  // prel >= -HI + LO > -16*NSL
+}
+
+// DMA of plane z (absolute, clamped into the array) of the column's owned
+// points into ring slot `slot`: row y is one instruction, lane = dword
+// (lane & 1) of point x = lane >> 1.  xoff: the lane's clamped x offset.
+template <int K>
+__device__ __forceinline__ void splane_dma(const CompDesc& cd, double* ring, int slot, int z, int Y0,
+                                           int xoff) {
+    using S = SSh<K>;
+    const int zc = min(max(z, cd.lo[2]), cd.hi[2]);
+    const char* pb = (const char*)(cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2) + 4 * (lane_id() & 1);
+    char* lb = (char*)(ring + slot * S::PV);
+#pragma unroll
+    for (int y = 0; y < COLY; ++y) {
+        const int yc = min(max(Y0 + y, cd.lo[1]), cd.hi[1]);
+        glds4(pb + 8 * ((int64_t)(yc - cd.lo[1]) * cd.s1 + xoff), lb + 256 * y);
+    }
+}
+
+// write-back of ring slot `slot` to plane z; lanes of points outside the owned,
+// in-array range (or every lane when !ok) store to p.sink instead
+template <int K>
+__device__ __forceinline__ void splane_store(const Params& p, const CompDesc& cd, const double* ring, int slot, int z,
+                                             bool ok, const int* loff, unsigned okxy) {
+    using S = SSh<K>;
+    const int lane = lane_id();
+    const int zc = min(max(z, cd.lo[2]), cd.hi[2]);
+    double* base = cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2;
+#pragma unroll
+    for (int k = 0; k < S::NPL; ++k) {
+        const int q = lane + k * SW;
+        double* dst = (ok && ((okxy >> k) & 1u)) ? base + loff[k] : p.sink + lane;
+        *dst = ring[slot * S::PV + swz(q & (COLX - 1), q / COLX)];
+    }
+}
+
+// The candidate ranges of anchor plane a for column (cx, cy), in sorted (bucket)
+// order, from the bucket-start table row t[r][i] = bs(a, col(cx-1, cy-1+r), 0) + i
+// (i < 28: bands of columns cx-1, cx, cx+1).  Row cy-1 (south): the markers
+// reaching north (yb = 2); row cy: those reaching the column (west: xb = 2, own:
+// all, east: xb = 0 -- one contiguous range); row cy+1: those reaching south.
+struct Ranges {
+    int start[SSh<K_IB_4>::NR];
+    int pre[SSh<K_IB_4>::NR + 1];
+};
+__device__ __forceinline__ void make_ranges(const int (*t)[28], Ranges& R) {
+    constexpr int NR = SSh<K_IB_4>::NR;
+    // (row, first index, last index + 1) of each range
+    constexpr int rr[NR] = {0, 0, 0, 0, 0, 1, 2, 2, 2, 2, 2};
+    constexpr int ib[NR] = {8, 11, 14, 17, 20, 6, 6, 9, 12, 15, 18};
+    constexpr int ie[NR] = {9, 12, 15, 18, 21, 21, 7, 10, 13, 16, 19};
+    int acc = 0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        R.start[r] = t[rr[r]][ib[r]];
+        R.pre[r] = acc;
+        acc += t[rr[r]][ie[r]] - t[rr[r]][ib[r]];
+    }
+    R.pre[NR] = acc;
+}
+// sorted position of candidate j (< pre[NR])
+__device__ __forceinline__ int range_pos(const Ranges& R, int j) {
+    constexpr int NR = SSh<K_IB_4>::NR;
+    int pos = R.start[0] + j;
+#pragma unroll
+    for (int r = 1; r < NR; ++r)
+        if (j >= R.pre[r]) pos = R.start[r] + (j - R.pre[r]);
+    return pos;
+}
+
+// candidate data of one lane
+struct Cand {
+    double X[3];
+    double V;
+    int s;
+};
+
+// The adds of n <= 64 staged candidates of anchor plane a, one lane per
+// candidate: the lane computes its three 1-D stencils, then walks its W^3
+// points (i2, i1, i0) issuing one ds_add_f64 per point; points outside the
+// owned range, the clipped stencil or the ring go to the lane's trash slot.
+// Within one instruction the lanes that hit the same point add in lane order,
+// so every point receives its contributions in a fixed order (bit-stable).
+template <int K>
+__device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat, int n,
+                                             int a, int X0, int Y0, int xlo, int xhi, int ylo, int yhi, int plo,
+                                             int phi, Clk& clk) {
+    using S = SSh<K>;
+    constexpr int W = S::W, FAM = S::FAM, LO = S::LO, NS = S::NS, NSL = S::NSL;
+    const int lane = lane_id();
+    const bool act = lane < n;
+    St<W> st[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const double Xraw = (FAM == 2) ? p.X[(int64_t)3 * cdat.s + d] : cdat.X[d];
+        stencil1d<K>(cdat.X[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis, p.K6,
+                     st[d]);
+    }
+    int ox = st[0].icl - X0, oy = st[1].icl - Y0, oz = st[2].icl - (p.cg.org[2] + a);
+    bool ok = act;
+    if (act && (ox < -60 || ox > 100 || oy < -60 || oy > 100 || oz < -60 || oz > 60)) {  // binning invariant
+        atomicOr(p.err, 2);
+        ok = false;
+    }
+    if (!ok) ox = oy = oz = 0;
+    const int x0 = max(st[0].ist, xlo - ox), x1 = min(st[0].isp, xhi - ox);
+    const int y0 = max(st[1].ist, ylo - oy), y1 = min(st[1].isp, yhi - oy);
+    int slot = (int)((unsigned)(a + oz + 64 * NSL) % (unsigned)NSL);  // ring slot of plane a + oz
+    const int trash = S::TRASH + lane;
+    const double V = cdat.V;
+    clk.lap(2);
+#pragma unroll
+    for (int i2 = 0; i2 < W; ++i2) {
+        const int k = oz - LO + i2, pr = a + oz + i2;  // plane a + LO + k
+        const bool vz = ok && i2 >= st[2].ist && i2 <= st[2].isp && k >= 0 && k < NS && pr >= plo && pr <= phi;
+        const int zb = slot * S::PV + oy * COLX + ox;
+        double wz;
+        if constexpr (FAM == 0) wz = st[2].w[i2] / p.h3;  // f.m4:1486
+        else wz = st[2].w[i2];
+#pragma unroll
+        for (int i1 = 0; i1 < W; ++i1) {
+            const bool vy = vz && i1 >= y0 && i1 <= y1;
+            const double t = st[1].w[i1] * wz;  // f.m4:1489-1492
+#pragma unroll
+            for (int i0 = 0; i0 < W; ++i0) {
+                const bool v = vy && i0 >= x0 && i0 <= x1;
+                double cv;
+                if constexpr (FAM == 0) cv = (st[0].w[i0] * t) * V;  // f.m4:1512-1513
+                else cv = st[0].w[i0] * t * V / p.h3;  // f.m4:668-672 (FAM 3: V/h3, f.m4:170)
+                const int ad = v ? zb + i1 * COLX + i0 : trash;
+                __hip_atomic_fetch_add(&ring[ad], cv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        if (++slot == NSL) slot = 0;
+    }
+    clk.lap(3);
+}
+
+// Spread work item = (segment, column, component).  Owned points: the column's
+// 32 x COLY (x, y) and planes [p0, p1) of the segment, intersected with the
+// component's ghost box.  Anchor planes a in [p0-HI, p1-1-LO] reach them: the
+// ring holds planes a+LO..a+HI (u_old, then accumulating) plus a+HI+1 in
+// flight; plane a+LO is written back after anchor a and its slot takes plane
+// a+HI+2.  The candidates of anchor a+1 are staged while anchor a is added.
+template <int K>
+__global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
+    using S = SSh<K>;
+    constexpr int LO = S::LO, HI = S::HI, NPL = S::NPL, PT = S::PT, TW = S::TW, NCD = S::NCD;
+    __shared__ double ring[S::NSL * S::PV + SW];  // + per-lane trash slots
+    __shared__ unsigned stg[NCD * SW];  // staged candidates: [dword][lane]
+    __shared__ int tab[2][S::TD * SW / TW + 1][3][28];  // whole DMA rows per buffer
+    const int nitems = p.cg.ncol * p.nseg * p.ncomp;
+    const int it = sweep_item(nitems);
+    if (it < 0) return;
+    const int c = it % p.ncomp;
+    const int cs = it / p.ncomp;
+    const int col = cs % p.cg.ncol, seg = cs / p.cg.ncol;
+    const int lane = lane_id();
+    const int ncx = p.cg.ncx;
+    const int cx = col % ncx, cy = col / ncx;
+    if (cx == 0 || cx == ncx - 1 || cy == 0 || cy == p.cg.ncy - 1) return;  // guard columns own no points
+    const CompDesc cd = p.comp[c];
+    const int X0 = p.cg.org[0] + cx * COLX, Y0 = p.cg.org[1] + cy * COLY;  // absolute
+    const int zorg = p.cg.org[2];
+    // owned, in-array ranges (column-local x/y, relative planes)
+    const int xlo = max(cd.lo[0] - X0, 0), xhi = min(cd.hi[0] - X0, COLX - 1);
+    const int ylo = max(cd.lo[1] - Y0, 0), yhi = min(cd.hi[1] - Y0, COLY - 1);
+    const int plo = max(seg * p.S, cd.lo[2] - zorg), phi = min(min(seg * p.S + p.S, p.cg.nz) - 1, cd.hi[2] - zorg);
+    if (xlo > xhi || ylo > yhi || plo > phi) return;
+    const int afirst = max(plo - HI, 0), alast = min(phi - LO, p.cg.nz - 1);
+    const int* bs = p.plane_start;
+    const int col0 = (cy - 1) * ncx + (cx - 1);  // column (cx-1, cy-1)
+    {
+        bool any = false;  // no candidate reaches the item: u unchanged
+        for (int a = afirst + lane; a <= alast; a += SW)
+            for (int r = 0; r < 3; ++r)
+                any = any || bs[bucket(p, a, col0 + r * ncx, 3 * NBAND)] > bs[bucket(p, a, col0 + r * ncx, 0)];
+        if (!__any(any)) return;
+    }
+    const int nlast = p.nsorted - 1;
+    // write-back offsets and owned bits of the lane's points; DMA x offsets
+    int loff[NPL];
+    unsigned okxy = 0;
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+        const int q = lane + k * SW;
+        const int xl = q & (COLX - 1), yl = q / COLX;
+        if (xl >= xlo && xl <= xhi && yl >= ylo && yl <= yhi) okxy |= 1u << k;
+        const int x = min(max(X0 + xl, cd.lo[0]), cd.hi[0]), y = min(max(Y0 + yl, cd.lo[1]), cd.hi[1]);
+        loff[k] = (x - cd.lo[0]) + (y - cd.lo[1]) * (int)cd.s1;
+    }
+    const int xoff = min(max(X0 + (lane >> 1), cd.lo[0]), cd.hi[0]) - cd.lo[0];
+    // bucket-start tables: buffer t & 1 holds anchor planes [afirst + t PT, afirst + (t+1) PT)
+    auto tab_dma = [&](int t) {
+        const int from = afirst + t * PT;
+        char* lb = (char*)&tab[t & 1][0][0][0];
+#pragma unroll
+        for (int i = 0; i < S::TD; ++i) {
+            const int d = min(lane + SW * i, PT * TW - 1);
+            const int pl = d / TW, r = (d / 28) % 3, k = d % 28;
+            const int a = min(from + pl, p.cg.nz - 1);
+            glds4(bs + bucket(p, a, col0 + r * ncx, 0) + k, lb + 256 * i);
+        }
+    };
+    auto tab_row = [&](int a) {
+        const int r = a - afirst;
+        return (const int(*)[28])tab[(r / PT) & 1][r % PT];
+    };
+    // candidate staging: lane j <- candidate j0 + j of the ranges (clamped)
+    auto cand_dma = [&](const Ranges& rg, int j0) {
+        const int e = min(range_pos(rg, j0 + lane), nlast);
+        const char* xs = (const char*)(p.sorted_X + (int64_t)3 * e);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) glds4(xs + 4 * k, (char*)stg + 256 * k);
+        const char* fs = (const char*)(p.sorted_F + (int64_t)c * p.nsorted + e);
+        glds4(fs, (char*)stg + 256 * 6);
+        glds4(fs + 4, (char*)stg + 256 * 7);
+        if constexpr (NCD == 9) glds4(p.sorted_s + e, (char*)stg + 256 * 8);
+    };
+    auto cand_get = [&](int j, Cand& d) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            d.X[k] = __hiloint2double((int)stg[SW * (2 * k + 1) + j], (int)stg[SW * (2 * k) + j]);
+        d.V = __hiloint2double((int)stg[SW * 7 + j], (int)stg[SW * 6 + j]);
+        d.s = NCD == 9 ? (int)stg[SW * 8 + j] : 0;
+    };
+    Clk clk;
+    auto process = [&](int a, int n) {  // n <= SW staged candidates
+        Cand d;
+        cand_get(lane, d);
+        spread_lanes<K>(p, cd, ring, d, n, a, X0, Y0, xlo, xhi, ylo, yhi, plo, phi, clk);
+    };
+
+    clk.start(p.stamps != nullptr);
+    // prologue, in the steady-state issue order: tables; ring planes; the
+    // candidates of afirst; (dummy plane stores); plane afirst+HI+1
+    tab_dma(0);
+    tab_dma(1);
+    wait_vm<0>();
+    for (int k = LO; k <= HI; ++k) splane_dma<K>(cd, ring, sslot<K>(afirst + k), zorg + afirst + k, Y0, xoff);
+    Ranges rg;
+    make_ranges(tab_row(afirst), rg);
+    int total = rg.pre[S::NR];
+    cand_dma(rg, 0);
+    mem_fence_compiler();
+    splane_dma<K>(cd, ring, sslot<K>(afirst + HI + 1), zorg + afirst + HI + 1, Y0, xoff);
+    mem_fence_compiler();
+
+    clk.lap(0);
+    for (int a = afirst; a <= alast; ++a) {
+        wait_vm<S::WAIT>();  // candidates of a and plane a+HI have landed
+        clk.lap(1);
+        process(a, min(total, SW));
+        for (int j0 = SW; j0 < total; j0 += SW) {  // dense planes: stage, wait, add
+            mem_fence_compiler();
+            cand_dma(rg, j0);
+            wait_vm<0>();
+            process(a, min(total - j0, SW));
+        }
+        // next: write-back of plane a+LO, table (every PT planes), candidates of
+        // a+1, plane a+HI+2 into the freed slot.  Stores may complete out of
+        // order with loads, so none is issued between a DMA and the counted
+        // wait that relies on it.
+        mem_fence_compiler();
+        const int pout = a + LO;
+        splane_store<K>(p, cd, ring, sslot<K>(pout), zorg + pout, pout >= plo && pout <= phi, loff, okxy);
+        mem_fence_compiler();
+        if (a + 1 <= alast) {
+            const int t = (a + 1 - afirst) / PT;
+            if ((a + 1 - afirst) % PT == 0 && afirst + (t + 1) * PT <= alast) tab_dma(t + 1);
+            make_ranges(tab_row(a + 1), rg);
+            total = rg.pre[S::NR];
+        } else {
+            total = 0;
+        }
+        cand_dma(rg, 0);
+        mem_fence_compiler();
+        splane_dma<K>(cd, ring, sslot<K>(a + HI + 2), zorg + a + HI + 2, Y0, xoff);
+        mem_fence_compiler();
+        clk.lap(4);
+    }
+    wait_vm<0>();  // drain the trailing DMAs before the wave's LDS is released
+    clk.lap(5);
+    clk.flush(p, it);
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+// Segment length: about 8192 (column, segment) items over the patch, but no
+// segment shorter than 32 planes (the z halo of a segment is HI-LO planes).
+void sweep_segments(const ColGeom& cg, int& S, int& nseg) {
+    long long want = 8192;
+    long long s = ((long long)cg.nz * cg.ncol + want - 1) / want;
+    if (s < 32) s = 32;
+    if (s > cg.nz) s = cg.nz;
+    if (s < 1) s = 1;
+    S = (int)s;
+    nseg = (cg.nz + S - 1) / S;
+}
+
+static int grid8(long items) { return (int)((items + 7) & ~7L); }
+
+template <int K> hipError_t launch_bin_col_t(const Params& p, int n, unsigned* keys, int* vals, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_bin_col<K>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, keys, vals);
+    return hipGetLastError();
+}
+template <int K>
+hipError_t launch_gather_col_t(const Params& p, int n, int* ss, double* sx, unsigned* sa, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gather_col<K>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, ss, sx, sa);
+    return hipGetLastError();
+}
+template <int K>
+hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    if (ev0) (void)hipEventRecord(ev0, s);
+    const long items = (long)p.cg.ncol * p.nseg * p.ncomp;
+    if (items > 0) hipLaunchKernelGGL(k_interp_sweep<K>, dim3(grid8(items)), dim3(SW), 0, s, p);
+    if (ev1) (void)hipEventRecord(ev1, s);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (n > 0) hipLaunchKernelGGL(k_interp_outside_col, dim3(64), dim3(BLOCK), 0, s, p, n);
+    return hipGetLastError();
+}
+// sorted_F[c * n + e] = Q(qcomp_c, s(e)): the spread values in sorted order
+__global__ __launch_bounds__(BLOCK) void k_gather_F_col(Params p, int n, double* out) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= n) return;
+    const int s = p.sorted_s[e];
+    for (int c = 0; c < p.ncomp; ++c) out[(int64_t)c * n + e] = p.Qin[(int64_t)p.Q_depth * s + p.comp[c].qcomp];
+}
+
+template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    if (ev0) (void)hipEventRecord(ev0, s);
+    if (p.nsorted > 0)
+        hipLaunchKernelGGL(k_gather_F_col, dim3((p.nsorted + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, p.nsorted,
+                           const_cast<double*>(p.sorted_F));
+    const long items = (long)p.cg.ncol * p.nseg * p.ncomp;
+    if (items > 0) hipLaunchKernelGGL(k_spread_sweep<K>, dim3(grid8(items)), dim3(SW), 0, s, p);
+    if (ev1) (void)hipEventRecord(ev1, s);
+    return hipGetLastError();
+}
+
+#define IBTK_LE_DISPATCH_K(KV, CALL)                                 \
+    switch (KV) {                                                    \
+    case K_PIECEWISE_CONSTANT: return CALL<K_PIECEWISE_CONSTANT>;    \
+    case K_DISCONTINUOUS_LINEAR: return CALL<K_DISCONTINUOUS_LINEAR>; \
+    case K_PIECEWISE_LINEAR: return CALL<K_PIECEWISE_LINEAR>;        \
+    case K_PIECEWISE_CUBIC: return CALL<K_PIECEWISE_CUBIC>;          \
+    case K_IB_3: return CALL<K_IB_3>;                                \
+    case K_IB_4: return CALL<K_IB_4>;                                \
+    case K_IB_4_W8: return CALL<K_IB_4_W8>;                          \
+    case K_IB_6: return CALL<K_IB_6>;                                \
+    case K_BSPLINE_4: return CALL<K_BSPLINE_4>;                      \
+    default: return nullptr;                                         \
+    }
+
+using BinColFn = hipError_t (*)(const Params&, int, unsigned*, int*, hipStream_t);
+using GatherColFn = hipError_t (*)(const Params&, int, int*, double*, unsigned*, hipStream_t);
+using InterpSwFn = hipError_t (*)(const Params&, int, hipStream_t, hipEvent_t, hipEvent_t);
+using SpreadSwFn = hipError_t (*)(const Params&, hipStream_t, hipEvent_t, hipEvent_t);
+static BinColFn pick_bin_col(int k) { IBTK_LE_DISPATCH_K(k, launch_bin_col_t) }
+static GatherColFn pick_gather_col(int k) { IBTK_LE_DISPATCH_K(k, launch_gather_col_t) }
+static InterpSwFn pick_interp_sweep(int k) { IBTK_LE_DISPATCH_K(k, launch_interp_sweep_t) }
+static SpreadSwFn pick_spread_sweep(int k) { IBTK_LE_DISPATCH_K(k, launch_spread_sweep_t) }
+
+hipError_t launch_bin_col(int kernel, const Params& p, int n, unsigned* keys, int* vals, hipStream_t s) {
+    BinColFn f = pick_bin_col(kernel);
+    return f ? f(p, n, keys, vals, s) : hipErrorInvalidValue;
+}
+hipError_t launch_gather_col(int kernel, const Params& p, int n, int* sorted_s, double* sorted_X, unsigned* sorted_a,
+                             hipStream_t s) {
+    GatherColFn f = pick_gather_col(kernel);
+    return f ? f(p, n, sorted_s, sorted_X, sorted_a, s) : hipErrorInvalidValue;
+}
+hipError_t launch_interp_sweep(int kernel, const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    InterpSwFn f = pick_interp_sweep(kernel);
+    return f ? f(p, n, s, ev0, ev1) : hipErrorInvalidValue;
+}
+hipError_t launch_spread_sweep(int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    SpreadSwFn f = pick_spread_sweep(kernel);
+    return f ? f(p, s, ev0, ev1) : hipErrorInvalidValue;
+}
+
+}  // namespace ibtk_le
