@@ -564,6 +564,28 @@ __device__ __forceinline__ int range_pos(const Ranges& R, int j) {
     return pos;
 }
 
+// Lane assignment of the staged candidates.  A ds_add_f64 runs as four 16-lane
+// quarters, each costing about the largest number of its lanes whose f64 index
+// agrees mod 16 (tools/ubench_lds2.hip); a ring point's index mod 16 is its x
+// mod 16 (rows are 32 doubles).  The candidates are ranked by that class
+// (stable in staging order; inactive lanes last) and dealt round-robin over
+// the quarters, so the candidates of one class land in different quarters.
+// Returns the staged index this lane processes.
+__device__ __forceinline__ int deal_lanes(int cls) {  // cls in [0, 16]; 32 = inactive
+    const int lane = __lane_id();
+    unsigned long long eq = ~0ull, lt = 0ull;
+#pragma unroll
+    for (int b = 5; b >= 0; --b) {
+        const bool bit = (cls >> b) & 1;
+        const unsigned long long m = __ballot(bit);
+        lt |= bit ? (eq & ~m) : 0ull;
+        eq &= bit ? m : ~m;
+    }
+    const int k = __popcll(lt) + __popcll(eq & ((1ull << lane) - 1ull));  // rank
+    const int t = ((k & 3) << 4) | (k >> 2);                               // dealt lane
+    return __builtin_amdgcn_ds_permute(t << 2, lane);
+}
+
 // candidate data of one lane
 struct Cand {
     double X[3];
@@ -573,18 +595,18 @@ struct Cand {
 
 // The adds of n <= 64 staged candidates of anchor plane a, one lane per
 // candidate: the lane computes its three 1-D stencils, then walks its W^3
-// points (i2, i1, i0) issuing one ds_add_f64 per point; points outside the
-// owned range, the clipped stencil or the ring go to the lane's trash slot.
+// points (i2, i1, i0) issuing one ds_add_f64 per point (lanes whose point is
+// outside the owned range, the clipped stencil or the ring add to their trash
+// slot: a branch per add would make the compiler wait for every LDS operation
+// in flight before each one).
 // Within one instruction the lanes that hit the same point add in lane order,
 // so every point receives its contributions in a fixed order (bit-stable).
 template <int K>
-__device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat, int n,
-                                             int a, int X0, int Y0, int xlo, int xhi, int ylo, int yhi, int plo,
+__device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
+                                             bool act, int a, int X0, int Y0, int xlo, int xhi, int ylo, int yhi, int plo,
                                              int phi, Clk& clk) {
     using S = SSh<K>;
     constexpr int W = S::W, FAM = S::FAM, LO = S::LO, NS = S::NS, NSL = S::NSL;
-    const int lane = lane_id();
-    const bool act = lane < n;
     St<W> st[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
@@ -602,7 +624,7 @@ __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd
     const int x0 = max(st[0].ist, xlo - ox), x1 = min(st[0].isp, xhi - ox);
     const int y0 = max(st[1].ist, ylo - oy), y1 = min(st[1].isp, yhi - oy);
     int slot = (int)((unsigned)(a + oz + 64 * NSL) % (unsigned)NSL);  // ring slot of plane a + oz
-    const int trash = S::TRASH + lane;
+    const int trash = S::TRASH + lane_id();
     const double V = cdat.V;
     clk.lap(2);
 #pragma unroll
@@ -721,10 +743,17 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         d.s = NCD == 9 ? (int)stg[SW * 8 + j] : 0;
     };
     Clk clk;
+    const double inv_dx = 1.0 / p.bg.dx[0];  // lane dealing only (approximate class)
     auto process = [&](int a, int n) {  // n <= SW staged candidates
+        int cls = 32;
+        if (lane < n) {
+            const double x = __hiloint2double((int)stg[SW + lane], (int)stg[lane]);
+            cls = (int)floor((x - cd.xlo[0]) * inv_dx + 0.5) & 15;
+        }
+        const int src = deal_lanes(cls);
         Cand d;
-        cand_get(lane, d);
-        spread_lanes<K>(p, cd, ring, d, n, a, X0, Y0, xlo, xhi, ylo, yhi, plo, phi, clk);
+        cand_get(src, d);
+        spread_lanes<K>(p, cd, ring, d, src < n, a, X0, Y0, xlo, xhi, ylo, yhi, plo, phi, clk);
     };
 
     clk.start(p.stamps != nullptr);

@@ -101,9 +101,9 @@ int ibtk_le_ctx_synchronize(ibtk_le_ctx ctx);
  * (LEInteractor.cpp:3031-3108) hands to the Fortran: it takes the list of
  * (local marker index, periodic shift) pairs -- `indices_dev`/`Xshift_dev`, or
  * NULL/NULL for the identity list 0..n-1 with zero shifts -- and sorts it on the
- * device by the stencil anchor cell of X(s)+Xshift (stable radix sort; bins of
- * 8^3 cells in 3-D, 16^2 in 2-D).  The sorted order is the canonical order
- * spreading sums in.  The handle keeps device copies of the sorted list. */
+ * device by the stencil anchor cell of X(s)+Xshift (stable radix sort; 3-D:
+ * buckets of (anchor plane, 32x16-cell column, reach band); 2-D: bricks of 16^2
+ * cells).  The handle keeps device copies of the sorted list. */
 int ibtk_le_markers_create(ibtk_le_ctx ctx, ibtk_le_markers* out);
 int ibtk_le_markers_destroy(ibtk_le_markers m);
 int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_patch_geom* geom, int kernel,
@@ -127,8 +127,9 @@ int ibtk_le_markers_order(ibtk_le_markers m, const int** order_dev);
  * interp:  Q(d, s) = sum_i w_i(X(s)+Xshift) q(i, d)   for every listed s
  *          (LEInteractor.cpp:970-1055 / lagrangian_<k>_interp3d, f.m4:1258-1385)
  * spread:  q(i, d) += sum_s w_i(X(s)+Xshift) Q(d, s) / (dx0 dx1 [dx2])
- *          summed per grid point in the list's canonical (binned) order, without
- *          atomics: deterministic and bit-stable run to run
+ *          summed per grid point in a fixed order (work-item-private LDS
+ *          accumulation, no global atomics): deterministic and bit-stable run
+ *          to run
  *          (LEInteractor.cpp:1828-1913 / lagrangian_<k>_spread3d, f.m4:1395-1522) */
 int ibtk_le_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                    const ibtk_le_patch_geom* geom, const double* const* q_dev, int q_depth, double* Q_dev,
