@@ -619,6 +619,8 @@ extern "C" int ibtk_le_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, in
         if (int rc = make_comps(geom, centering, axis, q_dev, q_depth, Q_depth, first, cnt, p)) return rc;
         const bool t = ctx->timing && first == 0;
         const char* dbg = getenv("IBTK_LE_STAMPS");
+        const char* dmode = getenv("IBTK_LE_DBG");  // diagnostics: variants of the add loop
+        p.dbg = dmode ? atoi(dmode) : 0;
         const size_t nst = (size_t)m->cg.ncol * m->nseg * cnt * 8;
         if (geom->ndim == 3 && dbg && dbg[0] == '1') {
             if (int rc = ctx->stamps.ensure(nst * sizeof(unsigned long long))) return rc;

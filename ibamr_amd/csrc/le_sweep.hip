@@ -473,17 +473,22 @@ template <int K> struct SSh {
     using T = KT<K>;
     static constexpr int W = T::W, LO = T::LO, HI = T::HI, FAM = T::FAM;
     static constexpr int NS = HI - LO + 1;              // planes an anchor plane reaches
-    static constexpr int NSL = NS + 1;                  // ring slots (+1 in flight)
+    static constexpr int NSL = NS;                      // ring slots: the planes one anchor reaches
     static constexpr int PV = COLX * COLY;              // owned points per plane
     static constexpr int NPL = PV / SW;
     static constexpr int PD = 2 * PV / SW;              // DMA instructions per plane (one row each)
     static constexpr int NCD = FAM == 2 ? 9 : 8;        // candidate dwords staged: X[3], V (, s)
-    static constexpr int PT = 8;                        // planes per bucket-start table
+    static constexpr int PT = 4;                        // planes per bucket-start table
     static constexpr int TW = 3 * 28;                   // table ints per plane
     static constexpr int TD = (PT * TW + SW - 1) / SW;  // DMA instructions per table
     static constexpr int NR = 11;                       // candidate ranges per anchor plane
     static constexpr int WAIT = PD;                     // step-start vmcnt: the plane DMA
-    static constexpr int TRASH = NSL * PV;              // ring offset of the per-lane trash slots
+    // ring slot stride: a 16-double gap after each plane takes the spill of the
+    // zero-weight adds of stencil columns that stick out of the column (x in
+    // [-3, 34] of rows 0..COLY-1); a multiple of 16 keeps every point's bank
+    // class = its x mod 16.  GUARD doubles before slot 0 take its low spill.
+    static constexpr int SLOT = PV + 16;
+    static constexpr int GUARD = 16;
     static_assert(NS <= 16, "plane field");
     static_assert(COLX == 32 && COLY >= 8, "32-point rows; bands need COLY >= 8");
 };
@@ -505,7 +510,7 @@ __device__ __forceinline__ void splane_dma(const CompDesc& cd, double* ring, int
     using S = SSh<K>;
     const int zc = min(max(z, cd.lo[2]), cd.hi[2]);
     const char* pb = (const char*)(cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2) + 4 * (lane_id() & 1);
-    char* lb = (char*)(ring + slot * S::PV);
+    char* lb = (char*)(ring + slot * S::SLOT);
 #pragma unroll
     for (int y = 0; y < COLY; ++y) {
         const int yc = min(max(Y0 + y, cd.lo[1]), cd.hi[1]);
@@ -526,7 +531,7 @@ __device__ __forceinline__ void splane_store(const Params& p, const CompDesc& cd
     for (int k = 0; k < S::NPL; ++k) {
         const int q = lane + k * SW;
         double* dst = (ok && ((okxy >> k) & 1u)) ? base + loff[k] : p.sink + lane;
-        *dst = ring[slot * S::PV + swz(q & (COLX - 1), q / COLX)];
+        *dst = ring[slot * S::SLOT + swz(q & (COLX - 1), q / COLX)];
     }
 }
 
@@ -586,6 +591,14 @@ __device__ __forceinline__ int deal_lanes(int cls) {  // cls in [0, 16]; 32 = in
     return __builtin_amdgcn_ds_permute(t << 2, lane);
 }
 
+// value of lane `src` (ds_bpermute on the two halves)
+__device__ __forceinline__ double shfl_f64(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b & 0xffffffffll));
+    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b >> 32));
+    return __hiloint2double(hi, lo);
+}
+
 // candidate data of one lane
 struct Cand {
     double X[3];
@@ -595,18 +608,24 @@ struct Cand {
 
 // The adds of n <= 64 staged candidates of anchor plane a, one lane per
 // candidate: the lane computes its three 1-D stencils, then walks its W^3
-// points (i2, i1, i0) issuing one ds_add_f64 per point (lanes whose point is
-// outside the owned range, the clipped stencil or the ring add to their trash
-// slot: a branch per add would make the compiler wait for every LDS operation
-// in flight before each one).
+// points (i2, i1, i0) issuing one ds_add_f64 per point.  A point outside the
+// owned range, the clipped stencil or the segment is added with weight 0 at a
+// harmless in-ring address: its row clamped into the column, its plane into
+// the live window, x left to spill (the slot gaps take it); an idle lane does
+// the same at its own x.  So an add is one multiply and one ds_add_f64 with an
+// immediate offset -- no mask, no select and no branch (a branch per add
+// makes the compiler wait for every LDS operation in flight before each one).
+// Adding +-0 changes no value, except that a -0.0 it lands on becomes +0.0.
+// Every lane's address moves by the same amount from one add to the next, so
+// lanes dealt to distinct bank classes stay conflict-free for all W^3 adds.
 // Within one instruction the lanes that hit the same point add in lane order,
 // so every point receives its contributions in a fixed order (bit-stable).
 template <int K>
 __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
                                              bool act, int a, int X0, int Y0, int xlo, int xhi, int ylo, int yhi, int plo,
-                                             int phi, Clk& clk) {
+                                             int phi, double inv_h3, Clk& clk) {
     using S = SSh<K>;
-    constexpr int W = S::W, FAM = S::FAM, LO = S::LO, NS = S::NS, NSL = S::NSL;
+    constexpr int W = S::W, FAM = S::FAM, LO = S::LO, HI = S::HI, NS = S::NS, NSL = S::NSL;
     St<W> st[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
@@ -616,41 +635,60 @@ __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd
     }
     int ox = st[0].icl - X0, oy = st[1].icl - Y0, oz = st[2].icl - (p.cg.org[2] + a);
     bool ok = act;
-    if (act && (ox < -60 || ox > 100 || oy < -60 || oy > 100 || oz < -60 || oz > 60)) {  // binning invariant
+    // binning invariant (and the memory bound of the spill: x in [-16, COLX + 15])
+    if (act && (ox < -S::GUARD || ox > COLX + 15 - (W - 1) || oy < -60 || oy > 60 || oz < -60 || oz > 60)) {
         atomicOr(p.err, 2);
         ok = false;
     }
-    if (!ok) ox = oy = oz = 0;
-    const int x0 = max(st[0].ist, xlo - ox), x1 = min(st[0].isp, xhi - ox);
-    const int y0 = max(st[1].ist, ylo - oy), y1 = min(st[1].isp, yhi - oy);
-    int slot = (int)((unsigned)(a + oz + 64 * NSL) % (unsigned)NSL);  // ring slot of plane a + oz
-    const int trash = S::TRASH + lane_id();
-    const double V = cdat.V;
+    if (!ok) {  // idle: weight 0 at a lane-distinct x
+        ox = lane_id() & 15;
+        oy = oz = 0;
+    }
+    // x: weight x value with the mask folded in (f.m4:1512-1513 order, V applied
+    // first: within rounding of the Fortran's (w0 (w1 w2/h)) V)
+    double w0v[W];
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        const bool vx = ok && i >= st[0].ist && i <= st[0].isp && ox + i >= xlo && ox + i <= xhi;
+        w0v[i] = vx ? st[0].w[i] * cdat.V : 0.0;
+    }
+    char* const base = reinterpret_cast<char*>(ring) + 8 * ox;
+    double dsum = 0.0;
     clk.lap(2);
 #pragma unroll
     for (int i2 = 0; i2 < W; ++i2) {
         const int k = oz - LO + i2, pr = a + oz + i2;  // plane a + LO + k
-        const bool vz = ok && i2 >= st[2].ist && i2 <= st[2].isp && k >= 0 && k < NS && pr >= plo && pr <= phi;
-        const int zb = slot * S::PV + oy * COLX + ox;
+        const bool vz = i2 >= st[2].ist && i2 <= st[2].isp && k >= 0 && k < NS && pr >= plo && pr <= phi;
+        const int prc = min(max(pr, a + LO), a + HI);  // a live plane of the ring
+        const int zb = (int)((unsigned)(prc + 64 * NSL) % (unsigned)NSL) * (8 * S::SLOT);
         double wz;
-        if constexpr (FAM == 0) wz = st[2].w[i2] / p.h3;  // f.m4:1486
-        else wz = st[2].w[i2];
+        if constexpr (FAM == 0) wz = st[2].w[i2] * inv_h3;  // f.m4:1486
+        else wz = st[2].w[i2] * inv_h3;
 #pragma unroll
         for (int i1 = 0; i1 < W; ++i1) {
-            const bool vy = vz && i1 >= y0 && i1 <= y1;
-            const double t = st[1].w[i1] * wz;  // f.m4:1489-1492
+            const bool vr = vz && i1 >= st[1].ist && i1 <= st[1].isp && oy + i1 >= ylo && oy + i1 <= yhi;
+            const double t = vr ? st[1].w[i1] * wz : 0.0;  // f.m4:1489-1492
+            double* const row =
+                reinterpret_cast<double*>(base + zb + 8 * COLX * min(max(oy + i1, 0), COLY - 1));
+            if (p.dbg == 1) {  // diagnostics: no LDS traffic
 #pragma unroll
-            for (int i0 = 0; i0 < W; ++i0) {
-                const bool v = vy && i0 >= x0 && i0 <= x1;
-                double cv;
-                if constexpr (FAM == 0) cv = (st[0].w[i0] * t) * V;  // f.m4:1512-1513
-                else cv = st[0].w[i0] * t * V / p.h3;  // f.m4:668-672 (FAM 3: V/h3, f.m4:170)
-                const int ad = v ? zb + i1 * COLX + i0 : trash;
-                __hip_atomic_fetch_add(&ring[ad], cv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                for (int i0 = 0; i0 < W; ++i0) dsum += w0v[i0] * t;
+            } else if (p.dbg == 2) {  // diagnostics: conflict-free addresses
+                double* r2 = ring + lane_id() + 64 * i1;
+#pragma unroll
+                for (int i0 = 0; i0 < W; ++i0)
+                    __hip_atomic_fetch_add(r2 + 256 * i0, w0v[i0] * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if (p.dbg == 3) {  // diagnostics: plain stores instead of atomics
+#pragma unroll
+                for (int i0 = 0; i0 < W; ++i0) row[i0] = w0v[i0] * t;
+            } else {
+#pragma unroll
+                for (int i0 = 0; i0 < W; ++i0)
+                    __hip_atomic_fetch_add(row + i0, w0v[i0] * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
-        if (++slot == NSL) slot = 0;
     }
+    if (p.dbg == 1 && dsum == 12345.678) ring[0] = dsum;  // keep the diagnostic sum alive
     clk.lap(3);
 }
 
@@ -663,9 +701,9 @@ __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd
 template <int K>
 __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     using S = SSh<K>;
-    constexpr int LO = S::LO, HI = S::HI, NPL = S::NPL, PT = S::PT, TW = S::TW, NCD = S::NCD;
-    __shared__ double ring[S::NSL * S::PV + SW];  // + per-lane trash slots
-    __shared__ unsigned stg[NCD * SW];  // staged candidates: [dword][lane]
+    constexpr int LO = S::LO, HI = S::HI, NS = S::NS, NPL = S::NPL, PT = S::PT, TW = S::TW, FAM = S::FAM;
+    __shared__ double ring_mem[S::GUARD + S::NSL * S::SLOT];
+    double* const ring = ring_mem + S::GUARD;
     __shared__ int tab[2][S::TD * SW / TW + 1][3][28];  // whole DMA rows per buffer
     const int nitems = p.cg.ncol * p.nseg * p.ncomp;
     const int it = sweep_item(nitems);
@@ -696,7 +734,8 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         if (!__any(any)) return;
     }
     const int nlast = p.nsorted - 1;
-    // write-back offsets and owned bits of the lane's points; DMA x offsets
+    // the lane's points q = lane + 64 k of a plane: array offsets (clamped into
+    // the array) and owned bits
     int loff[NPL];
     unsigned okxy = 0;
 #pragma unroll
@@ -707,8 +746,12 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         const int x = min(max(X0 + xl, cd.lo[0]), cd.hi[0]), y = min(max(Y0 + yl, cd.lo[1]), cd.hi[1]);
         loff[k] = (x - cd.lo[0]) + (y - cd.lo[1]) * (int)cd.s1;
     }
-    const int xoff = min(max(X0 + (lane >> 1), cd.lo[0]), cd.hi[0]) - cd.lo[0];
-    // bucket-start tables: buffer t & 1 holds anchor planes [afirst + t PT, afirst + (t+1) PT)
+    auto plane_ptr = [&](int z) {  // relative plane z, clamped into the array
+        const int zc = min(max(zorg + z, cd.lo[2]), cd.hi[2]);
+        return cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2;
+    };
+    // bucket-start tables by LDS-DMA: buffer t & 1 holds anchor planes
+    // [afirst + t PT, afirst + (t+1) PT), issued PT planes ahead
     auto tab_dma = [&](int t) {
         const int from = afirst + t * PT;
         char* lb = (char*)&tab[t & 1][0][0][0];
@@ -724,87 +767,106 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         const int r = a - afirst;
         return (const int(*)[28])tab[(r / PT) & 1][r % PT];
     };
-    // candidate staging: lane j <- candidate j0 + j of the ranges (clamped)
-    auto cand_dma = [&](const Ranges& rg, int j0) {
+    // candidate j0 + lane of the ranges (clamped to a valid entry)
+    auto cand_load = [&](const Ranges& rg, int j0, Cand& d) {
         const int e = min(range_pos(rg, j0 + lane), nlast);
-        const char* xs = (const char*)(p.sorted_X + (int64_t)3 * e);
-#pragma unroll
-        for (int k = 0; k < 6; ++k) glds4(xs + 4 * k, (char*)stg + 256 * k);
-        const char* fs = (const char*)(p.sorted_F + (int64_t)c * p.nsorted + e);
-        glds4(fs, (char*)stg + 256 * 6);
-        glds4(fs + 4, (char*)stg + 256 * 7);
-        if constexpr (NCD == 9) glds4(p.sorted_s + e, (char*)stg + 256 * 8);
-    };
-    auto cand_get = [&](int j, Cand& d) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-            d.X[k] = __hiloint2double((int)stg[SW * (2 * k + 1) + j], (int)stg[SW * (2 * k) + j]);
-        d.V = __hiloint2double((int)stg[SW * 7 + j], (int)stg[SW * 6 + j]);
-        d.s = NCD == 9 ? (int)stg[SW * 8 + j] : 0;
+        const double* xs = p.sorted_X + (int64_t)3 * e;
+        d.X[0] = xs[0];
+        d.X[1] = xs[1];
+        d.X[2] = xs[2];
+        d.V = p.sorted_F[(int64_t)c * p.nsorted + e];
+        d.s = FAM == 2 ? p.sorted_s[e] : 0;
     };
     Clk clk;
     const double inv_dx = 1.0 / p.bg.dx[0];  // lane dealing only (approximate class)
-    auto process = [&](int a, int n) {  // n <= SW staged candidates
-        int cls = 32;
-        if (lane < n) {
-            const double x = __hiloint2double((int)stg[SW + lane], (int)stg[lane]);
-            cls = (int)floor((x - cd.xlo[0]) * inv_dx + 0.5) & 15;
-        }
+    const double inv_h3 = 1.0 / p.h3;
+    // adds of the n <= 64 candidates held one per lane: dealt over the lanes by
+    // bank class, then spread
+    auto process = [&](int a, int n, const Cand& mine) {
+        const int cls = lane < n ? ((int)floor((mine.X[0] - cd.xlo[0]) * inv_dx + 0.5) & 15) : 32;
         const int src = deal_lanes(cls);
         Cand d;
-        cand_get(src, d);
-        spread_lanes<K>(p, cd, ring, d, src < n, a, X0, Y0, xlo, xhi, ylo, yhi, plo, phi, clk);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) d.X[k] = shfl_f64(mine.X[k], src);
+        d.V = shfl_f64(mine.V, src);
+        d.s = FAM == 2 ? __builtin_amdgcn_ds_bpermute(src << 2, mine.s) : 0;
+        spread_lanes<K>(p, cd, ring, d, src < n, a, X0, Y0, xlo, xhi, ylo, yhi, plo, phi, inv_h3, clk);
+    };
+    // plane z -> registers (the lane's NPL points); registers -> ring slot
+    auto plane_load = [&](int z, double* v) {
+        const double* pb = plane_ptr(z);
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) v[k] = pb[loff[k]];
+    };
+    auto plane_put = [&](int z, const double* v) {
+        double* sl = ring + sslot<K>(z) * S::SLOT;
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) sl[lane + k * SW] = v[k];
+    };
+    auto plane_writeback = [&](int z) {  // owned points of plane z, ring -> array
+        if (z < plo || z > phi) return;
+        const double* sl = ring + sslot<K>(z) * S::SLOT;
+        double* pb = const_cast<double*>(plane_ptr(z));
+        double v[NPL];
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) v[k] = sl[lane + k * SW];
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) {  // not-owned points store to the sink: no branch per store
+            double* dst = ((okxy >> k) & 1u) ? pb + loff[k] : p.sink + lane;
+            *dst = v[k];
+        }
     };
 
     clk.start(p.stamps != nullptr);
-    // prologue, in the steady-state issue order: tables; ring planes; the
-    // candidates of afirst; (dummy plane stores); plane afirst+HI+1
+    // prologue: tables; planes afirst+LO .. afirst+HI-1 into the ring; plane
+    // afirst+HI and the candidates of afirst into registers
     tab_dma(0);
     tab_dma(1);
     wait_vm<0>();
-    for (int k = LO; k <= HI; ++k) splane_dma<K>(cd, ring, sslot<K>(afirst + k), zorg + afirst + k, Y0, xoff);
+    double pv[NPL];
+    for (int z = afirst + LO; z < afirst + HI; ++z) {
+        plane_load(z, pv);
+        plane_put(z, pv);
+    }
+    plane_load(afirst + HI, pv);
     Ranges rg;
     make_ranges(tab_row(afirst), rg);
     int total = rg.pre[S::NR];
-    cand_dma(rg, 0);
-    mem_fence_compiler();
-    splane_dma<K>(cd, ring, sslot<K>(afirst + HI + 1), zorg + afirst + HI + 1, Y0, xoff);
-    mem_fence_compiler();
-
+    Cand nxt;
+    cand_load(rg, 0, nxt);
     clk.lap(0);
     for (int a = afirst; a <= alast; ++a) {
-        wait_vm<S::WAIT>();  // candidates of a and plane a+HI have landed
+        // top: plane a+LO-1 leaves the window (written back), plane a+HI takes
+        // its slot; the staged candidates of a become current
+        if (a > afirst) plane_writeback(a + LO - 1);
+        plane_put(a + HI, pv);
+        const Cand cur = nxt;
+        const int ntot = total;
+        const Ranges rcur = rg;
         clk.lap(1);
-        process(a, min(total, SW));
-        for (int j0 = SW; j0 < total; j0 += SW) {  // dense planes: stage, wait, add
-            mem_fence_compiler();
-            cand_dma(rg, j0);
-            wait_vm<0>();
-            process(a, min(total - j0, SW));
-        }
-        // next: write-back of plane a+LO, table (every PT planes), candidates of
-        // a+1, plane a+HI+2 into the freed slot.  Stores may complete out of
-        // order with loads, so none is issued between a DMA and the counted
-        // wait that relies on it.
-        mem_fence_compiler();
-        const int pout = a + LO;
-        splane_store<K>(p, cd, ring, sslot<K>(pout), zorg + pout, pout >= plo && pout <= phi, loff, okxy);
-        mem_fence_compiler();
+        // prefetch for a+1 (in flight during this step's adds): table, ranges,
+        // candidates, plane a+HI+1
         if (a + 1 <= alast) {
-            const int t = (a + 1 - afirst) / PT;
-            if ((a + 1 - afirst) % PT == 0 && afirst + (t + 1) * PT <= alast) tab_dma(t + 1);
+            const int r1 = a + 1 - afirst;
+            if (r1 % PT == 0) {
+                wait_vm<0>();  // table r1 / PT (issued PT planes ago) has landed
+                if (afirst + (r1 / PT + 1) * PT <= alast) tab_dma(r1 / PT + 1);
+            }
             make_ranges(tab_row(a + 1), rg);
             total = rg.pre[S::NR];
-        } else {
-            total = 0;
+            cand_load(rg, 0, nxt);
+            plane_load(a + HI + 1, pv);
         }
-        cand_dma(rg, 0);
-        mem_fence_compiler();
-        splane_dma<K>(cd, ring, sslot<K>(a + HI + 2), zorg + a + HI + 2, Y0, xoff);
-        mem_fence_compiler();
+        process(a, min(ntot, SW), cur);
+        for (int j0 = SW; j0 < ntot; j0 += SW) {  // dense planes: load and add the rest
+            Cand more;
+            cand_load(rcur, j0, more);
+            process(a, min(ntot - j0, SW), more);
+        }
         clk.lap(4);
     }
-    wait_vm<0>();  // drain the trailing DMAs before the wave's LDS is released
+    plane_writeback(alast + LO);
+    wait_vm<0>();  // no table DMA may outlive the wave's LDS
     clk.lap(5);
     clk.flush(p, it);
 }

@@ -1,0 +1,15 @@
+#!/bin/bash
+# two SQ counter passes over a 1-step bench: profiles/pmc2.sh <outdir>
+out=$1; shift
+export TMPDIR=/tmp
+mkdir -p "$out"
+groups=(
+  "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA"
+  "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR SQ_WAVES"
+)
+i=0
+for grp in "${groups[@]}"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$out/pass$i" -o pmc -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline "$@" > "$out/pass$i.log" 2>&1 || { echo "pass $i failed"; exit 1; }
+done
+python3 profiles/pmc_summary.py "$out" > "$out.json"

@@ -48,9 +48,15 @@ int main() {
     int ncu = 0;
     CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
     std::mt19937 rng(7);
-    const char* names[] = {"distinct (L mod 32)", "adjacent pairs", "random", "random dealt to quarters",
-                           "random dealt to halves", "random sorted (no deal)", "random, 44 active",
-                           "random 44 active dealt q", "8 per class in quarter"};
+    const char* names[] = {"distinct (L mod 32)",            // 0
+                           "random",                         // 1
+                           "q-distinct mod16, random rows",  // 2
+                           "  + rotate class by j",          // 3
+                           "  + x = c+j (no wrap, rows)",    // 4
+                           "q-distinct, x in [0,31] mod16",  // 5
+                           "q-distinct, trash rotate (row0)",// 6
+                           "same addr every j per lane",     // 7
+                           "q-distinct rows, +j, 44 busy"};  // 8
     const int NM = 9;
     int* dtab;
     double* out;
@@ -63,29 +69,35 @@ int main() {
         std::vector<unsigned long long> h(nb);
         for (int mode = 0; mode < NM; ++mode) {
             std::vector<int> tab(4 * NPAT * 64, -1);
-            for (int w = 0; w < 4; ++w)
+            for (int w = 0; w < 4; ++w) {
+                // per-lane persistent choices (a "step"): class, row
+                std::vector<int> cls(64), row(64), hi(64);
+                for (int q = 0; q < 4; ++q) {
+                    std::vector<int> perm(16);
+                    for (int k = 0; k < 16; ++k) perm[k] = k;
+                    std::shuffle(perm.begin(), perm.end(), rng);
+                    for (int k = 0; k < 16; ++k) cls[16 * q + k] = perm[k];
+                }
+                for (int l = 0; l < 64; ++l) { row[l] = rng() % 60; hi[l] = rng() % 2; }
                 for (int j = 0; j < NPAT; ++j) {
                     int* t = &tab[(w * NPAT + j) * 64];
-                    std::vector<int> cls(64);
-                    const int nact = (mode == 6 || mode == 7) ? 44 : 64;
-                    for (int l = 0; l < 64; ++l) cls[l] = rng() % 32;
-                    if (mode == 0)
-                        for (int l = 0; l < 64; ++l) cls[l] = l % 32;
-                    if (mode == 1)
-                        for (int l = 0; l < 64; ++l) cls[l] = l / 2;
-                    if (mode == 8)
-                        for (int l = 0; l < 64; ++l) cls[l] = (l % 16) / 8 * 16 + (l / 16) * 4 + (l % 4);
-                    std::vector<int> lane_of(64);
-                    for (int k = 0; k < 64; ++k) lane_of[k] = k;
-                    if (mode == 3 || mode == 4 || mode == 5 || mode == 7) {
-                        std::sort(cls.begin(), cls.begin() + nact);
-                        for (int k = 0; k < nact; ++k) {
-                            if (mode == 3 || mode == 7) lane_of[k] = (k % 4) * 16 + k / 4;
-                            if (mode == 4) lane_of[k] = (k % 2) * 32 + k / 2;
+                    for (int l = 0; l < 64; ++l) {
+                        int ad = 0;
+                        switch (mode) {
+                        case 0: ad = l + 64 * w; break;
+                        case 1: ad = rng() % 2048; break;
+                        case 2: ad = row[l] * 32 + cls[l]; break;
+                        case 3: ad = row[l] * 32 + ((cls[l] + j) & 15); break;
+                        case 4: ad = row[l] * 32 + cls[l] + (j & 3); break;
+                        case 5: ad = row[l] * 32 + cls[l] + 16 * hi[l]; break;
+                        case 6: ad = 2000 + 16 * (l / 16) + ((cls[l] + j) & 15); break;
+                        case 7: ad = 2000 + l; break;
+                        case 8: ad = (l % 16) < 11 ? row[l] * 32 + cls[l] + (j & 3) : 2000 + 16 * (l / 16) + ((cls[l] + j) & 15); break;
                         }
+                        t[l] = ad % SLOTS;
                     }
-                    for (int k = 0; k < nact; ++k) t[lane_of[k]] = cls[k] + 32 * (int)(rng() % (SLOTS / 32));
                 }
+            }
             CK(hipMemcpy(dtab, tab.data(), sizeof(int) * tab.size(), hipMemcpyHostToDevice));
             for (int rep = 0; rep < 2; ++rep) hipLaunchKernelGGL(k, dim3(nb), dim3(NT), 0, 0, dtab, out, clk);
             CK(hipDeviceSynchronize());
