@@ -191,47 +191,16 @@ template <int K> struct ISh {
     static constexpr int W = T::W, LO = T::LO, HI = T::HI, FAM = T::FAM;
     static constexpr int RX = COLX + HI - LO, RY = COLY + HI - LO;  // staged plane: column + stencil halo
     static constexpr int NS = HI - LO + 1;                          // planes an anchor plane reads (a+LO .. a+HI)
-    static constexpr int NSL = NS + 1;                              // ring slots (+1 in flight)
+    static constexpr int NSL = NS;                                  // ring slots
     static constexpr int PV = RX * RY;
-    static constexpr int PDW = 2 * PV;                              // dwords per plane
-    static constexpr int PD = (PDW + SW - 1) / SW;                  // DMA instructions per plane
-    static constexpr int PVP = PD * SW / 2;                         // ring slot stride (doubles): whole DMA rows
-    static constexpr int NMD = 7;                                   // marker dwords staged: s, X[3]
+    static constexpr int NPT = (PV + SW - 1) / SW;                  // staged points per lane and plane
+    static constexpr int PVP = PV;                                  // ring slot stride (doubles)
     static constexpr int PT = 64;                                   // planes per bucket-start table
-    static constexpr int WAIT = PD;                                 // step-start vmcnt: the plane DMA
 };
 
 template <int K> __device__ __forceinline__ int islot(int prel) {
     using S = ISh<K>;
     return (int)((unsigned)(prel - S::LO) % (unsigned)S::NSL);  // prel >= LO
-}
-
-// DMA of staged plane z (absolute, clamped into the array) into ring slot
-// `slot`; doff[i] = the lane's array offset (clamped) of dword 64 i + lane.
-template <int K>
-__device__ __forceinline__ void iplane_dma(const CompDesc& cd, double* ring, int slot, int z, const int* doff) {
-    using S = ISh<K>;
-    const int zc = min(max(z, cd.lo[2]), cd.hi[2]);
-    const char* pb = (const char*)(cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2) + 4 * (lane_id() & 1);
-    char* lb = (char*)(ring + slot * S::PVP);
-#pragma unroll
-    for (int i = 0; i < S::PD; ++i) glds4(pb + 8 * (int64_t)doff[i], lb + 256 * i);
-}
-
-// zero the ring entries of plane z (slot) that lie outside the component array
-// (clamped loads brought in neighbours' values): staged zeros keep acc + w*0 ==
-// acc for the clipped stencil points.  okm bit i: dword 64 i + lane in the array.
-template <int K>
-__device__ __forceinline__ void iplane_fix(const CompDesc& cd, double* ring, int slot, int z, unsigned okm) {
-    using S = ISh<K>;
-    const bool zin = z >= cd.lo[2] && z <= cd.hi[2];
-    unsigned* lb = (unsigned*)(ring + slot * S::PVP);
-    const int lane = lane_id();
-#pragma unroll
-    for (int i = 0; i < S::PD; ++i) {
-        const int d = lane + SW * i;
-        if ((S::PDW % SW == 0 || d < S::PDW) && !(zin && ((okm >> i) & 1u))) lb[d] = 0u;
-    }
 }
 
 template <int K>
@@ -314,16 +283,17 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
 
 
 // Interpolation work item = (segment, column, component).  The item sweeps its
-// anchor planes [a0, a1); the ring holds staged planes a+LO..a+HI plus plane
-// a+HI+1 in flight; the markers of anchor plane a+1 are staged while plane a is
-// summed.  One lane per marker sums its W^3 stencil from the ring (Fortran loop
-// order, bitwise the oracle's).
+// anchor planes [a0, a1); the ring holds staged planes a+LO..a+HI.  Plane
+// a+HI+1 and the markers of anchor plane a+1 are loaded into registers while
+// plane a is summed (plain loads, so no LDS-DMA issue cost), and written into
+// the slot plane a+LO leaves at the top of the next step.  Points outside the
+// component's array are staged as 0.  One lane per marker sums its W^3 stencil
+// from the ring (Fortran loop order, bitwise the oracle's).
 template <int K>
 __global__ __launch_bounds__(SW) void k_interp_sweep(Params p) {
     using S = ISh<K>;
-    constexpr int LO = S::LO, HI = S::HI, RX = S::RX, PD = S::PD, PT = S::PT, NMD = S::NMD;
+    constexpr int LO = S::LO, HI = S::HI, RX = S::RX, NPT = S::NPT, PT = S::PT;
     __shared__ double ring[S::NSL * S::PVP];
-    __shared__ unsigned stg[NMD * SW];   // staged markers: [dword][lane]
     __shared__ int tab[2][PT][2];        // [beg, end) of the column's markers per anchor plane
     const int nitems = p.cg.ncol * p.nseg * p.ncomp;
     const int it = sweep_item(nitems);
@@ -344,18 +314,38 @@ __global__ __launch_bounds__(SW) void k_interp_sweep(Params p) {
     const int gx0 = p.cg.org[0] + cx * COLX + LO, gy0 = p.cg.org[1] + cy * COLY + LO;
     const int zorg = p.cg.org[2];
     const int nlast = p.nsorted - 1;
-    const bool fringe = !(gx0 >= cd.lo[0] && gx0 + RX - 1 <= cd.hi[0] && gy0 >= cd.lo[1] && gy0 + S::RY - 1 <= cd.hi[1]);
-    // per-lane DMA source offsets and in-array bits of the plane's dwords
-    int doff[PD];
+    // the lane's staged points q = lane + 64 k: array offsets (clamped) and
+    // in-array bits (x, y)
+    int poff[NPT];
     unsigned okm = 0;
 #pragma unroll
-    for (int i = 0; i < PD; ++i) {
-        const int q = min((lane + SW * i) >> 1, S::PV - 1);
+    for (int k = 0; k < NPT; ++k) {
+        const int q = min(lane + SW * k, S::PV - 1);
         const int gxu = gx0 + q % RX, gyu = gy0 + q / RX;
         const int gx = min(max(gxu, cd.lo[0]), cd.hi[0]), gy = min(max(gyu, cd.lo[1]), cd.hi[1]);
-        doff[i] = (gx - cd.lo[0]) + (gy - cd.lo[1]) * (int)cd.s1;
-        if (gx == gxu && gy == gyu) okm |= 1u << i;
+        poff[k] = (gx - cd.lo[0]) + (gy - cd.lo[1]) * (int)cd.s1;
+        if (gx == gxu && gy == gyu) okm |= 1u << k;
     }
+    const int plast = a1 - 1 + HI;  // last plane the item reads
+    // relative plane zr -> registers: unconditional loads at clamped addresses
+    // (points outside the array are zeroed when the plane is put; a select
+    // right behind a load would become a branch around it, CodeGenPrepare)
+    auto plane_load = [&](int zr, double* v) {
+        const int z = zorg + min(zr, plast);
+        const int zc = min(max(z, cd.lo[2]), cd.hi[2]);
+        const double* pb = cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2;
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) v[k] = pb[poff[k]];
+    };
+    auto plane_put = [&](int zr, const double* v) {  // registers -> ring slot, 0 outside the array
+        const int z = zorg + min(zr, plast);
+        const bool zin = z >= cd.lo[2] && z <= cd.hi[2];
+        double* sl = ring + islot<K>(zr) * S::PVP;
+#pragma unroll
+        for (int k = 0; k < NPT; ++k)
+            if (S::PV % SW == 0 || k < NPT - 1 || lane + SW * k < S::PV)
+                sl[lane + SW * k] = (zin && ((okm >> k) & 1u)) ? v[k] : 0.0;
+    };
     // bucket-start tables: buffer b holds anchor planes [a0 + t PT, a0 + (t+1) PT), b = t & 1
     auto tab_dma = [&](int t) {
         const int from = a0 + t * PT;
@@ -368,93 +358,73 @@ __global__ __launch_bounds__(SW) void k_interp_sweep(Params p) {
         }
     };
     auto tab_at = [&](int a, int k) { const int r = a - a0; return tab[(r / PT) & 1][r % PT][k]; };
-    // marker staging: sorted position e -> s, X (7 dwords)
-    auto mk_dma = [&](int beg, int cnt) {
-        const int e = min(beg + min(lane, max(cnt - 1, 0)), nlast);
-        glds4(p.sorted_s + e, (char*)stg);
-        const char* xs = (const char*)(p.sorted_X + (int64_t)3 * e);
-#pragma unroll
-        for (int k = 0; k < 6; ++k) glds4(xs + 4 * k, (char*)stg + 256 * (k + 1));
+    struct Mk {
+        int s;
+        double X[3];
     };
-    auto mk_get = [&](int j, int& s, double* X) {
-        s = (int)stg[j];
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-            X[k] = __hiloint2double((int)stg[SW * (2 + 2 * k) + j], (int)stg[SW * (1 + 2 * k) + j]);
+    auto mk_load = [&](int beg, int cnt, Mk& m) {  // markers beg + lane (clamped)
+        const int e = min(beg + min(lane, max(cnt - 1, 0)), nlast);
+        m.s = p.sorted_s[e];
+        const double* xs = p.sorted_X + (int64_t)3 * e;
+        m.X[0] = xs[0];
+        m.X[1] = xs[1];
+        m.X[2] = xs[2];
     };
 
-    // prologue, in the steady-state issue order: tables, ring planes, markers of
-    // a0, plane a0+HI+1
+    // prologue: tables; planes a0+LO .. a0+HI-1 into the ring; plane a0+HI and
+    // the markers of a0 into registers
     tab_dma(0);
     tab_dma(1);
     wait_vm<0>();
-    for (int k = LO; k <= HI; ++k) iplane_dma<K>(cd, ring, islot<K>(a0 + k), zorg + a0 + k, doff);
-    int cur_n;
+    double pv[NPT];
+    for (int z = a0 + LO; z < a0 + HI; ++z) {
+        plane_load(z, pv);
+        plane_put(z, pv);
+    }
+    plane_load(a0 + HI, pv);
+    Mk nxt;
+    int nxt_n;
     {
         const int b = tab_at(a0, 0), e = tab_at(a0, 1);
-        cur_n = min(e - b, SW);
-        mk_dma(b, cur_n);
+        nxt_n = min(e - b, SW);
+        mk_load(b, nxt_n, nxt);
     }
-    mem_fence_compiler();
-    const int plast = a1 - 1 + HI;  // last plane the item reads
-    iplane_dma<K>(cd, ring, islot<K>(a0 + HI + 1), zorg + min(a0 + HI + 1, plast), doff);
-    wait_vm<S::WAIT>();
-    if (fringe)
-        for (int k = LO; k <= HI; ++k) iplane_fix<K>(cd, ring, islot<K>(a0 + k), zorg + a0 + k, okm);
-    else
-        for (int k = LO; k <= HI; ++k)
-            if (zorg + a0 + k < cd.lo[2] || zorg + a0 + k > cd.hi[2]) iplane_fix<K>(cd, ring, islot<K>(a0 + k), zorg + a0 + k, okm);
-
     for (int a = a0; a < a1; ++a) {
-        // step start: markers of a and plane a+HI have landed
-        if (a > a0) {
-            wait_vm<S::WAIT>();
-            const int zn = zorg + a + HI;
-            if (fringe || zn < cd.lo[2] || zn > cd.hi[2]) iplane_fix<K>(cd, ring, islot<K>(a + HI), zn, okm);
-        }
+        plane_put(a + HI, pv);  // into the slot plane a+LO-1 left
+        const Mk cur = nxt;
+        const int cur_n = nxt_n;
         const int beg = tab_at(a, 0), end = tab_at(a, 1);
-        // chunk 0 from the staged markers; the value is stored at the end of the step
-        double acc0 = 0.0;
-        int s0 = 0;
-        if (lane < cur_n) {
-            double X[3];
-            mk_get(lane, s0, X);
-            acc0 = interp_marker<K>(p, cd, ring, gx0, gy0, a, X, s0);
-        }
-        // further chunks of a dense plane: staged, waited for and stored here
-        for (int e0 = beg + SW; e0 < end; e0 += SW) {
-            const int n = min(end - e0, SW);
-            mem_fence_compiler();
-            mk_dma(e0, n);
-            wait_vm<0>();
-            if (lane < n) {
-                int s;
-                double X[3];
-                mk_get(lane, s, X);
-                p.Qout[(int64_t)p.Q_depth * s + cd.qcomp] = interp_marker<K>(p, cd, ring, gx0, gy0, a, X, s);
+        // prefetch for a+1: table (every PT planes), markers, plane a+HI+1
+        if (a + 1 < a1) {
+            const int r1 = a + 1 - a0;
+            if (r1 % PT == 0) {
+                wait_vm<0>();  // table r1 / PT (issued PT planes ago) has landed
+                if (a + 1 + PT < a1) tab_dma(r1 / PT + 1);
             }
-            mem_fence_compiler();
+            const int nb = tab_at(a + 1, 0);
+            nxt_n = min(tab_at(a + 1, 1) - nb, SW);
+            mk_load(nb, nxt_n, nxt);
+            plane_load(a + HI + 1, pv);
         }
-        // next: this chunk's store, bucket-start table (every PT planes),
-        // markers of a+1, plane a+HI+2 (into the slot plane a+LO leaves).
-        // Stores may complete out of order with loads, so none is issued
-        // between a DMA and the counted wait that relies on it.
-        mem_fence_compiler();
+        // chunk 0 from the prefetched markers
         {
-            double* dst = lane < cur_n ? p.Qout + ((int64_t)p.Q_depth * s0 + cd.qcomp) : p.sink + lane;
+            double acc0 = 0.0;
+            if (lane < cur_n) acc0 = interp_marker<K>(p, cd, ring, gx0, gy0, a, cur.X, cur.s);
+            double* dst = lane < cur_n ? p.Qout + ((int64_t)p.Q_depth * cur.s + cd.qcomp) : p.sink + lane;
             *dst = acc0;
         }
-        mem_fence_compiler();
-        if (a + 1 < a1 && ((a + 1 - a0) % PT) == 0 && a + 1 + PT < a1) tab_dma((a + 1 - a0) / PT + 1);
-        const int nb = a + 1 < a1 ? tab_at(a + 1, 0) : 0;
-        const int nn = a + 1 < a1 ? min(tab_at(a + 1, 1) - nb, SW) : 0;
-        mk_dma(nb, nn);
-        mem_fence_compiler();
-        iplane_dma<K>(cd, ring, islot<K>(a + HI + 2), zorg + min(a + HI + 2, plast), doff);
-        mem_fence_compiler();
-        cur_n = nn;
+        // further chunks of a dense plane
+        for (int e0 = beg + SW; e0 < end; e0 += SW) {
+            const int n = min(end - e0, SW);
+            Mk m;
+            mk_load(e0, n, m);
+            double acc = 0.0;
+            if (lane < n) acc = interp_marker<K>(p, cd, ring, gx0, gy0, a, m.X, m.s);
+            double* dst = lane < n ? p.Qout + ((int64_t)p.Q_depth * m.s + cd.qcomp) : p.sink + lane;
+            *dst = acc;
+        }
     }
-    wait_vm<0>();  // drain the dummy DMAs before the wave's LDS is released
+    wait_vm<0>();  // no table DMA may outlive the wave's LDS
 }
 
 // Entries binned "outside" (no stencil point can reach any array): V = 0.
