@@ -152,6 +152,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-rebin", action="store_true", help="bin once outside the timed loop")
+    ap.add_argument("--marker-order", default="cell", choices=["cell", "random"],
+                    help="storage order of the markers: 'cell' = sorted by cell (z, y, x), the order "
+                         "LDataManager's local numbering gives after redistribution (SURVEY.md 8d); "
+                         "'random' = generation order")
     args = ap.parse_args()
 
     import torch
@@ -180,6 +184,12 @@ def main():
 
     t_setup = time.perf_counter()
     X = make_markers(cfg["markers"], cfg["M"], slab, 1234, dev)
+    if args.marker_order == "cell":
+        # local numbering in cell order (LDataManager::computeNodeDistribution,
+        # LDataManager.cpp:2839-3027: interior markers in patch-cell iteration order)
+        ci = [torch.clamp((X[:, d] / slab.dx[d]).floor().long(), 0, N - 1) for d in range(3)]
+        X = X[torch.argsort((ci[2] * N + ci[1]) * N + ci[0])].contiguous()
+        del ci
     M_local = X.shape[0]
     gen = torch.Generator(device=dev).manual_seed(4321 + rank)
     F = torch.rand((M_local, 3), dtype=torch.float64, device=dev, generator=gen).mul_(2).sub_(1)
@@ -303,7 +313,7 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {"workload": cfg["desc"], "kernel": kernel, "grid": [N, N, N], "markers": M_total,
-                   "parallelism": f"z-slab x{world}", "ghost": ghost,
+                   "parallelism": f"z-slab x{world}", "ghost": ghost, "marker_order": args.marker_order,
                    "step": "bin + ghost fill + interp(3 comps) + zero ghosts + spread(3 comps) + ghost sum"},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
