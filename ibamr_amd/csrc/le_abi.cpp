@@ -474,13 +474,15 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     tb = ctx->temp.cap;
     HIP_TRY(launch_sort(ctx->temp.p, tb, ctx->keys_in.as<unsigned>(), m->sorted_key.as<unsigned>(),
                         ctx->vals_in.as<int>(), m->sorted_l.as<int>(), n, end_bit, s));
-    HIP_TRY(launch_brick_start(m->sorted_key.as<unsigned>(), n, nplanes,
-                               cols ? 0 : bg.shift - (geom->ndim == 3 ? 3 : 4), m->plane_start.as<int>(), s));
     p.sorted_l = m->sorted_l.as<int>();
-    if (cols)
-        HIP_TRY(launch_gather_col(kernel, p, n, m->sorted_s.as<int>(), m->sorted_X.as<double>(), nullptr, s));
-    else
+    if (cols) {  // gather fused with the bucket starts
+        HIP_TRY(launch_gather_col(kernel, p, n, m->sorted_s.as<int>(), m->sorted_X.as<double>(),
+                                  m->sorted_key.as<unsigned>(), nplanes, m->plane_start.as<int>(), s));
+    } else {
+        HIP_TRY(launch_brick_start(m->sorted_key.as<unsigned>(), n, nplanes, bg.shift - (geom->ndim == 3 ? 3 : 4),
+                                   m->plane_start.as<int>(), s));
         HIP_TRY(launch_gather_sorted(geom->ndim, p, n, m->sorted_s.as<int>(), m->sorted_X.as<double>(), s));
+    }
     return IBTK_LE_OK;
 }
 

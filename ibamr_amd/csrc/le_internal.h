@@ -143,7 +143,7 @@ hipError_t launch_scan(void* temp, size_t& temp_bytes, const int* in, int* out, 
 // 3-D column sweep (le_sweep.hip)
 hipError_t launch_bin_col(int kernel, const Params& p, int n, unsigned* keys, int* vals, hipStream_t s);
 hipError_t launch_gather_col(int kernel, const Params& p, int n, int* sorted_s, double* sorted_X,
-                             unsigned* sorted_a, hipStream_t s);
+                             const unsigned* sorted_key, int nbuckets, int* bucket_start, hipStream_t s);
 hipError_t launch_interp_sweep(int kernel, const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_spread_sweep(int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 void sweep_segments(const ColGeom& cg, int& S, int& nseg);

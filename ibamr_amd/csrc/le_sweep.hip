@@ -92,25 +92,27 @@ __global__ __launch_bounds__(BLOCK) void k_bin_col(Params p, int n, unsigned* ke
     vals[i] = i;
 }
 
+// Per sorted entry e: the marker index and the shifted position (coalesced for
+// the sweeps), fused with the bucket starts: entry e > 0 opens every bucket in
+// (key[e-1], key[e]] (keys >= nbuckets: binned outside).  The buckets before
+// the first key and after the last one are k_bucket_ends' (one thread each:
+// a single thread walking them would serialise the launch).  n > 0.
 template <int K>
 __global__ __launch_bounds__(BLOCK) void k_gather_col(Params p, int n, int* sorted_s, double* sorted_X,
-                                                      unsigned* sorted_a) {
+                                                      const unsigned* skeys, int nbuckets, int* bs) {
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     if (e >= n) return;
+    if (e > 0) {
+        const int bi = (int)min(skeys[e], (unsigned)nbuckets);
+        const int bp = (int)min(skeys[e - 1], (unsigned)nbuckets);
+        for (int b = bp + 1; b <= bi; ++b) bs[b] = e;
+    }
     const int l = p.sorted_l[e];
     const int s = p.indices ? p.indices[l] : l;
     sorted_s[e] = s;
-    double Xs[3];
 #pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        Xs[d] = p.X[(int64_t)3 * s + d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
-        sorted_X[(int64_t)3 * e + d] = Xs[d];
-    }
-    if (sorted_a) {
-        int ka[3];
-        col_key_cell<K>(p, Xs, ka);
-        sorted_a[e] = ((unsigned)ka[0] & 0xffffu) | ((unsigned)ka[1] << 16);
-    }
+    for (int d = 0; d < 3; ++d)
+        sorted_X[(int64_t)3 * e + d] = p.X[(int64_t)3 * s + d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
 }
 
 // ---------------------------------------------------------------------------
@@ -852,10 +854,23 @@ template <int K> hipError_t launch_bin_col_t(const Params& p, int n, unsigned* k
     hipLaunchKernelGGL(k_bin_col<K>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, keys, vals);
     return hipGetLastError();
 }
+// bucket starts before the first and after the last sorted key
+__global__ __launch_bounds__(BLOCK) void k_bucket_ends(const unsigned* skeys, int n, int nbuckets, int* bs) {
+    const int b = blockIdx.x * BLOCK + threadIdx.x;
+    if (b > nbuckets) return;
+    const int first = (int)min(skeys[0], (unsigned)nbuckets), last = (int)min(skeys[n - 1], (unsigned)nbuckets);
+    if (b <= first) bs[b] = 0;
+    else if (b > last) bs[b] = n;
+}
+
 template <int K>
-hipError_t launch_gather_col_t(const Params& p, int n, int* ss, double* sx, unsigned* sa, hipStream_t s) {
+hipError_t launch_gather_col_t(const Params& p, int n, int* ss, double* sx, const unsigned* skeys, int nbuckets,
+                               int* bs, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_gather_col<K>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, ss, sx, sa);
+    hipLaunchKernelGGL(k_bucket_ends, dim3((nbuckets + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, skeys, n, nbuckets,
+                       bs);
+    hipLaunchKernelGGL(k_gather_col<K>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, ss, sx, skeys,
+                       nbuckets, bs);
     return hipGetLastError();
 }
 template <int K>
@@ -903,7 +918,7 @@ template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s
     }
 
 using BinColFn = hipError_t (*)(const Params&, int, unsigned*, int*, hipStream_t);
-using GatherColFn = hipError_t (*)(const Params&, int, int*, double*, unsigned*, hipStream_t);
+using GatherColFn = hipError_t (*)(const Params&, int, int*, double*, const unsigned*, int, int*, hipStream_t);
 using InterpSwFn = hipError_t (*)(const Params&, int, hipStream_t, hipEvent_t, hipEvent_t);
 using SpreadSwFn = hipError_t (*)(const Params&, hipStream_t, hipEvent_t, hipEvent_t);
 static BinColFn pick_bin_col(int k) { IBTK_LE_DISPATCH_K(k, launch_bin_col_t) }
@@ -915,10 +930,10 @@ hipError_t launch_bin_col(int kernel, const Params& p, int n, unsigned* keys, in
     BinColFn f = pick_bin_col(kernel);
     return f ? f(p, n, keys, vals, s) : hipErrorInvalidValue;
 }
-hipError_t launch_gather_col(int kernel, const Params& p, int n, int* sorted_s, double* sorted_X, unsigned* sorted_a,
-                             hipStream_t s) {
+hipError_t launch_gather_col(int kernel, const Params& p, int n, int* sorted_s, double* sorted_X,
+                             const unsigned* sorted_key, int nbuckets, int* bucket_start, hipStream_t s) {
     GatherColFn f = pick_gather_col(kernel);
-    return f ? f(p, n, sorted_s, sorted_X, sorted_a, s) : hipErrorInvalidValue;
+    return f ? f(p, n, sorted_s, sorted_X, sorted_key, nbuckets, bucket_start, s) : hipErrorInvalidValue;
 }
 hipError_t launch_interp_sweep(int kernel, const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     InterpSwFn f = pick_interp_sweep(kernel);
