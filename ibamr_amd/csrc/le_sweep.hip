@@ -445,7 +445,7 @@ template <int K> struct SSh {
     using T = KT<K>;
     static constexpr int W = T::W, LO = T::LO, HI = T::HI, FAM = T::FAM;
     static constexpr int NS = HI - LO + 1;              // planes an anchor plane reaches
-    static constexpr int NSL = NS;                      // ring slots: the planes one anchor reaches
+    static constexpr int NSL = NS + 1;                  // ring slots: the planes two anchors reach
     static constexpr int PV = COLX * COLY;              // owned points per plane
     static constexpr int NPL = PV / SW;
     static constexpr int PD = 2 * PV / SW;              // DMA instructions per plane (one row each)
@@ -516,6 +516,23 @@ struct Ranges {
     int start[SSh<K_IB_4>::NR];
     int pre[SSh<K_IB_4>::NR + 1];
 };
+// rows held one entry per lane (lane k: entry k of the row): wave-uniform reads
+__device__ __forceinline__ void make_ranges_lanes(const int* rowv, Ranges& R) {
+    constexpr int NR = SSh<K_IB_4>::NR;
+    constexpr int rr[NR] = {0, 0, 0, 0, 0, 1, 2, 2, 2, 2, 2};
+    constexpr int ib[NR] = {8, 11, 14, 17, 20, 6, 6, 9, 12, 15, 18};
+    constexpr int ie[NR] = {9, 12, 15, 18, 21, 21, 7, 10, 13, 16, 19};
+    int acc = 0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int b = __builtin_amdgcn_readlane(rowv[rr[r]], ib[r]);
+        const int e = __builtin_amdgcn_readlane(rowv[rr[r]], ie[r]);
+        R.start[r] = b;
+        R.pre[r] = acc;
+        acc += e - b;
+    }
+    R.pre[NR] = acc;
+}
 __device__ __forceinline__ void make_ranges(const int (*t)[28], Ranges& R) {
     constexpr int NR = SSh<K_IB_4>::NR;
     // (row, first index, last index + 1) of each range
@@ -662,10 +679,9 @@ __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd
 template <int K>
 __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     using S = SSh<K>;
-    constexpr int LO = S::LO, HI = S::HI, NS = S::NS, NPL = S::NPL, PT = S::PT, TW = S::TW, FAM = S::FAM;
+    constexpr int LO = S::LO, HI = S::HI, NPL = S::NPL, FAM = S::FAM;
     __shared__ double ring_mem[S::GUARD + S::NSL * S::SLOT];
     double* const ring = ring_mem + S::GUARD;
-    __shared__ int tab[2][S::TD * SW / TW + 1][3][28];  // whole DMA rows per buffer
     const int nitems = p.cg.ncol * p.nseg * p.ncomp;
     const int it = sweep_item(nitems);
     if (it < 0) return;
@@ -711,26 +727,15 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         const int zc = min(max(zorg + z, cd.lo[2]), cd.hi[2]);
         return cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2;
     };
-    // bucket-start tables by LDS-DMA: buffer t & 1 holds anchor planes
-    // [afirst + t PT, afirst + (t+1) PT), issued PT planes ahead
-    auto tab_dma = [&](int t) {
-        const int from = afirst + t * PT;
-        char* lb = (char*)&tab[t & 1][0][0][0];
+    // bucket starts of anchor plane a: rows cy-1, cy, cy+1 (28 entries: bands of
+    // columns cx-1 .. cx+1), one entry per lane
+    auto rows_load = [&](int a, int* rowv) {
 #pragma unroll
-        for (int i = 0; i < S::TD; ++i) {
-            const int d = min(lane + SW * i, PT * TW - 1);
-            const int pl = d / TW, r = (d / 28) % 3, k = d % 28;
-            const int a = min(from + pl, p.cg.nz - 1);
-            glds4(bs + bucket(p, a, col0 + r * ncx, 0) + k, lb + 256 * i);
-        }
+        for (int r = 0; r < 3; ++r) rowv[r] = bs[bucket(p, a, col0 + r * ncx, 0) + min(lane, 27)];
     };
-    auto tab_row = [&](int a) {
-        const int r = a - afirst;
-        return (const int(*)[28])tab[(r / PT) & 1][r % PT];
-    };
-    // candidate j0 + lane of the ranges (clamped to a valid entry)
-    auto cand_load = [&](const Ranges& rg, int j0, Cand& d) {
-        const int e = min(range_pos(rg, j0 + lane), nlast);
+    // candidate data of sorted position e
+    auto cand_at = [&](int e, Cand& d) {
+        e = min(e, nlast);
         const double* xs = p.sorted_X + (int64_t)3 * e;
         d.X[0] = xs[0];
         d.X[1] = xs[1];
@@ -741,9 +746,9 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     Clk clk;
     const double inv_dx = 1.0 / p.bg.dx[0];  // lane dealing only (approximate class)
     const double inv_h3 = 1.0 / p.h3;
-    // adds of the n <= 64 candidates held one per lane: dealt over the lanes by
-    // bank class, then spread
-    auto process = [&](int a, int n, const Cand& mine) {
+    // adds of the n <= 64 candidates held one per lane (lane j's anchor plane:
+    // a - 1 for j < r, else a): dealt over the lanes by bank class, then spread
+    auto process = [&](int a, int r, int n, const Cand& mine) {
         const int cls = lane < n ? ((int)floor((mine.X[0] - cd.xlo[0]) * inv_dx + 0.5) & 15) : 32;
         const int src = deal_lanes(cls);
         Cand d;
@@ -751,7 +756,8 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         for (int k = 0; k < 3; ++k) d.X[k] = shfl_f64(mine.X[k], src);
         d.V = shfl_f64(mine.V, src);
         d.s = FAM == 2 ? __builtin_amdgcn_ds_bpermute(src << 2, mine.s) : 0;
-        spread_lanes<K>(p, cd, ring, d, src < n, a, X0, Y0, xlo, xhi, ylo, yhi, plo, phi, inv_h3, clk);
+        spread_lanes<K>(p, cd, ring, d, src < n, src < r ? a - 1 : a, X0, Y0, xlo, xhi, ylo, yhi, plo, phi, inv_h3,
+                        clk);
     };
     // plane z -> registers (the lane's NPL points); registers -> ring slot
     auto plane_load = [&](int z, double* v) {
@@ -778,56 +784,69 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         }
     };
 
+    // The candidates stream through 64-lane chunks across anchor planes.  Anchor
+    // a's chunk 1 holds the r leftover candidates of anchor a-1 (its last r, in
+    // lanes 0..r-1) and the first 64-r of a; full middle chunks of a follow;
+    // a's last partial chunk is carried into a+1's chunk 1.  The ring holds the
+    // planes of anchors a-1 and a: [a-1+LO, a+HI].
     clk.start(p.stamps != nullptr);
-    // prologue: tables; planes afirst+LO .. afirst+HI-1 into the ring; plane
-    // afirst+HI and the candidates of afirst into registers
-    tab_dma(0);
-    tab_dma(1);
-    wait_vm<0>();
+    // prologue: planes afirst+LO .. afirst+HI-1 into the ring; plane afirst+HI,
+    // the ranges and chunk 1 of afirst into registers
     double pv[NPL];
     for (int z = afirst + LO; z < afirst + HI; ++z) {
         plane_load(z, pv);
         plane_put(z, pv);
     }
     plane_load(afirst + HI, pv);
-    Ranges rg;
-    make_ranges(tab_row(afirst), rg);
-    int total = rg.pre[S::NR];
+    int rowv[3];
+    rows_load(afirst, rowv);
+    Ranges rgA;
+    make_ranges_lanes(rowv, rgA);
+    int tA = rgA.pre[S::NR];
     Cand nxt;
-    cand_load(rg, 0, nxt);
+    cand_at(range_pos(rgA, min(lane, max(tA - 1, 0))), nxt);
+    int r_prev = 0;                 // candidates of anchor a-1 carried into a's chunk 1
+    int n1 = min(tA, SW);           // lanes of a's chunk 1
+    if (afirst + 1 <= alast) rows_load(afirst + 1, rowv);
     clk.lap(0);
     for (int a = afirst; a <= alast; ++a) {
-        // top: plane a+LO-1 leaves the window (written back), plane a+HI takes
-        // its slot; the staged candidates of a become current
-        if (a > afirst) plane_writeback(a + LO - 1);
-        plane_put(a + HI, pv);
+        if (a >= afirst + 2) plane_writeback(a - 2 + LO);  // no anchor left reaches it
+        plane_put(a + HI, pv);                               // into its slot
         const Cand cur = nxt;
-        const int ntot = total;
-        const Ranges rcur = rg;
+        const int cur_r = r_prev, cur_n = n1;
+        const Ranges rgCur = rgA;
+        const int tCur = tA;
+        const int h = min(SW - r_prev, tCur);  // a's candidates in chunk 1
+        const int nmid = (tCur - h) / SW;       // full middle chunks
+        const int r_a = (tCur - h) % SW;        // carried into a+1
         clk.lap(1);
-        // prefetch for a+1 (in flight during this step's adds): table, ranges,
-        // candidates, plane a+HI+1
+        // prefetch for a+1: its ranges, its chunk 1, plane a+HI+1, the rows of a+2
         if (a + 1 <= alast) {
-            const int r1 = a + 1 - afirst;
-            if (r1 % PT == 0) {
-                wait_vm<0>();  // table r1 / PT (issued PT planes ago) has landed
-                if (afirst + (r1 / PT + 1) * PT <= alast) tab_dma(r1 / PT + 1);
-            }
-            make_ranges(tab_row(a + 1), rg);
-            total = rg.pre[S::NR];
-            cand_load(rg, 0, nxt);
+            make_ranges_lanes(rowv, rgA);
+            tA = rgA.pre[S::NR];
+            const int eA = range_pos(rgCur, min(tCur - r_a + lane, max(tCur - 1, 0)));
+            const int eB = range_pos(rgA, min(lane - r_a, max(tA - 1, 0)));
+            cand_at(lane < r_a ? eA : eB, nxt);
+            n1 = r_a + min(SW - r_a, tA);
+            r_prev = r_a;
             plane_load(a + HI + 1, pv);
+            if (a + 2 <= alast) rows_load(a + 2, rowv);
         }
-        process(a, min(ntot, SW), cur);
-        for (int j0 = SW; j0 < ntot; j0 += SW) {  // dense planes: load and add the rest
+        if (cur_n > 0) process(a, cur_r, cur_n, cur);
+        for (int k = 0; k < nmid; ++k) {  // dense planes: the full middle chunks
             Cand more;
-            cand_load(rcur, j0, more);
-            process(a, min(ntot - j0, SW), more);
+            cand_at(range_pos(rgCur, h + SW * k + lane), more);
+            process(a, 0, SW, more);
+        }
+        if (a == alast && r_a > 0) {  // the last anchor's leftovers
+            Cand last;
+            cand_at(range_pos(rgCur, tCur - r_a + min(lane, r_a - 1)), last);
+            process(a, 0, r_a, last);
         }
         clk.lap(4);
     }
+    plane_writeback(alast - 1 + LO);
     plane_writeback(alast + LO);
-    wait_vm<0>();  // no table DMA may outlive the wave's LDS
     clk.lap(5);
     clk.flush(p, it);
 }
