@@ -185,6 +185,38 @@ struct Clk {
     }
 };
 
+// Lane assignment of staged markers by LDS bank class.  An LDS instruction runs
+// as G lane groups, each costing about the largest number of its lanes that
+// share a bank: ds_add_f64 as 4 x 16 lanes, bank class = f64 index mod 16
+// (tools/ubench_lds2.hip; the microarchitecture guide's ds_write_b64 row);
+// ds_read_b64 as 2 x 32 lanes, class = f64 index mod 32.  The markers are
+// ranked by class (stable in staging order; idle lanes, class 63, last) and
+// dealt round-robin over the groups, so the markers of one class land in
+// different groups.  Returns the staged index this lane processes.
+template <int G = 4>  // lane groups: 4 x 16 (ds_add_f64, ds_write_b64) or 2 x 32 (ds_read_b64)
+__device__ __forceinline__ int deal_lanes(int cls) {  // cls in [0, 64); 63 = inactive
+    const int lane = __lane_id();
+    unsigned long long eq = ~0ull, lt = 0ull;
+#pragma unroll
+    for (int b = 5; b >= 0; --b) {
+        const bool bit = (cls >> b) & 1;
+        const unsigned long long m = __ballot(bit);
+        lt |= bit ? (eq & ~m) : 0ull;
+        eq &= bit ? m : ~m;
+    }
+    const int k = __popcll(lt) + __popcll(eq & ((1ull << lane) - 1ull));  // rank
+    const int t = (k % G) * (64 / G) + k / G;                              // dealt lane
+    return __builtin_amdgcn_ds_permute(t << 2, lane);
+}
+
+// value of lane `src` (ds_bpermute on the two halves)
+__device__ __forceinline__ double shfl_f64(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b & 0xffffffffll));
+    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b >> 32));
+    return __hiloint2double(hi, lo);
+}
+
 // ---------------------------------------------------------------------------
 // interpolation
 // ---------------------------------------------------------------------------
@@ -196,7 +228,9 @@ template <int K> struct ISh {
     static constexpr int NSL = NS;                                  // ring slots
     static constexpr int PV = RX * RY;
     static constexpr int NPT = (PV + SW - 1) / SW;                  // staged points per lane and plane
-    static constexpr int PVP = PV;                                  // ring slot stride (doubles)
+    // ring slot stride: a multiple of 32 doubles, so a point's LDS bank class
+    // (f64 index mod 32) does not depend on its plane
+    static constexpr int PVP = (PV + 31) / 32 * 32;
     static constexpr int PT = 64;                                   // planes per bucket-start table
 };
 
@@ -373,6 +407,18 @@ __global__ __launch_bounds__(SW) void k_interp_sweep(Params p) {
         m.X[2] = xs[2];
     };
 
+    // one chunk of n <= 64 markers held one per lane: summed, stored.  (Dealing
+    // the markers over the two 32-lane halves of a ds_read_b64 by bank class,
+    // as the spread does for its adds, measured 10 % slower: the ranking costs
+    // more than the reads' bank conflicts.)
+    auto process = [&](int a, int n, const Mk& m) {
+        const bool act = lane < n;
+        double acc = 0.0;
+        if (act) acc = interp_marker<K>(p, cd, ring, gx0, gy0, a, m.X, m.s);
+        double* dst = act ? p.Qout + ((int64_t)p.Q_depth * m.s + cd.qcomp) : p.sink + lane;
+        *dst = acc;
+    };
+
     // prologue: tables; planes a0+LO .. a0+HI-1 into the ring; plane a0+HI and
     // the markers of a0 into registers
     tab_dma(0);
@@ -408,22 +454,12 @@ __global__ __launch_bounds__(SW) void k_interp_sweep(Params p) {
             mk_load(nb, nxt_n, nxt);
             plane_load(a + HI + 1, pv);
         }
-        // chunk 0 from the prefetched markers
-        {
-            double acc0 = 0.0;
-            if (lane < cur_n) acc0 = interp_marker<K>(p, cd, ring, gx0, gy0, a, cur.X, cur.s);
-            double* dst = lane < cur_n ? p.Qout + ((int64_t)p.Q_depth * cur.s + cd.qcomp) : p.sink + lane;
-            *dst = acc0;
-        }
-        // further chunks of a dense plane
-        for (int e0 = beg + SW; e0 < end; e0 += SW) {
+        process(a, cur_n, cur);  // chunk 0 from the prefetched markers
+        for (int e0 = beg + SW; e0 < end; e0 += SW) {  // further chunks of a dense plane
             const int n = min(end - e0, SW);
             Mk m;
             mk_load(e0, n, m);
-            double acc = 0.0;
-            if (lane < n) acc = interp_marker<K>(p, cd, ring, gx0, gy0, a, m.X, m.s);
-            double* dst = lane < n ? p.Qout + ((int64_t)p.Q_depth * m.s + cd.qcomp) : p.sink + lane;
-            *dst = acc;
+            process(a, n, m);
         }
     }
     wait_vm<0>();  // no table DMA may outlive the wave's LDS
@@ -556,36 +592,6 @@ __device__ __forceinline__ int range_pos(const Ranges& R, int j) {
     for (int r = 1; r < NR; ++r)
         if (j >= R.pre[r]) pos = R.start[r] + (j - R.pre[r]);
     return pos;
-}
-
-// Lane assignment of the staged candidates.  A ds_add_f64 runs as four 16-lane
-// quarters, each costing about the largest number of its lanes whose f64 index
-// agrees mod 16 (tools/ubench_lds2.hip); a ring point's index mod 16 is its x
-// mod 16 (rows are 32 doubles).  The candidates are ranked by that class
-// (stable in staging order; inactive lanes last) and dealt round-robin over
-// the quarters, so the candidates of one class land in different quarters.
-// Returns the staged index this lane processes.
-__device__ __forceinline__ int deal_lanes(int cls) {  // cls in [0, 16]; 32 = inactive
-    const int lane = __lane_id();
-    unsigned long long eq = ~0ull, lt = 0ull;
-#pragma unroll
-    for (int b = 5; b >= 0; --b) {
-        const bool bit = (cls >> b) & 1;
-        const unsigned long long m = __ballot(bit);
-        lt |= bit ? (eq & ~m) : 0ull;
-        eq &= bit ? m : ~m;
-    }
-    const int k = __popcll(lt) + __popcll(eq & ((1ull << lane) - 1ull));  // rank
-    const int t = ((k & 3) << 4) | (k >> 2);                               // dealt lane
-    return __builtin_amdgcn_ds_permute(t << 2, lane);
-}
-
-// value of lane `src` (ds_bpermute on the two halves)
-__device__ __forceinline__ double shfl_f64(double v, int src) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b & 0xffffffffll));
-    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b >> 32));
-    return __hiloint2double(hi, lo);
 }
 
 // candidate data of one lane
@@ -749,8 +755,8 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // adds of the n <= 64 candidates held one per lane (lane j's anchor plane:
     // a - 1 for j < r, else a): dealt over the lanes by bank class, then spread
     auto process = [&](int a, int r, int n, const Cand& mine) {
-        const int cls = lane < n ? ((int)floor((mine.X[0] - cd.xlo[0]) * inv_dx + 0.5) & 15) : 32;
-        const int src = deal_lanes(cls);
+        const int cls = lane < n ? ((int)floor((mine.X[0] - cd.xlo[0]) * inv_dx + 0.5) & 15) : 63;
+        const int src = deal_lanes<4>(cls);
         Cand d;
 #pragma unroll
         for (int k = 0; k < 3; ++k) d.X[k] = shfl_f64(mine.X[k], src);
