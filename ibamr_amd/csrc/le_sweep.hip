@@ -225,7 +225,7 @@ template <int K> struct ISh {
     static constexpr int W = T::W, LO = T::LO, HI = T::HI, FAM = T::FAM;
     static constexpr int RX = COLX + HI - LO, RY = COLY + HI - LO;  // staged plane: column + stencil halo
     static constexpr int NS = HI - LO + 1;                          // planes an anchor plane reads (a+LO .. a+HI)
-    static constexpr int NSL = NS;                                  // ring slots
+    static constexpr int NSL = NS + 1;                              // ring slots: the planes two anchors read
     static constexpr int PV = RX * RY;
     static constexpr int NPT = (PV + SW - 1) / SW;                  // staged points per lane and plane
     // ring slot stride: a multiple of 32 doubles, so a point's LDS bank class
@@ -318,19 +318,22 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
 }
 
 
-// Interpolation work item = (segment, column, component).  The item sweeps its
-// anchor planes [a0, a1); the ring holds staged planes a+LO..a+HI.  Plane
-// a+HI+1 and the markers of anchor plane a+1 are loaded into registers while
-// plane a is summed (plain loads, so no LDS-DMA issue cost), and written into
-// the slot plane a+LO leaves at the top of the next step.  Points outside the
-// component's array are staged as 0.  One lane per marker sums its W^3 stencil
-// from the ring (Fortran loop order, bitwise the oracle's).
+// Interpolation work item = (segment, column, component), one workgroup of two
+// waves sharing one LDS ring (twice the waves per CU for the same LDS: the
+// per-marker sum is a dependent chain in the Fortran order, so the latency
+// wants waves).  The waves take the item's anchor planes in pairs: wave w sums
+// anchor a+w while the ring holds planes a+LO .. a+1+HI.  Per pair: barrier
+// (the previous pair's reads are done), each wave puts one new plane (a+w+HI)
+// into the slot a retired plane left, barrier, each wave prefetches its next
+// plane and markers into registers (plain loads) and sums its anchor.  Points
+// outside the component's array are staged as 0.  One lane per marker sums its
+// W^3 stencil from the ring (Fortran loop order, bitwise the oracle's).
+constexpr int IWAVES = 2;
 template <int K>
-__global__ __launch_bounds__(SW) void k_interp_sweep(Params p) {
+__global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     using S = ISh<K>;
-    constexpr int LO = S::LO, HI = S::HI, RX = S::RX, NPT = S::NPT, PT = S::PT;
+    constexpr int LO = S::LO, HI = S::HI, RX = S::RX, NPT = S::NPT;
     __shared__ double ring[S::NSL * S::PVP];
-    __shared__ int tab[2][PT][2];        // [beg, end) of the column's markers per anchor plane
     const int nitems = p.cg.ncol * p.nseg * p.ncomp;
     const int it = sweep_item(nitems);
     if (it < 0) return;
@@ -339,9 +342,10 @@ __global__ __launch_bounds__(SW) void k_interp_sweep(Params p) {
     const int col = cs % p.cg.ncol, seg = cs / p.cg.ncol;
     const int a0 = seg * p.S, a1 = min(a0 + p.S, p.cg.nz);
     const int lane = lane_id();
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int* bs = p.plane_start;
     {
-        bool any = false;
+        bool any = false;  // the same answer in both waves
         for (int a = a0 + lane; a < a1; a += SW) any = any || bs[bucket(p, a, col, NBAND)] > bs[bucket(p, a, col, 0)];
         if (!__any(any)) return;
     }
@@ -382,21 +386,15 @@ __global__ __launch_bounds__(SW) void k_interp_sweep(Params p) {
             if (S::PV % SW == 0 || k < NPT - 1 || lane + SW * k < S::PV)
                 sl[lane + SW * k] = (zin && ((okm >> k) & 1u)) ? v[k] : 0.0;
     };
-    // bucket-start tables: buffer b holds anchor planes [a0 + t PT, a0 + (t+1) PT), b = t & 1
-    auto tab_dma = [&](int t) {
-        const int from = a0 + t * PT;
-        char* lb = (char*)&tab[t & 1][0][0];
-#pragma unroll
-        for (int i = 0; i < (2 * PT + SW - 1) / SW; ++i) {
-            const int d = min(lane + SW * i, 2 * PT - 1);
-            const int a = min(from + (d >> 1), p.cg.nz - 1);
-            glds4(bs + bucket(p, a, col, (d & 1) ? NBAND : 0), lb + 256 * i);
-        }
-    };
-    auto tab_at = [&](int a, int k) { const int r = a - a0; return tab[(r / PT) & 1][r % PT][k]; };
     struct Mk {
         int s;
         double X[3];
+    };
+    // anchor a's markers [beg, end) (an empty range past a1)
+    auto span = [&](int a, int& beg, int& end) {
+        const int ac = min(a, p.cg.nz - 1);
+        beg = __builtin_amdgcn_readfirstlane(bs[bucket(p, ac, col, 0)]);
+        end = a < a1 ? __builtin_amdgcn_readfirstlane(bs[bucket(p, ac, col, NBAND)]) : beg;
     };
     auto mk_load = [&](int beg, int cnt, Mk& m) {  // markers beg + lane (clamped)
         const int e = min(beg + min(lane, max(cnt - 1, 0)), nlast);
@@ -406,7 +404,6 @@ __global__ __launch_bounds__(SW) void k_interp_sweep(Params p) {
         m.X[1] = xs[1];
         m.X[2] = xs[2];
     };
-
     // one chunk of n <= 64 markers held one per lane: summed, stored.  (Dealing
     // the markers over the two 32-lane halves of a ds_read_b64 by bank class,
     // as the spread does for its adds, measured 10 % slower: the ranking costs
@@ -418,51 +415,46 @@ __global__ __launch_bounds__(SW) void k_interp_sweep(Params p) {
         double* dst = act ? p.Qout + ((int64_t)p.Q_depth * m.s + cd.qcomp) : p.sink + lane;
         *dst = acc;
     };
+    // LDS barrier of the two waves; global loads in flight stay in flight
+    auto lds_barrier = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
 
-    // prologue: tables; planes a0+LO .. a0+HI-1 into the ring; plane a0+HI and
-    // the markers of a0 into registers
-    tab_dma(0);
-    tab_dma(1);
-    wait_vm<0>();
+    // prologue: planes a0+LO .. a0+HI-1 into the ring (alternately by the two
+    // waves); plane a0+w+HI and the markers of anchor a0+w into registers
     double pv[NPT];
-    for (int z = a0 + LO; z < a0 + HI; ++z) {
+    for (int z = a0 + LO + w; z < a0 + HI; z += IWAVES) {
         plane_load(z, pv);
         plane_put(z, pv);
     }
-    plane_load(a0 + HI, pv);
+    plane_load(a0 + w + HI, pv);
     Mk nxt;
-    int nxt_n;
-    {
-        const int b = tab_at(a0, 0), e = tab_at(a0, 1);
-        nxt_n = min(e - b, SW);
-        mk_load(b, nxt_n, nxt);
-    }
-    for (int a = a0; a < a1; ++a) {
-        plane_put(a + HI, pv);  // into the slot plane a+LO-1 left
+    int nb, ne;
+    span(a0 + w, nb, ne);
+    mk_load(nb, min(ne - nb, SW), nxt);
+    for (int a = a0; a < a1; a += IWAVES) {
+        const int my = a + w;  // this wave's anchor plane
+        lds_barrier();          // the previous pair's reads are done
+        plane_put(my + HI, pv);
+        lds_barrier();          // planes a+LO .. a+1+HI are in the ring
         const Mk cur = nxt;
-        const int cur_n = nxt_n;
-        const int beg = tab_at(a, 0), end = tab_at(a, 1);
-        // prefetch for a+1: table (every PT planes), markers, plane a+HI+1
-        if (a + 1 < a1) {
-            const int r1 = a + 1 - a0;
-            if (r1 % PT == 0) {
-                wait_vm<0>();  // table r1 / PT (issued PT planes ago) has landed
-                if (a + 1 + PT < a1) tab_dma(r1 / PT + 1);
+        const int beg = nb, end = ne;
+        // prefetch for the next pair: markers of my+2, plane my+2+HI
+        span(my + IWAVES, nb, ne);
+        mk_load(nb, min(ne - nb, SW), nxt);
+        plane_load(my + IWAVES + HI, pv);
+        if (my < a1) {
+            process(my, min(end - beg, SW), cur);
+            for (int e0 = beg + SW; e0 < end; e0 += SW) {  // further chunks of a dense plane
+                const int n = min(end - e0, SW);
+                Mk m;
+                mk_load(e0, n, m);
+                process(my, n, m);
             }
-            const int nb = tab_at(a + 1, 0);
-            nxt_n = min(tab_at(a + 1, 1) - nb, SW);
-            mk_load(nb, nxt_n, nxt);
-            plane_load(a + HI + 1, pv);
-        }
-        process(a, cur_n, cur);  // chunk 0 from the prefetched markers
-        for (int e0 = beg + SW; e0 < end; e0 += SW) {  // further chunks of a dense plane
-            const int n = min(end - e0, SW);
-            Mk m;
-            mk_load(e0, n, m);
-            process(a, n, m);
         }
     }
-    wait_vm<0>();  // no table DMA may outlive the wave's LDS
 }
 
 // Entries binned "outside" (no stencil point can reach any array): V = 0.
@@ -902,7 +894,7 @@ template <int K>
 hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     if (ev0) (void)hipEventRecord(ev0, s);
     const long items = (long)p.cg.ncol * p.nseg * p.ncomp;
-    if (items > 0) hipLaunchKernelGGL(k_interp_sweep<K>, dim3(grid8(items)), dim3(SW), 0, s, p);
+    if (items > 0) hipLaunchKernelGGL(k_interp_sweep<K>, dim3(grid8(items)), dim3(SW * IWAVES), 0, s, p);
     if (ev1) (void)hipEventRecord(ev1, s);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
