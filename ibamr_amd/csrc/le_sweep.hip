@@ -220,12 +220,14 @@ __device__ __forceinline__ double shfl_f64(double v, int src) {
 // ---------------------------------------------------------------------------
 // interpolation
 // ---------------------------------------------------------------------------
+constexpr int IWAVES = 4;  // waves per interp work item (one LDS ring)
+
 template <int K> struct ISh {
     using T = KT<K>;
     static constexpr int W = T::W, LO = T::LO, HI = T::HI, FAM = T::FAM;
     static constexpr int RX = COLX + HI - LO, RY = COLY + HI - LO;  // staged plane: column + stencil halo
     static constexpr int NS = HI - LO + 1;                          // planes an anchor plane reads (a+LO .. a+HI)
-    static constexpr int NSL = NS + 1;                              // ring slots: the planes two anchors read
+    static constexpr int NSL = NS + IWAVES - 1;                     // ring slots: the planes IWAVES anchors read
     static constexpr int PV = RX * RY;
     static constexpr int NPT = (PV + SW - 1) / SW;                  // staged points per lane and plane
     // ring slot stride: a multiple of 32 doubles, so a point's LDS bank class
@@ -328,7 +330,6 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
 // plane and markers into registers (plain loads) and sums its anchor.  Points
 // outside the component's array are staged as 0.  One lane per marker sums its
 // W^3 stencil from the ring (Fortran loop order, bitwise the oracle's).
-constexpr int IWAVES = 2;
 template <int K>
 __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     using S = ISh<K>;
