@@ -163,14 +163,17 @@ template <int KID> __device__ __forceinline__ int closed_weights(double X_o_dx, 
 //   xlo  = the component frame's x_lower(d);  ilo = its ilower(d)
 //   [glo, ghi] = the component array's ghost box in dim d
 //   axis_dim = (d == axis) for DISCONTINUOUS_LINEAR
-template <int K>
+//   MUL: X_o_dx by a multiply with inv_dx = 1/dx instead of the Fortran's
+//        division (closed-form kernels only): within an ulp of it, for the
+//        spread, whose sums are compared by tolerance, not bit for bit
+template <int K, bool MUL = false>
 __device__ __forceinline__ void stencil1d(double Xs, double Xraw, double xlo, double dx, int ilo, int glo, int ghi,
-                                          bool axis_dim, double K6, St<KT<K>::W>& st) {
+                                          bool axis_dim, double K6, St<KT<K>::W>& st, double inv_dx = 0.0) {
     constexpr int W = KT<K>::W;
     constexpr int FAM = KT<K>::FAM;
     if constexpr (FAM == 0) {
         // f.m4:1316 (X_o_dx), :1360-1365 (istart/istop)
-        const double X_o_dx = (Xs - xlo) / dx;
+        const double X_o_dx = MUL ? (Xs - xlo) * inv_dx : (Xs - xlo) / dx;
         st.icl = closed_weights<K>(X_o_dx, ilo, st.w, K6);
         const int icu = st.icl + (W - 1);
         st.ist = max(glo - st.icl, 0);

@@ -611,15 +611,15 @@ struct Cand {
 template <int K>
 __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
                                              bool act, int a, int X0, int Y0, int xlo, int xhi, int ylo, int yhi, int plo,
-                                             int phi, double inv_h3, Clk& clk) {
+                                             int phi, double inv_h3, const double* inv_d, Clk& clk) {
     using S = SSh<K>;
     constexpr int W = S::W, FAM = S::FAM, LO = S::LO, HI = S::HI, NS = S::NS, NSL = S::NSL;
     St<W> st[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
         const double Xraw = (FAM == 2) ? p.X[(int64_t)3 * cdat.s + d] : cdat.X[d];
-        stencil1d<K>(cdat.X[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis, p.K6,
-                     st[d]);
+        stencil1d<K, true>(cdat.X[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis,
+                           p.K6, st[d], inv_d[d]);
     }
     int ox = st[0].icl - X0, oy = st[1].icl - Y0, oz = st[2].icl - (p.cg.org[2] + a);
     bool ok = act;
@@ -635,10 +635,12 @@ __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd
     // x: weight x value with the mask folded in (f.m4:1512-1513 order, V applied
     // first: within rounding of the Fortran's (w0 (w1 w2/h)) V)
     double w0v[W];
+    bool vy[W];
 #pragma unroll
     for (int i = 0; i < W; ++i) {
         const bool vx = ok && i >= st[0].ist && i <= st[0].isp && ox + i >= xlo && ox + i <= xhi;
         w0v[i] = vx ? st[0].w[i] * cdat.V : 0.0;
+        vy[i] = i >= st[1].ist && i <= st[1].isp && oy + i >= ylo && oy + i <= yhi;
     }
     char* const base = reinterpret_cast<char*>(ring) + 8 * ox;
     clk.lap(2);
@@ -656,7 +658,7 @@ __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd
         else wz = st[2].w[i2] * inv_h3;
 #pragma unroll
         for (int i1 = 0; i1 < W; ++i1) {
-            const bool vr = vz && i1 >= st[1].ist && i1 <= st[1].isp && oy + i1 >= ylo && oy + i1 <= yhi;
+            const bool vr = vz && vy[i1];
             const double t = vr ? st[1].w[i1] * wz : 0.0;  // f.m4:1489-1492
             double* const row =
                 reinterpret_cast<double*>(base + zb + 8 * COLX * min(max(oy + i1, 0), COLY - 1));
@@ -745,6 +747,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     Clk clk;
     const double inv_dx = 1.0 / p.bg.dx[0];  // lane dealing only (approximate class)
     const double inv_h3 = 1.0 / p.h3;
+    const double inv_d[3] = {1.0 / p.bg.dx[0], 1.0 / p.bg.dx[1], 1.0 / p.bg.dx[2]};
     // adds of the n <= 64 candidates held one per lane (lane j's anchor plane:
     // a - 1 for j < r, else a): dealt over the lanes by bank class, then spread
     auto process = [&](int a, int r, int n, const Cand& mine) {
@@ -756,7 +759,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         d.V = shfl_f64(mine.V, src);
         d.s = FAM == 2 ? __builtin_amdgcn_ds_bpermute(src << 2, mine.s) : 0;
         spread_lanes<K>(p, cd, ring, d, src < n, src < r ? a - 1 : a, X0, Y0, xlo, xhi, ylo, yhi, plo, phi, inv_h3,
-                        clk);
+                        inv_d, clk);
     };
     // plane z -> registers (the lane's NPL points); registers -> ring slot
     auto plane_load = [&](int z, double* v) {
