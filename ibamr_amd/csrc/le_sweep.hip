@@ -163,8 +163,15 @@ template <int N> __device__ __forceinline__ void wait_vm() {
 }
 __device__ __forceinline__ void mem_fence_compiler() { asm volatile("" ::: "memory"); }
 
-// diagnostic phase clocks (Params::stamps != nullptr): per work item, cycles
-// spent per phase, accumulated in registers and written once at the end
+// Diagnostic phase clocks (Params::stamps != nullptr): per work item, cycles
+// spent per phase, accumulated in registers and written once at the end.
+// Phase clocks (s_memtime per work item, IBTK_LE_STAMPS=1 at run time) exist
+// only in builds with -DIBTK_LE_CLOCKS=1: their 64-bit accumulators would
+// otherwise hold 14 SGPRs through the sweep loop.
+#ifndef IBTK_LE_CLOCKS
+#define IBTK_LE_CLOCKS 0
+#endif
+#if IBTK_LE_CLOCKS
 struct Clk {
     unsigned long long t = 0, acc[6] = {0, 0, 0, 0, 0, 0};
     bool on = false;
@@ -184,6 +191,13 @@ struct Clk {
             for (int k = 0; k < 6; ++k) p.stamps[(int64_t)it * 8 + k] = acc[k];
     }
 };
+#else
+struct Clk {
+    __device__ __forceinline__ void start(bool) {}
+    __device__ __forceinline__ void lap(int) {}
+    __device__ __forceinline__ void flush(const Params&, int) {}
+};
+#endif
 
 // Lane assignment of staged markers by LDS bank class.  An LDS instruction runs
 // as G lane groups, each costing about the largest number of its lanes that

@@ -272,3 +272,38 @@ def test_empty_list_is_a_noop(le, ctx):
     le.interp(ctx, m, "IB_4", "side", geom, q, X, X)
     ctx.synchronize()
     assert all(bool((a == 1.5).all()) for a in q)
+
+
+@pytest.mark.parametrize("kernel", ALL)
+def test_dense_uniform_side(le, ctx, oracle, kernel):
+    """~2 markers per cell: hundreds of markers per (column, anchor plane), so
+    the sweeps run full middle chunks and carry leftovers from one anchor plane
+    into the next; interp bitwise-close and spread within tolerance of the oracle."""
+    from ibamr_amd.le import Geometry
+    geom = Geometry.periodic_unit([32, 32, 32], oracle.min_ghost_width(kernel) + 1)
+    g = torch.Generator(device="cuda:0").manual_seed(21)
+    M = 65_000
+    X = torch.rand((M, 3), dtype=torch.float64, device="cuda:0", generator=g)
+    F = torch.rand((M, 3), dtype=torch.float64, device="cuda:0", generator=g) - 0.5
+    u = geom.alloc("side")
+    for a in u:
+        a.uniform_(-1.0, 1.0, generator=g)
+    le.fill_periodic_ghosts(ctx, geom, "side", u)
+    u0 = [a.cpu().numpy().copy() for a in u]
+    U = torch.zeros((M, 3), dtype=torch.float64, device="cuda:0")
+    m = le.Markers(ctx).bin(geom, kernel, X)
+    le.interp(ctx, m, kernel, "side", geom, u, U, X)
+    q = geom.alloc("side")
+    le.spread(ctx, m, kernel, "side", geom, q, F, X)
+    ctx.synchronize()
+    Xn, Fn = X.cpu().numpy(), F.cpu().numpy()
+    idx = np.arange(M, dtype=np.int32)
+    xs = np.zeros((M, 3))
+    Uo = np.zeros((M, 3))
+    oracle.side_interp(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, u0, idx, xs, Xn, Uo)
+    assert rel_err(U.cpu().numpy(), Uo) <= INTERP_TOL
+    order = m.order().cpu().numpy()
+    uo = [np.zeros(tuple(a.shape)) for a in q]
+    oracle.side_spread(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, uo, idx[order], xs, Xn, Fn)
+    for a in range(3):
+        assert rel_err(q[a].cpu().numpy(), uo[a]) <= SPREAD_TOL, f"spread comp {a}"
