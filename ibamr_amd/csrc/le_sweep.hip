@@ -4,28 +4,28 @@
 // kernel function (IB_4 :1258-1522, IB_6 :1851-2255, IB_4_W8 :1532-1850, the
 // piecewise kernels :49-971).
 //
-// Decomposition (DESIGN.md §Kernels):
-//  * bin: key = (anchor plane z, column) with columns of COLX x COLY key cells;
-//    stable device radix sort; bucket starts; a coalescing pass writes the
-//    sorted marker index, the sorted shifted position X(s)+Xshift(l) and the
-//    packed key cell.  The sorted list is z-major.
-//  * one wavefront = one work item (column, z-segment, component); no
-//    barriers, the waves of a CU are independent workers.
-//  * interp: the item streams the z-planes of its column's staged region
-//    (column + stencil halo) through an LDS ring of HI-LO+1 planes (the next
-//    two planes prefetched in registers).  For anchor plane a, one lane per
+// Decomposition (DESIGN.md section 4):
+//  * bin: key = (anchor plane z, column, reach band) with columns of COLX x COLY
+//    key cells; stable device radix sort; a gather pass writes the sorted
+//    marker index and the sorted shifted position X(s)+Xshift(l), fused with
+//    the bucket starts.  The sorted list is z-major: one global order.
+//  * a sweep work item is (column, z-segment, component).  Everything it reads
+//    in its z loop is register-staged one anchor plane ahead with plain loads
+//    and put into an LDS ring at the top of the next step.
+//  * interp: IWAVES waves per item share the ring of the column's staged region
+//    (column + stencil halo) and take alternate anchor planes.  One lane per
 //    marker sums its W^3 stencil from the ring in the Fortran loop order (i2,
 //    i1, i0), so the value is bitwise the oracle's.
-//  * spread: the item owns the column's points in its z-segment.  Planes are
-//    loaded (u_old) when the first anchor plane that reaches them comes up and
-//    written back when the last one has passed.  Per anchor plane, the markers
-//    of the 3x3 neighbouring buckets whose stencil reaches the column (11
-//    contiguous ranges of the sorted list, by band) are staged 64 at a time,
-//    one lane per candidate; each lane computes its 1-D weights in registers
-//    and issues its W^3 adds as LDS f64 atomics (ds_add_f64) into the ring.
-//    Every grid point receives its contributions in a fixed order (staging
-//    order, lane order within an instruction): bit-stable from run to run,
-//    within rounding of the oracle's sequential l-loop.
+//  * spread: one wave per item owns the column's points in its z-segment.
+//    Planes are loaded (u_old) when the first anchor plane that reaches them
+//    comes up and written back when the last one has passed.  The candidates
+//    (markers of the 3x3 neighbouring buckets whose stencil reaches the column:
+//    11 contiguous ranges of the sorted list, by band) stream through full
+//    64-lane chunks across anchor planes; each lane computes its candidate's
+//    1-D weights in registers and issues its W^3 adds as LDS f64 atomics
+//    (ds_add_f64).  Every grid point receives its contributions in a fixed
+//    order (staging order, lane order within an instruction): bit-stable from
+//    run to run, within rounding of the oracle's sequential l-loop.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -138,14 +138,10 @@ __device__ __forceinline__ int bucket(const Params& p, int a, int col, int band)
 // ---------------------------------------------------------------------------
 // LDS-DMA and counted waits
 // ---------------------------------------------------------------------------
-// Everything the sweeps read inside their z loop (planes, marker data, bucket
-// starts) arrives by LDS-DMA (global_load_lds, per-lane source addresses, no
-// VGPR destination), issued one step ahead.  The loop then holds no ordinary
-// global load, so the compiler inserts no vmcnt waits of its own; each step
-// opens with one counted wait, vmcnt(N) with N = the memory operations the
-// previous step issued after the data this step needs (their order and number
-// per step are fixed: masked lanes load clamped addresses and store to
-// Params::sink).
+// The bucket-start tables of the interp prologue still arrive by LDS-DMA
+// (global_load_lds, per-lane source addresses, no VGPR destination) with a
+// counted wait.  The sweep loops themselves register-stage their data: an
+// LDS-DMA instruction costs 100-200 cycles to issue.
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void gbl_void_t;
 
@@ -816,13 +812,16 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     plane_load(afirst + HI, pv);
     int rowv[3];
     rows_load(afirst, rowv);
-    Ranges rgA;
-    make_ranges_lanes(rowv, rgA);
-    int tA = rgA.pre[S::NR];
+    Ranges rg;  // ranges of the anchor whose chunk 1 is prefetched (wave-uniform)
+    make_ranges_lanes(rowv, rg);
+    int tA = rg.pre[S::NR];
     Cand nxt;
-    cand_at(range_pos(rgA, min(lane, max(tA - 1, 0))), nxt);
-    int r_prev = 0;                 // candidates of anchor a-1 carried into a's chunk 1
-    int n1 = min(tA, SW);           // lanes of a's chunk 1
+    cand_at(range_pos(rg, min(lane, max(tA - 1, 0))), nxt);
+    // per lane l: sorted position of that anchor's candidate tA - 64 + l (its
+    // last 64; the carried ones are taken from here, so only one Ranges is live)
+    int etail = range_pos(rg, max(tA - SW + lane, 0));
+    int r_prev = 0;        // candidates of anchor a-1 carried into a's chunk 1
+    int n1 = min(tA, SW);  // lanes of a's chunk 1
     if (afirst + 1 <= alast) rows_load(afirst + 1, rowv);
     clk.lap(0);
     for (int a = afirst; a <= alast; ++a) {
@@ -830,33 +829,40 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         plane_put(a + HI, pv);                               // into its slot
         const Cand cur = nxt;
         const int cur_r = r_prev, cur_n = n1;
-        const Ranges rgCur = rgA;
         const int tCur = tA;
+        const int etCur = etail;
         const int h = min(SW - r_prev, tCur);  // a's candidates in chunk 1
         const int nmid = (tCur - h) / SW;       // full middle chunks
         const int r_a = (tCur - h) % SW;        // carried into a+1
         clk.lap(1);
         // prefetch for a+1: its ranges, its chunk 1, plane a+HI+1, the rows of a+2
         if (a + 1 <= alast) {
-            make_ranges_lanes(rowv, rgA);
-            tA = rgA.pre[S::NR];
-            const int eA = range_pos(rgCur, min(tCur - r_a + lane, max(tCur - 1, 0)));
-            const int eB = range_pos(rgA, min(lane - r_a, max(tA - 1, 0)));
+            make_ranges_lanes(rowv, rg);
+            tA = rg.pre[S::NR];
+            const int eA = __builtin_amdgcn_ds_bpermute((SW - r_a + lane) << 2, etCur);  // a's last r_a
+            const int eB = range_pos(rg, min(max(lane - r_a, 0), max(tA - 1, 0)));
             cand_at(lane < r_a ? eA : eB, nxt);
+            etail = range_pos(rg, max(tA - SW + lane, 0));
             n1 = r_a + min(SW - r_a, tA);
             r_prev = r_a;
             plane_load(a + HI + 1, pv);
             if (a + 2 <= alast) rows_load(a + 2, rowv);
         }
         if (cur_n > 0) process(a, cur_r, cur_n, cur);
-        for (int k = 0; k < nmid; ++k) {  // dense planes: the full middle chunks
-            Cand more;
-            cand_at(range_pos(rgCur, h + SW * k + lane), more);
-            process(a, 0, SW, more);
+        if (nmid > 0) {  // dense planes: the full middle chunks (ranges of a rebuilt)
+            int rowm[3];
+            rows_load(a, rowm);
+            Ranges rgm;
+            make_ranges_lanes(rowm, rgm);
+            for (int k = 0; k < nmid; ++k) {
+                Cand more;
+                cand_at(range_pos(rgm, h + SW * k + lane), more);
+                process(a, 0, SW, more);
+            }
         }
         if (a == alast && r_a > 0) {  // the last anchor's leftovers
             Cand last;
-            cand_at(range_pos(rgCur, tCur - r_a + min(lane, r_a - 1)), last);
+            cand_at(__builtin_amdgcn_ds_bpermute((SW - r_a + min(lane, r_a - 1)) << 2, etCur), last);
             process(a, 0, r_a, last);
         }
         clk.lap(4);
