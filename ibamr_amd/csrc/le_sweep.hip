@@ -136,28 +136,8 @@ __device__ __forceinline__ int bucket(const Params& p, int a, int col, int band)
 }
 
 // ---------------------------------------------------------------------------
-// LDS-DMA and counted waits
+// diagnostics
 // ---------------------------------------------------------------------------
-// The bucket-start tables of the interp prologue still arrive by LDS-DMA
-// (global_load_lds, per-lane source addresses, no VGPR destination) with a
-// counted wait.  The sweep loops themselves register-stage their data: an
-// LDS-DMA instruction costs 100-200 cycles to issue.
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void gbl_void_t;
-
-// global_load_lds_dword in inline asm rather than the builtin: the compiler then
-// does not track the LDS write and inserts no vmcnt(0) before every LDS read
-// that might alias it (it cannot tell ring slots apart) -- the counted waits
-// below are the synchronisation.  M0 = the wave-uniform LDS byte address.
-__device__ __forceinline__ void glds4(const void* g, void* l) {
-    const unsigned m = (unsigned)(uintptr_t)(lds_void_t*)l;
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(m) : "memory", "m0");
-}
-template <int N> __device__ __forceinline__ void wait_vm() {
-    static_assert(N >= 0 && N < 64, "vmcnt range");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-__device__ __forceinline__ void mem_fence_compiler() { asm volatile("" ::: "memory"); }
 
 // Diagnostic phase clocks (Params::stamps != nullptr): per work item, cycles
 // spent per phase, accumulated in registers and written once at the end.
@@ -243,7 +223,6 @@ template <int K> struct ISh {
     // ring slot stride: a multiple of 32 doubles, so a point's LDS bank class
     // (f64 index mod 32) does not depend on its plane
     static constexpr int PVP = (PV + 31) / 32 * 32;
-    static constexpr int PT = 64;                                   // planes per bucket-start table
 };
 
 template <int K> __device__ __forceinline__ int islot(int prel) {
@@ -487,13 +466,7 @@ template <int K> struct SSh {
     static constexpr int NSL = NS + 1;                  // ring slots: the planes two anchors reach
     static constexpr int PV = COLX * COLY;              // owned points per plane
     static constexpr int NPL = PV / SW;
-    static constexpr int PD = 2 * PV / SW;              // DMA instructions per plane (one row each)
-    static constexpr int NCD = FAM == 2 ? 9 : 8;        // candidate dwords staged: X[3], V (, s)
-    static constexpr int PT = 4;                        // planes per bucket-start table
-    static constexpr int TW = 3 * 28;                   // table ints per plane
-    static constexpr int TD = (PT * TW + SW - 1) / SW;  // DMA instructions per table
     static constexpr int NR = 11;                       // candidate ranges per anchor plane
-    static constexpr int WAIT = PD;                     // step-start vmcnt: the plane DMA
     // ring slot stride: a 16-double gap after each plane takes the spill of the
     // zero-weight adds of stencil columns that stick out of the column (x in
     // [-3, 34] of rows 0..COLY-1); a multiple of 16 keeps every point's bank
@@ -512,39 +485,7 @@ template <int K> __device__ __forceinline__ int sslot(int prel) {
     return (int)((unsigned)(prel + 16 * S::NSL) % (unsigned)S::NSL);  // prel >= -HI + LO > -16*NSL
 }
 
-// DMA of plane z (absolute, clamped into the array) of the column's owned
-// points into ring slot `slot`: row y is one instruction, lane = dword
-// (lane & 1) of point x = lane >> 1.  xoff: the lane's clamped x offset.
-template <int K>
-__device__ __forceinline__ void splane_dma(const CompDesc& cd, double* ring, int slot, int z, int Y0,
-                                           int xoff) {
-    using S = SSh<K>;
-    const int zc = min(max(z, cd.lo[2]), cd.hi[2]);
-    const char* pb = (const char*)(cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2) + 4 * (lane_id() & 1);
-    char* lb = (char*)(ring + slot * S::SLOT);
-#pragma unroll
-    for (int y = 0; y < COLY; ++y) {
-        const int yc = min(max(Y0 + y, cd.lo[1]), cd.hi[1]);
-        glds4(pb + 8 * ((int64_t)(yc - cd.lo[1]) * cd.s1 + xoff), lb + 256 * y);
-    }
-}
 
-// write-back of ring slot `slot` to plane z; lanes of points outside the owned,
-// in-array range (or every lane when !ok) store to p.sink instead
-template <int K>
-__device__ __forceinline__ void splane_store(const Params& p, const CompDesc& cd, const double* ring, int slot, int z,
-                                             bool ok, const int* loff, unsigned okxy) {
-    using S = SSh<K>;
-    const int lane = lane_id();
-    const int zc = min(max(z, cd.lo[2]), cd.hi[2]);
-    double* base = cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2;
-#pragma unroll
-    for (int k = 0; k < S::NPL; ++k) {
-        const int q = lane + k * SW;
-        double* dst = (ok && ((okxy >> k) & 1u)) ? base + loff[k] : p.sink + lane;
-        *dst = ring[slot * S::SLOT + swz(q & (COLX - 1), q / COLX)];
-    }
-}
 
 // The candidate ranges of anchor plane a for column (cx, cy), in sorted (bucket)
 // order, from the bucket-start table row t[r][i] = bs(a, col(cx-1, cy-1+r), 0) + i
@@ -569,21 +510,6 @@ __device__ __forceinline__ void make_ranges_lanes(const int* rowv, Ranges& R) {
         R.start[r] = b;
         R.pre[r] = acc;
         acc += e - b;
-    }
-    R.pre[NR] = acc;
-}
-__device__ __forceinline__ void make_ranges(const int (*t)[28], Ranges& R) {
-    constexpr int NR = SSh<K_IB_4>::NR;
-    // (row, first index, last index + 1) of each range
-    constexpr int rr[NR] = {0, 0, 0, 0, 0, 1, 2, 2, 2, 2, 2};
-    constexpr int ib[NR] = {8, 11, 14, 17, 20, 6, 6, 9, 12, 15, 18};
-    constexpr int ie[NR] = {9, 12, 15, 18, 21, 21, 7, 10, 13, 16, 19};
-    int acc = 0;
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-        R.start[r] = t[rr[r]][ib[r]];
-        R.pre[r] = acc;
-        acc += t[rr[r]][ie[r]] - t[rr[r]][ib[r]];
     }
     R.pre[NR] = acc;
 }
