@@ -211,6 +211,11 @@ __device__ __forceinline__ double shfl_f64(double v, int src) {
 // interpolation
 // ---------------------------------------------------------------------------
 constexpr int IWAVES = 4;  // waves per interp work item (one LDS ring)
+// 1: interp sums in the Fortran order, bitwise the oracle's (default);
+// 0: separable rows with FMAs, within tolerance (an experiment, not shipped)
+#ifndef IBTK_LE_INTERP_EXACT
+#define IBTK_LE_INTERP_EXACT 1
+#endif
 
 template <int K> struct ISh {
     using T = KT<K>;
@@ -267,17 +272,35 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
         // == acc bit for bit (acc is never -0), so the clipped sum of
         // f.m4:1366-1382 needs no per-point branch.
         const double* base = ring + oy * RX + ox;
+        if constexpr (IBTK_LE_INTERP_EXACT) {
 #pragma unroll
-        for (int i2 = 0; i2 < W; ++i2) {
-            const double* pl = base + islot<K>(oz + i2) * PV;
+            for (int i2 = 0; i2 < W; ++i2) {
+                const double* pl = base + islot<K>(oz + i2) * PV;
 #pragma unroll
-            for (int i1 = 0; i1 < W; ++i1) {
-                const double wyz = st[1].w[i1] * st[2].w[i2];  // f.m4:1349-1353
+                for (int i1 = 0; i1 < W; ++i1) {
+                    const double wyz = st[1].w[i1] * st[2].w[i2];  // f.m4:1349-1353
 #pragma unroll
-                for (int i0 = 0; i0 < W; ++i0) {
-                    const double wt = st[0].w[i0] * wyz;
-                    acc = acc + wt * pl[i1 * RX + i0];  // f.m4:1375
+                    for (int i0 = 0; i0 < W; ++i0) {
+                        const double wt = st[0].w[i0] * wyz;
+                        acc = acc + wt * pl[i1 * RX + i0];  // f.m4:1375
+                    }
                 }
+            }
+        } else {
+            // separable rows with fused multiply-adds: within a few ulp of the
+            // Fortran order, not bitwise (a tolerance build)
+#pragma unroll
+            for (int i2 = 0; i2 < W; ++i2) {
+                const double* pl = base + islot<K>(oz + i2) * PV;
+                double az = 0.0;
+#pragma unroll
+                for (int i1 = 0; i1 < W; ++i1) {
+                    double r = st[0].w[0] * pl[i1 * RX];
+#pragma unroll
+                    for (int i0 = 1; i0 < W; ++i0) r = __builtin_fma(st[0].w[i0], pl[i1 * RX + i0], r);
+                    az = __builtin_fma(st[1].w[i1], r, az);
+                }
+                acc = __builtin_fma(st[2].w[i2], az, acc);
             }
         }
     } else {
