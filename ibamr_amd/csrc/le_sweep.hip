@@ -618,12 +618,14 @@ __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd
 #pragma unroll
         for (int i1 = 0; i1 < W; ++i1) {
             const bool vr = vz && vy[i1];
-            const double t = vr ? st[1].w[i1] * wz : 0.0;  // f.m4:1489-1492
+            const double t = st[1].w[i1] * wz;  // f.m4:1489-1492
             double* const row =
                 reinterpret_cast<double*>(base + zb + 8 * COLX * min(max(oy + i1, 0), COLY - 1));
+            if (vr) {  // lanes whose row is clipped or not owned sit the row out
 #pragma unroll
-            for (int i0 = 0; i0 < W; ++i0)
-                __hip_atomic_fetch_add(row + i0, w0v[i0] * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                for (int i0 = 0; i0 < W; ++i0)
+                    __hip_atomic_fetch_add(row + i0, w0v[i0] * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
         }
     }
     }
