@@ -160,3 +160,54 @@ class SlabExchange:
             a[b0:b1].add_(rhi)   # from below first ...
             a[t0:t1].add_(rlo)   # ... then from above
         self.local_fold([1, 1, 0])
+
+
+def migrate(slab: Slab, X: torch.Tensor, fields: Sequence[torch.Tensor] = (), group=None, cell_order: bool = True):
+    """Move every marker to the rank whose slab holds its cell, after a position update.
+
+    The reference migrates at regrid (LDataManager::beginDataRedistribution /
+    endDataRedistribution, LDataManager.cpp:1337-1959, owner by
+    IndexUtilities::getCellIndex); SURVEY.md 8(e) asks for it after every update.
+    One all-to-all of counts and one of data (torch.distributed: RCCL on GPUs,
+    gloo on CPU).  Positions are wrapped into the periodic box [0, L)^3 first.
+
+    X: (M, 3) float64; fields: tensors with M rows (any trailing shape, cast to
+    float64 for the exchange and back).  Returns (X, fields) of the markers this
+    rank owns afterwards: received in source-rank order, each source's markers in
+    their previous order, then (cell_order) stably sorted by cell (z, y, x) -- the
+    local numbering LDataManager::computeNodeDistribution gives
+    (LDataManager.cpp:2839-3027).  Deterministic: the same inputs give the same
+    order on every run.
+    """
+    import torch.distributed as dist
+    M = X.shape[0]
+    L = torch.tensor(list(slab.L), dtype=X.dtype, device=X.device)
+    Xw = torch.remainder(X, L)
+    Xw = torch.where(Xw >= L, Xw - L, Xw)  # remainder can round up to L
+    cell = [torch.clamp((Xw[:, d] / slab.dx[d]).floor().long(), 0, slab.N[d] - 1) for d in range(3)]
+    dest = cell[2] // slab.nz
+    order = torch.argsort(dest, stable=True)
+    cols = [Xw] + [f.reshape(M, -1).to(X.dtype) for f in fields]
+    widths = [c.shape[1] for c in cols]
+    send = torch.cat(cols, dim=1)[order].contiguous()
+    send_counts = torch.bincount(dest, minlength=slab.P).to(torch.int64)
+    recv_counts = torch.empty_like(send_counts)
+    if slab.P == 1:
+        recv, recv_counts = send, send_counts
+    else:
+        dist.all_to_all_single(recv_counts, send_counts, group=group)
+        D = send.shape[1]
+        recv = torch.empty((int(recv_counts.sum().item()), D), dtype=send.dtype, device=send.device)
+        dist.all_to_all_single(recv, send, output_split_sizes=recv_counts.tolist(),
+                               input_split_sizes=send_counts.tolist(), group=group)
+    if cell_order and recv.shape[0]:
+        c = [torch.clamp((recv[:, d] / slab.dx[d]).floor().long(), 0, slab.N[d] - 1) for d in range(3)]
+        key = (c[2] * slab.N[1] + c[1]) * slab.N[0] + c[0]
+        recv = recv[torch.argsort(key, stable=True)]
+    outs, k = [], 0
+    for w in widths:
+        outs.append(recv[:, k:k + w])
+        k += w
+    Xn = outs[0].contiguous()
+    fn = [o.reshape((o.shape[0],) + tuple(f.shape[1:])).to(f.dtype).contiguous() for o, f in zip(outs[1:], fields)]
+    return Xn, fn

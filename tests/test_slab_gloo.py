@@ -158,3 +158,56 @@ def test_slab_exchange_gloo(world):
             p.kill()
     bad = [r for r in results if r[1] != "ok"]
     assert not bad, bad[0][1]
+
+
+def _migrate_worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ibamr_amd.slab import Slab, migrate
+    slab = Slab([16, 16, 32], world, rank, 3)
+    g = torch.Generator().manual_seed(100 + rank)
+    M = 500 + 37 * rank
+    X = torch.rand((M, 3), dtype=torch.float64, generator=g) * 1.4 - 0.2  # some outside [0, 1): periodic images
+    ids = (torch.arange(M, dtype=torch.int64) + 100000 * rank)
+    F = torch.rand((M, 3), dtype=torch.float64, generator=g)
+    Xn, (idn, Fn) = migrate(slab, X, [ids, F])
+    Xn2, (idn2, Fn2) = migrate(slab, X, [ids, F])  # determinism
+    ok = torch.equal(Xn, Xn2) and torch.equal(idn, idn2) and torch.equal(Fn, Fn2)
+    zc = (Xn[:, 2] / slab.dx[2]).floor().long()
+    owned = bool(((zc >= slab.z0) & (zc < slab.z1)).all())
+    inbox = bool(((Xn >= 0) & (Xn < 1)).all())
+    out_q.put((rank, ok, owned, inbox, idn.tolist(), Xn.numpy().copy(), Fn.numpy().copy(),
+               X.numpy().copy(), ids.numpy().copy(), F.numpy().copy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_marker_migration_gloo(world):
+    """Every marker ends on the rank owning its (wrapped) cell, exactly once, with
+    its fields; local order is cell order; repeated calls give identical results."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_migrate_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    res.sort(key=lambda r: r[0])
+    all_ids, before = [], {}
+    for rank, ok, owned, inbox, idn, Xn, Fn, X, ids, F in res:
+        assert ok and owned and inbox, (rank, ok, owned, inbox)
+        all_ids += idn
+        for i, x, f in zip(ids, X, F):
+            before[int(i)] = (np.mod(x, 1.0), f)
+        # cell order within the rank
+        c = np.floor(Xn / (1.0 / np.array([16, 16, 32]))).astype(np.int64)
+        key = (c[:, 2] * 16 + c[:, 1]) * 16 + c[:, 0]
+        assert np.all(np.diff(key) >= 0)
+    assert sorted(all_ids) == sorted(before)
+    for rank, ok, owned, inbox, idn, Xn, Fn, X, ids, F in res:
+        for i, x, f in zip(idn, Xn, Fn):
+            xb, fb = before[int(i)]
+            assert np.allclose(x, xb, atol=1e-15, rtol=0) and np.array_equal(f, fb)
