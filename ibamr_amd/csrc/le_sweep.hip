@@ -403,11 +403,22 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
         int s;
         double X[3];
     };
-    // anchor a's markers [beg, end) (an empty range past a1)
-    auto span = [&](int a, int& beg, int& end) {
+    // anchor a's markers [beg, end) (an empty range past a1): the two bucket
+    // starts are loaded into registers a group before they are read
+    // (readfirstlane), so no group waits on a load it has just issued
+    struct Span {
+        int beg, end;
+    };
+    auto span_load = [&](int a) {
         const int ac = min(a, p.cg.nz - 1);
-        beg = __builtin_amdgcn_readfirstlane(bs[bucket(p, ac, col, 0)]);
-        end = a < a1 ? __builtin_amdgcn_readfirstlane(bs[bucket(p, ac, col, NBAND)]) : beg;
+        Span sp;
+        sp.beg = bs[bucket(p, ac, col, 0)];
+        sp.end = a < a1 ? bs[bucket(p, ac, col, NBAND)] : sp.beg;
+        return sp;
+    };
+    auto span_get = [&](const Span& sp, int& beg, int& end) {
+        beg = __builtin_amdgcn_readfirstlane(sp.beg);
+        end = __builtin_amdgcn_readfirstlane(sp.end);
     };
     auto mk_load = [&](int beg, int cnt, Mk& m) {  // markers beg + lane (clamped)
         const int e = min(beg + min(lane, max(cnt - 1, 0)), nlast);
@@ -445,18 +456,21 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     plane_load(a0 + w + HI, pv);
     Mk nxt;
     int nb, ne;
-    span(a0 + w, nb, ne);
+    span_get(span_load(a0 + w), nb, ne);
     mk_load(nb, min(ne - nb, SW), nxt);
+    Span sp1 = span_load(a0 + w + IWAVES);
     for (int a = a0; a < a1; a += IWAVES) {
         const int my = a + w;  // this wave's anchor plane
-        lds_barrier();          // the previous pair's reads are done
+        lds_barrier();          // the previous group's reads are done
         plane_put(my + HI, pv);
-        lds_barrier();          // planes a+LO .. a+1+HI are in the ring
+        lds_barrier();          // planes a+LO .. a+IWAVES-1+HI are in the ring
         const Mk cur = nxt;
         const int beg = nb, end = ne;
-        // prefetch for the next pair: markers of my+2, plane my+2+HI
-        span(my + IWAVES, nb, ne);
+        // prefetch for the next group: markers of my+IWAVES (their bucket starts
+        // loaded a group ago), bucket starts of my+2 IWAVES, plane my+IWAVES+HI
+        span_get(sp1, nb, ne);
         mk_load(nb, min(ne - nb, SW), nxt);
+        sp1 = span_load(my + 2 * IWAVES);
         plane_load(my + IWAVES + HI, pv);
         if (my < a1) {
             process(my, min(end - beg, SW), cur);
