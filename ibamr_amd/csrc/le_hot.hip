@@ -901,7 +901,7 @@ template <int NDIM> static CandFn pick_cand(int k) { IBTK_LE_DISPATCH(NDIM, k, l
 template <int NDIM> static ClsFn pick_cls(int k) { IBTK_LE_DISPATCH(NDIM, k, cand_classes_t) }
 
 hipError_t launch_bin(int ndim, int kernel, const Params& p, int n, unsigned* keys, int* vals, hipStream_t s) {
-    BinFn f = ndim == 3 ? pick_bin<3>(kernel) : pick_bin<2>(kernel);
+    BinFn f = ndim == 2 ? pick_bin<2>(kernel) : nullptr;  // 3-D: the column sweeps (le_sweep.hip)
     return f ? f(p, n, keys, vals, s) : hipErrorInvalidValue;
 }
 hipError_t launch_brick_start(const unsigned* keys, int n, int nbricks, int shift, int* bs, hipStream_t s) {
@@ -911,29 +911,26 @@ hipError_t launch_brick_start(const unsigned* keys, int n, int nbricks, int shif
 }
 hipError_t launch_gather_sorted(int ndim, const Params& p, int n, int* sorted_s, double* sorted_X, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    if (ndim == 3)
-        hipLaunchKernelGGL(k_gather_sorted<3>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, sorted_s,
-                           sorted_X);
-    else
-        hipLaunchKernelGGL(k_gather_sorted<2>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, sorted_s,
-                           sorted_X);
+    if (ndim != 2) return hipErrorInvalidValue;  // 3-D: k_gather_col (le_sweep.hip)
+    hipLaunchKernelGGL(k_gather_sorted<2>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, sorted_s,
+                       sorted_X);
     return hipGetLastError();
 }
 hipError_t launch_interp(int ndim, int kernel, const Params& p, int n, hipStream_t s, hipEvent_t ev0,
                          hipEvent_t ev1) {
-    InterpFn f = ndim == 3 ? pick_interp<3>(kernel) : pick_interp<2>(kernel);
+    InterpFn f = ndim == 2 ? pick_interp<2>(kernel) : nullptr;
     return f ? f(p, n, s, ev0, ev1) : hipErrorInvalidValue;
 }
 hipError_t launch_cand(int ndim, int kernel, const Params& p, bool write, int* counts_or_offs, int* out, hipStream_t s) {
-    CandFn f = ndim == 3 ? pick_cand<3>(kernel) : pick_cand<2>(kernel);
+    CandFn f = ndim == 2 ? pick_cand<2>(kernel) : nullptr;
     return f ? f(p, write, counts_or_offs, out, s) : hipErrorInvalidValue;
 }
 int cand_classes(int ndim, int kernel) {
-    ClsFn f = ndim == 3 ? pick_cls<3>(kernel) : pick_cls<2>(kernel);
+    ClsFn f = ndim == 2 ? pick_cls<2>(kernel) : nullptr;
     return f ? f() : 0;
 }
 hipError_t launch_spread(int ndim, int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-    SpreadFn f = ndim == 3 ? pick_spread<3>(kernel) : pick_spread<2>(kernel);
+    SpreadFn f = ndim == 2 ? pick_spread<2>(kernel) : nullptr;
     return f ? f(p, s, ev0, ev1) : hipErrorInvalidValue;
 }
 
