@@ -307,3 +307,41 @@ def test_dense_uniform_side(le, ctx, oracle, kernel):
     oracle.side_spread(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, uo, idx[order], xs, Xn, Fn)
     for a in range(3):
         assert rel_err(q[a].cpu().numpy(), uo[a]) <= SPREAD_TOL, f"spread comp {a}"
+
+
+@pytest.mark.parametrize("kernel", ["IB_4", "IB_6", "BSPLINE_4"])
+def test_vertex_file_sphere(le, ctx, oracle, kernel):
+    """Markers from a reference input deck (tests/golden/vertex/sphere3d_32.vertex,
+    read by ibamr_amd.io as IBStandardInitializer would, scaled to radius 0.125 about
+    the box centre): interp and spread against the oracle."""
+    import os
+    from ibamr_amd import io
+    from ibamr_amd.le import Geometry
+    Xn = io.read_vertex(os.path.join(os.path.dirname(__file__), "golden", "vertex", "sphere3d_32.vertex"),
+                        length_scale=0.25, posn_shift=[2.0, 2.0, 2.0])
+    M = Xn.shape[0]
+    geom = Geometry.periodic_unit([32, 32, 32], oracle.min_ghost_width(kernel))
+    rng = np.random.default_rng(4)
+    Fn = rng.standard_normal((M, 3))
+    u = geom.alloc("side")
+    for a in u:
+        a.copy_(torch.from_numpy(rng.standard_normal(tuple(a.shape))))
+    u0 = [a.cpu().numpy().copy() for a in u]
+    X = torch.from_numpy(Xn).cuda()
+    F = torch.from_numpy(Fn).cuda()
+    U = torch.zeros((M, 3), dtype=torch.float64, device="cuda:0")
+    m = le.Markers(ctx).bin(geom, kernel, X)
+    le.interp(ctx, m, kernel, "side", geom, u, U, X)
+    q = geom.alloc("side")
+    le.spread(ctx, m, kernel, "side", geom, q, F, X)
+    ctx.synchronize()
+    idx = np.arange(M, dtype=np.int32)
+    xs = np.zeros((M, 3))
+    Uo = np.zeros((M, 3))
+    oracle.side_interp(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, u0, idx, xs, Xn, Uo)
+    assert rel_err(U.cpu().numpy(), Uo) <= INTERP_TOL
+    order = m.order().cpu().numpy()
+    uo = [np.zeros(tuple(a.shape)) for a in q]
+    oracle.side_spread(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, uo, idx[order], xs, Xn, Fn)
+    for a in range(3):
+        assert rel_err(q[a].cpu().numpy(), uo[a]) <= SPREAD_TOL, f"spread comp {a}"
