@@ -156,6 +156,9 @@ def main():
                     help="storage order of the markers: 'cell' = sorted by cell (z, y, x), the order "
                          "LDataManager's local numbering gives after redistribution (SURVEY.md 8d); "
                          "'random' = generation order")
+    ap.add_argument("--move", action="store_true",
+                    help="a full explicit coupling step: interp, X += dt U (ibtk_le_position_update), "
+                         "migrate the slab leavers (N > 1), re-bin, spread")
     args = ap.parse_args()
 
     import torch
@@ -174,7 +177,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from ibamr_amd import le
-    from ibamr_amd.slab import Slab, SlabExchange
+    from ibamr_amd.slab import Slab, SlabExchange, migrate
 
     N = cfg["N"]
     ghost = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
@@ -218,7 +221,39 @@ def main():
     E = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
     acc = {"bin": [], "interp": [], "spread": [], "exchange": []}
 
+    dt_move = 0.05 * slab.dx[0]  # |U| <= ~1: markers move <= 1/20 cell per step
+
+    def step_move(record):
+        # interp -> X += dt U -> migrate -> bin -> spread: one bin per step, as in
+        # IBMethod's explicit loop (interpolateVelocity, eulerStep, spreadForce)
+        nonlocal X, F, U
+        if record:
+            E[0].record()
+        ex_u.halo_fill()
+        le.interp(ctx, bins, kernel, "side", geom, u, U, X)
+        if record:
+            E[1].record()
+        le.position_update(ctx, "euler", dt_move, X, U, out=X)
+        if world > 1:
+            X, (F,) = migrate(slab, X, [F], cell_order=False)
+            if U.shape != X.shape:
+                U = torch.empty_like(X)
+        bins.bin(geom, kernel, X)
+        if record:
+            E[2].record()
+        le.zero_ghosts(ctx, geom, "side", f)
+        if record:
+            E[3].record()
+        le.spread(ctx, bins, kernel, "side", geom, f, F, X)
+        if record:
+            E[4].record()
+        ex_f.ghost_sum()
+        if record:
+            E[5].record()
+
     def step(record):
+        if args.move:
+            return step_move(record)
         if record:
             E[0].record()
         if not args.no_rebin:
@@ -241,8 +276,12 @@ def main():
 
     def collect():
         torch.cuda.synchronize()
-        acc["bin"].append(E[0].elapsed_time(E[1]))
-        acc["interp"].append(E[1].elapsed_time(E[2]))
+        if args.move:  # E0-E1 interp, E1-E2 update + migrate + bin
+            acc["interp"].append(E[0].elapsed_time(E[1]))
+            acc["bin"].append(E[1].elapsed_time(E[2]))
+        else:
+            acc["bin"].append(E[0].elapsed_time(E[1]))
+            acc["interp"].append(E[1].elapsed_time(E[2]))
         acc["spread"].append(E[3].elapsed_time(E[4]))
         acc["exchange"].append(E[2].elapsed_time(E[3]) + E[4].elapsed_time(E[5]))
 
@@ -329,7 +368,10 @@ def main():
         "data": "synthetic",
         "config": {"workload": cfg["desc"], "kernel": kernel, "grid": [N, N, N], "markers": M_total,
                    "parallelism": f"z-slab x{world}", "ghost": ghost, "marker_order": args.marker_order,
-                   "step": "bin + ghost fill + interp(3 comps) + zero ghosts + spread(3 comps) + ghost sum"},
+                   "move": args.move,
+                   "step": ("ghost fill + interp(3 comps) + position update + migrate + bin + zero ghosts + "
+                            "spread(3 comps) + ghost sum" if args.move else
+                            "bin + ghost fill + interp(3 comps) + zero ghosts + spread(3 comps) + ghost sum")},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per launch (PMC)",
                      "algorithmic_bytes": {"interp": B_i, "spread": B_s},

@@ -17,8 +17,12 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
-OBJ = PKG / "lib" / "obj"
-LIB = PKG / "lib" / "libibtk_le.so"
+# IBTK_LE_VARIANT=<name> with IBTK_LE_DEFS="-DNAME=V ..." builds an experiment
+# into lib/var/<name>/ (load it with IBTK_LE_LIB); the default build ignores both.
+_VAR = os.environ.get("IBTK_LE_VARIANT", "")
+_LIBDIR = PKG / "lib" / "var" / _VAR if _VAR else PKG / "lib"
+OBJ = _LIBDIR / "obj"
+LIB = _LIBDIR / "libibtk_le.so"
 INCLUDE = ROOT / "include"
 
 SOURCES = ["le_hot.hip", "le_sweep.hip", "le_aux.hip", "le_sort.hip", "le_abi.cpp", "le_fortran.cpp", "le_interactor.cpp"]
@@ -26,6 +30,8 @@ ARCH = os.environ.get("IBTK_LE_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", f"--offload-arch={ARCH}", f"-I{INCLUDE}",
           f"-I{CSRC}", "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-value", "-Wno-unused-result"]
+if _VAR:
+    CFLAGS += os.environ.get("IBTK_LE_DEFS", "").split()
 
 
 def _headers():

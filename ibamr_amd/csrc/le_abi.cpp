@@ -733,6 +733,19 @@ extern "C" int ibtk_le_fold_periodic_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch
                                             double* const* q_dev, int q_depth, const int* periodic) {
     return ghost_op(ctx, geom, centering, q_dev, q_depth, periodic, 1);
 }
+extern "C" int ibtk_le_position_update(ibtk_le_ctx ctx, int scheme, long long n, double dt, const double* X_cur_dev,
+                                       const double* U0_dev, const double* U1_dev, double* X_new_dev) {
+    if (!ctx) return fail(IBTK_LE_ERR_ARG, "null context");
+    if (scheme < IBTK_LE_EULER || scheme > IBTK_LE_TRAPEZOIDAL) return fail(IBTK_LE_ERR_ARG, "unknown update scheme");
+    if (n < 0) return fail(IBTK_LE_ERR_ARG, "negative length");
+    if (n == 0) return IBTK_LE_OK;
+    if (!X_cur_dev || !U0_dev || !X_new_dev || (scheme == IBTK_LE_TRAPEZOIDAL && !U1_dev))
+        return fail(IBTK_LE_ERR_ARG, "null array");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(launch_position_update(scheme, (long)n, dt, X_cur_dev, U0_dev, U1_dev, X_new_dev, ctx->stream));
+    return IBTK_LE_OK;
+}
+
 extern "C" int ibtk_le_zero_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int centering,
                                    double* const* q_dev, int q_depth) {
     return ghost_op(ctx, geom, centering, q_dev, q_depth, nullptr, 2);

@@ -267,4 +267,65 @@ hipError_t launch_image_write(const ImageDesc& d, const double* X, int n, const 
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// marker position update (IBMethod::eulerStep / midpointStep / trapezoidalStep,
+// IBMethod.cpp:619-681): PETSc VecWAXPY w = alpha x + y and VecAXPY y += alpha x,
+// each a rounded multiply then a rounded add (built with -ffp-contract=off, so
+// no fma), elementwise over the n doubles of the (M, NDIM) arrays.  HBM-bound:
+// 16-byte accesses, pairs of doubles per lane when every array is 16-byte aligned.
+// ---------------------------------------------------------------------------
+template <bool TRAP, typename V>
+__global__ __launch_bounds__(BLOCK) void k_position_update(long n, double dt, const V* X,
+                                                           const V* U0, const V* U1,
+                                                           V* Xn) {
+    const long stride = (long)gridDim.x * BLOCK;
+    for (long i = (long)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
+        if constexpr (sizeof(V) == 16) {
+            const V x = X[i], u = U0[i];
+            V w;
+            if constexpr (TRAP) {
+                const double h = 0.5 * dt;
+                const V v = U1[i];
+                w.x = (h * u.x + x.x) + h * v.x;
+                w.y = (h * u.y + x.y) + h * v.y;
+            } else {
+                w.x = dt * u.x + x.x;
+                w.y = dt * u.y + x.y;
+            }
+            Xn[i] = w;
+        } else {
+            if constexpr (TRAP) {
+                const double h = 0.5 * dt;
+                Xn[i] = (h * U0[i] + X[i]) + h * U1[i];
+            } else {
+                Xn[i] = dt * U0[i] + X[i];
+            }
+        }
+    }
+}
+
+hipError_t launch_position_update(int scheme, long n, double dt, const double* X, const double* U0, const double* U1,
+                                  double* Xn, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const bool trap = scheme == 2;
+    auto al = [](const void* q) { return q == nullptr || ((uintptr_t)q & 15u) == 0; };
+    const bool vec = (n % 2 == 0) && al(X) && al(U0) && al(U1) && al(Xn);
+    const long items = vec ? n / 2 : n;
+    const long want = (items + BLOCK - 1) / BLOCK;
+    const int grid = (int)(want < 65536 ? want : 65536);
+    if (vec) {
+        using V = double2;
+        auto x = (const V*)X;
+        auto u0 = (const V*)U0;
+        auto u1 = (const V*)U1;
+        auto xn = (V*)Xn;
+        if (trap) hipLaunchKernelGGL((k_position_update<true, V>), dim3(grid), dim3(BLOCK), 0, s, items, dt, x, u0, u1, xn);
+        else hipLaunchKernelGGL((k_position_update<false, V>), dim3(grid), dim3(BLOCK), 0, s, items, dt, x, u0, u1, xn);
+    } else {
+        if (trap) hipLaunchKernelGGL((k_position_update<true, double>), dim3(grid), dim3(BLOCK), 0, s, items, dt, X, U0, U1, Xn);
+        else hipLaunchKernelGGL((k_position_update<false, double>), dim3(grid), dim3(BLOCK), 0, s, items, dt, X, U0, U1, Xn);
+    }
+    return hipGetLastError();
+}
+
 }  // namespace ibtk_le

@@ -85,7 +85,11 @@ struct BinGeom {
 // ranges.  Columns 0 and ncx-1 (rows 0 and ncy-1) are empty guards, so every
 // real column has all eight neighbours.  nbuckets marks "outside".
 constexpr int COLX = 32;
-constexpr int COLY = 16;
+#ifndef IBTK_LE_COLY
+#define IBTK_LE_COLY 16
+#endif
+constexpr int COLY = IBTK_LE_COLY;  // even: a 32 x COLY plane is whole wave rows
+static_assert(COLY % 2 == 0 && COLY >= 8, "COLY: even, >= 8");
 constexpr int NBAND = 9;
 struct ColGeom {
     int org[3];     // absolute key cell of column (0,0) (a guard), plane 0
@@ -142,6 +146,8 @@ hipError_t launch_scan(void* temp, size_t& temp_bytes, const int* in, int* out, 
 
 // 3-D column sweep (le_sweep.hip)
 hipError_t launch_bin_col(int kernel, const Params& p, int n, unsigned* keys, int* vals, hipStream_t s);
+hipError_t launch_position_update(int scheme, long n, double dt, const double* X, const double* U0, const double* U1,
+                                  double* Xn, hipStream_t s);
 hipError_t launch_gather_col(int kernel, const Params& p, int n, int* sorted_s, double* sorted_X,
                              const unsigned* sorted_key, int nbuckets, int* bucket_start, hipStream_t s);
 hipError_t launch_interp_sweep(int kernel, const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);

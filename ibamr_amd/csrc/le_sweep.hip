@@ -68,7 +68,7 @@ template <int K> __device__ __forceinline__ bool col_key_cell(const Params& p, c
 template <int K> __device__ __forceinline__ int key_band(int kx, int ky) {
     constexpr int LO = KT<K>::LO, HI = KT<K>::HI;
     static_assert(-1 - LO < COLY - HI, "a stencil must not reach both neighbouring columns");
-    const int xl = kx & (COLX - 1), yl = ky & (COLY - 1);
+    const int xl = kx & (COLX - 1), yl = ky % COLY;  // kx, ky >= 0
     const int xb = xl <= -1 - LO ? 0 : (xl >= COLX - HI ? 2 : 1);
     const int yb = yl <= -1 - LO ? 0 : (yl >= COLY - HI ? 2 : 1);
     return 3 * xb + yb;

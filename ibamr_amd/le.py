@@ -242,6 +242,33 @@ def zero_ghosts(ctx: Context, geom: Geometry, centering: str, q, q_depth=1):
     check(ctx.lib.ibtk_le_zero_ghosts(ctx.h, ctypes.byref(geom.c), CENTERING[centering], _ptr_array(q), q_depth))
 
 
+UPDATE_SCHEMES = {"euler": 0, "midpoint": 1, "trapezoidal": 2}
+
+
+def position_update(ctx: Context, scheme: str, dt: float, X: torch.Tensor, U0: torch.Tensor,
+                    U1: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """X_new = X + dt U0 ("euler", "midpoint") or (X + dt/2 U0) + dt/2 U1 ("trapezoidal"), on the device.
+
+    IBMethod::eulerStep / midpointStep / trapezoidalStep (IBMethod.cpp:619-681).
+    ``out`` may be ``X`` itself (in-place update).  Returns ``out``.
+    """
+    if scheme not in UPDATE_SCHEMES:
+        raise ValueError(f"unknown scheme {scheme!r}")
+    if scheme == "trapezoidal" and U1 is None:
+        raise ValueError("trapezoidal needs U1")
+    arrs = [X, U0] + ([U1] if scheme == "trapezoidal" else [])
+    for t in arrs:
+        if t.dtype != torch.float64 or t.shape != X.shape:
+            raise ValueError("X, U0, U1 must be float64 of one shape")
+    if out is None:
+        out = torch.empty_like(X)
+    elif out.shape != X.shape or out.dtype != torch.float64:
+        raise ValueError("out must match X")
+    check(ctx.lib.ibtk_le_position_update(ctx.h, UPDATE_SCHEMES[scheme], X.numel(), float(dt), _ptr(X), _ptr(U0),
+                                          _ptr(U1) if scheme == "trapezoidal" else None, _ptr(out)))
+    return out
+
+
 def periodic_index_list(ctx: Context, geom: Geometry, X: torch.Tensor, ghost: int, periodic=None):
     """(indices int32, Xshift float64 [n, ndim]) device tensors, marker-major order."""
     M = X.shape[0]

@@ -173,10 +173,12 @@ def migrate(slab: Slab, X: torch.Tensor, fields: Sequence[torch.Tensor] = (), gr
 
     X: (M, 3) float64; fields: tensors with M rows (any trailing shape, cast to
     float64 for the exchange and back).  Returns (X, fields) of the markers this
-    rank owns afterwards: received in source-rank order, each source's markers in
-    their previous order, then (cell_order) stably sorted by cell (z, y, x) -- the
-    local numbering LDataManager::computeNodeDistribution gives
-    (LDataManager.cpp:2839-3027).  Deterministic: the same inputs give the same
+    rank owns afterwards.  With cell_order they are stably sorted by cell (z, y, x),
+    the local numbering LDataManager::computeNodeDistribution gives
+    (LDataManager.cpp:2839-3027).  Without it only the leavers move: the markers
+    that stay keep their order and the arrivals follow in source-rank order.  That
+    is the cheap per-step form, since after a small position update few markers
+    cross a slab face.  Deterministic either way: the same inputs give the same
     order on every run.
     """
     import torch.distributed as dist
@@ -186,10 +188,18 @@ def migrate(slab: Slab, X: torch.Tensor, fields: Sequence[torch.Tensor] = (), gr
     Xw = torch.where(Xw >= L, Xw - L, Xw)  # remainder can round up to L
     cell = [torch.clamp((Xw[:, d] / slab.dx[d]).floor().long(), 0, slab.N[d] - 1) for d in range(3)]
     dest = cell[2] // slab.nz
-    order = torch.argsort(dest, stable=True)
     cols = [Xw] + [f.reshape(M, -1).to(X.dtype) for f in fields]
     widths = [c.shape[1] for c in cols]
-    send = torch.cat(cols, dim=1)[order].contiguous()
+    data = torch.cat(cols, dim=1)
+    stay = None
+    if not cell_order:  # keep the stayers in place, send only the leavers
+        keep = dest == slab.rank
+        stay = data[keep]
+        go = (~keep).nonzero().squeeze(1)
+        dest = dest[go]
+        data = data[go]
+    order = torch.argsort(dest, stable=True)
+    send = data[order].contiguous()
     send_counts = torch.bincount(dest, minlength=slab.P).to(torch.int64)
     recv_counts = torch.empty_like(send_counts)
     if slab.P == 1:
@@ -200,6 +210,8 @@ def migrate(slab: Slab, X: torch.Tensor, fields: Sequence[torch.Tensor] = (), gr
         recv = torch.empty((int(recv_counts.sum().item()), D), dtype=send.dtype, device=send.device)
         dist.all_to_all_single(recv, send, output_split_sizes=recv_counts.tolist(),
                                input_split_sizes=send_counts.tolist(), group=group)
+    if stay is not None:
+        recv = torch.cat([stay, recv], dim=0)
     if cell_order and recv.shape[0]:
         c = [torch.clamp((recv[:, d] / slab.dx[d]).floor().long(), 0, slab.N[d] - 1) for d in range(3)]
         key = (c[2] * slab.N[1] + c[1]) * slab.N[0] + c[0]

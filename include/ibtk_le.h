@@ -169,6 +169,20 @@ int ibtk_le_periodic_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom,
 int ibtk_le_box_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev, int n_markers,
                            const int* box_lo, const int* box_hi, int* indices_dev, int capacity, int* count);
 
+/* Marker position update, elementwise over the n = M * NDIM doubles of the
+ * device arrays (any layout, as long as all four share it):
+ *   IBTK_LE_EULER, IBTK_LE_MIDPOINT:  X_new = dt * U0 + X_cur
+ *     (IBMethod::eulerStep / midpointStep, IBMethod.cpp:619-655: VecWAXPY with U0 =
+ *     U(current) or U(current + dt/2));
+ *   IBTK_LE_TRAPEZOIDAL:  X_new = (dt/2 * U0 + X_cur) + dt/2 * U1
+ *     (IBMethod::trapezoidalStep, IBMethod.cpp:657-681: VecWAXPY then VecAXPY, U0 =
+ *     U(current), U1 = U(new)).
+ * Each step is a rounded multiply and a rounded add, as PETSc's loops compute it.
+ * X_new may alias X_cur.  U1 is ignored (may be NULL) unless TRAPEZOIDAL. */
+enum { IBTK_LE_EULER = 0, IBTK_LE_MIDPOINT = 1, IBTK_LE_TRAPEZOIDAL = 2 };
+int ibtk_le_position_update(ibtk_le_ctx ctx, int scheme, long long n, double dt, const double* X_cur_dev,
+                            const double* U0_dev, const double* U1_dev, double* X_new_dev);
+
 /* Diagnostics: masks_dev[c] (one byte per point of component c's ghosted array,
  * same layout) gets 1 at every point some listed stencil touches after clipping.
  * bench.py sums the masks for the exact algorithmic byte count |S_a|. */

@@ -177,6 +177,14 @@ def _migrate_worker(rank, world, port, out_q):
     zc = (Xn[:, 2] / slab.dx[2]).floor().long()
     owned = bool(((zc >= slab.z0) & (zc < slab.z1)).all())
     inbox = bool(((Xn >= 0) & (Xn < 1)).all())
+    # leavers-only form: stayers keep their order, arrivals follow
+    Xl, (idl, Fl) = migrate(slab, X, [ids, F], cell_order=False)
+    zl = (Xl[:, 2] / slab.dx[2]).floor().long()
+    owned = owned and bool(((zl >= slab.z0) & (zl < slab.z1)).all())
+    zc0 = (torch.remainder(X[:, 2], 1.0) / slab.dx[2]).floor().long()
+    stay_ids = ids[(zc0 >= slab.z0) & (zc0 < slab.z1)].tolist()
+    ok = ok and idl[:len(stay_ids)].tolist() == stay_ids and sorted(idl.tolist()) == sorted(idn.tolist())
+    ok = ok and all(torch.equal(Fl[idl == i], Fn[idn == i]) for i in idl[::50].tolist())
     out_q.put((rank, ok, owned, inbox, idn.tolist(), Xn.numpy().copy(), Fn.numpy().copy(),
                X.numpy().copy(), ids.numpy().copy(), F.numpy().copy()))
     dist.destroy_process_group()
