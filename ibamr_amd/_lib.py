@@ -90,6 +90,9 @@ _SIGS = [
     ("ibtk_le_spread", c_int,
      [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_int,
       c_void_p, c_int, c_void_p]),
+    ("ibtk_le_spread_ds", c_int,
+     [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_int,
+      c_void_p, c_int, c_void_p, c_void_p]),
     ("ibtk_le_fill_periodic_ghosts", c_int,
      [c_void_p, ctypes.POINTER(PatchGeom), c_int, ctypes.POINTER(c_void_p), c_int, c_void_p]),
     ("ibtk_le_fold_periodic_ghosts", c_int,

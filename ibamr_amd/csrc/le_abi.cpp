@@ -595,9 +595,26 @@ static int build_candidates(ibtk_le_ctx ctx, ibtk_le_markers m, const Params& p)
     return IBTK_LE_OK;
 }
 
+static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                       const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
+                       int Q_depth, const double* ds_dev, const double* X_dev);
+
 extern "C" int ibtk_le_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                               const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
                               int Q_depth, const double* X_dev) {
+    return spread_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, nullptr, X_dev);
+}
+
+extern "C" int ibtk_le_spread_ds(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                                 const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth,
+                                 const double* Q_dev, int Q_depth, const double* ds_dev, const double* X_dev) {
+    if (!ds_dev && m && m->n > 0) return fail(IBTK_LE_ERR_ARG, "null ds");
+    return spread_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, ds_dev, X_dev);
+}
+
+static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                       const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
+                       int Q_depth, const double* ds_dev, const double* X_dev) {
     Params p;
     if (int rc = prepare(ctx, m, kernel, geom, X_dev, p)) return rc;
     const int nc = ncomponents(geom, centering, q_depth, Q_depth);
@@ -606,6 +623,7 @@ extern "C" int ibtk_le_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, in
     if (!Q_dev || !q_dev) return fail(IBTK_LE_ERR_ARG, "null Q or q");
     if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
     p.Qin = Q_dev;
+    p.ds = ds_dev;
     p.Q_depth = Q_depth;
     p.nsorted = m->n;
     if (int rc = ctx->fbuf.ensure(sizeof(double) * (size_t)m->n * (size_t)std::min(nc, MAXC))) return rc;

@@ -648,8 +648,12 @@ __global__ __launch_bounds__(BLOCK) void k_gather_F(Params p, int n, double* out
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     if (e >= n) return;
     const int s = p.sorted_s[e];
-    for (int c = 0; c < p.ncomp; ++c)
-        out[(int64_t)c * n + e] = p.Qin[(int64_t)p.Q_depth * s + p.comp[c].qcomp];
+    // density-weighted spread: F ds rounded once, as LDataManager.cpp:446-451 forms it
+    const double w = p.ds ? p.ds[s] : 1.0;
+    for (int c = 0; c < p.ncomp; ++c) {
+        const double v = p.Qin[(int64_t)p.Q_depth * s + p.comp[c].qcomp];
+        out[(int64_t)c * n + e] = p.ds ? v * w : v;
+    }
 }
 
 // Spread of one super-brick, component after component: u_old goes to LDS; in

@@ -122,6 +122,7 @@ struct Params {
     const int* nentries_dev;   // device copy of the list length
     const double* Qin;         // spread: marker values
     const double* sorted_F;    // spread: Qin gathered in sorted order, [comp][sorted position]
+    const double* ds;          // spread: per-marker weight (nullptr: none); sorted_F = Qin * ds
     int nsorted;               // list length
     double* Qout;              // interp: marker values
     int* err;                  // device error word (0 = fine)

@@ -210,13 +210,22 @@ def interp(ctx: Context, markers: Markers, kernel: str, centering: str, geom: Ge
 
 def spread(ctx: Context, markers: Markers, kernel: str, centering: str, geom: Geometry,
            q: Sequence[torch.Tensor], Q: torch.Tensor, X: torch.Tensor, q_depth: int = 1, Q_depth: Optional[int] = None,
-           axis: int = 0):
-    """q += S Q  (LEInteractor::spread), deterministic marker-ordered sums."""
+           axis: int = 0, ds: Optional[torch.Tensor] = None):
+    """q += S Q  (LEInteractor::spread), deterministic marker-ordered sums.
+
+    With ``ds`` (one float64 per marker): q += S (Q ds), the density-weighted
+    LDataManager::spread (LDataManager.cpp:398-470)."""
     if Q_depth is None:
         Q_depth = geom.ndim if centering in ("side", "edge") else q_depth
     arr = _ptr_array(q)
-    check(ctx.lib.ibtk_le_spread(ctx.h, markers.h, kernel_id(kernel), CENTERING[centering], axis,
-                                 ctypes.byref(geom.c), arr, q_depth, _ptr(Q), Q_depth, _ptr(X)))
+    if ds is None:
+        check(ctx.lib.ibtk_le_spread(ctx.h, markers.h, kernel_id(kernel), CENTERING[centering], axis,
+                                     ctypes.byref(geom.c), arr, q_depth, _ptr(Q), Q_depth, _ptr(X)))
+    else:
+        if ds.dtype != torch.float64 or ds.numel() * Q_depth != Q.numel():
+            raise ValueError("ds: one float64 per marker")
+        check(ctx.lib.ibtk_le_spread_ds(ctx.h, markers.h, kernel_id(kernel), CENTERING[centering], axis,
+                                        ctypes.byref(geom.c), arr, q_depth, _ptr(Q), Q_depth, _ptr(ds), _ptr(X)))
 
 
 def _periodic_arg(periodic, ndim):

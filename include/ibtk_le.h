@@ -138,6 +138,16 @@ int ibtk_le_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering
                    const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
                    int Q_depth, const double* X_dev);
 
+/* Density-weighted spread, f += S (F ds): LDataManager::spread with ds_data
+ * (LDataManager.cpp:398-470), which forms F_ds[k][d] = F[k][d] * ds[k] and then
+ * spreads it.  ds_dev holds one double per marker (indexed like Q_dev's markers).
+ * The product is formed in the gather that stages F for the spread kernel, so it
+ * costs no extra pass; the values spread are the rounded products, as in the
+ * reference. */
+int ibtk_le_spread_ds(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                      const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
+                      int Q_depth, const double* ds_dev, const double* X_dev);
+
 /* ---- helpers for a single periodic patch (uniform finest level) -----------------
  * Fill the ghost layers of the arrays of `centering` from the periodic interior
  * (the RefineSchedule::fillData the caller runs before interp, LDataManager.cpp:750). */
