@@ -173,6 +173,11 @@ __device__ __forceinline__ void stencil1d(double Xs, double Xraw, double xlo, do
     constexpr int FAM = KT<K>::FAM;
     if constexpr (FAM == 0) {
         // f.m4:1316 (X_o_dx), :1360-1365 (istart/istop)
+        // MUL: near a NINT tie the product can round to the other side of it than
+        // the quotient (which the bin key uses), moving the stencil one cell.
+        // At a tie the end weight of these kernels is 0 (r = 0 or 1), so the
+        // point that may then fall outside the key's bands carries a weight of
+        // an ulp's order: within the spread's tolerance.
         const double X_o_dx = MUL ? (Xs - xlo) * inv_dx : (Xs - xlo) / dx;
         st.icl = closed_weights<K>(X_o_dx, ilo, st.w, K6);
         const int icu = st.icl + (W - 1);

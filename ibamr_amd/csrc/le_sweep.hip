@@ -569,14 +569,15 @@ struct Cand {
 
 // The adds of n <= 64 staged candidates of anchor plane a, one lane per
 // candidate: the lane computes its three 1-D stencils, then walks its W^3
-// points (i2, i1, i0) issuing one ds_add_f64 per point.  A point outside the
-// owned range, the clipped stencil or the segment is added with weight 0 at a
-// harmless in-ring address: its row clamped into the column, its plane into
-// the live window, x left to spill (the slot gaps take it); an idle lane does
-// the same at its own x.  So an add is one multiply and one ds_add_f64 with an
-// immediate offset -- no mask, no select and no branch (a branch per add
-// makes the compiler wait for every LDS operation in flight before each one).
-// Adding +-0 changes no value, except that a -0.0 it lands on becomes +0.0.
+// points (i2, i1, i0) issuing one ds_add_f64 per point.  A stencil row (i1,
+// i2) outside the owned rows, the clipped stencil or the segment is skipped
+// by the lanes it concerns (one exec mask per row; idle lanes skip them all);
+// within a row, a point outside the owned x range is added with weight 0, its
+// x left to spill (the slot gaps take it).  So an add is one multiply and one
+// ds_add_f64 with an immediate offset -- no select and no branch per add (a
+// branch per add makes the compiler wait for every LDS operation in flight
+// before each one).  Adding +-0 changes no value, except that a -0.0 it lands
+// on becomes +0.0.
 // Every lane's address moves by the same amount from one add to the next, so
 // lanes dealt to distinct bank classes stay conflict-free for all W^3 adds.
 // Within one instruction the lanes that hit the same point add in lane order,
@@ -591,6 +592,7 @@ __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
         const double Xraw = (FAM == 2) ? p.X[(int64_t)3 * cdat.s + d] : cdat.X[d];
+        // X/dx by a multiply (see stencil1d for ties)
         stencil1d<K, true>(cdat.X[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis,
                            p.K6, st[d], inv_d[d]);
     }
@@ -608,34 +610,40 @@ __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd
     // x: weight x value with the mask folded in (f.m4:1512-1513 order, V applied
     // first: within rounding of the Fortran's (w0 (w1 w2/h)) V)
     double w0v[W];
-    bool vy[W];
+    unsigned ym = 0, zm = 0;  // bit i: stencil row / plane i is clipped in and owned
 #pragma unroll
     for (int i = 0; i < W; ++i) {
         const bool vx = ok && i >= st[0].ist && i <= st[0].isp && ox + i >= xlo && ox + i <= xhi;
         w0v[i] = vx ? st[0].w[i] * cdat.V : 0.0;
-        vy[i] = i >= st[1].ist && i <= st[1].isp && oy + i >= ylo && oy + i <= yhi;
+        if (i >= st[1].ist && i <= st[1].isp && oy + i >= ylo && oy + i <= yhi) ym |= 1u << i;
+        const int k = oz - LO + i, pr = a + oz + i;  // plane a + LO + k
+        if (i >= st[2].ist && i <= st[2].isp && k >= 0 && k < NS && pr >= plo && pr <= phi) zm |= 1u << i;
     }
-    char* const base = reinterpret_cast<char*>(ring) + 8 * ox;
+    // bit W i2 + i1: row (i1, i2) is added.  A masked row needs no address, so
+    // rows and planes are not clamped: row i1 of plane i2 is at a constant
+    // offset 8 COLX i1 from the plane's row 0 (folded into the ds_add offsets)
+    using RM = std::conditional_t<(W * W > 32), unsigned long long, unsigned>;
+    RM rm = 0;
+#pragma unroll
+    for (int i2 = 0; i2 < W; ++i2) rm |= ((zm >> i2) & 1u) ? (RM)ym << (W * i2) : (RM)0;
+    char* const base = reinterpret_cast<char*>(ring) + 8 * (ox + COLX * oy);
     clk.lap(2);
     // idle lanes sit the adds out (exec-masked, one branch around the loop: a
     // 16-lane group with no busy lane costs the LDS nothing)
     if (ok) {
+    int sl = (int)((unsigned)(a + oz + 64 * NSL) % (unsigned)NSL);  // ring slot of plane i2 = 0
 #pragma unroll
     for (int i2 = 0; i2 < W; ++i2) {
-        const int k = oz - LO + i2, pr = a + oz + i2;  // plane a + LO + k
-        const bool vz = i2 >= st[2].ist && i2 <= st[2].isp && k >= 0 && k < NS && pr >= plo && pr <= phi;
-        const int prc = min(max(pr, a + LO), a + HI);  // a live plane of the ring
-        const int zb = (int)((unsigned)(prc + 64 * NSL) % (unsigned)NSL) * (8 * S::SLOT);
+        char* const plane = base + sl * (8 * S::SLOT);
+        sl = sl + 1 == NSL ? 0 : sl + 1;
         double wz;
         if constexpr (FAM == 0) wz = st[2].w[i2] * inv_h3;  // f.m4:1486
         else wz = st[2].w[i2] * inv_h3;
 #pragma unroll
         for (int i1 = 0; i1 < W; ++i1) {
-            const bool vr = vz && vy[i1];
             const double t = st[1].w[i1] * wz;  // f.m4:1489-1492
-            double* const row =
-                reinterpret_cast<double*>(base + zb + 8 * COLX * min(max(oy + i1, 0), COLY - 1));
-            if (vr) {  // lanes whose row is clipped or not owned sit the row out
+            double* const row = reinterpret_cast<double*>(plane + 8 * COLX * i1);
+            if ((rm >> (W * i2 + i1)) & (RM)1) {  // lanes whose row is clipped or not owned sit the row out
 #pragma unroll
                 for (int i0 = 0; i0 < W; ++i0)
                     __hip_atomic_fetch_add(row + i0, w0v[i0] * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

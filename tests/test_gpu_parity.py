@@ -345,3 +345,38 @@ def test_vertex_file_sphere(le, ctx, oracle, kernel):
     oracle.side_spread(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, uo, idx[order], xs, Xn, Fn)
     for a in range(3):
         assert rel_err(q[a].cpu().numpy(), uo[a]) <= SPREAD_TOL, f"spread comp {a}"
+
+
+@pytest.mark.parametrize("kernel", ["IB_4", "BSPLINE_4", "IB_6"])
+def test_spread_at_rounding_ties(le, ctx, oracle, kernel):
+    """Markers where (X - xlo) * (1/dx) and (X - xlo) / dx round to different NINT
+    anchors (the spread stencil multiplies, the bin key divides): the stencil can
+    move one cell, onto a point whose weight is of an ulp's order, so the spread
+    still matches the oracle (which divides, as the Fortran does) within tolerance."""
+    from ibamr_amd.le import Geometry
+    dx, xlo, N = 0.1, -0.3, 14
+    geom = Geometry([0, 0, 0], [N - 1] * 3, oracle.min_ghost_width(kernel), [dx] * 3, [xlo] * 3)
+    ties = []
+    for k in range(2, N - 2):
+        base = xlo + (k + 0.5) * dx
+        for j in range(-40, 41):
+            X = base + j * np.spacing(base)
+            if np.floor((X - xlo) * (1.0 / dx) + 0.5) != np.floor((X - xlo) / dx + 0.5):
+                ties.append(X)
+    ties = np.array(ties)
+    assert ties.size >= 4
+    rng = np.random.default_rng(2)
+    M = 600
+    Xn = rng.choice(ties, size=(M, 3))
+    Fn = rng.standard_normal((M, 3))
+    X, F = torch.from_numpy(Xn).cuda(), torch.from_numpy(Fn).cuda()
+    m = le.Markers(ctx).bin(geom, kernel, X)
+    q = geom.alloc("side")
+    le.spread(ctx, m, kernel, "side", geom, q, F, X)
+    ctx.synchronize()
+    order = m.order().cpu().numpy()
+    uo = [np.zeros(tuple(a.shape)) for a in q]
+    oracle.side_spread(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, uo,
+                       np.arange(M, dtype=np.int32)[order], np.zeros((M, 3)), Xn, Fn)
+    for a in range(3):
+        assert rel_err(q[a].cpu().numpy(), uo[a]) <= SPREAD_TOL, f"spread comp {a}"
