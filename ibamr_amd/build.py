@@ -25,7 +25,7 @@ OBJ = _LIBDIR / "obj"
 LIB = _LIBDIR / "libibtk_le.so"
 INCLUDE = ROOT / "include"
 
-SOURCES = ["le_hot.hip", "le_sweep.hip", "le_aux.hip", "le_sort.hip", "le_abi.cpp", "le_fortran.cpp", "le_interactor.cpp"]
+SOURCES = ["le_hot.hip", "le_sweep.hip", "le_aux.hip", "le_bdry.hip", "le_sort.hip", "le_abi.cpp", "le_fortran.cpp", "le_interactor.cpp"]
 ARCH = os.environ.get("IBTK_LE_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", f"--offload-arch={ARCH}", f"-I{INCLUDE}",

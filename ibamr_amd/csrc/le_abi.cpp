@@ -751,6 +751,47 @@ extern "C" int ibtk_le_fold_periodic_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch
                                             double* const* q_dev, int q_depth, const int* periodic) {
     return ghost_op(ctx, geom, centering, q_dev, q_depth, periodic, 1);
 }
+// CartSideRobinPhysBdryOp::setPhysicalBoundaryConditions (adjoint = 0,
+// CartSideRobinPhysBdryOp.cpp:358-422) and accumulateFromPhysicalBoundaryData
+// (adjoint = 1, :429-493) on one patch of side data.
+extern "C" int ibtk_le_phys_bdry_side(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, double* const* u_dev,
+                                      const int* physical, const double* acoef, const double* bcoef,
+                                      const double* gcoef, int adjoint) {
+    if (!ctx || !u_dev || !physical || !acoef || !bcoef || !gcoef) return fail(IBTK_LE_ERR_ARG, "null argument");
+    if (int rc = check_geom(geom)) return rc;
+    const int nd = geom->ndim, g = geom->gcw[0];
+    for (int d = 1; d < nd; ++d)  // CartSideRobinPhysBdryOp.cpp:519-527
+        if (geom->gcw[d] != g) return fail(IBTK_LE_ERR_GHOST_WIDTH, "non-uniform ghost cell widths");
+    if (g > 16) return fail(IBTK_LE_ERR_GHOST_WIDTH, "ghost width %d above 16", g);
+    if (g == 0) return IBTK_LE_OK;  // ghost_width_to_fill == 0 (:432)
+    BdSide P;
+    std::memset(&P, 0, sizeof(P));
+    P.ndim = nd;
+    P.g = g;
+    for (int d = 0; d < nd; ++d) {
+        P.ilo[d] = geom->ilower[d];
+        P.ihi[d] = geom->iupper[d];
+        P.dx[d] = geom->dx[d];
+    }
+    for (int c = 0; c < nd; ++c) {
+        if (!u_dev[c]) return fail(IBTK_LE_ERR_ARG, "null side array %d", c);
+        P.u[c] = u_dev[c];
+        int64_t n[3] = {1, 1, 1};
+        for (int d = 0; d < nd; ++d) {
+            P.lo[c][d] = P.ilo[d] - g;
+            n[d] = (int64_t)(P.ihi[d] - P.ilo[d] + 1 + 2 * g + (d == c ? 1 : 0));
+        }
+        P.s1[c] = n[0];
+        P.s2[c] = n[0] * n[1];
+    }
+    int phys[6] = {0, 0, 0, 0, 0, 0};
+    BdCoef coef[18];
+    for (int loc = 0; loc < 2 * nd; ++loc) phys[loc] = physical[loc] != 0;
+    for (int i = 0; i < nd * 2 * nd; ++i) coef[i] = BdCoef{acoef[i], bcoef[i], gcoef[i]};
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    HIP_TRY(launch_phys_bdry_side(P, phys, coef, adjoint ? 1 : 0, ctx->stream));
+    return IBTK_LE_OK;
+}
 extern "C" int ibtk_le_position_update(ibtk_le_ctx ctx, int scheme, long long n, double dt, const double* X_cur_dev,
                                        const double* U0_dev, const double* U1_dev, double* X_new_dev) {
     if (!ctx) return fail(IBTK_LE_ERR_ARG, "null context");

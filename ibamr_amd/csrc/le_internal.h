@@ -179,6 +179,21 @@ hipError_t launch_image_count(const ImageDesc& d, const double* X, int n, int* c
 hipError_t launch_image_write(const ImageDesc& d, const double* X, int n, const int* offsets, int* idx,
                               double* xshift, int capacity, hipStream_t s);
 
+// Physical-boundary ghost operators on one side-centred patch (le_bdry.hip)
+struct BdSide {
+    double* u[3];
+    int lo[3][3];          // ghost-box lower corner of component c
+    int64_t s1[3], s2[3];  // strides of component c
+    int ilo[3], ihi[3];    // patch cell box (0 past ndim)
+    double dx[3];
+    int g, ndim;
+};
+struct BdCoef {
+    double a, b, g;
+};
+// coef[c * 2 ndim + loc]: Robin a, b, g of component c on face loc
+hipError_t launch_phys_bdry_side(const BdSide& P, const int* phys, const BdCoef* coef, int adjoint, hipStream_t s);
+
 }  // namespace ibtk_le
 
 // Internal entry used by the Fortran shims (skips the LEInteractor-level ghost check).

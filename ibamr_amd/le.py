@@ -11,6 +11,7 @@ import ctypes
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -249,6 +250,36 @@ def fold_periodic_ghosts(ctx: Context, geom: Geometry, centering: str, q, q_dept
 
 def zero_ghosts(ctx: Context, geom: Geometry, centering: str, q, q_depth=1):
     check(ctx.lib.ibtk_le_zero_ghosts(ctx.h, ctypes.byref(geom.c), CENTERING[centering], _ptr_array(q), q_depth))
+
+
+def phys_bdry_side(ctx: Context, geom: Geometry, u, physical, acoef, bcoef, gcoef, adjoint: bool):
+    """CartSideRobinPhysBdryOp on one patch of side data, on the device.
+
+    adjoint=False: setPhysicalBoundaryConditions (CartSideRobinPhysBdryOp.cpp:358-422), the
+    ghost fill before interp; adjoint=True: accumulateFromPhysicalBoundaryData (:429-493), the
+    fold LDataManager::spread runs after spreading (LDataManager.cpp:655-659).
+    physical[2 d + upper] flags a physical face; acoef/bcoef/gcoef broadcast to
+    (ndim, 2 ndim) = [component axis, face location] (constant Robin coefficients per face)."""
+    nd = geom.ndim
+    if len(physical) != 2 * nd:
+        raise ValueError("physical: one flag per face (2 ndim)")
+    if len(u) != nd:
+        raise ValueError("u: one side array per axis")
+    g = geom.c.gcw[0]
+    for a in range(nd):
+        n = 1
+        for d in range(nd):
+            n *= geom.c.iupper[d] - geom.c.ilower[d] + 1 + 2 * g + (1 if d == a else 0)
+        if u[a].numel() != n:
+            raise ValueError(f"u[{a}]: {u[a].numel()} values, the ghosted side box holds {n}")
+    phys = (ctypes.c_int * 6)(*([int(bool(p)) for p in physical] + [0] * (6 - 2 * nd)))
+    coefs = []
+    for c in (acoef, bcoef, gcoef):
+        a = np.ascontiguousarray(np.broadcast_to(np.asarray(c, np.float64), (nd, 2 * nd)))
+        coefs.append(a)
+    cp = [a.ctypes.data_as(ctypes.c_void_p) for a in coefs]
+    check(ctx.lib.ibtk_le_phys_bdry_side(ctx.h, ctypes.byref(geom.c), _ptr_array(u), ctypes.cast(phys, ctypes.c_void_p),
+                                         cp[0], cp[1], cp[2], int(bool(adjoint))))
 
 
 UPDATE_SCHEMES = {"euler": 0, "midpoint": 1, "trapezoidal": 2}

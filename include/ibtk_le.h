@@ -162,6 +162,23 @@ int ibtk_le_zero_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int cen
                         int q_depth);
 int ibtk_le_fold_periodic_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int centering,
                                  double* const* q_dev, int q_depth, const int* periodic);
+/* Physical-boundary ghost operators for side-centred data on one patch
+ * (CartSideRobinPhysBdryOp, CartSideRobinPhysBdryOp.cpp:358-493, arithmetic of
+ * cartphysbdryop{2,3}d.f.m4).  adjoint = 0: setPhysicalBoundaryConditions, the
+ * ghost fill before interpolation; adjoint = 1: accumulateFromPhysicalBoundary
+ * Data, the fold LDataManager::spread runs after spreading (LDataManager.cpp:
+ * 655-659).  u_dev[axis]: the ghosted side arrays; the ghost width must be the
+ * same in every dim (the reference asserts it, :519-527).  physical[2 d + upper]
+ * flags a face on a non-periodic physical boundary (edges/corners are boxes
+ * whose faces are all physical); acoef/bcoef/gcoef[c * 2 ndim + loc] are the
+ * Robin coefficients of component c on face loc, constant over the face
+ * (RobinBcCoefStrategy::setBcCoefs, index NDIM*depth + axis with depth 0).
+ * Periodic dims are folded/filled separately (ibtk_le_{fold,fill}_periodic_
+ * ghosts), before the physical fold and after the physical fill.  Bitwise equal
+ * to the serial Fortran order. */
+int ibtk_le_phys_bdry_side(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, double* const* u_dev,
+                           const int* physical, const double* acoef, const double* bcoef, const double* gcoef,
+                           int adjoint);
 /* Build the list of interior markers and of their periodic images that fall in the
  * ghost box (LIndexSetData::cacheLocalIndices, LIndexSetData.cpp:83-169, for one
  * patch covering a periodic domain; getCellIndex, IndexUtilities-inl.h:66-89).

@@ -37,6 +37,16 @@ int ora_spread(int kernel, int ndim, const double* dx, const double* x_lower, in
                const int* iupper, const int* nugc, double* u, const int* indices, const double* Xshift, int nindices,
                const double* X, const double* V);
 
+/* CartSideRobinPhysBdryOp on one side-centred patch (le_bdry_oracle.c):
+ * adjoint = 0 fills the physical-boundary ghosts (setPhysicalBoundaryConditions),
+ * adjoint = 1 folds them back (accumulateFromPhysicalBoundaryData).  u0..u2 are
+ * the ghosted side arrays of axes 0..ndim-1 (uniform ghost width gcw); phys[loc]
+ * flags face loc = 2 d + upper as physical; coefficient [c * 2 ndim + loc] is
+ * the Robin a/b/g of component c on face loc. */
+int ora_phys_bdry_side(int ndim, const int* ilower, const int* iupper, int gcw, const double* dx, double* u0,
+                       double* u1, double* u2, const int* phys, const double* acoef, const double* bcoef,
+                       const double* gcoef, int adjoint);
+
 #ifdef __cplusplus
 }
 #endif

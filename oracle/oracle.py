@@ -75,6 +75,8 @@ def lib():
         L.ora_ib_3_delta.argtypes = [ctypes.c_double]
         L.ora_piecewise_cubic_delta.restype = ctypes.c_double
         L.ora_piecewise_cubic_delta.argtypes = [ctypes.c_double]
+        L.ora_phys_bdry_side.restype = c_int
+        L.ora_phys_bdry_side.argtypes = [c_int, ip, ip, c_int, dp, dp, dp, dp, ip, dp, dp, dp, c_int]
         _lib = L
     return _lib
 
@@ -279,3 +281,37 @@ def periodic_index_list(X, x_lower, x_upper, dx, box_lo, box_hi, ghost, periodic
     order = np.lexsort((s, key))
     Xshift = off[order].astype(np.float64) * np.asarray(dx)[None, :]
     return s[order].astype(np.int32), Xshift, cell[order]
+
+
+# --------------------------------------------------------------------------
+# physical-boundary operators (le_bdry_oracle.c)
+# --------------------------------------------------------------------------
+def side_ghost_shape(box_lo, box_hi, gcw, axis):
+    """numpy shape (C order) of the ghosted side array of `axis` (uniform gcw)."""
+    lo, hi = side_box(box_lo, box_hi, axis)
+    return ghost_shape(lo, hi, [gcw] * len(box_lo))[1:]
+
+
+def phys_bdry_side(box_lo, box_hi, gcw, dx, u_axes, phys, acoef, bcoef, gcoef, adjoint):
+    """CartSideRobinPhysBdryOp on one patch of side data (in place).
+
+    adjoint=False: setPhysicalBoundaryConditions (CartSideRobinPhysBdryOp.cpp:358-422);
+    adjoint=True: accumulateFromPhysicalBoundaryData (:429-493).  phys[2d+upper]
+    flags a physical face; acoef/bcoef/gcoef have shape (ndim, 2 ndim):
+    [component axis, face location]."""
+    ndim = len(box_lo)
+    us = []
+    for a in range(ndim):
+        u = u_axes[a]
+        assert u.dtype == np.float64 and u.flags.c_contiguous
+        assert u.shape == side_ghost_shape(box_lo, box_hi, gcw, a)
+        us.append(u)
+    dummy = np.zeros(1)
+    while len(us) < 3:
+        us.append(dummy)
+    A, B, G = (_f64(np.broadcast_to(np.asarray(c, np.float64), (ndim, 2 * ndim))) for c in (acoef, bcoef, gcoef))
+    rc = lib().ora_phys_bdry_side(ndim, _ip(_i32(box_lo)), _ip(_i32(box_hi)), int(gcw), _dp(_f64(dx)), _dp(us[0]),
+                                  _dp(us[1]), _dp(us[2]), _ip(_i32(phys)), _dp(A), _dp(B), _dp(G), int(adjoint))
+    if rc != 0:
+        raise RuntimeError(f"ora_phys_bdry_side failed ({rc})")
+    return u_axes
