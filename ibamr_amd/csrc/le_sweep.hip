@@ -97,22 +97,40 @@ __global__ __launch_bounds__(BLOCK) void k_bin_col(Params p, int n, unsigned* ke
 // (key[e-1], key[e]] (keys >= nbuckets: binned outside).  The buckets before
 // the first key and after the last one are k_bucket_ends' (one thread each:
 // a single thread walking them would serialise the launch).  n > 0.
+// The block's 3 BLOCK positions leave through LDS as 16-byte stores (a wave's
+// 8-byte stores at a 24-byte stride would write each cache line in thirds).
 template <int K>
 __global__ __launch_bounds__(BLOCK) void k_gather_col(Params p, int n, int* sorted_s, double* sorted_X,
                                                       const unsigned* skeys, int nbuckets, int* bs) {
-    const int e = blockIdx.x * BLOCK + threadIdx.x;
-    if (e >= n) return;
-    if (e > 0) {
-        const int bi = (int)min(skeys[e], (unsigned)nbuckets);
-        const int bp = (int)min(skeys[e - 1], (unsigned)nbuckets);
-        for (int b = bp + 1; b <= bi; ++b) bs[b] = e;
-    }
-    const int l = p.sorted_l[e];
-    const int s = p.indices ? p.indices[l] : l;
-    sorted_s[e] = s;
+    __shared__ double sx[3 * BLOCK];
+    const int e0 = blockIdx.x * BLOCK;
+    const int e = e0 + threadIdx.x;
+    if (e < n) {
+        if (e > 0) {
+            const int bi = (int)min(skeys[e], (unsigned)nbuckets);
+            const int bp = (int)min(skeys[e - 1], (unsigned)nbuckets);
+            for (int b = bp + 1; b <= bi; ++b) bs[b] = e;
+        }
+        const int l = p.sorted_l[e];
+        const int s = p.indices ? p.indices[l] : l;
+        sorted_s[e] = s;
 #pragma unroll
-    for (int d = 0; d < 3; ++d)
-        sorted_X[(int64_t)3 * e + d] = p.X[(int64_t)3 * s + d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
+        for (int d = 0; d < 3; ++d)
+            sx[3 * threadIdx.x + d] = p.X[(int64_t)3 * s + d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
+    }
+    __syncthreads();
+    const int cnt = 3 * min(BLOCK, n - e0);  // doubles this block writes
+    double* out = sorted_X + (int64_t)3 * e0;  // 16-byte aligned: 3 BLOCK e0 doubles in
+    for (int i = threadIdx.x; 2 * i < cnt; i += BLOCK) {
+        if (2 * i + 1 < cnt) {
+            double2 v;
+            v.x = sx[2 * i];
+            v.y = sx[2 * i + 1];
+            *reinterpret_cast<double2*>(out + 2 * i) = v;
+        } else {
+            out[2 * i] = sx[2 * i];
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
