@@ -228,7 +228,10 @@ __device__ __forceinline__ double shfl_f64(double v, int src) {
 // ---------------------------------------------------------------------------
 // interpolation
 // ---------------------------------------------------------------------------
-constexpr int IWAVES = 4;  // waves per interp work item (one LDS ring)
+#ifndef IBTK_LE_IWAVES
+#define IBTK_LE_IWAVES 4
+#endif
+constexpr int IWAVES = IBTK_LE_IWAVES;  // waves per interp work item (one LDS ring)
 // 1: interp sums in the Fortran order, bitwise the oracle's (default);
 // 0: separable rows with FMAs, within tolerance (an experiment, not shipped)
 #ifndef IBTK_LE_INTERP_EXACT
