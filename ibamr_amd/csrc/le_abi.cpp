@@ -735,11 +735,9 @@ static int ghost_op(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int centeri
     for (int d = 0; d < geom->ndim; ++d)
         if (per[d] && geom->iupper[d] - geom->ilower[d] + 1 < 2 * geom->gcw[d] + 1)
             return fail(IBTK_LE_ERR_ARG, "periodic dim %d narrower than 2*ghost+1", d);
-    for (int i = 0; i < n; ++i) {
-        if (mode == 0) HIP_TRY(launch_fill_periodic(geom->ndim, gds[i], per, ctx->stream));
-        else if (mode == 1) HIP_TRY(launch_fold_periodic(geom->ndim, gds[i], per, ctx->stream));
-        else HIP_TRY(launch_zero_ghosts(geom->ndim, gds[i], ctx->stream));
-    }
+    if (mode == 0) HIP_TRY(launch_fill_periodic(geom->ndim, gds, n, per, ctx->stream));
+    else if (mode == 1) HIP_TRY(launch_fold_periodic(geom->ndim, gds, n, per, ctx->stream));
+    else HIP_TRY(launch_zero_ghosts(geom->ndim, gds, n, ctx->stream));
     return IBTK_LE_OK;
 }
 

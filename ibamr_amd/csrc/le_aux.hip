@@ -4,6 +4,9 @@
 // LEInteractor::buildLocalIndices for one patch).  The hot path is le_hot.hip.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstring>
+
 #include "le_internal.h"
 #include "le_stencil.h"
 
@@ -77,24 +80,15 @@ hipError_t launch_mark(int ndim, int kernel, const Params& p, int n, unsigned ch
 // ---------------------------------------------------------------------------
 // The ghost region of dim d (d = 0..NDIM-1): dims > d interior, dim d outside
 // the interior, dims < d anything in the ghost box.
-__device__ __forceinline__ bool ghost_point(const GhostDesc& g, int ndim, int dreg, int64_t t, int* pt) {
-    int64_t rem = t;
-    int ext[3];
-    for (int d = 0; d < ndim; ++d) {
-        if (d < dreg) ext[d] = g.hi[d] - g.lo[d] + 1;
+// Extents of pass dreg: dims below dreg over the whole ghost box, dim dreg over
+// its ghost layers only, dims above over the interior.
+__device__ __host__ __forceinline__ void ghost_ext(const GhostDesc& g, int ndim, int dreg, int* ext) {
+    for (int d = 0; d < 3; ++d) {
+        if (d >= ndim) ext[d] = 1;
+        else if (d < dreg) ext[d] = g.hi[d] - g.lo[d] + 1;
         else if (d == dreg) ext[d] = (g.ilo[d] - g.lo[d]) + (g.hi[d] - g.ihi[d]);
         else ext[d] = g.ihi[d] - g.ilo[d] + 1;
     }
-    for (int d = 0; d < ndim; ++d) {
-        const int q = (int)(rem % ext[d]);
-        rem /= ext[d];
-        if (d < dreg) pt[d] = g.lo[d] + q;
-        else if (d == dreg) {
-            const int nlo = g.ilo[d] - g.lo[d];
-            pt[d] = q < nlo ? g.lo[d] + q : g.ihi[d] + 1 + (q - nlo);
-        } else pt[d] = g.ilo[d] + q;
-    }
-    return rem == 0;
 }
 
 __device__ __forceinline__ int64_t goff(const GhostDesc& g, int ndim, const int* pt) {
@@ -110,15 +104,27 @@ __device__ __forceinline__ int wrap(int i, int lo, int n) {
     return lo + r;
 }
 
+// One pass over the ghost points of dim dreg of up to GSET arrays (blockIdx.z =
+// array): dims 0 and 1 flattened over x blocks (one 32-bit division per
+// thread), dim 2 over blockIdx.y.
 // mode 0: fill (ghost <- periodic interior, all dims wrapped at once)
 // mode 1: fold dim dreg (interior-in-dreg point += ghost point), one source per destination
 // mode 2: zero
-__global__ __launch_bounds__(BLOCK) void k_ghost(GhostDesc g, int ndim, int dreg, int mode, int64_t count, int p0,
-                                                  int p1, int p2) {
-    const int64_t t = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (t >= count) return;
+__global__ __launch_bounds__(BLOCK) void k_ghost(GhostSet gs, int ndim, int dreg, int mode, int p0, int p1, int p2) {
+    const GhostDesc& g = gs.g[blockIdx.z];
+    int ext[3];
+    ghost_ext(g, ndim, dreg, ext);
+    const unsigned t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= (unsigned)ext[0] * (unsigned)ext[1] || (int)blockIdx.y >= ext[2]) return;
+    const int q[3] = {(int)(t % (unsigned)ext[0]), (int)(t / (unsigned)ext[0]), (int)blockIdx.y};
     int pt[3] = {0, 0, 0};
-    if (!ghost_point(g, ndim, dreg, t, pt)) return;
+    for (int d = 0; d < ndim; ++d) {
+        if (d < dreg) pt[d] = g.lo[d] + q[d];
+        else if (d == dreg) {
+            const int nlo = g.ilo[d] - g.lo[d];
+            pt[d] = q[d] < nlo ? g.lo[d] + q[d] : g.ihi[d] + 1 + (q[d] - nlo);
+        } else pt[d] = g.ilo[d] + q[d];
+    }
     const int per[3] = {p0, p1, p2};
     if (mode == 2) {
         g.u[goff(g, ndim, pt)] = 0.0;
@@ -143,45 +149,51 @@ __global__ __launch_bounds__(BLOCK) void k_ghost(GhostDesc g, int ndim, int dreg
     g.u[od] = g.u[od] + g.u[os];
 }
 
-static int64_t ghost_count(const GhostDesc& g, int ndim, int dreg) {
-    int64_t c = 1;
-    for (int d = 0; d < ndim; ++d) {
-        if (d < dreg) c *= g.hi[d] - g.lo[d] + 1;
-        else if (d == dreg) c *= (g.ilo[d] - g.lo[d]) + (g.hi[d] - g.ihi[d]);
-        else c *= g.ihi[d] - g.ilo[d] + 1;
-    }
-    return c;
-}
-
-static hipError_t ghost_pass(const GhostDesc& g, int ndim, int dreg, int mode, const int* per, hipStream_t s) {
-    const int64_t cnt = ghost_count(g, ndim, dreg);
-    if (cnt <= 0) return hipSuccess;
-    const int64_t nb = (cnt + BLOCK - 1) / BLOCK;
-    hipLaunchKernelGGL(k_ghost, dim3((unsigned)nb), dim3(BLOCK), 0, s, g, ndim, dreg, mode, cnt, per[0], per[1],
-                       ndim > 2 ? per[2] : 0);
-    return hipGetLastError();
-}
-
-hipError_t launch_fill_periodic(int ndim, const GhostDesc& g, const int* periodic, hipStream_t s) {
-    for (int d = 0; d < ndim; ++d) {
-        hipError_t e = ghost_pass(g, ndim, d, 0, periodic, s);
+static hipError_t ghost_pass(const GhostDesc* gds, int n, int ndim, int dreg, int mode, const int* per,
+                             hipStream_t s) {
+    for (int first = 0; first < n; first += GSET) {
+        GhostSet gs;
+        std::memset(&gs, 0, sizeof(gs));
+        const int cnt = std::min(GSET, n - first);
+        long long m01 = 0;
+        int m2 = 0;
+        for (int i = 0; i < cnt; ++i) {
+            gs.g[i] = gds[first + i];
+            int ext[3];
+            ghost_ext(gs.g[i], ndim, dreg, ext);
+            m01 = std::max(m01, (long long)ext[0] * ext[1]);
+            m2 = std::max(m2, ext[2]);
+        }
+        if (m01 <= 0 || m2 <= 0) continue;
+        if (m01 >= (1LL << 32) || m2 > 65535) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_ghost, dim3((unsigned)((m01 + BLOCK - 1) / BLOCK), (unsigned)m2, (unsigned)cnt),
+                           dim3(BLOCK), 0, s, gs, ndim, dreg, mode, per[0], per[1], ndim > 2 ? per[2] : 0);
+        hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
 }
-hipError_t launch_fold_periodic(int ndim, const GhostDesc& g, const int* periodic, hipStream_t s) {
+
+hipError_t launch_fill_periodic(int ndim, const GhostDesc* g, int n, const int* periodic, hipStream_t s) {
+    for (int d = 0; d < ndim; ++d) {
+        hipError_t e = ghost_pass(g, n, ndim, d, 0, periodic, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+hipError_t launch_fold_periodic(int ndim, const GhostDesc* g, int n, const int* periodic, hipStream_t s) {
     // slowest dim first: a point that is ghost in several dims is carried into
     // the interior one dim at a time, each step with one source per destination
     for (int d = ndim - 1; d >= 0; --d) {
-        hipError_t e = ghost_pass(g, ndim, d, 1, periodic, s);
+        hipError_t e = ghost_pass(g, n, ndim, d, 1, periodic, s);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
 }
-hipError_t launch_zero_ghosts(int ndim, const GhostDesc& g, hipStream_t s) {
+hipError_t launch_zero_ghosts(int ndim, const GhostDesc* g, int n, hipStream_t s) {
     const int per[3] = {1, 1, 1};
     for (int d = 0; d < ndim; ++d) {
-        hipError_t e = ghost_pass(g, ndim, d, 2, per, s);
+        hipError_t e = ghost_pass(g, n, ndim, d, 2, per, s);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;

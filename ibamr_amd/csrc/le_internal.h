@@ -162,9 +162,14 @@ struct GhostDesc {
     int ilo[3], ihi[3];   // unique (interior) index range per dim
     int64_t s1, s2;
 };
-hipError_t launch_fill_periodic(int ndim, const GhostDesc& g, const int* periodic, hipStream_t s);
-hipError_t launch_fold_periodic(int ndim, const GhostDesc& g, const int* periodic, hipStream_t s);
-hipError_t launch_zero_ghosts(int ndim, const GhostDesc& g, hipStream_t s);
+constexpr int GSET = 4;  // arrays per ghost launch
+struct GhostSet {
+    GhostDesc g[GSET];
+};
+// every pass covers all n arrays (GSET per launch)
+hipError_t launch_fill_periodic(int ndim, const GhostDesc* g, int n, const int* periodic, hipStream_t s);
+hipError_t launch_fold_periodic(int ndim, const GhostDesc* g, int n, const int* periodic, hipStream_t s);
+hipError_t launch_zero_ghosts(int ndim, const GhostDesc* g, int n, hipStream_t s);
 
 struct ImageDesc {
     int ndim;
