@@ -97,6 +97,8 @@ _SIGS = [
      [c_void_p, ctypes.POINTER(PatchGeom), c_int, ctypes.POINTER(c_void_p), c_int, c_void_p]),
     ("ibtk_le_fold_periodic_ghosts", c_int,
      [c_void_p, ctypes.POINTER(PatchGeom), c_int, ctypes.POINTER(c_void_p), c_int, c_void_p]),
+    ("ibtk_le_local_numbering", c_int,
+     [c_void_p, ctypes.POINTER(PatchGeom), c_void_p, c_int, c_void_p, ctypes.POINTER(c_int)]),
     ("ibtk_le_phys_bdry_side", c_int,
      [c_void_p, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_void_p, c_void_p, c_void_p, c_void_p,
       c_int]),

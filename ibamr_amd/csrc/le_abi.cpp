@@ -875,6 +875,58 @@ static int index_list_impl(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, cons
     return IBTK_LE_OK;
 }
 
+// LDataManager::computeNodeDistribution's local numbering (LDataManager.cpp:
+// 2839-3027) for one patch: order_dev[i] = the input index of the marker that
+// gets local index i; markers in cells of the patch box first, in box order (x
+// fastest) and input order within a cell, then the markers outside the box in
+// input order.  *n_interior (host, may be null) = the count inside the box.
+extern "C" int ibtk_le_local_numbering(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
+                                       int n_markers, int* order_dev, int* n_interior) {
+    if (!ctx) return fail(IBTK_LE_ERR_ARG, "null context");
+    if (int rc = check_geom(geom)) return rc;
+    if (n_markers < 0) return fail(IBTK_LE_ERR_ARG, "negative size");
+    if (n_markers > 0 && (!X_dev || !order_dev)) return fail(IBTK_LE_ERR_ARG, "null array");
+    if (n_interior) *n_interior = 0;
+    if (n_markers == 0) return IBTK_LE_OK;
+    unsigned long long ncells = 1;
+    for (int k = 0; k < geom->ndim; ++k) ncells *= (unsigned long long)(geom->iupper[k] - geom->ilower[k] + 1);
+    if (ncells >= 0xffffffffull) return fail(IBTK_LE_ERR_RANGE, "patch box has %llu cells", ncells);
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    ImageDesc d;
+    std::memset(&d, 0, sizeof(d));
+    d.ndim = geom->ndim;
+    for (int k = 0; k < geom->ndim; ++k) {
+        d.xlo[k] = geom->x_lower[k];
+        d.xup[k] = geom->x_upper[k];
+        d.dx[k] = geom->dx[k];
+        d.ilo[k] = geom->ilower[k];
+        d.ihi[k] = geom->iupper[k];
+    }
+    int rc;
+    const size_t n = (size_t)n_markers;
+    if ((rc = ctx->keys_in.ensure(2 * sizeof(unsigned) * n))) return rc;  // keys in | keys out
+    if ((rc = ctx->vals_in.ensure(sizeof(int) * n))) return rc;
+    if ((rc = ctx->counts.ensure(sizeof(int)))) return rc;
+    const hipStream_t s = ctx->stream;
+    unsigned* kin = ctx->keys_in.as<unsigned>();
+    unsigned* kout = kin + n;
+    HIP_TRY(hipMemsetAsync(ctx->counts.p, 0, sizeof(int), s));
+    HIP_TRY(launch_cell_keys(d, X_dev, n_markers, (unsigned)ncells, kin, ctx->vals_in.as<int>(), ctx->counts.as<int>(),
+                             s));
+    int end_bit = 1;
+    while ((1ull << end_bit) <= ncells) ++end_bit;
+    size_t tb = 0;
+    HIP_TRY(launch_sort(nullptr, tb, kin, kout, ctx->vals_in.as<int>(), order_dev, n_markers, end_bit, s));
+    if ((rc = ctx->temp.ensure(tb))) return rc;
+    tb = ctx->temp.cap;
+    HIP_TRY(launch_sort(ctx->temp.p, tb, kin, kout, ctx->vals_in.as<int>(), order_dev, n_markers, end_bit, s));
+    if (n_interior) {
+        HIP_TRY(hipMemcpyAsync(n_interior, ctx->counts.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    return IBTK_LE_OK;
+}
+
 extern "C" int ibtk_le_mark_stencils(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                                      const ibtk_le_patch_geom* geom, unsigned char* const* masks_dev, int q_depth,
                                      const double* X_dev) {

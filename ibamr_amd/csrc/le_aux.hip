@@ -266,6 +266,37 @@ __global__ __launch_bounds__(BLOCK) void k_image_write(ImageDesc d, const double
     image_walk(d, X + (int64_t)d.ndim * s, idx, xs, offsets[s], capacity, s);
 }
 
+// Local numbering keys (LDataManager::computeNodeDistribution, LDataManager.cpp:
+// 2839-3027): the linear index of the marker's cell in the patch box, x fastest
+// (the box iteration order of LNodeSetData), by getCellIndex; markers whose
+// cell is outside the box get key ncells (numbered last).  vals = input index,
+// so a stable sort keeps input order within a cell.
+__global__ __launch_bounds__(BLOCK) void k_cell_keys(ImageDesc d, const double* X, int n, unsigned ncells,
+                                                     unsigned* keys, int* vals, int* inside) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    int c[3] = {0, 0, 0};
+    cell_index(d, X + (int64_t)d.ndim * i, c);
+    unsigned key = 0, stride = 1;
+    bool in = true;
+    for (int k = 0; k < d.ndim; ++k) {
+        in = in && c[k] >= d.ilo[k] && c[k] <= d.ihi[k];
+        key += (unsigned)(c[k] - d.ilo[k]) * stride;
+        stride *= (unsigned)(d.ihi[k] - d.ilo[k] + 1);
+    }
+    keys[i] = in ? key : ncells;
+    vals[i] = i;
+    if (in) atomicAdd(inside, 1);
+}
+
+hipError_t launch_cell_keys(const ImageDesc& d, const double* X, int n, unsigned ncells, unsigned* keys, int* vals,
+                            int* inside, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_cell_keys, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, d, X, n, ncells, keys, vals,
+                       inside);
+    return hipGetLastError();
+}
+
 hipError_t launch_image_count(const ImageDesc& d, const double* X, int n, int* counts, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_image_count, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, d, X, n, counts);

@@ -180,6 +180,8 @@ struct ImageDesc {
     int filter;           // 1: emit (s, 0) iff the cell lies in [flo, fhi] (no images)
     int flo[3], fhi[3];
 };
+hipError_t launch_cell_keys(const ImageDesc& d, const double* X, int n, unsigned ncells, unsigned* keys, int* vals,
+                            int* inside, hipStream_t s);
 hipError_t launch_image_count(const ImageDesc& d, const double* X, int n, int* counts, hipStream_t s);
 hipError_t launch_image_write(const ImageDesc& d, const double* X, int n, const int* offsets, int* idx,
                               double* xshift, int capacity, hipStream_t s);

@@ -252,6 +252,21 @@ def zero_ghosts(ctx: Context, geom: Geometry, centering: str, q, q_depth=1):
     check(ctx.lib.ibtk_le_zero_ghosts(ctx.h, ctypes.byref(geom.c), CENTERING[centering], _ptr_array(q), q_depth))
 
 
+def local_numbering(ctx: Context, geom: Geometry, X: torch.Tensor):
+    """LDataManager::computeNodeDistribution's local numbering for one patch, on the device.
+
+    Returns (order, n_interior): order[i] = input index of the marker with local index i
+    (cells of the patch box in box order, x fastest, input order within a cell; markers
+    outside the box last, in input order)."""
+    if X.dtype != torch.float64 or not X.is_cuda or not X.is_contiguous() or X.dim() != 2 or X.shape[1] != geom.ndim:
+        raise ValueError("X: contiguous (M, ndim) float64 device tensor")
+    n = X.shape[0]
+    order = torch.empty(n, dtype=torch.int32, device=X.device)
+    nin = ctypes.c_int(0)
+    check(ctx.lib.ibtk_le_local_numbering(ctx.h, ctypes.byref(geom.c), _ptr(X), n, _ptr(order), ctypes.byref(nin)))
+    return order, nin.value
+
+
 def phys_bdry_side(ctx: Context, geom: Geometry, u, physical, acoef, bcoef, gcoef, adjoint: bool):
     """CartSideRobinPhysBdryOp on one patch of side data, on the device.
 

@@ -179,6 +179,15 @@ int ibtk_le_fold_periodic_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom
 int ibtk_le_phys_bdry_side(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, double* const* u_dev,
                            const int* physical, const double* acoef, const double* bcoef, const double* gcoef,
                            int adjoint);
+/* Local numbering of one patch's markers (LDataManager::computeNodeDistribution,
+ * LDataManager.cpp:2839-3027, cells by IndexUtilities::getCellIndex): order_dev[i]
+ * is the input index of the marker given local index i.  Markers whose cell is in
+ * the patch box come first, in box iteration order (x fastest), input order within
+ * a cell (a stable device radix sort); the others follow in input order.  If
+ * n_interior is not NULL it receives the count inside the box (this synchronises
+ * the stream). */
+int ibtk_le_local_numbering(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev, int n_markers,
+                            int* order_dev, int* n_interior);
 /* Build the list of interior markers and of their periodic images that fall in the
  * ghost box (LIndexSetData::cacheLocalIndices, LIndexSetData.cpp:83-169, for one
  * patch covering a periodic domain; getCellIndex, IndexUtilities-inl.h:66-89).
