@@ -81,12 +81,17 @@ hipError_t launch_mark(int ndim, int kernel, const Params& p, int n, unsigned ch
 // The ghost region of dim d (d = 0..NDIM-1): dims > d interior, dim d outside
 // the interior, dims < d anything in the ghost box.
 // Extents of pass dreg: dims below dreg over the whole ghost box, dim dreg over
-// its ghost layers only, dims above over the interior.
-__device__ __host__ __forceinline__ void ghost_ext(const GhostDesc& g, int ndim, int dreg, int* ext) {
+// its ghost layers only, dims above over the interior if periodic (their ghosts
+// are another pass's) and over the whole ghost box if not (their ghosts are
+// physical: the fill copies them from the periodic image, which the physical
+// fill has set before; the fold carries them to the image, for the physical
+// fold that follows).
+__device__ __host__ __forceinline__ bool full_dim(int d, int dreg, const int* per) { return d < dreg || !per[d]; }
+__device__ __host__ __forceinline__ void ghost_ext(const GhostDesc& g, int ndim, int dreg, const int* per, int* ext) {
     for (int d = 0; d < 3; ++d) {
         if (d >= ndim) ext[d] = 1;
-        else if (d < dreg) ext[d] = g.hi[d] - g.lo[d] + 1;
         else if (d == dreg) ext[d] = (g.ilo[d] - g.lo[d]) + (g.hi[d] - g.ihi[d]);
+        else if (full_dim(d, dreg, per)) ext[d] = g.hi[d] - g.lo[d] + 1;
         else ext[d] = g.ihi[d] - g.ilo[d] + 1;
     }
 }
@@ -107,38 +112,39 @@ __device__ __forceinline__ int wrap(int i, int lo, int n) {
 // One pass over the ghost points of dim dreg of up to GSET arrays (blockIdx.z =
 // array): dims 0 and 1 flattened over x blocks (one 32-bit division per
 // thread), dim 2 over blockIdx.y.
-// mode 0: fill (ghost <- periodic interior, all dims wrapped at once)
+// mode 0: fill (ghost <- its image with every periodic dim wrapped at once)
 // mode 1: fold dim dreg (interior-in-dreg point += ghost point), one source per destination
 // mode 2: zero
 __global__ __launch_bounds__(BLOCK) void k_ghost(GhostSet gs, int ndim, int dreg, int mode, int p0, int p1, int p2) {
     const GhostDesc& g = gs.g[blockIdx.z];
+    const int per[3] = {p0, p1, p2};
     int ext[3];
-    ghost_ext(g, ndim, dreg, ext);
+    ghost_ext(g, ndim, dreg, per, ext);
     const unsigned t = blockIdx.x * BLOCK + threadIdx.x;
     if (t >= (unsigned)ext[0] * (unsigned)ext[1] || (int)blockIdx.y >= ext[2]) return;
     const int q[3] = {(int)(t % (unsigned)ext[0]), (int)(t / (unsigned)ext[0]), (int)blockIdx.y};
     int pt[3] = {0, 0, 0};
     for (int d = 0; d < ndim; ++d) {
-        if (d < dreg) pt[d] = g.lo[d] + q[d];
-        else if (d == dreg) {
+        if (d == dreg) {
             const int nlo = g.ilo[d] - g.lo[d];
             pt[d] = q[d] < nlo ? g.lo[d] + q[d] : g.ihi[d] + 1 + (q[d] - nlo);
-        } else pt[d] = g.ilo[d] + q[d];
+        } else if (full_dim(d, dreg, per)) pt[d] = g.lo[d] + q[d];
+        else pt[d] = g.ilo[d] + q[d];
     }
-    const int per[3] = {p0, p1, p2};
     if (mode == 2) {
         g.u[goff(g, ndim, pt)] = 0.0;
         return;
     }
     if (mode == 0) {
         int src[3] = {pt[0], pt[1], pt[2]};
+        bool moved = false;  // wrapped in some periodic dim (a non-periodic ghost coordinate is kept)
         for (int d = 0; d < ndim; ++d) {
-            if (src[d] < g.ilo[d] || src[d] > g.ihi[d]) {
-                if (!per[d]) return;
+            if (per[d] && (src[d] < g.ilo[d] || src[d] > g.ihi[d])) {
                 src[d] = wrap(src[d], g.ilo[d], g.ihi[d] - g.ilo[d] + 1);
+                moved = true;
             }
         }
-        g.u[goff(g, ndim, pt)] = g.u[goff(g, ndim, src)];
+        if (moved) g.u[goff(g, ndim, pt)] = g.u[goff(g, ndim, src)];
         return;
     }
     // fold along dreg only
@@ -160,7 +166,7 @@ static hipError_t ghost_pass(const GhostDesc* gds, int n, int ndim, int dreg, in
         for (int i = 0; i < cnt; ++i) {
             gs.g[i] = gds[first + i];
             int ext[3];
-            ghost_ext(gs.g[i], ndim, dreg, ext);
+            ghost_ext(gs.g[i], ndim, dreg, per, ext);
             m01 = std::max(m01, (long long)ext[0] * ext[1]);
             m2 = std::max(m2, ext[2]);
         }
@@ -174,6 +180,8 @@ static hipError_t ghost_pass(const GhostDesc* gds, int n, int ndim, int dreg, in
     return hipSuccess;
 }
 
+// After the physical fill when some dims are not periodic (their ghost layers
+// are copied from the periodic image like any other point).
 hipError_t launch_fill_periodic(int ndim, const GhostDesc* g, int n, const int* periodic, hipStream_t s) {
     for (int d = 0; d < ndim; ++d) {
         hipError_t e = ghost_pass(g, n, ndim, d, 0, periodic, s);

@@ -8,6 +8,7 @@ handed to libibtk_le.so by pointer.  Arrays follow SAMRAI's Fortran layout, so a
 from __future__ import annotations
 
 import ctypes
+import sys
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -120,6 +121,10 @@ class Context:
             self.h = None
 
     def __del__(self):
+        # at interpreter exit the HIP runtime may already be torn down: leave the
+        # device memory to the process exit rather than free it into a dead runtime
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:
@@ -175,6 +180,10 @@ class Markers:
             self.h = None
 
     def __del__(self):
+        # at interpreter exit the HIP runtime may already be torn down: leave the
+        # device memory to the process exit rather than free it into a dead runtime
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:
