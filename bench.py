@@ -94,7 +94,8 @@ def make_markers(kind, M, slab, seed, device):
 
 
 def cpu_baseline(cfg, kernel, seconds_target=15.0):
-    """The oracle (single-thread C restatement) timed on a bounded, same-density sample.
+    """The oracle (the C restatement) timed on a bounded, same-density sample, on 1 thread and
+    on up to 16 host threads (one replica each).
 
     Sample: a periodic N_s^3 grid with the workload's marker density (cell-sorted
     order, as on the GPU), IB_4 side-centred interp + spread (periodic images in the
@@ -126,20 +127,58 @@ def cpu_baseline(cfg, kernel, seconds_target=15.0):
     idx_i = np.arange(Ms, dtype=np.int32)
     xs_i = np.zeros((Ms, 3))
     idx_s, xs_s, _ = ora.periodic_index_list(X, [0, 0, 0], [1, 1, 1], dx, lo, hi, g)
+    def one_pass(uu, ff, UU):
+        ora.side_interp(kernel, dx, [0, 0, 0], lo, hi, [g] * 3, uu, idx_i, xs_i, X, UU)
+        ora.side_spread(kernel, dx, [0, 0, 0], lo, hi, [g] * 3, ff, idx_s, xs_s, X, F)
+
+    # one thread
     U = np.zeros((Ms, 3))
     reps, elapsed = 0, 0.0
-    while elapsed < seconds_target or reps < 2:
+    t_one = 0.4 * seconds_target
+    while elapsed < t_one or reps < 2:
         t0 = time.perf_counter()
-        ora.side_interp(kernel, dx, [0, 0, 0], lo, hi, [g] * 3, u, idx_i, xs_i, X, U)
-        ora.side_spread(kernel, dx, [0, 0, 0], lo, hi, [g] * 3, f, idx_s, xs_s, X, F)
+        one_pass(u, f, U)
         elapsed += time.perf_counter() - t0
         reps += 1
         if reps >= 50:
             break
-    rate = 2.0 * Ms * reps / elapsed
-    return {"value": rate, "unit": "marker-ops/s", "cores": 1, "kind": "port",
+    rate1 = 2.0 * Ms * reps / elapsed
+    # T threads, one replica of the sample each (as MPI ranks each holding a patch,
+    # SURVEY.md 8(d)); ctypes releases the GIL inside the C calls
+    import threading
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    T = max(1, min(ncpu, int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
+    reps_t = [0] * T
+    t_multi = 0.6 * seconds_target
+    start = threading.Barrier(T + 1)
+
+    def worker(k):
+        uu = [a.copy() for a in u]
+        ff = [np.zeros_like(a) for a in u]
+        UU = np.zeros((Ms, 3))
+        start.wait()
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < t_multi or reps_t[k] < 1:
+            one_pass(uu, ff, UU)
+            reps_t[k] += 1
+
+    threads = [threading.Thread(target=worker, args=(k,)) for k in range(T)]
+    for th in threads:
+        th.start()
+    start.wait()
+    t0 = time.perf_counter()
+    for th in threads:
+        th.join()
+    wall = time.perf_counter() - t0
+    rateT = 2.0 * Ms * sum(reps_t) / wall
+    return {"value": rateT, "unit": "marker-ops/s", "cores": T, "kind": "port", "value_1thread": rate1,
             "sample": f"{Ns}^3 periodic grid, {Ms} uniform markers (same density as the workload), "
-                      f"{kernel} side interp+spread, cell-sorted, {reps} reps, {elapsed:.1f} s, 1 thread (oracle C)"}
+                      f"{kernel} side interp+spread, cell-sorted (oracle C); {T} threads, one replica of the "
+                      f"sample each: {sum(reps_t)} passes in {wall:.1f} s; 1 thread: {reps} passes in "
+                      f"{elapsed:.1f} s"}
 
 
 def main():
