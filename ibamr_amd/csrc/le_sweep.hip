@@ -353,16 +353,17 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
 }
 
 
-// Interpolation work item = (segment, column, component), one workgroup of two
-// waves sharing one LDS ring (twice the waves per CU for the same LDS: the
+// Interpolation work item = (segment, column, component), one workgroup of
+// IWAVES waves sharing one LDS ring (more waves per CU for the same LDS: the
 // per-marker sum is a dependent chain in the Fortran order, so the latency
-// wants waves).  The waves take the item's anchor planes in pairs: wave w sums
-// anchor a+w while the ring holds planes a+LO .. a+1+HI.  Per pair: barrier
-// (the previous pair's reads are done), each wave puts one new plane (a+w+HI)
-// into the slot a retired plane left, barrier, each wave prefetches its next
-// plane and markers into registers (plain loads) and sums its anchor.  Points
-// outside the component's array are staged as 0.  One lane per marker sums its
-// W^3 stencil from the ring (Fortran loop order, bitwise the oracle's).
+// wants waves).  The waves take the item's anchor planes in groups of IWAVES:
+// the ring holds planes a+LO .. a+IWAVES-1+HI.  Per group: barrier (the
+// previous group's reads are done), wave w puts one new plane (a+w+HI) into
+// the slot a retired plane left, barrier, each wave prefetches its next plane
+// and markers into registers (plain loads) and sums its chunks of the group's
+// pooled markers.  Points outside the component's array are staged as 0.  One
+// lane per marker sums its W^3 stencil from the ring (Fortran loop order,
+// bitwise the oracle's).
 template <int K>
 __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     using S = ISh<K>;
@@ -424,25 +425,54 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
         int s;
         double X[3];
     };
-    // anchor a's markers [beg, end) (an empty range past a1): the two bucket
-    // starts are loaded into registers a group before they are read
-    // (readfirstlane), so no group waits on a load it has just issued
-    struct Span {
-        int beg, end;
+    // LDS barrier of the two waves; global loads in flight stay in flight
+    auto lds_barrier = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
     };
-    auto span_load = [&](int a) {
-        const int ac = min(a, p.cg.nz - 1);
-        Span sp;
-        sp.beg = bs[bucket(p, ac, col, 0)];
-        sp.end = a < a1 ? bs[bucket(p, ac, col, NBAND)] : sp.beg;
-        return sp;
+
+    // The markers of a group's IWAVES anchor planes are pooled and dealt in
+    // 64-lane chunks (chunk c to wave c mod IWAVES): the ring holds every plane
+    // the group's markers read, so any wave can sum any of them, and about
+    // 3.5 chunks per group replace 4 three-quarter-full ones.  Each marker is
+    // still summed by one lane in the Fortran order (bitwise unchanged).
+    // Group spans: lane k < IWAVES holds the first sorted entry of anchor a+k,
+    // lane IWAVES+k its end (loaded a group ahead, read with readlane).
+    struct GSpan {
+        int beg[IWAVES];
+        int pre[IWAVES + 1];
     };
-    auto span_get = [&](const Span& sp, int& beg, int& end) {
-        beg = __builtin_amdgcn_readfirstlane(sp.beg);
-        end = __builtin_amdgcn_readfirstlane(sp.end);
+    auto gspan_load = [&](int a) {
+        const int k = lane < IWAVES ? lane : min(lane - IWAVES, IWAVES - 1);
+        const int ac = min(a + k, p.cg.nz - 1);
+        return bs[bucket(p, ac, col, lane >= IWAVES && lane < 2 * IWAVES ? NBAND : 0)];
     };
-    auto mk_load = [&](int beg, int cnt, Mk& m) {  // markers beg + lane (clamped)
-        const int e = min(beg + min(lane, max(cnt - 1, 0)), nlast);
+    auto gspan_get = [&](int a, int v, GSpan& gsp) {
+        int acc = 0;
+#pragma unroll
+        for (int k = 0; k < IWAVES; ++k) {
+            const int b = __builtin_amdgcn_readlane(v, k);
+            const int e = a + k < a1 ? __builtin_amdgcn_readlane(v, IWAVES + k) : b;
+            gsp.beg[k] = b;
+            gsp.pre[k] = acc;
+            acc += e - b;
+        }
+        gsp.pre[IWAVES] = acc;
+    };
+    // chunk c of a group: entry 64 c + lane (clamped), with its anchor plane
+    auto chunk_load = [&](const GSpan& gsp, int a, int c, Mk& m, int& am) {
+        const int tot = gsp.pre[IWAVES];
+        const int j = min(SW * c + lane, max(tot - 1, 0));
+        int e = gsp.beg[0] + j, k = 0;
+#pragma unroll
+        for (int q = 1; q < IWAVES; ++q)
+            if (j >= gsp.pre[q]) {
+                e = gsp.beg[q] + (j - gsp.pre[q]);
+                k = q;
+            }
+        am = a + k;
+        e = min(e, nlast);
         m.s = p.sorted_s[e];
         const double* xs = p.sorted_X + (int64_t)3 * e;
         m.X[0] = xs[0];
@@ -453,54 +483,46 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     // the markers over the two 32-lane halves of a ds_read_b64 by bank class,
     // as the spread does for its adds, measured 10 % slower: the ranking costs
     // more than the reads' bank conflicts.)
-    auto process = [&](int a, int n, const Mk& m) {
+    auto process_pool = [&](int n, const Mk& m, int am) {
         const bool act = lane < n;
         double acc = 0.0;
-        if (act) acc = interp_marker<K>(p, cd, ring, gx0, gy0, a, m.X, m.s);
+        if (act) acc = interp_marker<K>(p, cd, ring, gx0, gy0, am, m.X, m.s);
         double* dst = act ? p.Qout + ((int64_t)p.Q_depth * m.s + cd.qcomp) : p.sink + lane;
         *dst = acc;
     };
-    // LDS barrier of the two waves; global loads in flight stay in flight
-    auto lds_barrier = [&]() {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    };
-
-    // prologue: planes a0+LO .. a0+HI-1 into the ring (alternately by the two
-    // waves); plane a0+w+HI and the markers of anchor a0+w into registers
     double pv[NPT];
     for (int z = a0 + LO + w; z < a0 + HI; z += IWAVES) {
         plane_load(z, pv);
         plane_put(z, pv);
     }
     plane_load(a0 + w + HI, pv);
+    GSpan gs;
+    gspan_get(a0, gspan_load(a0), gs);
     Mk nxt;
-    int nb, ne;
-    span_get(span_load(a0 + w), nb, ne);
-    mk_load(nb, min(ne - nb, SW), nxt);
-    Span sp1 = span_load(a0 + w + IWAVES);
+    int anx;
+    chunk_load(gs, a0, w, nxt, anx);
+    int vsp1 = gspan_load(a0 + IWAVES);
     for (int a = a0; a < a1; a += IWAVES) {
-        const int my = a + w;  // this wave's anchor plane
-        lds_barrier();          // the previous group's reads are done
+        const int my = a + w;
+        lds_barrier();  // the previous group's reads are done
         plane_put(my + HI, pv);
-        lds_barrier();          // planes a+LO .. a+IWAVES-1+HI are in the ring
+        lds_barrier();  // planes a+LO .. a+IWAVES-1+HI are in the ring
         const Mk cur = nxt;
-        const int beg = nb, end = ne;
-        // prefetch for the next group: markers of my+IWAVES (their bucket starts
-        // loaded a group ago), bucket starts of my+2 IWAVES, plane my+IWAVES+HI
-        span_get(sp1, nb, ne);
-        mk_load(nb, min(ne - nb, SW), nxt);
-        sp1 = span_load(my + 2 * IWAVES);
+        const int acur = anx;
+        const GSpan gc = gs;
+        // prefetch for the next group: its spans (loaded a group ago), its chunk
+        // w, the spans of the group after it, plane my+IWAVES+HI
+        gspan_get(a + IWAVES, vsp1, gs);
+        chunk_load(gs, a + IWAVES, w, nxt, anx);
+        vsp1 = gspan_load(a + 2 * IWAVES);
         plane_load(my + IWAVES + HI, pv);
-        if (my < a1) {
-            process(my, min(end - beg, SW), cur);
-            for (int e0 = beg + SW; e0 < end; e0 += SW) {  // further chunks of a dense plane
-                const int n = min(end - e0, SW);
-                Mk m;
-                mk_load(e0, n, m);
-                process(my, n, m);
-            }
+        const int tot = gc.pre[IWAVES];
+        if (SW * w < tot) process_pool(min(tot - SW * w, SW), cur, acur);
+        for (int c = w + IWAVES; SW * c < tot; c += IWAVES) {  // dense groups
+            Mk m;
+            int am;
+            chunk_load(gc, a, c, m, am);
+            process_pool(min(tot - SW * c, SW), m, am);
         }
     }
 }
