@@ -82,3 +82,17 @@ def test_cpp_facade_methods_exported(lib):
     assert {"interpolate", "spread", "getStencilSize", "getMinimumGhostWidth"} <= set(methods)
     for m in methods:
         assert f"IBTK::LEInteractor::{m}(" in out, m
+
+
+def test_argument_errors_before_any_device_call(lib):
+    """Entry points reject bad arguments with IBTK_LE_ERR_ARG (4) before touching a
+    device, as the reference's TBOX_ERROR checks come before any work."""
+    import ctypes
+    from ibamr_amd import _lib
+    g = _lib.PatchGeom.make([0, 0, 0], [7, 7, 7], [2, 2, 2], [0.1] * 3, [0.0] * 3, [0.8] * 3)
+    n = ctypes.c_int(0)
+    assert lib.ibtk_le_phys_bdry_side(None, ctypes.byref(g), None, None, None, None, None, 1) == 4
+    assert lib.ibtk_le_local_numbering(None, ctypes.byref(g), None, 10, None, ctypes.byref(n)) == 4
+    assert lib.ibtk_le_position_update(None, 0, 10, 0.1, None, None, None, None) == 4
+    msg = lib.ibtk_le_last_error().decode()
+    assert msg, "the last error carries a message"
