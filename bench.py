@@ -208,12 +208,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # IBTK_BENCH_DEVICE / IBTK_BENCH_BACKEND=gloo: a multi-rank rehearsal with every
+    # rank on one GPU (exchanges staged through the host); the default is one rank
+    # per GPU over RCCL
+    local_dev = int(os.environ.get("IBTK_BENCH_DEVICE", local))
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if os.environ.get("IBTK_BENCH_BACKEND", "nccl") == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from ibamr_amd import le
     from ibamr_amd.slab import Slab, SlabExchange, migrate
@@ -222,7 +229,7 @@ def main():
     ghost = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
     slab = Slab([N, N, N], world, rank, ghost)
     geom = slab.geometry()
-    ctx = le.Context(local)
+    ctx = le.Context(local_dev)
 
     t_setup = time.perf_counter()
     X = make_markers(cfg["markers"], cfg["M"], slab, 1234, dev)

@@ -107,14 +107,25 @@ class SlabExchange:
     # -- exchanges -------------------------------------------------------------------
     def _p2p(self, sends, recvs):
         import torch.distributed as dist
-        ops = []
+        # gloo moves host memory only: device tensors are staged through the host
+        # (the multi-rank rehearsal on one GPU; RCCL sends device memory directly)
+        stage = dist.get_backend(self.group) == "gloo"
+        ops, back = [], []
         for t, peer, tag in sends:
+            if stage and t.is_cuda:
+                t = t.cpu()
             ops.append(dist.P2POp(dist.isend, t, peer, group=self.group, tag=tag))
         for t, peer, tag in recvs:
+            if stage and t.is_cuda:
+                h = torch.empty(t.shape, dtype=t.dtype)
+                back.append((h, t))
+                t = h
             ops.append(dist.P2POp(dist.irecv, t, peer, group=self.group, tag=tag))
         if ops:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
+        for h, t in back:
+            t.copy_(h)
 
     def halo_fill(self):
         """Every ghost point := its periodic interior value (before interpolation)."""
@@ -205,11 +216,17 @@ def migrate(slab: Slab, X: torch.Tensor, fields: Sequence[torch.Tensor] = (), gr
     if slab.P == 1:
         recv, recv_counts = send, send_counts
     else:
-        dist.all_to_all_single(recv_counts, send_counts, group=group)
+        # gloo moves host memory only (the one-GPU rehearsal): stage through the host
+        host = dist.get_backend(group) == "gloo" and send.is_cuda
+        sc = send_counts.cpu() if host else send_counts
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc, group=group)
+        recv_counts = rc.to(send_counts.device)
         D = send.shape[1]
-        recv = torch.empty((int(recv_counts.sum().item()), D), dtype=send.dtype, device=send.device)
-        dist.all_to_all_single(recv, send, output_split_sizes=recv_counts.tolist(),
-                               input_split_sizes=send_counts.tolist(), group=group)
+        sd = send.cpu() if host else send
+        recv = torch.empty((int(rc.sum().item()), D), dtype=send.dtype, device=sd.device)
+        dist.all_to_all_single(recv, sd, output_split_sizes=rc.tolist(), input_split_sizes=sc.tolist(), group=group)
+        recv = recv.to(send.device)
     if stay is not None:
         recv = torch.cat([stay, recv], dim=0)
     if cell_order and recv.shape[0]:

@@ -3,9 +3,10 @@
 Checks the z-halo fill and the ghost-region sum of ibamr_amd.slab against the
 global periodic answer.  The local x/y periodic pieces, which run as HIP kernels
 in the product, are replaced here by a numpy restatement of the same kernel
-semantics (ibamr_amd/csrc/le_kernels.hip, k_ghost): fill wraps all dims of a
-ghost point at once; fold walks dims slowest first, region d = (dims < d any,
-dim d ghost, dims > d interior), one source per destination per pass.
+semantics (ibamr_amd/csrc/le_aux.hip, k_ghost): fill wraps every periodic dim
+of a ghost point at once; fold walks dims slowest first, region d = (dims < d
+any, dim d ghost, dims > d interior if periodic, any if not), one source per
+destination per pass.
 Values are small integers so every sum is exact and the comparison is bitwise.
 """
 import os
@@ -44,16 +45,15 @@ def _np_local(arrays, periodic, slab, mode):
                 inside = all(rng[d][0] <= pt[d] < rng[d][1] for d in range(nd))
                 if inside:
                     continue
+                # wrap the periodic dims only; a non-periodic ghost coordinate is kept
                 src = list(pt)
-                ok = True
+                moved = False
                 for d in range(nd):
-                    if not (rng[d][0] <= pt[d] < rng[d][1]):
-                        if not periodic[d]:
-                            ok = False
-                            break
+                    if periodic[d] and not (rng[d][0] <= pt[d] < rng[d][1]):
                         n = rng[d][1] - rng[d][0]
                         src[d] = rng[d][0] + (pt[d] - rng[d][0]) % n
-                if ok:
+                        moved = True
+                if moved:
                     a[pt[2], pt[1], pt[0]] = a[src[2], src[1], src[0]]
         else:
             for dreg in (2, 1, 0):
@@ -61,7 +61,7 @@ def _np_local(arrays, periodic, slab, mode):
                     continue
                 sl = [slice(None)] * 3  # in (x, y, z) order
                 for d in range(nd):
-                    if d > dreg:
+                    if d > dreg and periodic[d]:  # non-periodic dims: their ghost layers too
                         sl[d] = slice(*rng[d])
                 n = rng[dreg][1] - rng[dreg][0]
                 for j in list(range(0, rng[dreg][0])) + list(range(rng[dreg][1], shape[dreg])):
