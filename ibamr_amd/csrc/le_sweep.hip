@@ -892,10 +892,16 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-// Segment length: about 8192 (column, segment) items over the patch, but no
-// segment shorter than 32 planes (the z halo of a segment is HI-LO planes).
+// Segment length: about IBTK_LE_SEG_ITEMS (column, segment) items over the
+// patch, but no segment shorter than 32 planes (the z halo of a segment is HI-LO
+// planes).  16384 is measured (cfg4: S = 141, 8 segments): both sweeps ran
+// 10-12 % faster than at 8192 (S = 281); 4096, 12288, 17952, 20480, 24576 and
+// 32768 were all slower than 16384.
+#ifndef IBTK_LE_SEG_ITEMS
+#define IBTK_LE_SEG_ITEMS 16384
+#endif
 void sweep_segments(const ColGeom& cg, int& S, int& nseg) {
-    long long want = 8192;
+    long long want = IBTK_LE_SEG_ITEMS;
     long long s = ((long long)cg.nz * cg.ncol + want - 1) / want;
     if (s < 32) s = 32;
     if (s > cg.nz) s = cg.nz;
