@@ -99,6 +99,8 @@ struct ibtk_le_ctx_s {
     DevBuf err;   // one int
     DevBuf sink;  // 64 doubles (Params::sink)
     DevBuf stamps;  // diagnostic phase clocks (IBTK_LE_STAMPS=1)
+    bool stamps_on = false;  // IBTK_LE_STAMPS=1, read once at ctx_create
+    int dbg = 0;             // IBTK_LE_DBG, read once at ctx_create
     bool timing = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool ev_valid = false;
@@ -115,8 +117,10 @@ struct ibtk_le_markers_s {
     ibtk_le_patch_geom geom{};
     DevBuf sorted_key, sorted_l, sorted_s, sorted_X, sorted_a, plane_start, indices, xshift;
     DevBuf cand_cnt, cand_off, cand_idx;  // spread candidate lists, built on first use after a bin
+    DevBuf last, qdst;                    // interp with duplicate list entries (Params::qdst)
     bool has_indices = false, has_xshift = false;
     bool cand_valid = false;
+    bool dedup_done = false, has_dups = false;
 };
 
 static int set_device(ibtk_le_ctx ctx) {
@@ -132,6 +136,8 @@ extern "C" int ibtk_le_ctx_create(int device, void* stream, ibtk_le_ctx* out) {
     auto* c = new ibtk_le_ctx_s();
     c->device = device;
     c->stream = static_cast<hipStream_t>(stream);
+    if (const char* e = getenv("IBTK_LE_STAMPS")) c->stamps_on = e[0] == '1';
+    if (const char* e = getenv("IBTK_LE_DBG")) c->dbg = atoi(e);
     HIP_TRY(hipSetDevice(device));
     int rc = c->err.ensure(sizeof(int));
     if (!rc) rc = c->sink.ensure(64 * sizeof(double));
@@ -150,7 +156,8 @@ extern "C" int ibtk_le_ctx_destroy(ibtk_le_ctx ctx) {
     if (!ctx) return IBTK_LE_OK;
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
-    for (DevBuf* b : {&ctx->keys_in, &ctx->vals_in, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->fbuf, &ctx->err, &ctx->sink})
+    for (DevBuf* b : {&ctx->keys_in, &ctx->vals_in, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->fbuf, &ctx->err, &ctx->sink,
+                       &ctx->stamps})
         b->release();
     if (ctx->ev0) hipEventDestroy(ctx->ev0);
     if (ctx->ev1) hipEventDestroy(ctx->ev1);
@@ -386,7 +393,7 @@ extern "C" int ibtk_le_markers_destroy(ibtk_le_markers m) {
     hipSetDevice(m->ctx->device);
     hipStreamSynchronize(m->ctx->stream);
     for (DevBuf* b : {&m->sorted_key, &m->sorted_l, &m->sorted_s, &m->sorted_X, &m->sorted_a, &m->plane_start, &m->indices,
-                      &m->xshift, &m->cand_cnt, &m->cand_off, &m->cand_idx})
+                      &m->xshift, &m->cand_cnt, &m->cand_off, &m->cand_idx, &m->last, &m->qdst})
         b->release();
     delete m;
     return IBTK_LE_OK;
@@ -429,6 +436,8 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     m->has_indices = indices_dev != nullptr;
     m->has_xshift = Xshift_dev != nullptr;
     m->cand_valid = false;
+    m->dedup_done = false;
+    m->has_dups = false;
     int rc = 0;
     const int B = geom->ndim == 3 ? BRICK3 : BRICK2;
     const int nplanes = cols ? cg.nbuckets : bg.nbricks * B;  // bucket starts: nplanes + 1
@@ -530,6 +539,38 @@ static int prepare(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const ibtk_le
     return IBTK_LE_OK;
 }
 
+// A list that names a marker more than once (LIndexSetData's ghost-box list holds
+// periodic images) writes V(:,s) from its last entry, as the Fortran's
+// sequential l-loop does.  Built once per binning, on the first interp after it
+// (two host syncs; identity lists skip it).
+static int build_dedup(ibtk_le_ctx ctx, ibtk_le_markers m) {
+    if (m->dedup_done) return IBTK_LE_OK;
+    m->dedup_done = true;
+    m->has_dups = false;
+    if (!m->has_indices || m->n <= 1) return IBTK_LE_OK;
+    const hipStream_t s = ctx->stream;
+    int rc;
+    if ((rc = ctx->counts.ensure(2 * sizeof(int)))) return rc;
+    int* dv = ctx->counts.as<int>();
+    HIP_TRY(hipMemsetAsync(dv, 0xff, sizeof(int), s));
+    HIP_TRY(hipMemsetAsync(dv + 1, 0, sizeof(int), s));
+    HIP_TRY(launch_max_index(m->indices.as<int>(), m->n, dv, s));
+    int mx = -1;
+    HIP_TRY(hipMemcpyAsync(&mx, dv, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (mx < 0) return fail(IBTK_LE_ERR_ARG, "negative marker index in the list");
+    if ((rc = m->last.ensure(sizeof(int) * ((size_t)mx + 1)))) return rc;
+    if ((rc = m->qdst.ensure(sizeof(int) * (size_t)m->n))) return rc;
+    HIP_TRY(hipMemsetAsync(m->last.p, 0xff, sizeof(int) * ((size_t)mx + 1), s));
+    HIP_TRY(launch_dedup(m->indices.as<int>(), m->sorted_l.as<int>(), m->sorted_s.as<int>(), m->n, m->last.as<int>(),
+                         m->qdst.as<int>(), dv + 1, s));
+    int ndup = 0;
+    HIP_TRY(hipMemcpyAsync(&ndup, dv + 1, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    m->has_dups = ndup > 0;
+    return IBTK_LE_OK;
+}
+
 int ibtk_le::interp_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis, const void* geomv,
                          const double* const* q_dev, int q_depth, double* Q_dev, int Q_depth, const double* X_dev,
                          bool check_ghosts) {
@@ -548,6 +589,8 @@ int ibtk_le::interp_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cen
     if (m->n == 0) return IBTK_LE_OK;  // LEInteractor.cpp:2427
     if (!Q_dev || !q_dev) return fail(IBTK_LE_ERR_ARG, "null Q or q");
     if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    if (int rc = build_dedup(ctx, m)) return rc;
+    p.qdst = m->has_dups ? m->qdst.as<int>() : nullptr;
     p.Qout = Q_dev;
     p.Q_depth = Q_depth;
     ctx->ev_valid = false;
@@ -638,11 +681,9 @@ static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cente
         const int cnt = std::min(MAXC, nc - first);
         if (int rc = make_comps(geom, centering, axis, q_dev, q_depth, Q_depth, first, cnt, p)) return rc;
         const bool t = ctx->timing && first == 0;
-        const char* dbg = getenv("IBTK_LE_STAMPS");
-        const char* dmode = getenv("IBTK_LE_DBG");  // diagnostics: variants of the add loop
-        p.dbg = dmode ? atoi(dmode) : 0;
+        p.dbg = ctx->dbg;  // diagnostics: variants of the add loop
         const size_t nst = (size_t)m->cg.ncol * m->nseg * cnt * 8;
-        if (geom->ndim == 3 && dbg && dbg[0] == '1') {
+        if (geom->ndim == 3 && ctx->stamps_on) {
             if (int rc = ctx->stamps.ensure(nst * sizeof(unsigned long long))) return rc;
             HIP_TRY(hipMemsetAsync(ctx->stamps.p, 0, nst * sizeof(unsigned long long), ctx->stream));
             p.stamps = ctx->stamps.as<unsigned long long>();

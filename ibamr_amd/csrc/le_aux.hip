@@ -319,6 +319,46 @@ hipError_t launch_image_write(const ImageDesc& d, const double* X, int n, const 
 }
 
 // ---------------------------------------------------------------------------
+// interpolation lists that name a marker more than once (the ghost-box list of
+// LIndexSetData holds a marker and its periodic images): the Fortran l-loop
+// overwrites V(:,s) entry after entry, so the LAST list entry of s wins
+// (lagrangian_interaction3d.f.m4:1366-1382).  qdst[e] = s for that entry, -1
+// for the earlier ones (their sums go to the sink).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(BLOCK) void k_max_index(const int* idx, int n, int* out) {
+    const int l = blockIdx.x * BLOCK + threadIdx.x;
+    int v = l < n ? idx[l] : -1;
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    if ((threadIdx.x & 63) == 0 && v >= 0) atomicMax(out, v);
+}
+__global__ __launch_bounds__(BLOCK) void k_last_entry(const int* idx, int n, int* last) {
+    const int l = blockIdx.x * BLOCK + threadIdx.x;
+    if (l < n) atomicMax(last + idx[l], l);
+}
+__global__ __launch_bounds__(BLOCK) void k_qdst(const int* sorted_l, const int* sorted_s, const int* last, int n,
+                                                int* qdst, int* ndup) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= n) return;
+    const int s = sorted_s[e];
+    const bool keep = last[s] == sorted_l[e];
+    qdst[e] = keep ? s : -1;
+    if (!keep) atomicAdd(ndup, 1);
+}
+hipError_t launch_max_index(const int* idx, int n, int* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_max_index, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, idx, n, out);
+    return hipGetLastError();
+}
+hipError_t launch_dedup(const int* indices, const int* sorted_l, const int* sorted_s, int n, int* last, int* qdst,
+                        int* ndup, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const dim3 g((n + BLOCK - 1) / BLOCK);
+    hipLaunchKernelGGL(k_last_entry, g, dim3(BLOCK), 0, s, indices, n, last);
+    hipLaunchKernelGGL(k_qdst, g, dim3(BLOCK), 0, s, sorted_l, sorted_s, last, n, qdst, ndup);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // marker position update (IBMethod::eulerStep / midpointStep / trapezoidalStep,
 // IBMethod.cpp:619-681): PETSc VecWAXPY w = alpha x + y and VecAXPY y += alpha x,
 // each a rounded multiply then a rounded add (built with -ffp-contract=off, so

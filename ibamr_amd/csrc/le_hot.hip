@@ -1,29 +1,29 @@
-// le_hot.hip -- the hot path on CDNA4 (gfx950): marker binning, interpolation
-// and spreading.  Replaces the l-loops of
-// ibtk/src/lagrangian/fortran/lagrangian_interaction{2,3}d.f.m4.
+// le_hot.hip -- the 2-D hot path on CDNA4 (gfx950): brick binning,
+// interpolation and spreading.  Replaces the l-loops of
+// ibtk/src/lagrangian/fortran/lagrangian_interaction2d.f.m4.  (The 3-D path is
+// le_sweep.hip's column sweeps; the templates below are written for NDIM = 2
+// or 3 but only NDIM = 2 is instantiated -- see the dispatchers at the end.)
 //
-// Work decomposition (DESIGN.md §Kernels):
-//  * bin: key = brick id (tiled, le_bricks.h) << 9 | cell-in-brick of the
-//    marker's cell-frame stencil anchor; stable device radix sort; brick CSR;
-//    then one coalescing pass writes the sorted marker index and the sorted
-//    shifted position X(s)+Xshift(l), so the interp/spread kernels read their
-//    markers contiguously.
+// Work decomposition (DESIGN.md section 4):
+//  * bin: key = brick id (tiled, le_bricks.h) << 8 | cell-in-brick of the
+//    marker's cell-frame stencil anchor (16^2-cell bricks); stable device radix
+//    sort; brick CSR; then one coalescing pass writes the sorted marker index
+//    and the sorted shifted position X(s)+Xshift(l), so the interp/spread
+//    kernels read their markers contiguously.
 //  * interp: one workgroup item = (brick, component).  The union stencil region
-//    of the brick's markers, (8+HI-LO)^3 points of that component, is loaded
-//    from HBM with every load of a thread in flight at once and staged in LDS
-//    (13.8 KB for IB_4, so ~11 items are resident per CU); one thread per marker
-//    then sums its W^3 stencil from LDS in the Fortran loop order, so the result
-//    is bitwise the oracle's.
-//  * spread: one workgroup item = (super-brick of 16^3 cells, component).  The
-//    workgroup loads u_old of its 4096 points into LDS, walks the sorted entries
-//    of the 4x4x4 surrounding bricks in canonical (sorted) order, keeps those
-//    whose stencil can reach the super-brick (parallel filter + ordered block
+//    of the brick's markers is loaded from HBM with every load of a thread in
+//    flight at once and staged in LDS; one thread per marker then sums its W^2
+//    stencil from LDS in the Fortran loop order, so the result is bitwise the
+//    oracle's.
+//  * spread: one workgroup item = (super-brick of 2x2 bricks, component).  The
+//    workgroup loads u_old of its points into LDS, walks the sorted entries of
+//    the surrounding bricks in canonical (sorted) order, keeps those whose
+//    stencil can reach the super-brick (parallel filter + ordered block
 //    compaction), computes their 1-D weights in parallel, and one wave then adds
 //    candidate after candidate with lane = stencil point (ds_add_f64 into LDS).
 //    Each grid point therefore receives its contributions in list order exactly
 //    like the Fortran's sequential l-loop: no global atomics, deterministic,
-//    bitwise the oracle's on the same list.  16^3 super-bricks keep the halo
-//    over-processing at (20/16)^3 = 1.95x the owned markers for IB_4.
+//    bitwise the oracle's on the same list.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -335,7 +335,8 @@ __global__ __launch_bounds__(BLOCK) void k_interp(Params p) {
                         }
                     }
                 }
-                p.Qout[(int64_t)p.Q_depth * s + cd.qcomp] = acc;
+                const int sq = p.qdst ? p.qdst[e] : s;
+                if (sq >= 0) p.Qout[(int64_t)p.Q_depth * sq + cd.qcomp] = acc;
             }
         }
     }
@@ -345,7 +346,8 @@ __global__ __launch_bounds__(BLOCK) void k_interp(Params p) {
 __global__ __launch_bounds__(BLOCK) void k_interp_outside(Params p, int n) {
     const int first = p.plane_start[p.bg.nbricks * (p.bg.ndim == 3 ? BRICK3 : BRICK2)];
     for (int e = first + blockIdx.x * BLOCK + threadIdx.x; e < n; e += gridDim.x * BLOCK) {
-        const int s = p.sorted_s[e];
+        const int s = p.qdst ? p.qdst[e] : p.sorted_s[e];
+        if (s < 0) continue;
         for (int c = 0; c < p.ncomp; ++c) p.Qout[(int64_t)p.Q_depth * s + p.comp[c].qcomp] = 0.0;
     }
 }
@@ -431,7 +433,8 @@ __global__ __launch_bounds__(BLOCK) void k_interp_direct(Params p, int n) {
                 }
             }
         }
-        p.Qout[(int64_t)p.Q_depth * s + cd.qcomp] = acc;
+        const int sq = p.qdst ? p.qdst[e] : s;
+        if (sq >= 0) p.Qout[(int64_t)p.Q_depth * sq + cd.qcomp] = acc;
     }
 }
 

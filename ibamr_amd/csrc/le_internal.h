@@ -125,6 +125,9 @@ struct Params {
     const double* ds;          // spread: per-marker weight (nullptr: none); sorted_F = Qin * ds
     int nsorted;               // list length
     double* Qout;              // interp: marker values
+    const int* qdst;           // interp: per sorted entry, the marker whose Q it writes, or -1 when a later
+                               // list entry of the same marker writes it (the Fortran's sequential l-loop
+                               // overwrites: the last occurrence wins); nullptr = sorted_s (no duplicates)
     int* err;                  // device error word (0 = fine)
     double* sink;              // 64 doubles: the store target of masked-off lanes (branch-free stores)
     unsigned long long* stamps;  // diagnostic phase clocks (nullptr: off)
@@ -183,6 +186,10 @@ struct ImageDesc {
 hipError_t launch_cell_keys(const ImageDesc& d, const double* X, int n, unsigned ncells, unsigned* keys, int* vals,
                             int* inside, hipStream_t s);
 hipError_t launch_image_count(const ImageDesc& d, const double* X, int n, int* counts, hipStream_t s);
+// interp with duplicate list entries: qdst[e] (see Params::qdst); *ndup (device) counts the -1s
+hipError_t launch_max_index(const int* idx, int n, int* out, hipStream_t s);
+hipError_t launch_dedup(const int* indices, const int* sorted_l, const int* sorted_s, int n, int* last, int* qdst,
+                        int* ndup, hipStream_t s);
 hipError_t launch_image_write(const ImageDesc& d, const double* X, int n, const int* offsets, int* idx,
                               double* xshift, int capacity, hipStream_t s);
 

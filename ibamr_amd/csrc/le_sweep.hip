@@ -423,6 +423,7 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     };
     struct Mk {
         int s;
+        int q;  // the marker whose Q this entry writes (-1: a later duplicate entry does)
         double X[3];
     };
     // LDS barrier of the two waves; global loads in flight stay in flight
@@ -474,6 +475,7 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
         am = a + k;
         e = min(e, nlast);
         m.s = p.sorted_s[e];
+        m.q = p.qdst ? p.qdst[e] : m.s;
         const double* xs = p.sorted_X + (int64_t)3 * e;
         m.X[0] = xs[0];
         m.X[1] = xs[1];
@@ -487,7 +489,7 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
         const bool act = lane < n;
         double acc = 0.0;
         if (act) acc = interp_marker<K>(p, cd, ring, gx0, gy0, am, m.X, m.s);
-        double* dst = act ? p.Qout + ((int64_t)p.Q_depth * m.s + cd.qcomp) : p.sink + lane;
+        double* dst = (act && m.q >= 0) ? p.Qout + ((int64_t)p.Q_depth * m.q + cd.qcomp) : p.sink + lane;
         *dst = acc;
     };
     double pv[NPT];
@@ -531,7 +533,8 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
 __global__ __launch_bounds__(BLOCK) void k_interp_outside_col(Params p, int n) {
     const int first = p.plane_start[p.cg.nbuckets];
     for (int e = first + blockIdx.x * BLOCK + threadIdx.x; e < n; e += gridDim.x * BLOCK) {
-        const int s = p.sorted_s[e];
+        const int s = p.qdst ? p.qdst[e] : p.sorted_s[e];
+        if (s < 0) continue;
         for (int c = 0; c < p.ncomp; ++c) p.Qout[(int64_t)p.Q_depth * s + p.comp[c].qcomp] = 0.0;
     }
 }

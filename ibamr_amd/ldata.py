@@ -50,6 +50,7 @@ class LDataLevel:
     periodic: Sequence[int] = (1, 1, 1)
     bc: Optional[RobinBc] = None
     _bins: Optional[le.Markers] = field(default=None, init=False, repr=False)
+    _old: Optional[list] = field(default=None, init=False, repr=False)
 
     def __post_init__(self):
         nd = self.geom.ndim
@@ -80,7 +81,13 @@ class LDataLevel:
         """f += S F (folded), LDataManager::spread (LDataManager.cpp:555-675)."""
         if self._bins is None:
             raise RuntimeError("bin() the markers first")
-        old = [t.clone() for t in f]  # swapData with the cloned index (:590-592)
+        # swapData with the cloned index (:590-592): the copy lives in scratch
+        # arrays allocated once per level, not per call
+        if self._old is None or any(o.shape != t.shape or o.device != t.device for o, t in zip(self._old, f)):
+            self._old = [torch.empty_like(t) for t in f]
+        old = self._old
+        for o, t in zip(old, f):
+            o.copy_(t)
         for t in f:
             t.zero_()  # setToScalar(0, interior_only=false) (:593)
         le.spread(self.ctx, self._bins, self.kernel, "side", self.geom, f, F, X, ds=ds)

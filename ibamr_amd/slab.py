@@ -111,16 +111,16 @@ class SlabExchange:
         # (the multi-rank rehearsal on one GPU; RCCL sends device memory directly)
         stage = dist.get_backend(self.group) == "gloo"
         ops, back = [], []
-        for t, peer, tag in sends:
+        for t, peer in sends:
             if stage and t.is_cuda:
                 t = t.cpu()
-            ops.append(dist.P2POp(dist.isend, t, peer, group=self.group, tag=tag))
-        for t, peer, tag in recvs:
+            ops.append(dist.P2POp(dist.isend, t, peer, group=self.group))
+        for t, peer in recvs:
             if stage and t.is_cuda:
                 h = torch.empty(t.shape, dtype=t.dtype)
                 back.append((h, t))
                 t = h
-            ops.append(dist.P2POp(dist.irecv, t, peer, group=self.group, tag=tag))
+            ops.append(dist.P2POp(dist.irecv, t, peer, group=self.group))
         if ops:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
@@ -140,11 +140,14 @@ class SlabExchange:
             b0, b1 = b["bot_int"]
             lo0, lo1 = b["lo_ghost"]
             hi0, hi1 = b["hi_ghost"]
-            # tags pair each send with its receive (gloo matches by tag; RCCL by order)
-            sends.append((a[t0:t1], s.up, 8 * c + 0))      # my top planes -> up's lower ghosts
-            sends.append((a[b0:b1], s.down, 8 * c + 1))    # my bottom planes -> down's upper ghosts
-            recvs.append((a[lo0:lo1], s.down, 8 * c + 0))
-            recvs.append((a[hi0:hi1], s.up, 8 * c + 1))
+            # RCCL matches a peer's sends and receives in issue order and ignores
+            # tags, so every exchange posts its receives from a peer in the order
+            # that peer posts the matching sends (with P = 2, up == down), and
+            # uses one tag, so gloo matches the same way
+            sends.append((a[t0:t1], s.up))      # my top planes -> up's lower ghosts
+            sends.append((a[b0:b1], s.down))    # my bottom planes -> down's upper ghosts
+            recvs.append((a[lo0:lo1], s.down))  # down's top planes (its first send)
+            recvs.append((a[hi0:hi1], s.up))    # up's bottom planes (its second send)
         self._p2p(sends, recvs)
 
     def ghost_sum(self):
@@ -158,10 +161,13 @@ class SlabExchange:
             lo0, lo1 = b["lo_ghost"]
             hi0, hi1 = b["hi_ghost"]
             rlo, rhi = self.bufs[c]
-            sends.append((a[lo0:lo1], s.down, 8 * c + 2))
-            sends.append((a[hi0:hi1], s.up, 8 * c + 3))
-            recvs.append((rhi, s.down, 8 * c + 3))   # down's upper ghosts land on my bottom planes
-            recvs.append((rlo, s.up, 8 * c + 2))     # up's lower ghosts land on my top planes
+            sends.append((a[lo0:lo1], s.down))  # first send
+            sends.append((a[hi0:hi1], s.up))    # second send
+            # receives in the peers' send order: up's lower ghosts (its first send,
+            # they land on my top planes), then down's upper ghosts (its second
+            # send, my bottom planes)
+            recvs.append((rlo, s.up))
+            recvs.append((rhi, s.down))
         self._p2p(sends, recvs)
         for c, a in enumerate(self.arrays):
             b = s.blocks(c)

@@ -123,6 +123,9 @@ int ibtk_le_markers_order(ibtk_le_markers m, const int** order_dev);
  * Q_dev is the marker array in LData layout: AoS, Q_depth values per marker
  * (SIDE/EDGE: Q_depth == NDIM).  X_dev: AoS NDIM positions per marker.
  * The marker list is the one last binned into `m` (same kernel and geometry).
+ * A list may name a marker several times (LIndexSetData's ghost-box list holds
+ * its periodic images): spread adds every entry; interp writes Q(:, s) from the
+ * LAST entry naming s, as the Fortran's sequential l-loop overwrites it.
  *
  * interp:  Q(d, s) = sum_i w_i(X(s)+Xshift) q(i, d)   for every listed s
  *          (LEInteractor.cpp:970-1055 / lagrangian_<k>_interp3d, f.m4:1258-1385)

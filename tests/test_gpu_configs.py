@@ -1,0 +1,373 @@
+"""GPU: every BASELINE.json configuration against the oracle (or, at sizes the
+oracle cannot finish, through size-independent properties), and the z-slab
+decomposition at N = 2, 4, 8 ranks against one rank.
+
+* cfg1 -- examples/IB/explicit/ex1: 2-D 64^2 periodic grid, ghost 3, IB_4, the
+  304-marker ellipse of tests/golden/vertex/curve2d_64.vertex (a data file of
+  the reference's example deck).  LDataManager's two entry points on one patch:
+  interp over the interior list, spread over the ghost-box list with the
+  periodic images (LIndexSetData::cacheLocalIndices), then the periodic fold.
+* cfg2 -- 128^3, 1e5 markers on a sphere of radius 0.35 (Fibonacci lattice),
+  IB_4.  Interp bitwise, spread <= 1e-12, in both the identity-list form and
+  the ghost-box-list form.  128^3 spans several sweep columns and z-segments,
+  so the multi-column x multi-segment x XCD item mapping is checked against the
+  oracle point by point.
+* cfg3 -- BSPLINE_4 (and IB_6) at the full 512^3 / 1e7 size: properties in
+  test_gpu_fullsize.py; here a reduced 96^3 uniform case against the oracle.
+* cfg5 -- clustered sheets and fibre bundles (80 % of the markers in 4 sheets
+  one cell thick, 20 % in 2 bundles): a reduced 128^3 / 2e5 case against the
+  oracle (hundreds of markers per sweep bucket: the dense-chunk paths), and the
+  full 512^3 / 1e7 case through the properties.
+* cfg4 -- the z-slab split: N ranks share cuda:0 (gloo for the exchanges,
+  RCCL's send/recv matching order), interp after the halo fill must equal one
+  rank's bit for bit, spread + ghost sum within 1e-12 of one rank's, also after
+  a moving step (position update + marker migration + re-bin).
+
+Tolerances: interp <= 1e-13 relative (bitwise in fact), spread <= 1e-12
+relative (BASELINE.json north_star).
+"""
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+INTERP_TOL = 1e-13
+SPREAD_TOL = 1e-12
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "vertex")
+
+
+@pytest.fixture(scope="module")
+def le():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ibamr_amd import le as _le
+    return _le
+
+
+@pytest.fixture(scope="module")
+def ctx(le):
+    return le.Context(0)
+
+
+def rel_err(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    if not a.size:
+        return 0.0
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+def sphere_markers(M, r=0.35, c=0.5):
+    i = np.arange(M) + 0.5
+    phi = np.arccos(1 - 2 * i / M)
+    th = math.pi * (1 + 5 ** 0.5) * i
+    return np.stack([c + r * np.cos(th) * np.sin(phi), c + r * np.sin(th) * np.sin(phi), c + r * np.cos(phi)], 1)
+
+
+def clustered_markers(M, N, rng):
+    """4 sheets one cell thick (z = 0.2, 0.4, 0.6, 0.8) + 2 fibre bundles of radius
+    0.02 along z (bench.py's cfg5 generator, numpy form)."""
+    n_sheet = int(M * 0.8) // 4
+    n_fib = (M - 4 * n_sheet) // 2
+    h = 1.0 / N
+    parts = []
+    for z in (0.2, 0.4, 0.6, 0.8):
+        s = rng.uniform(0, 1, (n_sheet, 3))
+        s[:, 2] = z + (s[:, 2] - 0.5) * h
+        parts.append(s)
+    for cx, cy in ((0.3, 0.3), (0.7, 0.6)):
+        f = rng.uniform(0, 1, (n_fib, 3))
+        r = 0.02 * np.sqrt(f[:, 0])
+        t = 2 * math.pi * f[:, 1]
+        f[:, 0] = cx + r * np.cos(t)
+        f[:, 1] = cy + r * np.sin(t)
+        parts.append(f)
+    return np.concatenate(parts)
+
+
+def _identity_case(le, ctx, oracle, geom, kernel, Xn, seed, fill=True):
+    """interp (bitwise) and spread (<= 1e-12) of the identity list against the oracle."""
+    rng = np.random.default_rng(seed)
+    M, nd = Xn.shape
+    Fn = rng.uniform(-1, 1, (M, nd))
+    u = geom.alloc("side")
+    for a in u:
+        a.copy_(torch.from_numpy(rng.uniform(-1, 1, tuple(a.shape))))
+    if fill:
+        le.fill_periodic_ghosts(ctx, geom, "side", u)
+    u0 = [a.cpu().numpy().copy() for a in u]
+    X, F = torch.from_numpy(Xn).cuda(), torch.from_numpy(Fn).cuda()
+    U = torch.full((M, nd), np.nan, dtype=torch.float64, device="cuda:0")
+    m = le.Markers(ctx).bin(geom, kernel, X)
+    le.interp(ctx, m, kernel, "side", geom, u, U, X)
+    q = geom.alloc("side")
+    le.spread(ctx, m, kernel, "side", geom, q, F, X)
+    ctx.synchronize()
+    idx = np.arange(M, dtype=np.int32)
+    xs = np.zeros((M, nd))
+    Uo = np.zeros((M, nd))
+    oracle.side_interp(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, u0, idx, xs, Xn, Uo)
+    Ug = U.cpu().numpy()
+    assert rel_err(Ug, Uo) <= INTERP_TOL
+    assert np.array_equal(Ug, Uo), "interp is expected bitwise (Fortran summation order)"
+    order = m.order().cpu().numpy()
+    uo = [np.zeros(tuple(a.shape)) for a in q]
+    oracle.side_spread(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, uo, idx[order], xs, Xn, Fn)
+    for a in range(nd):
+        assert rel_err(q[a].cpu().numpy(), uo[a]) <= SPREAD_TOL, f"spread comp {a}"
+    return m
+
+
+def _ldata_case(le, ctx, oracle, geom, kernel, Xn, seed):
+    """LDataManager's pipeline on one periodic patch: interp of the interior
+    markers after the ghost fill; spread of the ghost-box list (markers plus
+    their periodic images, LIndexSetData::cacheLocalIndices) then the fold of the
+    duplicated periodic faces.  Against the oracle running the same list."""
+    rng = np.random.default_rng(seed)
+    M, nd = Xn.shape
+    Fn = rng.standard_normal((M, nd))
+    g = geom.gcw[0]
+    xu = [geom.x_lower[d] + (geom.iupper[d] - geom.ilower[d] + 1) * geom.dx[d] for d in range(nd)]
+    idx, xs, _ = oracle.periodic_index_list(Xn, geom.x_lower, xu, geom.dx, geom.ilower, geom.iupper, g)
+    u = geom.alloc("side")
+    for a in u:
+        a.copy_(torch.from_numpy(rng.standard_normal(tuple(a.shape))))
+    le.fill_periodic_ghosts(ctx, geom, "side", u)
+    u0 = [a.cpu().numpy().copy() for a in u]
+    X, F = torch.from_numpy(Xn).cuda(), torch.from_numpy(Fn).cuda()
+    # interp: the interior list (LDataManager.cpp:763-807 passes idx_data->getBox())
+    U = torch.zeros((M, nd), dtype=torch.float64, device="cuda:0")
+    mi = le.Markers(ctx).bin(geom, kernel, X)
+    le.interp(ctx, mi, kernel, "side", geom, u, U, X)
+    # spread: the ghost-box list (LDataManager.cpp:634-654)
+    ms = le.Markers(ctx).bin(geom, kernel, X, torch.from_numpy(idx).cuda(), torch.from_numpy(xs).cuda())
+    q = geom.alloc("side")
+    le.spread(ctx, ms, kernel, "side", geom, q, F, X)
+    # the ghost-box list also interpolates (each marker from its LAST entry)
+    U2 = torch.zeros((M, nd), dtype=torch.float64, device="cuda:0")
+    le.interp(ctx, ms, kernel, "side", geom, u, U2, X)
+    ctx.synchronize()
+    Uo = np.zeros((M, nd))
+    oracle.side_interp(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, u0,
+                       np.arange(M, dtype=np.int32), np.zeros((M, nd)), Xn, Uo)
+    assert np.array_equal(U.cpu().numpy(), Uo)
+    U2o = np.zeros((M, nd))
+    oracle.side_interp(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, u0, idx, xs, Xn, U2o)
+    assert np.array_equal(U2.cpu().numpy(), U2o), "duplicate list entries: the last one must win"
+    order = ms.order().cpu().numpy()
+    uo = [np.zeros(tuple(a.shape)) for a in q]
+    oracle.side_spread(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, uo, idx[order], xs[order],
+                       Xn, Fn)
+    for a in range(nd):
+        assert rel_err(q[a].cpu().numpy(), uo[a]) <= SPREAD_TOL, f"spread comp {a}"
+    # conservation over the unique points of the ghost-box spread: every marker
+    # once (its own cell) -- the images land in ghost cells only
+    h = float(np.prod(geom.dx))
+    for a in range(nd):
+        sl = tuple(slice(g, g + geom.iupper[d] - geom.ilower[d] + 1) for d in reversed(range(nd)))
+        tot = q[a].cpu().numpy()[sl].sum() * h
+        assert abs(tot - Fn[:, a].sum()) <= 1e-11 * np.abs(Fn[:, a]).sum()
+
+
+# ---------------------------------------------------------------------------- cfg1
+def test_cfg1_ex1_ellipse_2d(le, ctx, oracle):
+    from ibamr_amd import io
+    Xn = io.read_vertex(os.path.join(GOLD, "curve2d_64.vertex"), ndim=2)
+    assert Xn.shape == (304, 2)
+    geom = le.Geometry.periodic_unit([64, 64], 3)
+    _identity_case(le, ctx, oracle, geom, "IB_4", Xn, seed=1)
+    _ldata_case(le, ctx, oracle, geom, "IB_4", Xn, seed=2)
+
+
+def test_cfg1_regenerated_ellipse_matches_deck():
+    """the ellipse of examples/IB/explicit/ex1/generate_curve2d.m,
+    alpha = 0.25^2/0.35, beta = 0.35, centre 0.5, theta_l = 2 pi l / 304."""
+    from ibamr_amd import io
+    Xn = io.read_vertex(os.path.join(GOLD, "curve2d_64.vertex"), ndim=2)
+    th = 2 * np.pi * np.arange(304) / 304
+    Xr = np.stack([0.5 + 0.25 ** 2 / 0.35 * np.cos(th), 0.5 + 0.35 * np.sin(th)], 1)
+    assert np.abs(Xr - Xn).max() < 1e-14
+
+
+# ---------------------------------------------------------------------------- cfg2
+def test_cfg2_sphere_128(le, ctx, oracle):
+    geom = le.Geometry.periodic_unit([128] * 3, 3)
+    Xn = sphere_markers(100_000)
+    m = _identity_case(le, ctx, oracle, geom, "IB_4", Xn, seed=3)
+    assert m.count() == 100_000
+    _ldata_case(le, ctx, oracle, geom, "IB_4", Xn, seed=4)
+
+
+# ---------------------------------------------------------------------------- cfg3 (reduced)
+@pytest.mark.parametrize("kernel", ["BSPLINE_4", "IB_6"])
+def test_cfg3_uniform_reduced(le, ctx, oracle, kernel):
+    g = oracle.min_ghost_width(kernel)
+    geom = le.Geometry.periodic_unit([96] * 3, g)
+    rng = np.random.default_rng(1234)
+    Xn = rng.uniform(0, 1, (70_000, 3))  # the cfg3 density, 1e7 / 512^3
+    _identity_case(le, ctx, oracle, geom, kernel, Xn, seed=5)
+
+
+# ---------------------------------------------------------------------------- cfg5 (reduced)
+@pytest.mark.parametrize("kernel", ["IB_4", "IB_6"])
+def test_cfg5_clustered_reduced(le, ctx, oracle, kernel):
+    g = oracle.min_ghost_width(kernel)
+    N = 128
+    geom = le.Geometry.periodic_unit([N] * 3, g)
+    rng = np.random.default_rng(77)
+    Xn = clustered_markers(200_000, N, rng)
+    _identity_case(le, ctx, oracle, geom, kernel, Xn, seed=6)
+
+
+@pytest.mark.parametrize("kernel", ["IB_4"])
+def test_cfg5_clustered_fullsize_properties(le, ctx, kernel):
+    """512^3, 1e7 clustered markers: conservation, adjointness, constant field,
+    bit-stable spread (the oracle would take minutes)."""
+    N, M = 512, 10_000_000
+    g = 3
+    geom = le.Geometry.periodic_unit([N] * 3, g)
+    h3 = geom.dx[0] * geom.dx[1] * geom.dx[2]
+    rng = np.random.default_rng(1234)
+    X = torch.from_numpy(clustered_markers(M, N, rng)).cuda()
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    F = torch.rand((X.shape[0], 3), dtype=torch.float64, device="cuda", generator=gen) * 2 - 1
+    m = le.Markers(ctx).bin(geom, kernel, X)
+    f = geom.alloc("side")
+    le.spread(ctx, m, kernel, "side", geom, f, F, X)
+    le.fold_periodic_ghosts(ctx, geom, "side", f)
+    f2 = geom.alloc("side")
+    le.spread(ctx, m, kernel, "side", geom, f2, F, X)
+    le.fold_periodic_ghosts(ctx, geom, "side", f2)
+    ctx.synchronize()
+    for a in range(3):
+        assert torch.equal(f[a], f2[a])
+    del f2
+    un = lambda t: t[g:g + N, g:g + N, g:g + N]
+    for a in range(3):
+        tot = un(f[a]).sum().item() * h3
+        assert abs(tot - F[:, a].sum().item()) <= 1e-10 * F[:, a].abs().sum().item()
+    u = geom.alloc("side")
+    for t in u:
+        t.uniform_(-1, 1, generator=gen)
+    le.fill_periodic_ghosts(ctx, geom, "side", u)
+    Q = torch.zeros_like(F)
+    le.interp(ctx, m, kernel, "side", geom, u, Q, X)
+    ctx.synchronize()
+    lhs = (Q * F).sum().item()
+    rhs = h3 * sum((un(u[a]) * un(f[a])).sum().item() for a in range(3))
+    assert abs(lhs - rhs) <= 1e-10 * (Q.abs() * F.abs()).sum().item()
+
+
+# ---------------------------------------------------------------------------- cfg4 slabs
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _global_problem(N, M, seed=1234):
+    rng = np.random.default_rng(seed)
+    X = rng.uniform(0, 1, (M, 3))
+    F = rng.uniform(-1, 1, (M, 3))
+    G = [rng.uniform(-1, 1, (N, N, N)) for _ in range(3)]  # unique side values, (z, y, x)
+    return X, F, G
+
+
+def _fill_interior(a, G, g, z0, nz, N):
+    a[g:g + nz, g:g + N, g:g + N] = torch.from_numpy(G[z0:z0 + nz])
+
+
+def _slab_run(le, ctx, N, M, world, rank, kernel="IB_4", move=False):
+    """One rank's interp + spread on its slab; returns (ids, U, f interior planes)."""
+    from ibamr_amd.slab import Slab, SlabExchange, migrate
+    g = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
+    slab = Slab([N, N, N], world, rank, g)
+    geom = slab.geometry()
+    Xg, Fg, G = _global_problem(N, M)
+    z = Xg[:, 2]
+    mine = np.nonzero((z >= slab.z0 * slab.dx[2]) & (z < slab.z1 * slab.dx[2]))[0]
+    X = torch.from_numpy(Xg[mine]).cuda()
+    F = torch.from_numpy(Fg[mine]).cuda()
+    ids = torch.from_numpy(mine.astype(np.int64)).cuda()
+    u = geom.alloc("side")
+    for c in range(3):
+        _fill_interior(u[c], G[c], g, slab.z0, slab.nz, N)
+    SlabExchange(slab, u, ctx).halo_fill()
+    m = le.Markers(ctx).bin(geom, kernel, X)
+    U = torch.zeros_like(X)
+    le.interp(ctx, m, kernel, "side", geom, u, U, X)
+    if move:
+        le.position_update(ctx, "euler", 0.5 * slab.dx[0], X, U, out=X)
+        X, (F, ids) = migrate(slab, X, [F, ids], cell_order=False)
+        m = le.Markers(ctx).bin(geom, kernel, X)
+    f = geom.alloc("side")
+    le.zero_ghosts(ctx, geom, "side", f)
+    le.spread(ctx, m, kernel, "side", geom, f, F, X)
+    SlabExchange(slab, f, ctx).ghost_sum()
+    ctx.synchronize()
+    fin = [t[g:g + slab.nz, g:g + N, g:g + N].cpu().numpy().copy() for t in f]
+    return mine, U.cpu().numpy(), fin, slab.z0, slab.nz
+
+
+def _slab_worker(rank, world, port, N, M, move, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from ibamr_amd import le
+        ctx = le.Context(0)
+        ids, U, fin, z0, nz = _slab_run(le, ctx, N, M, world, rank, move=move)
+        out_q.put((rank, "ok", ids, U, fin, z0, nz))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        out_q.put((rank, traceback.format_exc(), None, None, None, 0, 0))
+
+
+@pytest.mark.parametrize("world,move", [(2, False), (4, False), (8, False), (2, True), (4, True)])
+def test_cfg4_slab_split_matches_one_rank(le, ctx, world, move):
+    import torch.multiprocessing as mp
+    N, M = 64, 150_000
+    ref_ids, ref_U, ref_f, _, _ = _slab_run(le, ctx, N, M, 1, 0, move=move)
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_slab_worker, args=(r, world, port, N, M, move, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = []
+    for _ in range(world):
+        try:
+            res.append(q.get(timeout=240))
+        except Exception:
+            res.append((-1, "worker died: " + str([p.exitcode for p in procs]), None, None, None, 0, 0))
+            break
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    bad = [r for r in res if r[1] != "ok"]
+    assert not bad, bad[0][1]
+    # interp (before any move): every marker's U, bit for bit
+    U1 = np.empty_like(ref_U)
+    U1[ref_ids] = ref_U
+    seen = 0
+    for rank, _, ids, U, fin, z0, nz in res:
+        assert np.array_equal(U, U1[ids]), f"rank {rank}: interp differs from one rank"
+        seen += ids.size
+    assert seen == M
+    # spread + ghost sum: each rank's unique planes against one rank's
+    for rank, _, ids, U, fin, z0, nz in res:
+        for c in range(3):
+            assert rel_err(fin[c], ref_f[c][z0:z0 + nz]) <= SPREAD_TOL, f"rank {rank} comp {c}"

@@ -1,5 +1,6 @@
 """GPU: size-independent properties at BASELINE.json's full sizes (cfg4: 1024^3
-periodic staggered grid, 1e8 uniform markers, IB_4; cfg3: 512^3, 1e7, IB_6), where
+periodic staggered grid, 1e8 uniform markers, IB_4; cfg3: 512^3, 1e7, IB_6 and
+BSPLINE_4), where
 the oracle would take hours.
 
 * conservation: sum over the unique grid points of S F times h^3 equals sum F, per
@@ -36,7 +37,7 @@ def _unique(t, g, N):
 
 
 @pytest.mark.parametrize("N,M,kernel", [(256, 2_000_000, "IB_4"), (512, 10_000_000, "IB_6"),
-                                        (1024, 100_000_000, "IB_4")])
+                                        (512, 10_000_000, "BSPLINE_4"), (1024, 100_000_000, "IB_4")])
 def test_fullsize_properties(le, ctx, N, M, kernel):
     g = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
     geom = le.Geometry.periodic_unit([N] * 3, ghost=g)
