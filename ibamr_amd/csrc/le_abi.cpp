@@ -101,6 +101,7 @@ struct ibtk_le_ctx_s {
     DevBuf stamps;  // diagnostic phase clocks (IBTK_LE_STAMPS=1)
     bool stamps_on = false;  // IBTK_LE_STAMPS=1, read once at ctx_create
     int dbg = 0;             // IBTK_LE_DBG, read once at ctx_create
+    SweepTune tune;          // ibtk_le_ctx_tune (diagnostics)
     bool timing = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool ev_valid = false;
@@ -183,6 +184,20 @@ extern "C" int ibtk_le_ctx_synchronize(ibtk_le_ctx ctx) {
                     "device invariant failed (flag %d): a stencil left its staged region (1) or its bin bounds (2)",
                     flag);
     }
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_ctx_tune(ibtk_le_ctx ctx, const char* key, int value) {
+    if (!ctx || !key) return fail(IBTK_LE_ERR_ARG, "null argument");
+    SweepTune& t = ctx->tune;
+    const std::string k = key;
+    if (k == "interp_tile_w") t.itw = value;
+    else if (k == "interp_tile_h") t.ith = value;
+    else if (k == "spread_tile_w") t.stw = value;
+    else if (k == "spread_tile_h") t.sth = value;
+    else if (k == "component_fastest") t.cfast = value != 0;
+    else if (k == "seg_items") t.seg_items = value;
+    else return fail(IBTK_LE_ERR_ARG, "unknown tuning key %s", key);
     return IBTK_LE_OK;
 }
 
@@ -431,7 +446,7 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     m->ndim = geom->ndim;
     m->bg = bg;
     m->cg = cg;
-    if (cols) sweep_segments(cg, m->S, m->nseg);
+    if (cols) sweep_segments(cg, m->S, m->nseg, ctx->tune.seg_items);
     m->geom = *geom;
     m->has_indices = indices_dev != nullptr;
     m->has_xshift = Xshift_dev != nullptr;
@@ -534,6 +549,7 @@ static int prepare(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const ibtk_le
     p.plane_start = m->plane_start.as<int>();
     p.err = ctx->err.as<int>();
     p.sink = ctx->sink.as<double>();
+    p.tune = ctx->tune;
     p.K6 = ib6_K();
     p.h3 = geom->ndim == 3 ? (geom->dx[0] * geom->dx[1]) * geom->dx[2] : geom->dx[0] * geom->dx[1];
     return IBTK_LE_OK;

@@ -98,11 +98,21 @@ struct ColGeom {
     int nbuckets;   // nz * ncol * NBAND
 };
 
+// Diagnostic tuning of the 3-D sweeps (ibtk_le_ctx_tune); 0 = the default.
+struct SweepTune {
+    int itw = 0, ith = 0;  // interp column tile (item_decode)
+    int stw = 0, sth = 0;  // spread column tile
+    int cfast = 1;         // 1: component fastest in the item order
+    int seg_items = 0;     // sweep_segments' item target
+};
+
 struct Params {
     BinGeom bg;
     ColGeom cg;                // 3-D column binning
     const unsigned* sorted_a;  // sorted position -> packed key cell (x | y << 16), relative to cg.org
     int S, nseg;               // sweep segment length (planes) and segments per column
+    int tw, th, cfast;         // item order (item_decode): column tile, component fastest
+    SweepTune tune;
     int ncomp;
     CompDesc comp[MAXC];
     int Q_depth;
@@ -156,7 +166,7 @@ hipError_t launch_gather_col(int kernel, const Params& p, int n, int* sorted_s, 
                              const unsigned* sorted_key, int nbuckets, int* bucket_start, hipStream_t s);
 hipError_t launch_interp_sweep(int kernel, const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_spread_sweep(int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
-void sweep_segments(const ColGeom& cg, int& S, int& nseg);
+void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items);
 
 // Periodic helpers
 struct GhostDesc {

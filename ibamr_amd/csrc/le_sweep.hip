@@ -148,6 +148,34 @@ __device__ __forceinline__ int sweep_item(int nitems) {
     return it < nitems ? it : -1;
 }
 
+// Work item -> (component c, column col, segment seg).  Segment-major (with 8
+// segments each XCD sweeps one); within a segment either component fastest
+// (p.cfast) or component-major, and the columns in tiles of tw x th columns:
+// the items an XCD runs at once then cover a compact block of neighbouring
+// columns, whose shared halo rows and the cache lines straddling column edges
+// come from HBM once and from the XCD's L2 after.  tw = ncx, th = 1 is the
+// plain row-major column order.
+__device__ __forceinline__ void item_decode(const Params& p, int it, int& c, int& col, int& seg) {
+    const int ncol = p.cg.ncol, per_seg = ncol * p.ncomp;
+    seg = it / per_seg;
+    int k = it - seg * per_seg;
+    if (p.cfast) {
+        c = k % p.ncomp;
+        k /= p.ncomp;
+    } else {
+        c = k / ncol;
+        k -= c * ncol;
+    }
+    const int ncx = p.cg.ncx, ncy = p.cg.ncy, TW = p.tw, TH = p.th;
+    const int tr = k / (ncx * TH);  // tile row (TH column rows; the last may be short)
+    int k2 = k - tr * ncx * TH;
+    const int th = min(TH, ncy - tr * TH);
+    const int tc = k2 / (TW * th);  // tile in the row (TW columns; the last may be narrow)
+    k2 -= tc * TW * th;
+    const int tw = min(TW, ncx - tc * TW);
+    col = (tr * TH + k2 / tw) * ncx + tc * TW + k2 % tw;
+}
+
 // bucket index of (anchor plane a, column col, band)
 __device__ __forceinline__ int bucket(const Params& p, int a, int col, int band) {
     return (a * p.cg.ncol + col) * NBAND + band;
@@ -372,9 +400,8 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     const int nitems = p.cg.ncol * p.nseg * p.ncomp;
     const int it = sweep_item(nitems);
     if (it < 0) return;
-    const int c = it % p.ncomp;
-    const int cs = it / p.ncomp;
-    const int col = cs % p.cg.ncol, seg = cs / p.cg.ncol;
+    int c, col, seg;
+    item_decode(p, it, c, col, seg);
     const int a0 = seg * p.S, a1 = min(a0 + p.S, p.cg.nz);
     const int lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -715,9 +742,8 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     const int nitems = p.cg.ncol * p.nseg * p.ncomp;
     const int it = sweep_item(nitems);
     if (it < 0) return;
-    const int c = it % p.ncomp;
-    const int cs = it / p.ncomp;
-    const int col = cs % p.cg.ncol, seg = cs / p.cg.ncol;
+    int c, col, seg;
+    item_decode(p, it, c, col, seg);
     const int lane = lane_id();
     const int ncx = p.cg.ncx;
     const int cx = col % ncx, cy = col / ncx;
@@ -903,8 +929,8 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
 #ifndef IBTK_LE_SEG_ITEMS
 #define IBTK_LE_SEG_ITEMS 16384
 #endif
-void sweep_segments(const ColGeom& cg, int& S, int& nseg) {
-    long long want = IBTK_LE_SEG_ITEMS;
+void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items) {
+    long long want = seg_items > 0 ? seg_items : IBTK_LE_SEG_ITEMS;
     long long s = ((long long)cg.nz * cg.ncol + want - 1) / want;
     if (s < 32) s = 32;
     if (s > cg.nz) s = cg.nz;
@@ -939,8 +965,20 @@ hipError_t launch_gather_col_t(const Params& p, int n, int* ss, double* sx, cons
                        nbuckets, bs);
     return hipGetLastError();
 }
+// Column tiles of the item order (item_decode): tw x th columns, about the
+// columns an XCD's CUs hold at once (interp: 3 workgroups per CU, 96 per XCD;
+// spread: 6, 192).  Tuning overrides: ibtk_le_ctx_tune.
+static void set_tiles(Params& q, const SweepTune& t, bool spread) {
+    const int tw = spread ? t.stw : t.itw, th = spread ? t.sth : t.ith;
+    q.cfast = t.cfast;
+    q.tw = tw > 0 ? min(tw, q.cg.ncx) : q.cg.ncx;
+    q.th = tw > 0 ? max(th, 1) : 1;
+}
+
 template <int K>
-hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+hipError_t launch_interp_sweep_t(const Params& p0, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    Params p = p0;
+    set_tiles(p, p0.tune, false);
     if (ev0) (void)hipEventRecord(ev0, s);
     const long items = (long)p.cg.ncol * p.nseg * p.ncomp;
     if (items > 0) hipLaunchKernelGGL(k_interp_sweep<K>, dim3(grid8(items)), dim3(SW * IWAVES), 0, s, p);
@@ -963,7 +1001,9 @@ __global__ __launch_bounds__(BLOCK) void k_gather_F_col(Params p, int n, double*
     }
 }
 
-template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+template <int K> hipError_t launch_spread_sweep_t(const Params& p0, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    Params p = p0;
+    set_tiles(p, p0.tune, true);
     if (p.nsorted > 0)
         hipLaunchKernelGGL(k_gather_F_col, dim3((p.nsorted + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, p.nsorted,
                            const_cast<double*>(p.sorted_F));

@@ -112,6 +112,10 @@ class Context:
     def enable_timing(self, on=True):
         check(self.lib.ibtk_le_ctx_enable_timing(self.h, int(on)))
 
+    def tune(self, key: str, value: int):
+        """Diagnostic overrides of the 3-D sweeps' work-item order (ibtk_le_ctx_tune)."""
+        check(self.lib.ibtk_le_ctx_tune(self.h, key.encode(), int(value)))
+
     def last_kernel_ms(self) -> float:
         return float(self.lib.ibtk_le_ctx_last_kernel_ms(self.h))
 

@@ -19,9 +19,11 @@ decomposition at N = 2, 4, 8 ranks against one rank.
   oracle (hundreds of markers per sweep bucket: the dense-chunk paths), and the
   full 512^3 / 1e7 case through the properties.
 * cfg4 -- the z-slab split: N ranks share cuda:0 (gloo for the exchanges,
-  RCCL's send/recv matching order), interp after the halo fill must equal one
-  rank's bit for bit, spread + ghost sum within 1e-12 of one rank's, also after
-  a moving step (position update + marker migration + re-bin).
+  RCCL's send/recv matching order), interp after the halo fill within 1e-13 of
+  one rank's (bit for bit wherever the slab's x_lower leaves (X - x_lower)/dx
+  unrounded, i.e. almost everywhere),
+  spread + ghost sum within 1e-12 of one rank's, also after a moving step
+  (position update + marker migration + re-bin).
 
 Tolerances: interp <= 1e-13 relative (bitwise in fact), spread <= 1e-12
 relative (BASELINE.json north_star).
@@ -359,15 +361,22 @@ def test_cfg4_slab_split_matches_one_rank(le, ctx, world, move):
             p.kill()
     bad = [r for r in res if r[1] != "ok"]
     assert not bad, bad[0][1]
-    # interp (before any move): every marker's U, bit for bit
+    # interp (before any move): every marker's U.  A slab is a patch with its own
+    # x_lower = z0 dz (as SAMRAI's patch geometry), so (X - x_lower)/dx can round
+    # differently from one patch's (X + dz/2 rounds when it crosses a binade; X -
+    # (z0 dz - dz/2) does not): bitwise for almost every marker, within the interp
+    # tolerance for all.
     U1 = np.empty_like(ref_U)
     U1[ref_ids] = ref_U
-    seen = 0
-    for rank, _, ids, U, fin, z0, nz in res:
-        assert np.array_equal(U, U1[ids]), f"rank {rank}: interp differs from one rank"
+    seen = same = 0
+    for rank, _, ids, U, fin, z0, nz in sorted(res, key=lambda r: r[0]):
+        assert rel_err(U, U1[ids]) <= INTERP_TOL, f"rank {rank}: interp differs from one rank"
+        same += int((U == U1[ids]).all(axis=1).sum())
         seen += ids.size
     assert seen == M
+    assert same >= 0.95 * M, f"only {same} of {M} markers bitwise"
+    print(f"world {world}: {same} of {M} markers' interp bitwise equal to one rank")
     # spread + ghost sum: each rank's unique planes against one rank's
-    for rank, _, ids, U, fin, z0, nz in res:
+    for rank, _, ids, U, fin, z0, nz in sorted(res, key=lambda r: r[0]):
         for c in range(3):
             assert rel_err(fin[c], ref_f[c][z0:z0 + nz]) <= SPREAD_TOL, f"rank {rank} comp {c}"
