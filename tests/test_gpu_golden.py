@@ -1,0 +1,81 @@
+"""GPU: the device kernels' 1-D weights against the known-answer vectors of
+tests/golden/kernel_weights.json (60-digit Decimal evaluations of the
+reference's formulas, made by tests/golden/make_golden.py independently of both
+the oracle and le_stencil.h).
+
+The device stencil code (ibamr_amd/csrc/le_stencil.h) and the oracle
+(oracle/le_oracle.c) restate the same Fortran, so a transcription slip common to
+both would pass every GPU-vs-oracle parity test; this test pins the device side
+directly.  Method: cell-centred data (no frame shift), dx = 1, x_lower = 0,
+ilower = 0, so X_o_dx = x exactly; the marker's y (and z) sit at a cell centre;
+u = 1 on the whole grid plane x-index j, 0 elsewhere.  Then V = w(j) times the
+partition-of-unity sums of the other dims (1 up to rounding; 1 + 6e-15 for
+IB_3, whose truncated Fortran constants are kept).  Every point of every
+stencil is checked, and the points just outside it must give exactly 0.
+"""
+import json
+from decimal import Decimal
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = json.loads((Path(__file__).parent / "golden" / "kernel_weights.json").read_text())
+KERNELS = sorted({c["kernel"] for c in GOLDEN["cases"]})
+
+
+@pytest.fixture(scope="module")
+def le():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ibamr_amd import le as _le
+    return _le
+
+
+@pytest.fixture(scope="module")
+def ctx(le):
+    return le.Context(0)
+
+
+@pytest.mark.parametrize("ndim", [2, 3])
+@pytest.mark.parametrize("kernel", KERNELS + ["DISCONTINUOUS_LINEAR-offaxis"])
+def test_device_weights_known_answer(le, ctx, kernel, ndim):
+    off = kernel.endswith("-offaxis")
+    kname = kernel.replace("-offaxis", "")
+    cases = [c for c in GOLDEN["cases"] if c["kernel"] == kname and c.get("axis_dim", True) != off]
+    assert cases
+    axis = 1 if off else 0
+    g = 6
+    nx, ny = 21, 4
+    ilo = [0] * ndim
+    ihi = [nx - 1] + [ny - 1] * (ndim - 1)
+    geom = le.Geometry(ilo, ihi, g, [1.0] * ndim, [0.0] * ndim)
+    M = len(cases)
+    X = np.full((M, ndim), 1.5)
+    X[:, 0] = [float(c["X_o_dx"]) for c in cases]
+    Xd = torch.from_numpy(X).cuda()
+    m = le.Markers(ctx).bin(geom, kname, Xd)
+    jmin = min(c["ic_lower"] for c in cases) - 1
+    jmax = max(c["ic_lower"] + len(c["w"]) for c in cases)
+    assert jmin >= -g and jmax <= nx - 1 + g
+    got = np.zeros((M, jmax - jmin + 1))
+    u = geom.alloc("cell")
+    Q = torch.zeros((M, 1), dtype=torch.float64, device="cuda:0")
+    for j in range(jmin, jmax + 1):
+        u[0].zero_()
+        u[0][..., j + g] = 1.0  # the whole plane x-index j (x is the fastest array dim)
+        le.interp(ctx, m, kname, "cell", geom, u, Q, Xd, q_depth=1, axis=axis)
+        ctx.synchronize()
+        got[:, j - jmin] = Q[:, 0].cpu().numpy()
+    tol = 2e-14
+    for i, c in enumerate(cases):
+        w = np.array([float(Decimal(v)) for v in c["w"]])
+        k0 = c["ic_lower"] - jmin
+        np.testing.assert_allclose(got[i, k0:k0 + w.size], w, rtol=0, atol=tol,
+                                   err_msg=f"{kernel} {ndim}-D at X_o_dx = {c['X_o_dx']}")
+        outside = np.delete(got[i], np.arange(k0, k0 + w.size))
+        assert not outside.any(), f"{kernel} {ndim}-D at {c['X_o_dx']}: weight outside the stencil"

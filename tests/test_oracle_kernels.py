@@ -20,7 +20,7 @@ ALL = ["PIECEWISE_CONSTANT", "DISCONTINUOUS_LINEAR", "PIECEWISE_LINEAR", "PIECEW
 SMOOTH = ["PIECEWISE_LINEAR", "PIECEWISE_CUBIC", "IB_3", "IB_4", "IB_4_W8", "IB_6", "BSPLINE_4"]
 
 
-@pytest.mark.parametrize("case", [c for c in GOLDEN["cases"] if c["kernel"] in ("IB_4", "BSPLINE_4", "IB_4_W8")],
+@pytest.mark.parametrize("case", [c for c in GOLDEN["cases"] if c["kernel"] in ("IB_4", "BSPLINE_4", "IB_4_W8", "IB_6")],
                          ids=lambda c: f"{c['kernel']}@{c['X_o_dx']}")
 def test_closed_form_weights_known_answer(oracle, case):
     icl, w = oracle.weights_1d(case["kernel"], float(case["X_o_dx"]))
@@ -50,6 +50,37 @@ def test_pointwise_kernels_known_answer(oracle, case):
         got.append(V[0])
     # the y-sum of weights is 1 (partition of unity) up to rounding
     np.testing.assert_allclose(got, expect, rtol=0, atol=4e-15)
+
+
+def _indicator_interp(oracle, kernel, x, j, axis=0):
+    """V at X_o_dx = x (2-D, dx = 1, x_lower = 0, y at a cell centre) of the field
+    that is 1 on the whole grid column x-index j: the x weight of point j."""
+    # x_lower = 0 and ilower = 0, so X_o_dx = x exactly (NINT is not shift-invariant:
+    # NINT(-0.5) = -1 puts X = 0 in cell -1 for the low-order kernels)
+    lo, hi, g = [0, 0], [20, 0], [4, 4]
+    u = np.zeros(oracle.ghost_shape(lo, hi, g))
+    u[0, :, j - (lo[0] - g[0])] = 1.0
+    V = np.zeros(1)
+    oracle.interp(kernel, [1.0, 1.0], [0.0, 0.0], lo, hi, g, u, [0], np.zeros((1, 2)),
+                  np.array([[x, 0.5]]), V, axis=axis)
+    return V[0]
+
+
+LOW = [c for c in GOLDEN["cases"] if c["kernel"] in ("PIECEWISE_LINEAR", "DISCONTINUOUS_LINEAR", "PIECEWISE_CONSTANT")]
+
+
+@pytest.mark.parametrize("case", LOW, ids=lambda c: f"{c['kernel']}@{c['X_o_dx']}{'' if c.get('axis_dim', True) else '-offaxis'}")
+def test_low_order_kernels_known_answer(oracle, case):
+    """PIECEWISE_LINEAR / DISCONTINUOUS_LINEAR / PIECEWISE_CONSTANT: the weight of
+    every stencil point, and zero just outside the stencil (its placement)."""
+    x = float(case["X_o_dx"])
+    axis = 0 if case.get("axis_dim", True) else 1  # DISCONTINUOUS_LINEAR: x is the axis dim or not
+    expect = [float(Decimal(v)) for v in case["w"]]
+    icl = case["ic_lower"]
+    got = [_indicator_interp(oracle, case["kernel"], x, icl + k, axis) for k in range(len(expect))]
+    np.testing.assert_allclose(got, expect, rtol=0, atol=4e-15)
+    for j in (icl - 1, icl + len(expect)):
+        assert _indicator_interp(oracle, case["kernel"], x, j, axis) == 0.0
 
 
 def test_nint_half_away_from_zero(oracle):
