@@ -262,6 +262,9 @@ __device__ __forceinline__ double shfl_f64(double v, int src) {
 constexpr int IWAVES = IBTK_LE_IWAVES;  // waves per interp work item (one LDS ring)
 // 1: interp sums in the Fortran order, bitwise the oracle's (default);
 // 0: separable rows with FMAs, within tolerance (an experiment, not shipped)
+#ifndef IBTK_LE_IDEAL
+#define IBTK_LE_IDEAL 1  // interp: deal markers over lanes by LDS bank class
+#endif
 #ifndef IBTK_LE_INTERP_EXACT
 #define IBTK_LE_INTERP_EXACT 1
 #endif
@@ -322,16 +325,29 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
         // f.m4:1366-1382 needs no per-point branch.
         const double* base = ring + oy * RX + ox;
         if constexpr (IBTK_LE_INTERP_EXACT) {
+            // The reads of a block of R stencil rows (R W ~ 16 values) go out back
+            // to back before the block is summed, so one LDS latency is exposed
+            // per block rather than one per pair of reads (the sum itself stays
+            // the Fortran's sequential chain).
+            constexpr int R = W <= 4 ? W : (W <= 6 ? 3 : 2);  // rows per block; divides W
 #pragma unroll
             for (int i2 = 0; i2 < W; ++i2) {
                 const double* pl = base + islot<K>(oz + i2) * PV;
 #pragma unroll
-                for (int i1 = 0; i1 < W; ++i1) {
-                    const double wyz = st[1].w[i1] * st[2].w[i2];  // f.m4:1349-1353
+                for (int r0 = 0; r0 < W; r0 += R) {
+                    double v[R * W];
 #pragma unroll
-                    for (int i0 = 0; i0 < W; ++i0) {
-                        const double wt = st[0].w[i0] * wyz;
-                        acc = acc + wt * pl[i1 * RX + i0];  // f.m4:1375
+                    for (int r = 0; r < R; ++r)
+#pragma unroll
+                        for (int i0 = 0; i0 < W; ++i0) v[r * W + i0] = pl[(r0 + r) * RX + i0];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const double wyz = st[1].w[r0 + r] * st[2].w[i2];  // f.m4:1349-1353
+#pragma unroll
+                        for (int i0 = 0; i0 < W; ++i0) {
+                            const double wt = st[0].w[i0] * wyz;
+                            acc = acc + wt * v[r * W + i0];  // f.m4:1375
+                        }
                     }
                 }
             }
@@ -512,8 +528,29 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     // the markers over the two 32-lane halves of a ds_read_b64 by bank class,
     // as the spread does for its adds, measured 10 % slower: the ranking costs
     // more than the reads' bank conflicts.)
-    auto process_pool = [&](int n, const Mk& m, int am) {
-        const bool act = lane < n;
+    // The markers are dealt over the lanes by the LDS bank class of their
+    // stencil start (deal_lanes: ds_read2_b64 serves 4 groups of 16 lanes, a
+    // group conflict-free when its f64 indices differ mod 16; the ring row
+    // stride RX = 36 = 4 mod 16 gives class (4 y + x) mod 16, the same for
+    // every read of the stencil).  IBTK_LE_IDEAL=0 turns it off.
+    const double inv_dx0 = 1.0 / p.bg.dx[0], inv_dx1 = 1.0 / p.bg.dx[1];
+    auto process_pool = [&](int n, const Mk& m0, int am0) {
+        Mk m = m0;
+        int am = am0;
+        bool act = lane < n;
+        if constexpr (IBTK_LE_IDEAL) {
+            const int kx = (int)floor((m0.X[0] - cd.xlo[0]) * inv_dx0);
+            const int ky = (int)floor((m0.X[1] - cd.xlo[1]) * inv_dx1);
+            const int cls = act ? ((4 * ky + kx) & 15) : 63;
+            const int src = deal_lanes<4>(cls);
+            m.X[0] = shfl_f64(m0.X[0], src);
+            m.X[1] = shfl_f64(m0.X[1], src);
+            m.X[2] = shfl_f64(m0.X[2], src);
+            m.s = __builtin_amdgcn_ds_bpermute(src << 2, m0.s);
+            m.q = __builtin_amdgcn_ds_bpermute(src << 2, m0.q);
+            am = __builtin_amdgcn_ds_bpermute(src << 2, am0);
+            act = src < n;
+        }
         double acc = 0.0;
         if (act) acc = interp_marker<K>(p, cd, ring, gx0, gy0, am, m.X, m.s);
         double* dst = (act && m.q >= 0) ? p.Qout + ((int64_t)p.Q_depth * m.q + cd.qcomp) : p.sink + lane;
