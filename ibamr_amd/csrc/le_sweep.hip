@@ -265,6 +265,9 @@ constexpr int IWAVES = IBTK_LE_IWAVES;  // waves per interp work item (one LDS r
 #ifndef IBTK_LE_IDEAL
 #define IBTK_LE_IDEAL 1  // interp: deal markers over lanes by LDS bank class
 #endif
+#ifndef IBTK_LE_IBLOCK
+#define IBTK_LE_IBLOCK 1  // interp: read blocks of stencil rows before summing them
+#endif
 #ifndef IBTK_LE_INTERP_EXACT
 #define IBTK_LE_INTERP_EXACT 1
 #endif
@@ -329,7 +332,7 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
             // to back before the block is summed, so one LDS latency is exposed
             // per block rather than one per pair of reads (the sum itself stays
             // the Fortran's sequential chain).
-            constexpr int R = W <= 4 ? W : (W <= 6 ? 3 : 2);  // rows per block; divides W
+            constexpr int R = !IBTK_LE_IBLOCK ? 1 : (W <= 4 ? W : (W <= 6 ? 3 : 2));  // rows per block; divides W
 #pragma unroll
             for (int i2 = 0; i2 < W; ++i2) {
                 const double* pl = base + islot<K>(oz + i2) * PV;
