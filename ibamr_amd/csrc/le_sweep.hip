@@ -263,7 +263,7 @@ constexpr int IWAVES = IBTK_LE_IWAVES;  // waves per interp work item (one LDS r
 // 1: interp sums in the Fortran order, bitwise the oracle's (default);
 // 0: separable rows with FMAs, within tolerance (an experiment, not shipped)
 #ifndef IBTK_LE_IDEAL
-#define IBTK_LE_IDEAL 1  // interp: deal markers over lanes by LDS bank class
+#define IBTK_LE_IDEAL 0  // interp: deal markers over lanes by LDS bank class (measured slower: off)
 #endif
 #ifndef IBTK_LE_IBLOCK
 #define IBTK_LE_IBLOCK 1  // interp: read blocks of stencil rows before summing them
@@ -586,12 +586,16 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
         vsp1 = gspan_load(a + 2 * IWAVES);
         plane_load(my + IWAVES + HI, pv);
         const int tot = gc.pre[IWAVES];
-        if (SW * w < tot) process_pool(min(tot - SW * w, SW), cur, acur);
-        for (int c = w + IWAVES; SW * c < tot; c += IWAVES) {  // dense groups
-            Mk m;
-            int am;
-            chunk_load(gc, a, c, m, am);
-            process_pool(min(tot - SW * c, SW), m, am);
+        if (SW * w < tot) {
+            // dense groups: the wave's next chunk loads while this one is summed
+            Mk m = cur;
+            int am = acur;
+            for (int c = w; SW * c < tot; c += IWAVES) {
+                const Mk now = m;
+                const int anow = am;
+                if (SW * (c + IWAVES) < tot) chunk_load(gc, a, c + IWAVES, m, am);
+                process_pool(min(tot - SW * c, SW), now, anow);
+            }
         }
     }
 }
@@ -939,10 +943,14 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
             rows_load(a, rowm);
             Ranges rgm;
             make_ranges_lanes(rowm, rgm);
+            // chunk k + 1's candidates load while chunk k is added (a dense plane,
+            // e.g. a sheet of markers, is hundreds of chunks of one wave)
+            Cand more;
+            cand_at(range_pos(rgm, h + lane), more);
             for (int k = 0; k < nmid; ++k) {
-                Cand more;
-                cand_at(range_pos(rgm, h + SW * k + lane), more);
-                process(a, 0, SW, more);
+                const Cand now = more;
+                if (k + 1 < nmid) cand_at(range_pos(rgm, h + SW * (k + 1) + lane), more);
+                process(a, 0, SW, now);
             }
         }
         if (a == alast && r_a > 0) {  // the last anchor's leftovers
