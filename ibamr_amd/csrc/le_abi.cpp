@@ -2,6 +2,7 @@
 // the interp/spread entry points over device-resident data.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstdarg>
@@ -715,15 +716,20 @@ static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cente
             HIP_TRY(hipStreamSynchronize(ctx->stream));
             double tot[6] = {0, 0, 0, 0, 0, 0};
             long items = 0;
+            std::vector<unsigned long long> sums;
             for (size_t i = 0; i < nst / 8; ++i) {
                 unsigned long long sum = 0;
                 for (int k = 0; k < 6; ++k) sum += h[i * 8 + k];
                 if (!sum) continue;
                 ++items;
+                sums.push_back(sum);
                 for (int k = 0; k < 6; ++k) tot[k] += (double)h[i * 8 + k];
             }
-            fprintf(stderr, "spread stamps: %ld items; mean cycles/item: prologue %.0f wait %.0f chunk0 %.0f dense %.0f tail %.0f drain %.0f\n",
-                    items, tot[0] / items, tot[1] / items, tot[2] / items, tot[3] / items, tot[4] / items, tot[5] / items);
+            std::sort(sums.begin(), sums.end());
+            const double q99 = sums.empty() ? 0.0 : (double)sums[(size_t)(0.99 * (sums.size() - 1))];
+            const double mx = sums.empty() ? 0.0 : (double)sums.back();
+            fprintf(stderr, "spread stamps: %ld items; mean cycles/item: prologue %.0f wait %.0f chunk0 %.0f dense %.0f tail %.0f drain %.0f; item total p99 %.0f max %.0f\n",
+                    items, tot[0] / items, tot[1] / items, tot[2] / items, tot[3] / items, tot[4] / items, tot[5] / items, q99, mx);
             p.stamps = nullptr;
         }
         if (t) ctx->ev_valid = true;

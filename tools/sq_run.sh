@@ -1,16 +1,16 @@
 #!/bin/bash
 # SQ/LDS counters of the sweep kernels over tools/tune_sweep.py (one setting),
 # one counter group per rocprofv3 pass (<= 8 SQ counters each).
-# Usage: tools/sq_run.sh <outdir> ['<settings json>']
+# Usage: tools/sq_run.sh <outdir> ['<settings json>'] [tune_sweep args...]
 set -o pipefail
-out=$1; st=${2:-'[{}]'}
+out=$1; st=${2:-'[{}]'}; shift 2
 mkdir -p $out
 export TMPDIR=/tmp
 i=0
 for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_LDS" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $out/g$i -o pmc -- python3 -u tools/tune_sweep.py "$st" > $out/g$i.log 2>&1 || { echo "pass $i failed"; tail -3 $out/g$i.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $out/g$i -o pmc -- python3 -u tools/tune_sweep.py "$st" "$@" > $out/g$i.log 2>&1 || { echo "pass $i failed"; tail -3 $out/g$i.log; exit 1; }
 done
 python3 - $out <<'PY'
 import csv, glob, json, sys, collections
@@ -20,9 +20,9 @@ for path in glob.glob(f"{out}/g*/**/pmc_counter_collection.csv", recursive=True)
     per = collections.defaultdict(float)
     for r in csv.DictReader(open(path)):
         k = r["Kernel_Name"]
-        if "sweep" not in k:
+        if "k_interp_sweep" not in k and "k_spread_sweep" not in k:
             continue
-        kk = "interp" if "interp" in k else "spread"
+        kk = "interp" if "k_interp_sweep" in k else "spread"
         per[(kk, r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
     for (kk, d, c), v in per.items():
         acc[kk][c].append(v)
