@@ -120,6 +120,8 @@ struct ibtk_le_markers_s {
     DevBuf sorted_key, sorted_l, sorted_s, sorted_X, sorted_a, plane_start, indices, xshift;
     DevBuf cand_cnt, cand_off, cand_idx;  // spread candidate lists, built on first use after a bin
     DevBuf last, qdst;                    // interp with duplicate list entries (Params::qdst)
+    DevBuf items, nsub, isub, nitems;     // 3-D sweep item table
+    int item_bound = 0;
     bool has_indices = false, has_xshift = false;
     bool cand_valid = false;
     bool dedup_done = false, has_dups = false;
@@ -192,12 +194,8 @@ extern "C" int ibtk_le_ctx_tune(ibtk_le_ctx ctx, const char* key, int value) {
     if (!ctx || !key) return fail(IBTK_LE_ERR_ARG, "null argument");
     SweepTune& t = ctx->tune;
     const std::string k = key;
-    if (k == "interp_tile_w") t.itw = value;
-    else if (k == "interp_tile_h") t.ith = value;
-    else if (k == "spread_tile_w") t.stw = value;
-    else if (k == "spread_tile_h") t.sth = value;
-    else if (k == "component_fastest") t.cfast = value != 0;
-    else if (k == "seg_items") t.seg_items = value;
+    if (k == "seg_items") t.seg_items = value;
+    else if (k == "split_target") t.split_target = value;
     else return fail(IBTK_LE_ERR_ARG, "unknown tuning key %s", key);
     return IBTK_LE_OK;
 }
@@ -409,7 +407,8 @@ extern "C" int ibtk_le_markers_destroy(ibtk_le_markers m) {
     hipSetDevice(m->ctx->device);
     hipStreamSynchronize(m->ctx->stream);
     for (DevBuf* b : {&m->sorted_key, &m->sorted_l, &m->sorted_s, &m->sorted_X, &m->sorted_a, &m->plane_start, &m->indices,
-                      &m->xshift, &m->cand_cnt, &m->cand_off, &m->cand_idx, &m->last, &m->qdst})
+                      &m->xshift, &m->cand_cnt, &m->cand_off, &m->cand_idx, &m->last, &m->qdst, &m->items,
+                      &m->nsub, &m->isub, &m->nitems})
         b->release();
     delete m;
     return IBTK_LE_OK;
@@ -420,6 +419,38 @@ extern "C" int ibtk_le_markers_count(ibtk_le_markers m) { return m ? m->n : -1; 
 extern "C" int ibtk_le_markers_order(ibtk_le_markers m, const int** order_dev) {
     if (!m || !order_dev) return fail(IBTK_LE_ERR_ARG, "markers_order: null argument");
     *order_dev = m->sorted_l.as<int>();
+    return IBTK_LE_OK;
+}
+
+// The 3-D sweep item table of the binned list (launch_item_table): one item per
+// (column, segment), heavy ones cut into sub-segments.  No host sync: the
+// sweeps launch over an upper bound of the item count and read the count on
+// the device.
+#ifndef IBTK_LE_SPLIT_TARGET
+#define IBTK_LE_SPLIT_TARGET 12288  // own markers per item above which it is cut (cfg4 items hold ~6.8K)
+#endif
+static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel) {
+    const int nj = m->cg.ncol * m->nseg;
+    const int target = ctx->tune.split_target > 0 ? ctx->tune.split_target : IBTK_LE_SPLIT_TARGET;
+    const long long bound = (long long)nj + (long long)m->n / target + 1;
+    if (bound * 3 >= (1LL << 31)) return fail(IBTK_LE_ERR_RANGE, "too many sweep items");
+    m->item_bound = (int)bound;
+    int rc;
+    if ((rc = m->items.ensure(sizeof(SweepItem) * (size_t)bound))) return rc;
+    if ((rc = m->nsub.ensure(sizeof(int) * (size_t)std::max(nj, 1)))) return rc;
+    if ((rc = m->isub.ensure(sizeof(int) * (size_t)std::max(nj, 1)))) return rc;
+    if ((rc = m->nitems.ensure(sizeof(int)))) return rc;
+    Params p;
+    std::memset(&p, 0, sizeof(p));
+    p.cg = m->cg;
+    p.S = m->S;
+    p.nseg = m->nseg;
+    p.plane_start = m->plane_start.as<int>();
+    size_t tb = 0;
+    HIP_TRY(launch_scan(nullptr, tb, m->nsub.as<int>(), m->isub.as<int>(), std::max(nj, 1), ctx->stream));
+    if ((rc = ctx->temp.ensure(tb))) return rc;
+    HIP_TRY(launch_item_table(kernel, p, target, m->nsub.as<int>(), m->isub.as<int>(), m->items.as<SweepItem>(),
+                              m->nitems.as<int>(), ctx->temp.p, ctx->temp.cap, ctx->stream));
     return IBTK_LE_OK;
 }
 
@@ -460,6 +491,7 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     if ((rc = m->plane_start.ensure(sizeof(int) * (size_t)(nplanes + 1)))) return rc;
     if (n == 0) {
         HIP_TRY(hipMemsetAsync(m->plane_start.p, 0, sizeof(int) * (size_t)(nplanes + 1), s));
+        if (cols) return build_items(ctx, m, kernel);
         return IBTK_LE_OK;
     }
     if ((rc = m->sorted_key.ensure(sizeof(unsigned) * (size_t)n))) return rc;
@@ -503,6 +535,7 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     if (cols) {  // gather fused with the bucket starts
         HIP_TRY(launch_gather_col(kernel, p, n, m->sorted_s.as<int>(), m->sorted_X.as<double>(),
                                   m->sorted_key.as<unsigned>(), nplanes, m->plane_start.as<int>(), s));
+        if (int rc2 = build_items(ctx, m, kernel)) return rc2;
     } else {
         HIP_TRY(launch_brick_start(m->sorted_key.as<unsigned>(), n, nplanes, bg.shift - (geom->ndim == 3 ? 3 : 4),
                                    m->plane_start.as<int>(), s));
@@ -538,6 +571,9 @@ static int prepare(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const ibtk_le
     p.cg = m->cg;
     p.S = m->S;
     p.nseg = m->nseg;
+    p.items = m->items.as<SweepItem>();
+    p.nitems = m->nitems.as<int>();
+    p.item_bound = m->item_bound;
     p.sorted_a = m->sorted_a.as<unsigned>();
     p.nsorted = m->n;
     p.X = X;
@@ -699,7 +735,7 @@ static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cente
         if (int rc = make_comps(geom, centering, axis, q_dev, q_depth, Q_depth, first, cnt, p)) return rc;
         const bool t = ctx->timing && first == 0;
         p.dbg = ctx->dbg;  // diagnostics: variants of the add loop
-        const size_t nst = (size_t)m->cg.ncol * m->nseg * cnt * 8;
+        const size_t nst = (size_t)m->item_bound * cnt * 8;
         if (geom->ndim == 3 && ctx->stamps_on) {
             if (int rc = ctx->stamps.ensure(nst * sizeof(unsigned long long))) return rc;
             HIP_TRY(hipMemsetAsync(ctx->stamps.p, 0, nst * sizeof(unsigned long long), ctx->stream));

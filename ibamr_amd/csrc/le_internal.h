@@ -100,10 +100,12 @@ struct ColGeom {
 
 // Diagnostic tuning of the 3-D sweeps (ibtk_le_ctx_tune); 0 = the default.
 struct SweepTune {
-    int itw = 0, ith = 0;  // interp column tile (item_decode)
-    int stw = 0, sth = 0;  // spread column tile
-    int cfast = 1;         // 1: component fastest in the item order
     int seg_items = 0;     // sweep_segments' item target
+    int split_target = 0;  // own markers above which a (column, segment) is cut (k_item_counts)
+};
+// One 3-D sweep item: a column and its owned planes [p0, p1) (relative to cg.org[2]).
+struct SweepItem {
+    int col, p0, p1;
 };
 
 struct Params {
@@ -111,7 +113,9 @@ struct Params {
     ColGeom cg;                // 3-D column binning
     const unsigned* sorted_a;  // sorted position -> packed key cell (x | y << 16), relative to cg.org
     int S, nseg;               // sweep segment length (planes) and segments per column
-    int tw, th, cfast;         // item order (item_decode): column tile, component fastest
+    const SweepItem* items;    // 3-D sweep item table (k_item_write)
+    const int* nitems;         // device: its length
+    int item_bound;            // host: an upper bound of the length (the launch grid)
     SweepTune tune;
     int ncomp;
     CompDesc comp[MAXC];
@@ -167,6 +171,8 @@ hipError_t launch_gather_col(int kernel, const Params& p, int n, int* sorted_s, 
 hipError_t launch_interp_sweep(int kernel, const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_spread_sweep(int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items);
+hipError_t launch_item_table(int kernel, const Params& p, int target, int* nsub, int* start, SweepItem* tab, int* ntot,
+                             void* temp, size_t temp_bytes, hipStream_t s);
 
 // Periodic helpers
 struct GhostDesc {

@@ -148,32 +148,18 @@ __device__ __forceinline__ int sweep_item(int nitems) {
     return it < nitems ? it : -1;
 }
 
-// Work item -> (component c, column col, segment seg).  Segment-major (with 8
-// segments each XCD sweeps one); within a segment either component fastest
-// (p.cfast) or component-major, and the columns in tiles of tw x th columns:
-// the items an XCD runs at once then cover a compact block of neighbouring
-// columns, whose shared halo rows and the cache lines straddling column edges
-// come from HBM once and from the XCD's L2 after.  tw = ncx, th = 1 is the
-// plain row-major column order.
-__device__ __forceinline__ void item_decode(const Params& p, int it, int& c, int& col, int& seg) {
-    const int ncol = p.cg.ncol, per_seg = ncol * p.ncomp;
-    seg = it / per_seg;
-    int k = it - seg * per_seg;
-    if (p.cfast) {
-        c = k % p.ncomp;
-        k /= p.ncomp;
-    } else {
-        c = k / ncol;
-        k -= c * ncol;
-    }
-    const int ncx = p.cg.ncx, ncy = p.cg.ncy, TW = p.tw, TH = p.th;
-    const int tr = k / (ncx * TH);  // tile row (TH column rows; the last may be short)
-    int k2 = k - tr * ncx * TH;
-    const int th = min(TH, ncy - tr * TH);
-    const int tc = k2 / (TW * th);  // tile in the row (TW columns; the last may be narrow)
-    k2 -= tc * TW * th;
-    const int tw = min(TW, ncx - tc * TW);
-    col = (tr * TH + k2 / tw) * ncx + tc * TW + k2 % tw;
+// Work item -> (component c, table entry t): component fastest, so the three
+// components of a column run on one XCD at about the same time (their Q
+// stores fill the same AoS lines; tools/tune_sweep.py measured the component-
+// major and column-tiled orders slower).  The table (k_item_write) lists the
+// (column, owned planes [p0, p1)) of every item, segment-major.  Returns false
+// past the table's end.
+__device__ __forceinline__ bool item_decode(const Params& p, int it, int& c, SweepItem& si) {
+    const int t = it / p.ncomp;
+    c = it - t * p.ncomp;
+    if (t >= *p.nitems) return false;
+    si = p.items[t];
+    return true;
 }
 
 // bucket index of (anchor plane a, column col, band)
@@ -416,12 +402,13 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     using S = ISh<K>;
     constexpr int LO = S::LO, HI = S::HI, RX = S::RX, NPT = S::NPT;
     __shared__ double ring[S::NSL * S::PVP];
-    const int nitems = p.cg.ncol * p.nseg * p.ncomp;
-    const int it = sweep_item(nitems);
+    const int it = sweep_item(p.item_bound * p.ncomp);
     if (it < 0) return;
-    int c, col, seg;
-    item_decode(p, it, c, col, seg);
-    const int a0 = seg * p.S, a1 = min(a0 + p.S, p.cg.nz);
+    int c;
+    SweepItem si;
+    if (!item_decode(p, it, c, si)) return;
+    const int col = si.col;
+    const int a0 = si.p0, a1 = si.p1;  // the item's anchor planes
     const int lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int* bs = p.plane_start;
@@ -783,11 +770,12 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     constexpr int LO = S::LO, HI = S::HI, NPL = S::NPL, FAM = S::FAM;
     __shared__ double ring_mem[S::GUARD + S::NSL * S::SLOT];
     double* const ring = ring_mem + S::GUARD;
-    const int nitems = p.cg.ncol * p.nseg * p.ncomp;
-    const int it = sweep_item(nitems);
+    const int it = sweep_item(p.item_bound * p.ncomp);
     if (it < 0) return;
-    int c, col, seg;
-    item_decode(p, it, c, col, seg);
+    int c;
+    SweepItem si;
+    if (!item_decode(p, it, c, si)) return;
+    const int col = si.col;
     const int lane = lane_id();
     const int ncx = p.cg.ncx;
     const int cx = col % ncx, cy = col / ncx;
@@ -798,7 +786,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // owned, in-array ranges (column-local x/y, relative planes)
     const int xlo = max(cd.lo[0] - X0, 0), xhi = min(cd.hi[0] - X0, COLX - 1);
     const int ylo = max(cd.lo[1] - Y0, 0), yhi = min(cd.hi[1] - Y0, COLY - 1);
-    const int plo = max(seg * p.S, cd.lo[2] - zorg), phi = min(min(seg * p.S + p.S, p.cg.nz) - 1, cd.hi[2] - zorg);
+    const int plo = max(si.p0, cd.lo[2] - zorg), phi = min(si.p1 - 1, cd.hi[2] - zorg);
     if (xlo > xhi || ylo > yhi || plo > phi) return;
     const int afirst = max(plo - HI, 0), alast = min(phi - LO, p.cg.nz - 1);
     const int* bs = p.plane_start;
@@ -987,7 +975,51 @@ void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items) {
     nseg = (cg.nz + S - 1) / S;
 }
 
+// Sweep item table.  A (column, segment) whose own markers exceed `target` is
+// cut into sub-segments of its planes (at least NS planes each): a fibre bundle
+// along z is then many items instead of one wave's serial walk.  Sub-items own
+// disjoint planes, so every grid point still gets its contributions from one
+// item, in the same order: results do not depend on the split.  The interp
+// item of a sub-segment sums the markers anchored in its planes; the spread
+// item owns its planes and takes the candidates of the anchors reaching them
+// (NS - 1 extra anchor planes per cut).
+template <int K>
+__global__ __launch_bounds__(BLOCK) void k_item_counts(Params p, int target, int* nsub) {
+    constexpr int NS = KT<K>::HI - KT<K>::LO + 1;
+    const int j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= p.nseg * p.cg.ncol) return;
+    const int seg = j / p.cg.ncol, col = j - seg * p.cg.ncol;
+    const int a0 = seg * p.S, a1 = min(a0 + p.S, p.cg.nz);
+    const int* bs = p.plane_start;
+    long load = 0;
+    for (int a = a0; a < a1; ++a) load += bs[bucket(p, a, col, NBAND)] - bs[bucket(p, a, col, 0)];
+    const int maxsub = max((a1 - a0) / max(NS, 8), 1);
+    nsub[j] = (int)min((long)maxsub, max(1L, (load + target - 1) / target));
+}
+__global__ __launch_bounds__(BLOCK) void k_item_write(Params p, const int* nsub, const int* start, SweepItem* tab,
+                                                      int* ntot) {
+    const int j = blockIdx.x * BLOCK + threadIdx.x;
+    const int nj = p.nseg * p.cg.ncol;
+    if (j >= nj) return;
+    const int seg = j / p.cg.ncol, col = j - seg * p.cg.ncol;
+    const int a0 = seg * p.S, a1 = min(a0 + p.S, p.cg.nz), len = a1 - a0;
+    const int n = nsub[j], s0 = start[j];
+    for (int k = 0; k < n; ++k) tab[s0 + k] = SweepItem{col, a0 + (len * k) / n, a0 + (len * (k + 1)) / n};
+    if (j == nj - 1) *ntot = s0 + n;
+}
+
 static int grid8(long items) { return (int)((items + 7) & ~7L); }
+
+template <int K> hipError_t launch_item_table_t(const Params& p, int target, int* nsub, int* start, SweepItem* tab,
+                                                int* ntot, void* temp, size_t temp_bytes, hipStream_t s) {
+    const int nj = p.nseg * p.cg.ncol;
+    if (nj <= 0) return hipMemsetAsync(ntot, 0, sizeof(int), s);
+    hipLaunchKernelGGL(k_item_counts<K>, dim3((nj + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, target, nsub);
+    hipError_t e = launch_scan(temp, temp_bytes, nsub, start, nj, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_item_write, dim3((nj + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, nsub, start, tab, ntot);
+    return hipGetLastError();
+}
 
 template <int K> hipError_t launch_bin_col_t(const Params& p, int n, unsigned* keys, int* vals, hipStream_t s) {
     if (n <= 0) return hipSuccess;
@@ -1013,22 +1045,10 @@ hipError_t launch_gather_col_t(const Params& p, int n, int* ss, double* sx, cons
                        nbuckets, bs);
     return hipGetLastError();
 }
-// Column tiles of the item order (item_decode): tw x th columns, about the
-// columns an XCD's CUs hold at once (interp: 3 workgroups per CU, 96 per XCD;
-// spread: 6, 192).  Tuning overrides: ibtk_le_ctx_tune.
-static void set_tiles(Params& q, const SweepTune& t, bool spread) {
-    const int tw = spread ? t.stw : t.itw, th = spread ? t.sth : t.ith;
-    q.cfast = t.cfast;
-    q.tw = tw > 0 ? min(tw, q.cg.ncx) : q.cg.ncx;
-    q.th = tw > 0 ? max(th, 1) : 1;
-}
-
 template <int K>
-hipError_t launch_interp_sweep_t(const Params& p0, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-    Params p = p0;
-    set_tiles(p, p0.tune, false);
+hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     if (ev0) (void)hipEventRecord(ev0, s);
-    const long items = (long)p.cg.ncol * p.nseg * p.ncomp;
+    const long items = (long)p.item_bound * p.ncomp;
     if (items > 0) hipLaunchKernelGGL(k_interp_sweep<K>, dim3(grid8(items)), dim3(SW * IWAVES), 0, s, p);
     if (ev1) (void)hipEventRecord(ev1, s);
     hipError_t e = hipGetLastError();
@@ -1049,14 +1069,12 @@ __global__ __launch_bounds__(BLOCK) void k_gather_F_col(Params p, int n, double*
     }
 }
 
-template <int K> hipError_t launch_spread_sweep_t(const Params& p0, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-    Params p = p0;
-    set_tiles(p, p0.tune, true);
+template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     if (p.nsorted > 0)
         hipLaunchKernelGGL(k_gather_F_col, dim3((p.nsorted + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, p.nsorted,
                            const_cast<double*>(p.sorted_F));
     if (ev0) (void)hipEventRecord(ev0, s);  // the events bracket the sweep kernel alone
-    const long items = (long)p.cg.ncol * p.nseg * p.ncomp;
+    const long items = (long)p.item_bound * p.ncomp;
     if (items > 0) hipLaunchKernelGGL(k_spread_sweep<K>, dim3(grid8(items)), dim3(SW), 0, s, p);
     if (ev1) (void)hipEventRecord(ev1, s);
     return hipGetLastError();
@@ -1076,6 +1094,13 @@ template <int K> hipError_t launch_spread_sweep_t(const Params& p0, hipStream_t 
     default: return nullptr;                                         \
     }
 
+using ItemTabFn = hipError_t (*)(const Params&, int, int*, int*, SweepItem*, int*, void*, size_t, hipStream_t);
+static ItemTabFn pick_item_table(int k) { IBTK_LE_DISPATCH_K(k, launch_item_table_t) }
+hipError_t launch_item_table(int kernel, const Params& p, int target, int* nsub, int* start, SweepItem* tab, int* ntot,
+                             void* temp, size_t temp_bytes, hipStream_t s) {
+    ItemTabFn f = pick_item_table(kernel);
+    return f ? f(p, target, nsub, start, tab, ntot, temp, temp_bytes, s) : hipErrorInvalidValue;
+}
 using BinColFn = hipError_t (*)(const Params&, int, unsigned*, int*, hipStream_t);
 using GatherColFn = hipError_t (*)(const Params&, int, int*, double*, const unsigned*, int, int*, hipStream_t);
 using InterpSwFn = hipError_t (*)(const Params&, int, hipStream_t, hipEvent_t, hipEvent_t);

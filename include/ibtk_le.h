@@ -233,11 +233,11 @@ int ibtk_le_mark_stencils(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int ce
  * call on this context, and the per-step timing of the last call's main kernel (ms,
  * measured with HIP events on the context stream when enabled). */
 int ibtk_le_ctx_enable_timing(ibtk_le_ctx ctx, int enable);
-/* Diagnostics: tuning overrides of the 3-D sweeps' work-item order (0 = default):
- * "interp_tile_w"/"interp_tile_h", "spread_tile_w"/"spread_tile_h" (column tiles),
- * "component_fastest" (0/1), "seg_items" (segment-length target, takes effect at
- * the next bin).  Results do not depend on them (each grid point's order of
- * contributions is fixed by the sorted list). */
+/* Diagnostics: tuning overrides of the 3-D sweeps' work items (0 = default), both
+ * taking effect at the next bin: "seg_items" (target number of (column, segment)
+ * items, which sets the segment length) and "split_target" (own markers above
+ * which a (column, segment) is cut into sub-segments).  Results do not depend on
+ * them (each grid point's order of contributions is fixed by the sorted list). */
 int ibtk_le_ctx_tune(ibtk_le_ctx ctx, const char* key, int value);
 double ibtk_le_ctx_last_kernel_ms(ibtk_le_ctx ctx);
 

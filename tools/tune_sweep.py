@@ -6,7 +6,7 @@ dispatches appear in the order printed here (REPS interp + REPS spread per
 setting), so the per-dispatch counters map onto the settings.
 
 Usage: python tools/tune_sweep.py [--config cfg4] [--reps 3] '<json list of settings>'
-A setting is a dict of ctx_tune keys, e.g. {"component_fastest": 0, "interp_tile_w": 12, ...}.
+A setting is a dict of ctx_tune keys, e.g. {"seg_items": 16384, "split_target": 8192}.
 """
 import argparse
 import json
@@ -52,9 +52,8 @@ def main():
     f = geom.alloc("side", device=dev)
     bins = le.Markers(ctx)
     settings = json.loads(args.settings)
-    keys = ["interp_tile_w", "interp_tile_h", "spread_tile_w", "spread_tile_h", "component_fastest", "seg_items"]
-    defaults = {"interp_tile_w": 0, "interp_tile_h": 0, "spread_tile_w": 0, "spread_tile_h": 0,
-                "component_fastest": 1, "seg_items": 0}
+    keys = ["seg_items", "split_target"]
+    defaults = {"seg_items": 0, "split_target": 0}
     Uref = fref = None
     for i, st in enumerate(settings):
         full = dict(defaults, **st)
