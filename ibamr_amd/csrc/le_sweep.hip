@@ -139,11 +139,13 @@ __global__ __launch_bounds__(BLOCK) void k_gather_col(Params p, int n, int* sort
 // Items are (segment, column, component), component fastest; blocks are dealt
 // round-robin over the 8 XCDs, so give XCD x a contiguous range of items: the
 // three components of a column and its x-neighbours run on one XCD at about the
-// same time and share marker data and halo planes through its L2.
+// same time and share marker data and halo planes through its L2.  The range
+// is cut from the table's actual length (read on the device; the grid is an
+// upper bound of it): an over-sized grid must not leave XCDs idle.
 __device__ __forceinline__ int sweep_item(int nitems) {
-    const int G = gridDim.x;  // multiple of 8
-    const int per = G >> 3;
+    const int per = (nitems + 7) >> 3;
     const int b = blockIdx.x;
+    if ((b >> 3) >= per) return -1;
     const int it = (b & 7) * per + (b >> 3);
     return it < nitems ? it : -1;
 }
@@ -152,14 +154,11 @@ __device__ __forceinline__ int sweep_item(int nitems) {
 // components of a column run on one XCD at about the same time (their Q
 // stores fill the same AoS lines; tools/tune_sweep.py measured the component-
 // major and column-tiled orders slower).  The table (k_item_write) lists the
-// (column, owned planes [p0, p1)) of every item, segment-major.  Returns false
-// past the table's end.
-__device__ __forceinline__ bool item_decode(const Params& p, int it, int& c, SweepItem& si) {
+// (column, owned planes [p0, p1)) of every item, segment-major.
+__device__ __forceinline__ void item_decode(const Params& p, int it, int& c, SweepItem& si) {
     const int t = it / p.ncomp;
     c = it - t * p.ncomp;
-    if (t >= *p.nitems) return false;
     si = p.items[t];
-    return true;
 }
 
 // bucket index of (anchor plane a, column col, band)
@@ -402,11 +401,11 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     using S = ISh<K>;
     constexpr int LO = S::LO, HI = S::HI, RX = S::RX, NPT = S::NPT;
     __shared__ double ring[S::NSL * S::PVP];
-    const int it = sweep_item(p.item_bound * p.ncomp);
+    const int it = sweep_item(*p.nitems * p.ncomp);
     if (it < 0) return;
     int c;
     SweepItem si;
-    if (!item_decode(p, it, c, si)) return;
+    item_decode(p, it, c, si);
     const int col = si.col;
     const int a0 = si.p0, a1 = si.p1;  // the item's anchor planes
     const int lane = lane_id();
@@ -770,11 +769,11 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     constexpr int LO = S::LO, HI = S::HI, NPL = S::NPL, FAM = S::FAM;
     __shared__ double ring_mem[S::GUARD + S::NSL * S::SLOT];
     double* const ring = ring_mem + S::GUARD;
-    const int it = sweep_item(p.item_bound * p.ncomp);
+    const int it = sweep_item(*p.nitems * p.ncomp);
     if (it < 0) return;
     int c;
     SweepItem si;
-    if (!item_decode(p, it, c, si)) return;
+    item_decode(p, it, c, si);
     const int col = si.col;
     const int lane = lane_id();
     const int ncx = p.cg.ncx;
