@@ -109,6 +109,12 @@ _SIGS = [
     ("ibtk_le_mark_stencils", c_int,
      [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_int,
       c_void_p]),
+    ("ibtk_le_index_set_list", c_int,
+     [c_void_p, ctypes.POINTER(PatchGeom), c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
+      c_int, ctypes.POINTER(c_int)]),
+    ("ibtk_le_node_distribution", c_int,
+     [c_void_p, ctypes.POINTER(PatchGeom), c_void_p, c_void_p, c_int, c_int, c_void_p, ctypes.POINTER(c_int),
+      ctypes.POINTER(c_int)]),
     ("ibtk_le_periodic_index_list", c_int,
      [c_void_p, ctypes.POINTER(PatchGeom), c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
       ctypes.POINTER(c_int)]),

@@ -97,6 +97,7 @@ struct ibtk_le_ctx_s {
     int device = 0;
     hipStream_t stream = nullptr;
     DevBuf keys_in, vals_in, temp, counts, offsets, fbuf;
+    DevBuf lst_idx, lst_xs, lst_key, lst_perm;  // index-list / node-distribution scratch
     DevBuf err;   // one int
     DevBuf sink;  // 64 doubles (Params::sink)
     DevBuf stamps;  // diagnostic phase clocks (IBTK_LE_STAMPS=1)
@@ -161,7 +162,7 @@ extern "C" int ibtk_le_ctx_destroy(ibtk_le_ctx ctx) {
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->keys_in, &ctx->vals_in, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->fbuf, &ctx->err, &ctx->sink,
-                       &ctx->stamps})
+                       &ctx->stamps, &ctx->lst_idx, &ctx->lst_xs, &ctx->lst_key, &ctx->lst_perm})
         b->release();
     if (ctx->ev0) hipEventDestroy(ctx->ev0);
     if (ctx->ev1) hipEventDestroy(ctx->ev1);
@@ -907,34 +908,34 @@ extern "C" int ibtk_le_zero_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* ge
     return ghost_op(ctx, geom, centering, q_dev, q_depth, nullptr, 2);
 }
 
-static int index_list_impl(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev, int n_markers,
-                           int ghost, const int* periodic, const int* box_lo, const int* box_hi, int* indices_dev,
-                           double* Xshift_dev, int capacity, int* count);
+static int index_list_impl(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev, const int* lag_dev,
+                           int n_markers, int ghost, const int* periodic, int which, const int* box_lo,
+                           const int* box_hi, int* indices_dev, double* Xshift_dev, int capacity, int* count);
 
 extern "C" int ibtk_le_periodic_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
                                            int n_markers, int ghost, const int* periodic, int* indices_dev,
                                            double* Xshift_dev, int capacity, int* count) {
-    return index_list_impl(ctx, geom, X_dev, n_markers, ghost, periodic, nullptr, nullptr, indices_dev, Xshift_dev,
-                           capacity, count);
+    return index_list_impl(ctx, geom, X_dev, nullptr, n_markers, ghost, periodic, 0, nullptr, nullptr, indices_dev,
+                           Xshift_dev, capacity, count);
+}
+
+extern "C" int ibtk_le_index_set_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
+                                      const int* lag_dev, int n_markers, int ghost, const int* periodic, int which,
+                                      int* indices_dev, double* Xshift_dev, int capacity, int* count) {
+    if (which < 0 || which > 2) return fail(IBTK_LE_ERR_ARG, "which: 0 all, 1 interior, 2 ghost");
+    return index_list_impl(ctx, geom, X_dev, lag_dev, n_markers, ghost, periodic, which, nullptr, nullptr,
+                           indices_dev, Xshift_dev, capacity, count);
 }
 
 extern "C" int ibtk_le_box_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
                                       int n_markers, const int* box_lo, const int* box_hi, int* indices_dev,
                                       int capacity, int* count) {
     if (!box_lo || !box_hi) return fail(IBTK_LE_ERR_ARG, "null box");
-    return index_list_impl(ctx, geom, X_dev, n_markers, 0, nullptr, box_lo, box_hi, indices_dev, nullptr, capacity,
-                           count);
+    return index_list_impl(ctx, geom, X_dev, nullptr, n_markers, 0, nullptr, 0, box_lo, box_hi, indices_dev, nullptr,
+                           capacity, count);
 }
 
-static int index_list_impl(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev, int n_markers,
-                           int ghost, const int* periodic, const int* box_lo, const int* box_hi, int* indices_dev,
-                           double* Xshift_dev, int capacity, int* count) {
-    if (!ctx || !count) return fail(IBTK_LE_ERR_ARG, "null argument");
-    if (int rc = check_geom(geom)) return rc;
-    if (n_markers < 0 || ghost < 0) return fail(IBTK_LE_ERR_ARG, "negative size");
-    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
-    *count = 0;
-    if (n_markers == 0) return IBTK_LE_OK;
+static ImageDesc image_desc(const ibtk_le_patch_geom* geom, int ghost) {
     ImageDesc d;
     std::memset(&d, 0, sizeof(d));
     d.ndim = geom->ndim;
@@ -945,13 +946,61 @@ static int index_list_impl(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, cons
         d.dx[k] = geom->dx[k];
         d.ilo[k] = geom->ilower[k];
         d.ihi[k] = geom->iupper[k];
+    }
+    return d;
+}
+
+// Two stable radix passes: by the Lagrangian index (lag, or the marker index
+// idx[i] / i when lag is null), then by the cell key; perm[i] = the entry of
+// rank i.  The sorted keys are left in kbuf's upper half.
+static int sort_cell_lag(ibtk_le_ctx ctx, const unsigned* cell_keys, const int* idx, const int* lag, int n,
+                         unsigned long long key_end, int* perm, DevBuf& kbuf, DevBuf& vbuf) {
+    const hipStream_t s = ctx->stream;
+    int rc;
+    if ((rc = kbuf.ensure(2 * sizeof(unsigned) * (size_t)n))) return rc;
+    if ((rc = vbuf.ensure(sizeof(int) * (size_t)n))) return rc;
+    unsigned* k0 = kbuf.as<unsigned>();
+    unsigned* k1 = k0 + n;
+    int* v0 = vbuf.as<int>();
+    size_t tb = 0;
+    HIP_TRY(launch_sort(nullptr, tb, k0, k1, v0, perm, n, 32, s));
+    if ((rc = ctx->temp.ensure(tb))) return rc;
+    tb = ctx->temp.cap;
+    HIP_TRY(launch_iota(v0, n, s));
+    if (lag) {  // pass 1 (entries are generated in marker order: the marker index needs no pass)
+        HIP_TRY(launch_perm_keys(0, nullptr, idx, lag, nullptr, n, k0, s));
+        HIP_TRY(launch_sort(ctx->temp.p, tb, k0, k1, v0, perm, n, 32, s));
+        HIP_TRY(hipMemcpyAsync(v0, perm, sizeof(int) * (size_t)n, hipMemcpyDeviceToDevice, s));
+    }
+    HIP_TRY(launch_perm_keys(1, v0, nullptr, nullptr, cell_keys, n, k0, s));
+    int end_bit = 1;
+    while (end_bit < 32 && (1ull << end_bit) <= key_end) ++end_bit;
+    HIP_TRY(launch_sort(ctx->temp.p, tb, k0, k1, v0, perm, n, end_bit, s));
+    return IBTK_LE_OK;
+}
+
+static int index_list_impl(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev, const int* lag_dev,
+                           int n_markers, int ghost, const int* periodic, int which, const int* box_lo,
+                           const int* box_hi, int* indices_dev, double* Xshift_dev, int capacity, int* count) {
+    if (!ctx || !count) return fail(IBTK_LE_ERR_ARG, "null argument");
+    if (int rc = check_geom(geom)) return rc;
+    if (n_markers < 0 || ghost < 0) return fail(IBTK_LE_ERR_ARG, "negative size");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    *count = 0;
+    if (n_markers == 0) return IBTK_LE_OK;
+    ImageDesc d = image_desc(geom, ghost);
+    d.which = which;
+    unsigned long long gcells = 1;
+    for (int k = 0; k < geom->ndim; ++k) {
         d.periodic[k] = periodic ? periodic[k] : 1;
         if (box_lo) {
             d.filter = 1;
             d.flo[k] = box_lo[k];
             d.fhi[k] = box_hi[k];
         }
+        gcells *= (unsigned long long)(geom->iupper[k] - geom->ilower[k] + 1 + 2 * ghost);
     }
+    if (gcells >= 0xffffffffull) return fail(IBTK_LE_ERR_RANGE, "ghost box has %llu cells", gcells);
     int rc;
     if ((rc = ctx->counts.ensure(sizeof(int) * (size_t)n_markers))) return rc;
     if ((rc = ctx->offsets.ensure(sizeof(int) * (size_t)n_markers))) return rc;
@@ -970,7 +1019,80 @@ static int index_list_impl(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, cons
     *count = total;
     if (total > capacity || !indices_dev || (!Xshift_dev && !box_lo))
         return fail(IBTK_LE_ERR_ARG, "index list needs %d entries, capacity %d", total, capacity);
-    HIP_TRY(launch_image_write(d, X_dev, n_markers, ctx->offsets.as<int>(), indices_dev, Xshift_dev, capacity, s));
+    if (box_lo) {  // LEInteractor.cpp:3110-3139: marker order
+        HIP_TRY(launch_image_write(d, X_dev, n_markers, ctx->offsets.as<int>(), indices_dev, Xshift_dev, nullptr,
+                                   capacity, s));
+        return IBTK_LE_OK;
+    }
+    if (total == 0) return IBTK_LE_OK;
+    // entries in marker order into scratch, then the reference's order: cells of
+    // the ghost box in iteration order (x fastest), Lagrangian index within a cell
+    const size_t nd = (size_t)geom->ndim;
+    if ((rc = ctx->lst_idx.ensure(sizeof(int) * (size_t)total))) return rc;
+    if ((rc = ctx->lst_xs.ensure(sizeof(double) * nd * (size_t)total))) return rc;
+    if ((rc = ctx->lst_key.ensure(sizeof(unsigned) * (size_t)total))) return rc;
+    if ((rc = ctx->lst_perm.ensure(sizeof(int) * (size_t)total))) return rc;
+    HIP_TRY(launch_image_write(d, X_dev, n_markers, ctx->offsets.as<int>(), ctx->lst_idx.as<int>(),
+                               ctx->lst_xs.as<double>(), ctx->lst_key.as<unsigned>(), total, s));
+    if ((rc = sort_cell_lag(ctx, ctx->lst_key.as<unsigned>(), ctx->lst_idx.as<int>(), lag_dev, total, gcells,
+                            ctx->lst_perm.as<int>(), ctx->keys_in, ctx->vals_in)))
+        return rc;
+    HIP_TRY(launch_perm_list(ctx->lst_perm.as<int>(), ctx->lst_idx.as<int>(), ctx->lst_xs.as<double>(), geom->ndim,
+                             total, indices_dev, Xshift_dev, s));
+    return IBTK_LE_OK;
+}
+
+// LDataManager::computeNodeDistribution (LDataManager.cpp:2839-3027) for one
+// patch whose LNodeSetData has `ghost` ghost cells: the local nodes -- markers
+// whose getCellIndex cell is in the patch box -- first, cell by cell in box
+// order (x fastest), each cell's set in Lagrangian-index order and uniqued
+// (LDataManager.cpp:1487-1493); then the nonlocal nodes of the ghost cells in
+// ghost-box order.  order_dev[i] = the input index of the node numbered i.
+extern "C" int ibtk_le_node_distribution(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
+                                         const int* lag_dev, int n_markers, int ghost, int* order_dev, int* n_local,
+                                         int* n_nonlocal) {
+    if (!ctx || !n_local || !n_nonlocal) return fail(IBTK_LE_ERR_ARG, "null argument");
+    if (int rc = check_geom(geom)) return rc;
+    if (n_markers < 0 || ghost < 0) return fail(IBTK_LE_ERR_ARG, "negative size");
+    if (n_markers > 0 && (!X_dev || !order_dev)) return fail(IBTK_LE_ERR_ARG, "null array");
+    *n_local = *n_nonlocal = 0;
+    if (n_markers == 0) return IBTK_LE_OK;
+    unsigned long long ncell = 1, gcells = 1;
+    for (int k = 0; k < geom->ndim; ++k) {
+        ncell *= (unsigned long long)(geom->iupper[k] - geom->ilower[k] + 1);
+        gcells *= (unsigned long long)(geom->iupper[k] - geom->ilower[k] + 1 + 2 * ghost);
+    }
+    if (ncell + gcells >= 0xffffffffull) return fail(IBTK_LE_ERR_RANGE, "patch too large for 32-bit cell keys");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    const ImageDesc d = image_desc(geom, ghost);
+    const hipStream_t s = ctx->stream;
+    const int n = n_markers;
+    int rc;
+    if ((rc = ctx->lst_key.ensure(sizeof(unsigned) * (size_t)n))) return rc;
+    if ((rc = ctx->lst_perm.ensure(sizeof(int) * (size_t)n))) return rc;
+    if ((rc = ctx->lst_idx.ensure(2 * sizeof(int) * (size_t)n))) return rc;  // flags | positions
+    if ((rc = ctx->counts.ensure(2 * sizeof(int)))) return rc;
+    HIP_TRY(launch_node_keys(d, X_dev, n, ctx->lst_key.as<unsigned>(), s));
+    if ((rc = sort_cell_lag(ctx, ctx->lst_key.as<unsigned>(), nullptr, lag_dev, n, 0xffffffffull,
+                            ctx->lst_perm.as<int>(), ctx->keys_in, ctx->vals_in)))
+        return rc;
+    const unsigned* skeys = ctx->keys_in.as<unsigned>() + n;  // sorted keys (sort_cell_lag)
+    int* flag = ctx->lst_idx.as<int>();
+    int* pos = flag + n;
+    HIP_TRY(launch_unique_flags(skeys, ctx->lst_perm.as<int>(), lag_dev, n, flag, s));
+    size_t tb = 0;
+    HIP_TRY(launch_scan(nullptr, tb, flag, pos, n, s));
+    if ((rc = ctx->temp.ensure(tb))) return rc;
+    tb = ctx->temp.cap;
+    HIP_TRY(launch_scan(ctx->temp.p, tb, flag, pos, n, s));
+    HIP_TRY(hipMemsetAsync(ctx->counts.p, 0, 2 * sizeof(int), s));
+    HIP_TRY(launch_compact(ctx->lst_perm.as<int>(), flag, pos, skeys, (unsigned)ncell, (unsigned)(ncell + gcells), n,
+                           order_dev, ctx->counts.as<int>(), s));
+    int cnt[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(cnt, ctx->counts.p, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *n_local = cnt[0];
+    *n_nonlocal = cnt[1];
     return IBTK_LE_OK;
 }
 

@@ -220,7 +220,7 @@ __device__ __forceinline__ void cell_index(const ImageDesc& d, const double* X, 
 }
 
 __device__ __forceinline__ int image_walk(const ImageDesc& d, const double* X, int* idx_out, double* xs_out,
-                                          int base, int capacity, int s) {
+                                          unsigned* key_out, int base, int capacity, int s) {
     int c[3] = {0, 0, 0};
     cell_index(d, X, c);
     if (d.filter) {  // LEInteractor.cpp:3129-3137: keep markers whose cell is in the box
@@ -249,8 +249,20 @@ __device__ __forceinline__ int image_walk(const ImageDesc& d, const double* X, i
             ok = ok && ci >= d.ilo[k] - d.ghost && ci <= d.ihi[k] + d.ghost;
         }
         if (!ok) continue;
+        // the image's cell: in the patch box (interior entry) or a ghost cell
+        bool interior = true;
+        unsigned key = 0, stride = 1;
+        for (int k = 0; k < d.ndim; ++k) {
+            const int n = d.ihi[k] - d.ilo[k] + 1;
+            const int ci = c[k] + sh[k] * n;
+            interior = interior && ci >= d.ilo[k] && ci <= d.ihi[k];
+            key += (unsigned)(ci - (d.ilo[k] - d.ghost)) * stride;  // ghost-box linear index, x fastest
+            stride *= (unsigned)(n + 2 * d.ghost);
+        }
+        if ((d.which == 1 && !interior) || (d.which == 2 && interior)) continue;
         if (idx_out && base + cnt < capacity) {
             idx_out[base + cnt] = s;
+            if (key_out) key_out[base + cnt] = key;
             for (int k = 0; k < d.ndim; ++k) {
                 const int n = d.ihi[k] - d.ilo[k] + 1;
                 // LIndexSetData.cpp:141: static_cast<double>(offset[d]) * dx[d]
@@ -265,13 +277,125 @@ __device__ __forceinline__ int image_walk(const ImageDesc& d, const double* X, i
 __global__ __launch_bounds__(BLOCK) void k_image_count(ImageDesc d, const double* X, int n, int* counts) {
     const int s = blockIdx.x * BLOCK + threadIdx.x;
     if (s >= n) return;
-    counts[s] = image_walk(d, X + (int64_t)d.ndim * s, nullptr, nullptr, 0, 0, s);
+    counts[s] = image_walk(d, X + (int64_t)d.ndim * s, nullptr, nullptr, nullptr, 0, 0, s);
 }
 __global__ __launch_bounds__(BLOCK) void k_image_write(ImageDesc d, const double* X, int n, const int* offsets,
-                                                        int* idx, double* xs, int capacity) {
+                                                        int* idx, double* xs, unsigned* cellkey, int capacity) {
     const int s = blockIdx.x * BLOCK + threadIdx.x;
     if (s >= n) return;
-    image_walk(d, X + (int64_t)d.ndim * s, idx, xs, offsets[s], capacity, s);
+    image_walk(d, X + (int64_t)d.ndim * s, idx, xs, cellkey, offsets[s], capacity, s);
+}
+
+// ---------------------------------------------------------------------------
+// reference-ordered lists: LIndexSetData::cacheLocalIndices walks the ghost
+// box's cells in iteration order and, in each cell, its LNodeSet -- sorted by
+// Lagrangian index and uniqued at redistribution (LDataManager.cpp:1487-1493).
+// Two stable radix passes (Lagrangian index, then cell) give that order.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(BLOCK) void k_iota(int* v, int n) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < n) v[i] = i;
+}
+__global__ __launch_bounds__(BLOCK) void k_perm_keys(int mode, const int* perm, const int* idx, const int* lag,
+                                                     const unsigned* keys, int n, unsigned* out) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const int j = perm ? perm[i] : i;
+    if (mode == 0) {
+        const int s = idx ? idx[j] : j;
+        out[i] = (unsigned)(lag ? lag[s] : s);
+    } else {
+        out[i] = keys[j];
+    }
+}
+__global__ __launch_bounds__(BLOCK) void k_perm_list(const int* perm, const int* idx, const double* xs, int ndim,
+                                                     int n, int* idx_out, double* xs_out) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const int j = perm[i];
+    idx_out[i] = idx[j];
+    if (xs_out)
+        for (int k = 0; k < ndim; ++k) xs_out[(int64_t)ndim * i + k] = xs[(int64_t)ndim * j + k];
+}
+// computeNodeDistribution (LDataManager.cpp:2874-2947) for one patch: key =
+// patch-box linear index (local nodes, numbered first), then ncell + ghost-box
+// linear index (the nonlocal nodes in the ghost cells), 0xffffffff outside.
+__global__ __launch_bounds__(BLOCK) void k_node_keys(ImageDesc d, const double* X, int n, unsigned* keys) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    int c[3] = {0, 0, 0};
+    cell_index(d, X + (int64_t)d.ndim * i, c);
+    bool in = true, ing = true;
+    unsigned kin = 0, sin = 1, kg = 0, sg = 1;
+    for (int k = 0; k < d.ndim; ++k) {
+        const int nk = d.ihi[k] - d.ilo[k] + 1;
+        in = in && c[k] >= d.ilo[k] && c[k] <= d.ihi[k];
+        ing = ing && c[k] >= d.ilo[k] - d.ghost && c[k] <= d.ihi[k] + d.ghost;
+        kin += (unsigned)(c[k] - d.ilo[k]) * sin;
+        sin *= (unsigned)nk;
+        kg += (unsigned)(c[k] - (d.ilo[k] - d.ghost)) * sg;
+        sg *= (unsigned)(nk + 2 * d.ghost);
+    }
+    keys[i] = in ? kin : (ing ? sin + kg : 0xffffffffu);
+}
+__global__ __launch_bounds__(BLOCK) void k_unique_flags(const unsigned* skeys, const int* sorder, const int* lag, int n,
+                                                        int* flag) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    bool first = i == 0 || skeys[i] != skeys[i - 1];
+    if (!first) {
+        const int a = sorder[i], b = sorder[i - 1];
+        first = (lag ? lag[a] : a) != (lag ? lag[b] : b);
+    }
+    flag[i] = first && skeys[i] != 0xffffffffu ? 1 : 0;
+}
+__global__ __launch_bounds__(BLOCK) void k_compact(const int* sorder, const int* flag, const int* pos,
+                                                   const unsigned* skeys, unsigned local_end, unsigned ghost_end, int n,
+                                                   int* out, int* counts) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    if (flag[i]) {
+        out[pos[i]] = sorder[i];
+        atomicAdd(counts + (skeys[i] < local_end ? 0 : 1), 1);
+    }
+}
+hipError_t launch_iota(int* v, int n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_iota, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, v, n);
+    return hipGetLastError();
+}
+hipError_t launch_perm_keys(int mode, const int* perm, const int* idx, const int* lag, const unsigned* keys, int n,
+                            unsigned* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_perm_keys, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, mode, perm, idx, lag, keys, n,
+                       out);
+    return hipGetLastError();
+}
+hipError_t launch_perm_list(const int* perm, const int* idx, const double* xs, int ndim, int n, int* idx_out,
+                            double* xs_out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_perm_list, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, perm, idx, xs, ndim, n, idx_out,
+                       xs_out);
+    return hipGetLastError();
+}
+hipError_t launch_node_keys(const ImageDesc& d, const double* X, int n, unsigned* keys, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_node_keys, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, d, X, n, keys);
+    return hipGetLastError();
+}
+hipError_t launch_unique_flags(const unsigned* skeys, const int* sorder, const int* lag, int n, int* flag,
+                               hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_unique_flags, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, skeys, sorder, lag, n, flag);
+    return hipGetLastError();
+}
+hipError_t launch_compact(const int* sorder, const int* flag, const int* pos, const unsigned* skeys,
+                          unsigned local_end, unsigned ghost_end, int n, int* out, int* counts, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    (void)ghost_end;
+    hipLaunchKernelGGL(k_compact, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, sorder, flag, pos, skeys,
+                       local_end, ghost_end, n, out, counts);
+    return hipGetLastError();
 }
 
 // Local numbering keys (LDataManager::computeNodeDistribution, LDataManager.cpp:
@@ -311,10 +435,10 @@ hipError_t launch_image_count(const ImageDesc& d, const double* X, int n, int* c
     return hipGetLastError();
 }
 hipError_t launch_image_write(const ImageDesc& d, const double* X, int n, const int* offsets, int* idx,
-                              double* xshift, int capacity, hipStream_t s) {
+                              double* xshift, unsigned* cellkey, int capacity, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_image_write, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, d, X, n, offsets, idx,
-                       xshift, capacity);
+                       xshift, cellkey, capacity);
     return hipGetLastError();
 }
 

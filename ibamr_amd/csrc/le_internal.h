@@ -198,6 +198,7 @@ struct ImageDesc {
     int periodic[3];
     int filter;           // 1: emit (s, 0) iff the cell lies in [flo, fhi] (no images)
     int flo[3], fhi[3];
+    int which;            // images: 0 every cell of the ghost box, 1 patch-box cells, 2 the others
 };
 hipError_t launch_cell_keys(const ImageDesc& d, const double* X, int n, unsigned ncells, unsigned* keys, int* vals,
                             int* inside, hipStream_t s);
@@ -207,7 +208,21 @@ hipError_t launch_max_index(const int* idx, int n, int* out, hipStream_t s);
 hipError_t launch_dedup(const int* indices, const int* sorted_l, const int* sorted_s, int n, int* last, int* qdst,
                         int* ndup, hipStream_t s);
 hipError_t launch_image_write(const ImageDesc& d, const double* X, int n, const int* offsets, int* idx,
-                              double* xshift, int capacity, hipStream_t s);
+                              double* xshift, unsigned* cellkey, int capacity, hipStream_t s);
+// small helpers of the reference-ordered lists (le_aux.hip)
+hipError_t launch_iota(int* v, int n, hipStream_t s);
+// out[i] = key_of(src[perm[i]]): mode 0 lag[idx[perm[i]]] (lag null: idx[perm[i]]), mode 1 keys[perm[i]]
+hipError_t launch_perm_keys(int mode, const int* perm, const int* idx, const int* lag, const unsigned* keys, int n,
+                            unsigned* out, hipStream_t s);
+hipError_t launch_perm_list(const int* perm, const int* idx, const double* xs, int ndim, int n, int* idx_out,
+                            double* xs_out, hipStream_t s);
+// node distribution: region/cell keys (local cells, then the ghost box's others, then out)
+hipError_t launch_node_keys(const ImageDesc& d, const double* X, int n, unsigned* keys, hipStream_t s);
+// unique by (key, lag) over the sorted order: flag[i] = 1 for a first occurrence
+hipError_t launch_unique_flags(const unsigned* skeys, const int* sorder, const int* lag, int n, int* flag,
+                               hipStream_t s);
+hipError_t launch_compact(const int* sorder, const int* flag, const int* pos, const unsigned* skeys,
+                          unsigned local_end, unsigned ghost_end, int n, int* out, int* counts, hipStream_t s);
 
 // Physical-boundary ghost operators on one side-centred patch (le_bdry.hip)
 struct BdSide {

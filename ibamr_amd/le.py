@@ -337,8 +337,43 @@ def position_update(ctx: Context, scheme: str, dt: float, X: torch.Tensor, U0: t
     return out
 
 
+def index_set_list(ctx: Context, geom: Geometry, X: torch.Tensor, ghost: int, lag: Optional[torch.Tensor] = None,
+                   periodic=None, which: str = "all"):
+    """LIndexSetData::cacheLocalIndices' lists on the device (ibtk_le_index_set_list):
+    (indices int32, Xshift float64 [n, ndim]) in the reference's order (ghost-box
+    cells in iteration order, Lagrangian index within a cell).  which: "all",
+    "interior" or "ghost"."""
+    M = X.shape[0]
+    cnt = ctypes.c_int(0)
+    pa = _periodic_arg(periodic, geom.ndim)
+    w = {"all": 0, "interior": 1, "ghost": 2}[which]
+    if lag is not None and (lag.dtype != torch.int32 or lag.numel() != M):
+        raise ValueError("lag: one int32 per marker")
+    cap = M * (3 ** geom.ndim) if ghost > 0 else M
+    idx = torch.empty(max(1, cap), dtype=torch.int32, device=X.device)
+    xs = torch.empty((max(1, cap), geom.ndim), dtype=torch.float64, device=X.device)
+    check(ctx.lib.ibtk_le_index_set_list(ctx.h, ctypes.byref(geom.c), _ptr(X), _ptr(lag), M, ghost,
+                                         pa[0] if pa else None, w, _ptr(idx), _ptr(xs), cap, ctypes.byref(cnt)))
+    n = cnt.value
+    return idx[:n].contiguous(), xs[:n].contiguous()
+
+
+def node_distribution(ctx: Context, geom: Geometry, X: torch.Tensor, ghost: int, lag: Optional[torch.Tensor] = None):
+    """LDataManager::computeNodeDistribution for one patch (ibtk_le_node_distribution):
+    (order int32 device tensor, n_local, n_nonlocal)."""
+    M = X.shape[0]
+    if lag is not None and (lag.dtype != torch.int32 or lag.numel() != M):
+        raise ValueError("lag: one int32 per marker")
+    order = torch.empty(max(M, 1), dtype=torch.int32, device=X.device)
+    nl, ng = ctypes.c_int(0), ctypes.c_int(0)
+    check(ctx.lib.ibtk_le_node_distribution(ctx.h, ctypes.byref(geom.c), _ptr(X), _ptr(lag), M, ghost, _ptr(order),
+                                            ctypes.byref(nl), ctypes.byref(ng)))
+    return order[:nl.value + ng.value].contiguous(), nl.value, ng.value
+
+
 def periodic_index_list(ctx: Context, geom: Geometry, X: torch.Tensor, ghost: int, periodic=None):
-    """(indices int32, Xshift float64 [n, ndim]) device tensors, marker-major order."""
+    """(indices int32, Xshift float64 [n, ndim]) device tensors, in the reference's
+    order (ghost-box cells in iteration order, marker index within a cell)."""
     M = X.shape[0]
     cnt = ctypes.c_int(0)
     pa = _periodic_arg(periodic, geom.ndim)

@@ -194,13 +194,37 @@ int ibtk_le_local_numbering(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, con
 /* Build the list of interior markers and of their periodic images that fall in the
  * ghost box (LIndexSetData::cacheLocalIndices, LIndexSetData.cpp:83-169, for one
  * patch covering a periodic domain; getCellIndex, IndexUtilities-inl.h:66-89).
- * Writes up to `capacity` entries into indices_dev / Xshift_dev (NDIM per entry)
- * and the entry count into *count (host).  ghost = 0 gives the interior list.
+ * Order: the reference's -- the ghost box's cells in iteration order (x fastest;
+ * an image sits in its shifted cell), each cell's markers by index.  Writes up to
+ * `capacity` entries into indices_dev / Xshift_dev (NDIM per entry) and the
+ * entry count into *count (host).  ghost = 0 gives the interior list.
  * If the list needs more than `capacity` entries, nothing is written, *count
- * holds the required size and IBTK_LE_ERR_ARG is returned. */
+ * holds the required size and IBTK_LE_ERR_ARG is returned.  Synchronises. */
 int ibtk_le_periodic_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
                                 int n_markers, int ghost, const int* periodic, int* indices_dev,
                                 double* Xshift_dev, int capacity, int* count);
+/* The same lists with the Lagrangian index of every marker (lag_dev[s]; NULL = s):
+ * within a cell the entries follow the LNodeSet order, sorted by Lagrangian index
+ * (LDataManager.cpp:1487-1493).  which = 0: every entry (d_local_petsc_indices /
+ * d_periodic_shifts), 1: the cells of the patch box (d_interior_*), 2: the other
+ * ghost-box cells (d_ghost_*) -- the three lists cacheLocalIndices caches.
+ * SAMRAI's IndexData walks its items in insertion order; the lists take the
+ * box iteration order, which that insertion order follows for sets appended
+ * cell by cell (LDataManager.cpp:1446-1482 walks the cells in box order). */
+int ibtk_le_index_set_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev, const int* lag_dev,
+                           int n_markers, int ghost, const int* periodic, int which, int* indices_dev,
+                           double* Xshift_dev, int capacity, int* count);
+/* LDataManager::computeNodeDistribution (LDataManager.cpp:2839-3027) for one patch
+ * whose marker index data has `ghost` ghost cells: order_dev[i] = the input index
+ * of the marker numbered i.  The local nodes (getCellIndex cell in the patch box)
+ * come first, cell by cell in box order (x fastest), each cell by Lagrangian index
+ * (lag_dev; NULL = input index) with repeated (cell, Lagrangian index) pairs kept
+ * once (LDataManager.cpp:1487-1493); then the nonlocal nodes of the ghost cells in
+ * ghost-box order.  Markers outside the ghost box are dropped.  *n_local and
+ * *n_nonlocal (host) receive the counts.  Synchronises. */
+int ibtk_le_node_distribution(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
+                              const int* lag_dev, int n_markers, int ghost, int* order_dev, int* n_local,
+                              int* n_nonlocal);
 
 /* Markers whose cell (IndexUtilities::getCellIndex against the patch box) lies in
  * [box_lo, box_hi], no periodic shifts: the list LEInteractor's X-only overloads

@@ -238,14 +238,18 @@ def get_cell_index(X, x_lower, x_upper, dx, ilower, iupper):
     return out
 
 
-def periodic_index_list(X, x_lower, x_upper, dx, box_lo, box_hi, ghost, periodic=None):
+def periodic_index_list(X, x_lower, x_upper, dx, box_lo, box_hi, ghost, periodic=None, lag=None, which="all"):
     """(indices, Xshift, cells) for one patch covering a periodic domain.
 
     Every marker appears once at its own cell (interior) and once per periodic
     image whose cell falls in the ghost box, with Xshift = +/-L in the
     wrapped dims -- the lists LIndexSetData::cacheLocalIndices builds
     (LIndexSetData.cpp:111-166: offset = -periodic_shift below the patch,
-    +periodic_shift above it).  Order: cell-major (x fastest), then marker.
+    +periodic_shift above it).  Order: the ghost box's cells in iteration order
+    (x fastest), within a cell by Lagrangian index (lag[s]; the marker index s
+    when lag is None) -- the LNodeSet order after LDataManager.cpp:1487-1493's
+    sort.  which: "all" (d_local_petsc_indices), "interior" (cells in the patch
+    box, d_interior_*) or "ghost" (the others, d_ghost_*), LIndexSetData.cpp:143-165.
     """
     X = np.asarray(X, dtype=np.float64)
     M, ndim = X.shape
@@ -272,15 +276,55 @@ def periodic_index_list(X, x_lower, x_upper, dx, box_lo, box_hi, ghost, periodic
     s = np.concatenate(ents_s)
     off = np.concatenate(ents_off)
     cell = np.concatenate(ents_cell)
-    # cell-major order (x fastest) then marker index: the IndexData iteration order
+    # cell-major order (x fastest) then Lagrangian index: the IndexData iteration order
     key = np.zeros(s.size, dtype=np.int64)
     stride = 1
+    interior = np.ones(s.size, dtype=bool)
     for d in range(ndim):
         key += (cell[:, d] - (box_lo[d] - ghost)) * stride
         stride *= N[d] + 2 * ghost
-    order = np.lexsort((s, key))
+        interior &= (cell[:, d] >= box_lo[d]) & (cell[:, d] <= box_hi[d])
+    sel = {"all": np.ones(s.size, dtype=bool), "interior": interior, "ghost": ~interior}[which]
+    s, off, cell, key = s[sel], off[sel], cell[sel], key[sel]
+    lagv = s if lag is None else np.asarray(lag)[s]
+    order = np.lexsort((lagv, key))
     Xshift = off[order].astype(np.float64) * np.asarray(dx)[None, :]
     return s[order].astype(np.int32), Xshift, cell[order]
+
+
+def node_distribution(X, x_lower, x_upper, dx, box_lo, box_hi, ghost, lag=None):
+    """LDataManager::computeNodeDistribution (LDataManager.cpp:2874-2947) for one
+    patch: (order, n_local, n_nonlocal).  Local nodes (getCellIndex cell in the
+    patch box) in box order (x fastest), each cell's LNodeSet sorted by Lagrangian
+    index and uniqued (LDataManager.cpp:1487-1493); then the nonlocal nodes of the
+    ghost cells (ghost-box order, same within-cell rule); markers beyond the ghost
+    box are not numbered.  order[i] = input index of the node numbered i."""
+    X = np.asarray(X, dtype=np.float64)
+    M, ndim = X.shape
+    lagv = np.arange(M) if lag is None else np.asarray(lag, dtype=np.int64)
+    c = get_cell_index(X, x_lower, x_upper, dx, box_lo, box_hi)
+    N = [box_hi[d] - box_lo[d] + 1 for d in range(ndim)]
+    inside = np.ones(M, dtype=bool)
+    ing = np.ones(M, dtype=bool)
+    kin = np.zeros(M, dtype=np.int64)
+    kg = np.zeros(M, dtype=np.int64)
+    si = sg = 1
+    for d in range(ndim):
+        inside &= (c[:, d] >= box_lo[d]) & (c[:, d] <= box_hi[d])
+        ing &= (c[:, d] >= box_lo[d] - ghost) & (c[:, d] <= box_hi[d] + ghost)
+        kin += (c[:, d] - box_lo[d]) * si
+        kg += (c[:, d] - (box_lo[d] - ghost)) * sg
+        si *= N[d]
+        sg *= N[d] + 2 * ghost
+    key = np.where(inside, kin, np.where(ing, si + kg, np.iinfo(np.int64).max))
+    order = np.lexsort((np.arange(M), lagv, key))
+    ks, ls = key[order], lagv[order]
+    keep = np.ones(M, dtype=bool)
+    keep[1:] = (ks[1:] != ks[:-1]) | (ls[1:] != ls[:-1])
+    keep &= ks != np.iinfo(np.int64).max
+    order = order[keep]
+    n_local = int((key[order] < si).sum())
+    return order.astype(np.int32), n_local, int(order.size - n_local)
 
 
 # --------------------------------------------------------------------------
