@@ -256,7 +256,16 @@ def periodic_index_list(X, x_lower, x_upper, dx, box_lo, box_hi, ghost, periodic
     periodic = [True] * ndim if periodic is None else periodic
     N = [box_hi[d] - box_lo[d] + 1 for d in range(ndim)]
     cells = get_cell_index(X, x_lower, x_upper, dx, box_lo, box_hi)
-    ents_s, ents_off, ents_cell = [np.arange(M)], [np.zeros((M, ndim), np.int64)], [cells]
+    # the patch's own markers: beginDataRedistribution keeps a marker in the patch
+    # whose box holds its cell (LDataManager.cpp:1457-1482); the ghost cells get
+    # the periodic images of those
+    own = np.ones(M, dtype=bool)
+    for d in range(ndim):
+        own &= (cells[:, d] >= box_lo[d]) & (cells[:, d] <= box_hi[d])
+    ids = np.nonzero(own)[0]
+    cells = cells[ids]
+    M = ids.size
+    ents_s, ents_off, ents_cell = [ids], [np.zeros((M, ndim), np.int64)], [cells]
     # images: shift the cell by -N (image below) or +N (image above) per dim
     import itertools
     for shifts in itertools.product(*[(-1, 0, 1) if periodic[d] else (0,) for d in range(ndim)]):
@@ -270,7 +279,7 @@ def periodic_index_list(X, x_lower, x_upper, dx, box_lo, box_hi, ghost, periodic
             inside &= (c[:, d] >= box_lo[d] - ghost) & (c[:, d] <= box_hi[d] + ghost)
         if inside.any():
             sel = np.nonzero(inside)[0]
-            ents_s.append(sel)
+            ents_s.append(ids[sel])
             ents_off.append(np.tile(np.array(shifts, np.int64) * np.array(N), (sel.size, 1)))
             ents_cell.append(c[sel])
     s = np.concatenate(ents_s)

@@ -49,7 +49,7 @@ def test_device_weights_known_answer(le, ctx, kernel, ndim):
     cases = [c for c in GOLDEN["cases"] if c["kernel"] == kname and c.get("axis_dim", True) != off]
     assert cases
     axis = 1 if off else 0
-    g = 6
+    g = 8
     nx, ny = 21, 4
     ilo = [0] * ndim
     ihi = [nx - 1] + [ny - 1] * (ndim - 1)

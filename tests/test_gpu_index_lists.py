@@ -42,9 +42,10 @@ def _case(le, ndim, M, seed, dup_lag=False):
     geom = le.Geometry.periodic_unit(N, 3)
     rng = np.random.default_rng(seed)
     X = rng.uniform(0.0, 1.0, (M, ndim))
-    # some exactly on cell faces (getCellIndex's lower/upper corner rule), some at the domain faces
+    # some exactly on cell faces (getCellIndex's lower/upper corner rule), the
+    # domain's lower face included (positions are wrapped into [0, 1))
     k = max(1, M // 10)
-    X[:k] = np.round(X[:k] * np.array(N)) / np.array(N)
+    X[:k] = np.floor(X[:k] * np.array(N)) / np.array(N)
     lag = rng.permutation(M).astype(np.int32) * 3 + 7
     if dup_lag and M > 10:
         lag[M // 2:M // 2 + 5] = lag[:5]  # repeated Lagrangian indices (a marker registered twice)
