@@ -109,6 +109,13 @@ _SIGS = [
     ("ibtk_le_mark_stencils", c_int,
      [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_int,
       c_void_p]),
+    ("ibtk_le_level_bin", c_int,
+     [c_void_p, c_void_p, c_int, ctypes.POINTER(PatchGeom), c_int, c_void_p, ctypes.POINTER(c_int), c_void_p,
+      c_void_p]),
+    ("ibtk_le_level_interp", c_int,
+     [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(c_void_p), c_int, c_void_p, c_int, c_void_p]),
+    ("ibtk_le_level_spread", c_int,
+     [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(c_void_p), c_int, c_void_p, c_int, c_void_p]),
     ("ibtk_le_index_set_list", c_int,
      [c_void_p, ctypes.POINTER(PatchGeom), c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
       c_int, ctypes.POINTER(c_int)]),

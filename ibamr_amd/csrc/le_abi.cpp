@@ -123,6 +123,12 @@ struct ibtk_le_markers_s {
     DevBuf last, qdst;                    // interp with duplicate list entries (Params::qdst)
     DevBuf items, nsub, isub, nitems;     // 3-D sweep item table
     int item_bound = 0;
+    // a level of patches (ibtk_le_level_bin): 0 = one patch (the fields above)
+    int npatch = 0;
+    std::vector<ibtk_le_patch_geom> geoms;
+    std::vector<PatchDesc> pdh;           // host copy of the patch table (comps filled per call)
+    DevBuf pd, entry_off;
+    int nbuckets_total = 0, njobs = 0;
     bool has_indices = false, has_xshift = false;
     bool cand_valid = false;
     bool dedup_done = false, has_dups = false;
@@ -409,7 +415,7 @@ extern "C" int ibtk_le_markers_destroy(ibtk_le_markers m) {
     hipStreamSynchronize(m->ctx->stream);
     for (DevBuf* b : {&m->sorted_key, &m->sorted_l, &m->sorted_s, &m->sorted_X, &m->sorted_a, &m->plane_start, &m->indices,
                       &m->xshift, &m->cand_cnt, &m->cand_off, &m->cand_idx, &m->last, &m->qdst, &m->items,
-                      &m->nsub, &m->isub, &m->nitems})
+                      &m->nsub, &m->isub, &m->nitems, &m->pd, &m->entry_off})
         b->release();
     delete m;
     return IBTK_LE_OK;
@@ -431,7 +437,7 @@ extern "C" int ibtk_le_markers_order(ibtk_le_markers m, const int** order_dev) {
 #define IBTK_LE_SPLIT_TARGET 12288  // own markers per item above which it is cut (cfg4 items hold ~6.8K)
 #endif
 static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel) {
-    const int nj = m->cg.ncol * m->nseg;
+    const int nj = m->npatch ? m->njobs : m->cg.ncol * m->nseg;
     const int target = ctx->tune.split_target > 0 ? ctx->tune.split_target : IBTK_LE_SPLIT_TARGET;
     const long long bound = (long long)nj + (long long)m->n / target + 1;
     if (bound * 3 >= (1LL << 31)) return fail(IBTK_LE_ERR_RANGE, "too many sweep items");
@@ -446,7 +452,12 @@ static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel) {
     p.cg = m->cg;
     p.S = m->S;
     p.nseg = m->nseg;
+    p.njobs = nj;
     p.plane_start = m->plane_start.as<int>();
+    if (m->npatch) {
+        p.pd = m->pd.as<PatchDesc>();
+        p.npatch = m->npatch;
+    }
     size_t tb = 0;
     HIP_TRY(launch_scan(nullptr, tb, m->nsub.as<int>(), m->isub.as<int>(), std::max(nj, 1), ctx->stream));
     if ((rc = ctx->temp.ensure(tb))) return rc;
@@ -479,6 +490,8 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     m->ndim = geom->ndim;
     m->bg = bg;
     m->cg = cg;
+    m->npatch = 0;
+    m->nbuckets_total = cg.nbuckets;
     if (cols) sweep_segments(cg, m->S, m->nseg, ctx->tune.seg_items);
     m->geom = *geom;
     m->has_indices = indices_dev != nullptr;
@@ -514,6 +527,7 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     std::memset(&p, 0, sizeof(p));
     p.bg = bg;
     p.cg = cg;
+    p.nbuckets_total = cg.nbuckets;
     p.X = X_dev;
     p.indices = m->has_indices ? m->indices.as<int>() : nullptr;
     p.Xshift = m->has_xshift ? m->xshift.as<double>() : nullptr;
@@ -565,6 +579,7 @@ static int prepare(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const ibtk_le
     if (m->kernel != kernel)
         return fail(IBTK_LE_ERR_ARG, "markers were binned for kernel %s, not %s",
                     m->kernel >= 0 ? kNames[m->kernel] : "(none)", kNames[kernel]);
+    if (m->npatch) return fail(IBTK_LE_ERR_ARG, "markers were binned for a level: use ibtk_le_level_interp/spread");
     if (!same_geom(m->geom, *geom)) return fail(IBTK_LE_ERR_ARG, "markers were binned for a different patch geometry");
     if (m->n > 0 && !X) return fail(IBTK_LE_ERR_ARG, "null X");
     std::memset(&p, 0, sizeof(p));
@@ -575,6 +590,7 @@ static int prepare(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const ibtk_le
     p.items = m->items.as<SweepItem>();
     p.nitems = m->nitems.as<int>();
     p.item_bound = m->item_bound;
+    p.nbuckets_total = m->nbuckets_total;
     p.sorted_a = m->sorted_a.as<unsigned>();
     p.nsorted = m->n;
     p.X = X;
@@ -771,6 +787,222 @@ static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cente
         }
         if (t) ctx->ev_valid = true;
     }
+    return IBTK_LE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// a level of patches: LDataManager::spread / interp's patch loop
+// (LDataManager.cpp:625-660, 763-807) as one launch per sweep
+// ---------------------------------------------------------------------------
+extern "C" int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch, const ibtk_le_patch_geom* geoms,
+                                 int kernel, const double* X_dev, const int* entry_offsets, const int* indices_dev,
+                                 const double* Xshift_dev) {
+    if (!ctx || !m || !geoms || !entry_offsets) return fail(IBTK_LE_ERR_ARG, "level_bin: null argument");
+    if (npatch <= 0) return fail(IBTK_LE_ERR_ARG, "level_bin: no patches");
+    if (kernel < 0 || kernel >= K_COUNT) return fail(IBTK_LE_ERR_UNKNOWN_KERNEL, "Unknown kernel function %d", kernel);
+    for (int q = 0; q < npatch; ++q) {
+        if (int rc = check_geom(&geoms[q])) return rc;
+        if (geoms[q].ndim != 3) return fail(IBTK_LE_ERR_ARG, "level_bin: 3-D patches only");
+        for (int d = 0; d < 3; ++d)
+            if (geoms[q].dx[d] != geoms[0].dx[d]) return fail(IBTK_LE_ERR_ARG, "level_bin: patches of one level share dx");
+        if (entry_offsets[q + 1] < entry_offsets[q]) return fail(IBTK_LE_ERR_ARG, "level_bin: decreasing offsets");
+    }
+    if (entry_offsets[0] != 0) return fail(IBTK_LE_ERR_ARG, "level_bin: entry_offsets[0] must be 0");
+    const int n = entry_offsets[npatch];
+    if (n > 0 && !X_dev) return fail(IBTK_LE_ERR_ARG, "null X");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    const hipStream_t s = ctx->stream;
+    m->npatch = npatch;
+    m->geoms.assign(geoms, geoms + npatch);
+    m->pdh.assign((size_t)npatch, PatchDesc{});
+    long long nb = 0, nj = 0;
+    BinGeom bg0{};
+    for (int q = 0; q < npatch; ++q) {
+        BinGeom bg;
+        ColGeom cg;
+        if (int rc = make_col_geom(&geoms[q], kernel, bg, cg)) return rc;
+        if (q == 0) bg0 = bg;
+        PatchDesc& P = m->pdh[q];
+        std::memset(&P, 0, sizeof(P));
+        P.cg = cg;
+        P.bucket_base = (int)nb;
+        P.jbase = (int)nj;
+        sweep_segments(cg, P.S, P.nseg, ctx->tune.seg_items);
+        for (int d = 0; d < 3; ++d) {
+            P.xlo[d] = geoms[q].x_lower[d];
+            P.ilower[d] = geoms[q].ilower[d];
+        }
+        nb += cg.nbuckets;
+        nj += (long long)cg.ncol * P.nseg;
+        if (nb + 1 >= (1LL << 31) || nj >= (1LL << 30)) return fail(IBTK_LE_ERR_RANGE, "level too large for 31-bit keys");
+    }
+    m->nbuckets_total = (int)nb;
+    m->njobs = (int)nj;
+    m->n = n;
+    m->kernel = kernel;
+    m->ndim = 3;
+    m->bg = bg0;
+    m->cg = m->pdh[0].cg;
+    m->S = m->pdh[0].S;
+    m->nseg = m->pdh[0].nseg;
+    m->geom = geoms[0];
+    m->has_indices = indices_dev != nullptr;
+    m->has_xshift = Xshift_dev != nullptr;
+    m->cand_valid = false;
+    m->dedup_done = false;
+    m->has_dups = false;
+    int rc;
+    if ((rc = m->pd.ensure(sizeof(PatchDesc) * (size_t)npatch))) return rc;
+    if ((rc = m->entry_off.ensure(sizeof(int) * (size_t)(npatch + 1)))) return rc;
+    HIP_TRY(hipMemcpyAsync(m->pd.p, m->pdh.data(), sizeof(PatchDesc) * (size_t)npatch, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(m->entry_off.p, entry_offsets, sizeof(int) * (size_t)(npatch + 1), hipMemcpyHostToDevice,
+                           s));
+    if ((rc = m->plane_start.ensure(sizeof(int) * (size_t)(nb + 1)))) return rc;
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(m->plane_start.p, 0, sizeof(int) * (size_t)(nb + 1), s));
+        return build_items(ctx, m, kernel);
+    }
+    if ((rc = m->sorted_key.ensure(sizeof(unsigned) * (size_t)n))) return rc;
+    if ((rc = m->sorted_l.ensure(sizeof(int) * (size_t)n))) return rc;
+    if ((rc = m->sorted_s.ensure(sizeof(int) * (size_t)n))) return rc;
+    if ((rc = m->sorted_X.ensure(sizeof(double) * (size_t)n * 3))) return rc;
+    if ((rc = ctx->keys_in.ensure(sizeof(unsigned) * (size_t)n))) return rc;
+    if ((rc = ctx->vals_in.ensure(sizeof(int) * (size_t)n))) return rc;
+    if (m->has_indices) {
+        if ((rc = m->indices.ensure(sizeof(int) * (size_t)n))) return rc;
+        HIP_TRY(hipMemcpyAsync(m->indices.p, indices_dev, sizeof(int) * (size_t)n, hipMemcpyDeviceToDevice, s));
+    }
+    if (m->has_xshift) {
+        if ((rc = m->xshift.ensure(sizeof(double) * (size_t)n * 3))) return rc;
+        HIP_TRY(hipMemcpyAsync(m->xshift.p, Xshift_dev, sizeof(double) * (size_t)n * 3, hipMemcpyDeviceToDevice, s));
+    }
+    Params p;
+    std::memset(&p, 0, sizeof(p));
+    p.bg = bg0;
+    p.cg = m->cg;
+    p.pd = m->pd.as<PatchDesc>();
+    p.npatch = npatch;
+    p.entry_off = m->entry_off.as<int>();
+    p.nbuckets_total = (int)nb;
+    p.X = X_dev;
+    p.indices = m->has_indices ? m->indices.as<int>() : nullptr;
+    p.Xshift = m->has_xshift ? m->xshift.as<double>() : nullptr;
+    HIP_TRY(launch_bin_col(kernel, p, n, ctx->keys_in.as<unsigned>(), ctx->vals_in.as<int>(), s));
+    int end_bit = 1;
+    while ((1ULL << end_bit) <= (unsigned long long)nb) ++end_bit;
+    size_t tb = 0;
+    HIP_TRY(launch_sort(nullptr, tb, ctx->keys_in.as<unsigned>(), m->sorted_key.as<unsigned>(), ctx->vals_in.as<int>(),
+                        m->sorted_l.as<int>(), n, end_bit, s));
+    if ((rc = ctx->temp.ensure(tb))) return rc;
+    tb = ctx->temp.cap;
+    HIP_TRY(launch_sort(ctx->temp.p, tb, ctx->keys_in.as<unsigned>(), m->sorted_key.as<unsigned>(),
+                        ctx->vals_in.as<int>(), m->sorted_l.as<int>(), n, end_bit, s));
+    p.sorted_l = m->sorted_l.as<int>();
+    HIP_TRY(launch_gather_col(kernel, p, n, m->sorted_s.as<int>(), m->sorted_X.as<double>(),
+                              m->sorted_key.as<unsigned>(), (int)nb, m->plane_start.as<int>(), s));
+    return build_items(ctx, m, kernel);
+}
+
+// Params of a level call: the patch table with the component arrays of this
+// call (q_dev: the arrays of patch 0, then patch 1, ...; per patch NDIM side or
+// edge arrays, or one cell / node array), uploaded in stream order.
+static int level_params(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                        double* const* q_dev, int q_depth, int Q_depth, const double* X, bool interp, Params& p,
+                        int& nc) {
+    if (!ctx || !m) return fail(IBTK_LE_ERR_ARG, "null ctx/markers");
+    if (!m->npatch) return fail(IBTK_LE_ERR_ARG, "markers were not binned for a level (ibtk_le_level_bin)");
+    if (kernel != m->kernel) return fail(IBTK_LE_ERR_ARG, "markers were binned for another kernel");
+    if (m->n > 0 && !X) return fail(IBTK_LE_ERR_ARG, "null X");
+    nc = ncomponents(&m->geoms[0], centering, q_depth, Q_depth);
+    if (nc < 0) return -nc;
+    if (nc > MAXC) return fail(IBTK_LE_ERR_ARG, "level calls take at most %d components", MAXC);
+    if (!q_dev) return fail(IBTK_LE_ERR_ARG, "null q");
+    const int per = (centering == IBTK_LE_SIDE || centering == IBTK_LE_EDGE) ? 3 : 1;
+    for (int q = 0; q < m->npatch; ++q) {
+        const ibtk_le_patch_geom& g = m->geoms[q];
+        if (interp) {  // LEInteractor.cpp:2416-2426
+            const int gmin = std::min(g.gcw[0], std::min(g.gcw[1], g.gcw[2]));
+            if (gmin < ibtk_le_min_ghost_width(kernel))
+                return fail(IBTK_LE_ERR_GHOST_WIDTH, "LEInteractor::interpolate(): insufficient ghost cells in patch %d",
+                            q);
+        }
+        Params t;
+        std::memset(&t, 0, sizeof(t));
+        if (int rc = make_comps(&g, centering, axis, q_dev + (size_t)q * per, q_depth, Q_depth, 0, nc, t)) return rc;
+        std::memcpy(m->pdh[q].comp, t.comp, sizeof(t.comp));
+        if (q == 0) std::memcpy(p.comp, t.comp, sizeof(t.comp));
+    }
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    HIP_TRY(hipMemcpyAsync(m->pd.p, m->pdh.data(), sizeof(PatchDesc) * (size_t)m->npatch, hipMemcpyHostToDevice,
+                           ctx->stream));
+    p.ncomp = nc;
+    p.bg = m->bg;
+    p.cg = m->cg;
+    p.S = m->S;
+    p.nseg = m->nseg;
+    p.pd = m->pd.as<PatchDesc>();
+    p.npatch = m->npatch;
+    p.entry_off = m->entry_off.as<int>();
+    p.nbuckets_total = m->nbuckets_total;
+    p.njobs = m->njobs;
+    p.items = m->items.as<SweepItem>();
+    p.nitems = m->nitems.as<int>();
+    p.item_bound = m->item_bound;
+    p.nsorted = m->n;
+    p.X = X;
+    p.indices = m->has_indices ? m->indices.as<int>() : nullptr;
+    p.Xshift = m->has_xshift ? m->xshift.as<double>() : nullptr;
+    p.sorted_l = m->sorted_l.as<int>();
+    p.sorted_s = m->sorted_s.as<int>();
+    p.sorted_X = m->sorted_X.as<double>();
+    p.sorted_key = m->sorted_key.as<unsigned>();
+    p.plane_start = m->plane_start.as<int>();
+    p.err = ctx->err.as<int>();
+    p.sink = ctx->sink.as<double>();
+    p.K6 = ib6_K();
+    p.h3 = (m->geoms[0].dx[0] * m->geoms[0].dx[1]) * m->geoms[0].dx[2];
+    p.Q_depth = Q_depth;
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_level_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                                    const double* const* q_dev, int q_depth, double* Q_dev, int Q_depth,
+                                    const double* X_dev) {
+    Params p;
+    std::memset(&p, 0, sizeof(p));
+    int nc = 0;
+    if (int rc = level_params(ctx, m, kernel, centering, axis, const_cast<double* const*>(q_dev), q_depth, Q_depth,
+                              X_dev, true, p, nc))
+        return rc;
+    if (m->n == 0) return IBTK_LE_OK;
+    if (!Q_dev) return fail(IBTK_LE_ERR_ARG, "null Q");
+    if (int rc = build_dedup(ctx, m)) return rc;
+    p.qdst = m->has_dups ? m->qdst.as<int>() : nullptr;
+    p.Qout = Q_dev;
+    const bool t = ctx->timing;
+    ctx->ev_valid = false;
+    HIP_TRY(launch_interp_sweep(kernel, p, m->n, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
+    if (t) ctx->ev_valid = true;
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_level_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                                    double* const* q_dev, int q_depth, const double* Q_dev, int Q_depth,
+                                    const double* X_dev) {
+    Params p;
+    std::memset(&p, 0, sizeof(p));
+    int nc = 0;
+    if (int rc = level_params(ctx, m, kernel, centering, axis, q_dev, q_depth, Q_depth, X_dev, false, p, nc))
+        return rc;
+    if (m->n == 0) return IBTK_LE_OK;
+    if (!Q_dev) return fail(IBTK_LE_ERR_ARG, "null Q");
+    p.Qin = Q_dev;
+    if (int rc = ctx->fbuf.ensure(sizeof(double) * (size_t)m->n * (size_t)nc)) return rc;
+    p.sorted_F = ctx->fbuf.as<double>();
+    const bool t = ctx->timing;
+    ctx->ev_valid = false;
+    HIP_TRY(launch_spread_sweep(kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
+    if (t) ctx->ev_valid = true;
     return IBTK_LE_OK;
 }
 

@@ -103,9 +103,21 @@ struct SweepTune {
     int seg_items = 0;     // sweep_segments' item target
     int split_target = 0;  // own markers above which a (column, segment) is cut (k_item_counts)
 };
-// One 3-D sweep item: a column and its owned planes [p0, p1) (relative to cg.org[2]).
+// One 3-D sweep item: a patch, a column and its owned planes [p0, p1) (relative
+// to the patch's cg.org[2]).
 struct SweepItem {
-    int col, p0, p1;
+    int col, p0, p1, patch;
+};
+// One patch of a level (3-D, ibtk_le_level_*): its column grid, its range of the
+// level's bucket table and item enumeration, its cell frame, and its arrays.
+struct PatchDesc {
+    ColGeom cg;
+    int bucket_base;  // first bucket of the patch in the level's table
+    int jbase;        // first (segment, column) pair of the patch (item table)
+    int S, nseg;      // sweep segments
+    double xlo[3];    // cell-frame x_lower
+    int ilower[3];
+    CompDesc comp[MAXC];
 };
 
 struct Params {
@@ -113,6 +125,11 @@ struct Params {
     ColGeom cg;                // 3-D column binning
     const unsigned* sorted_a;  // sorted position -> packed key cell (x | y << 16), relative to cg.org
     int S, nseg;               // sweep segment length (planes) and segments per column
+    const PatchDesc* pd;       // 3-D level: per-patch descriptors (nullptr: one patch, cg/comp/bg above)
+    int npatch;
+    const int* entry_off;      // level: list entries of patch q are [entry_off[q], entry_off[q+1])
+    int nbuckets_total;        // buckets of every patch (entries keyed >= it are outside)
+    int njobs;                 // (segment, column) pairs of every patch
     const SweepItem* items;    // 3-D sweep item table (k_item_write)
     const int* nitems;         // device: its length
     int item_bound;            // host: an upper bound of the length (the launch grid)

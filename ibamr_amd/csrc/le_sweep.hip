@@ -47,20 +47,33 @@ __device__ __forceinline__ int lane_id() { return __lane_id(); }
 // Key cell of a marker relative to the column grid (cell-frame anchor, the same
 // rule the stencils use); false if it lies outside the grid (no stencil point
 // of it can reach any array).
-template <int K> __device__ __forceinline__ bool col_key_cell(const Params& p, const double* Xs, int* ka) {
+template <int K>
+__device__ __forceinline__ bool col_key_cell(const double* xlo, const double* dx, const int* ilower, const ColGeom& cg,
+                                             const double* Xs, int* ka) {
     bool in = true;
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
-        const double xo = (Xs[d] - p.bg.xlo[d]) / p.bg.dx[d];
+        const double xo = (Xs[d] - xlo[d]) / dx[d];
         if (!(fabs(xo) < 1.0e9)) {  // also catches NaN
             in = false;
             ka[d] = 0;
             continue;
         }
-        ka[d] = key_anchor<K>(xo) + p.bg.ilower[d] - p.cg.org[d];
-        if (ka[d] < 0 || ka[d] >= p.cg.ext[d]) in = false;
+        ka[d] = key_anchor<K>(xo) + ilower[d] - cg.org[d];
+        if (ka[d] < 0 || ka[d] >= cg.ext[d]) in = false;
     }
     return in;
+}
+
+// The patch of list entry l of a level (binary search of the entry offsets).
+__device__ __forceinline__ int entry_patch(const Params& p, int l) {
+    int lo = 0, hi = p.npatch - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (p.entry_off[mid] <= l) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
 }
 
 // band of a key cell in its column: xb = 0 if its stencil reaches the x-1
@@ -83,8 +96,14 @@ __global__ __launch_bounds__(BLOCK) void k_bin_col(Params p, int n, unsigned* ke
 #pragma unroll
     for (int d = 0; d < 3; ++d) Xs[d] = p.X[(int64_t)3 * s + d] + (p.Xshift ? p.Xshift[(int64_t)3 * i + d] : 0.0);
     int ka[3];
-    unsigned key = (unsigned)p.cg.nbuckets;
-    if (col_key_cell<K>(p, Xs, ka)) {
+    unsigned key = (unsigned)p.nbuckets_total;
+    if (p.pd) {  // a level: the entry's patch, its frame and its range of buckets
+        const PatchDesc& P = p.pd[entry_patch(p, i)];
+        if (col_key_cell<K>(P.xlo, p.bg.dx, P.ilower, P.cg, Xs, ka)) {
+            const int col = (ka[1] / COLY) * P.cg.ncx + ka[0] / COLX;
+            key = (unsigned)(P.bucket_base + (ka[2] * P.cg.ncol + col) * NBAND + key_band<K>(ka[0], ka[1]));
+        }
+    } else if (col_key_cell<K>(p.bg.xlo, p.bg.dx, p.bg.ilower, p.cg, Xs, ka)) {
         const int col = (ka[1] / COLY) * p.cg.ncx + ka[0] / COLX;
         key = (unsigned)((ka[2] * p.cg.ncol + col) * NBAND + key_band<K>(ka[0], ka[1]));
     }
@@ -161,10 +180,26 @@ __device__ __forceinline__ void item_decode(const Params& p, int it, int& c, Swe
     si = p.items[t];
 }
 
-// bucket index of (anchor plane a, column col, band)
-__device__ __forceinline__ int bucket(const Params& p, int a, int col, int band) {
-    return (a * p.cg.ncol + col) * NBAND + band;
+// bucket index of (anchor plane a, column col, band) in the patch's table
+__device__ __forceinline__ int bucket(const ColGeom& cg, int a, int col, int band) {
+    return (a * cg.ncol + col) * NBAND + band;
 }
+
+// The item's patch: its column grid, the component's array and its bucket table.
+__device__ __forceinline__ void item_patch(const Params& p, const SweepItem& si, int c, ColGeom& cg, CompDesc& cd,
+                                           const int*& bs) {
+    if (p.pd) {
+        const PatchDesc& P = p.pd[si.patch];
+        cg = P.cg;
+        cd = P.comp[c];
+        bs = p.plane_start + P.bucket_base;
+    } else {
+        cg = p.cg;
+        cd = p.comp[c];
+        bs = p.plane_start;
+    }
+}
+
 
 // ---------------------------------------------------------------------------
 // diagnostics
@@ -277,7 +312,7 @@ template <int K> __device__ __forceinline__ int islot(int prel) {
 
 template <int K>
 __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc& cd, const double* ring, int gx0,
-                                                int gy0, int a, const double* Xs, int s) {
+                                                int gy0, int zorg, int a, const double* Xs, int s) {
     using S = ISh<K>;
     constexpr int W = S::W, FAM = S::FAM, RX = S::RX, PV = S::PVP;  // PV: ring slot stride
     St<W> st[3];
@@ -286,7 +321,7 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
         const double Xraw = (FAM == 2) ? p.X[(int64_t)3 * s + d] : Xs[d];
         stencil1d<K>(Xs[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis, p.K6, st[d]);
     }
-    const int ox = st[0].icl - gx0, oy = st[1].icl - gy0, oz = st[2].icl - p.cg.org[2];
+    const int ox = st[0].icl - gx0, oy = st[1].icl - gy0, oz = st[2].icl - zorg;
     // binning invariant: the points read lie in the staged column region and
     // ring (FAM 0 reads all W per dim, clipped ones as staged zeros)
     bool ok;
@@ -410,16 +445,18 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     const int a0 = si.p0, a1 = si.p1;  // the item's anchor planes
     const int lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int* bs = p.plane_start;
+    ColGeom cg;
+    CompDesc cd;
+    const int* bs;
+    item_patch(p, si, c, cg, cd, bs);
     {
         bool any = false;  // the same answer in both waves
-        for (int a = a0 + lane; a < a1; a += SW) any = any || bs[bucket(p, a, col, NBAND)] > bs[bucket(p, a, col, 0)];
+        for (int a = a0 + lane; a < a1; a += SW) any = any || bs[bucket(cg, a, col, NBAND)] > bs[bucket(cg, a, col, 0)];
         if (!__any(any)) return;
     }
-    const CompDesc cd = p.comp[c];
-    const int cx = col % p.cg.ncx, cy = col / p.cg.ncx;
-    const int gx0 = p.cg.org[0] + cx * COLX + LO, gy0 = p.cg.org[1] + cy * COLY + LO;
-    const int zorg = p.cg.org[2];
+    const int cx = col % cg.ncx, cy = col / cg.ncx;
+    const int gx0 = cg.org[0] + cx * COLX + LO, gy0 = cg.org[1] + cy * COLY + LO;
+    const int zorg = cg.org[2];
     const int nlast = p.nsorted - 1;
     // the lane's staged points q = lane + 64 k: array offsets (clamped) and
     // in-array bits (x, y)
@@ -478,8 +515,8 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     };
     auto gspan_load = [&](int a) {
         const int k = lane < IWAVES ? lane : min(lane - IWAVES, IWAVES - 1);
-        const int ac = min(a + k, p.cg.nz - 1);
-        return bs[bucket(p, ac, col, lane >= IWAVES && lane < 2 * IWAVES ? NBAND : 0)];
+        const int ac = min(a + k, cg.nz - 1);
+        return bs[bucket(cg, ac, col, lane >= IWAVES && lane < 2 * IWAVES ? NBAND : 0)];
     };
     auto gspan_get = [&](int a, int v, GSpan& gsp) {
         int acc = 0;
@@ -541,7 +578,7 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
             act = src < n;
         }
         double acc = 0.0;
-        if (act) acc = interp_marker<K>(p, cd, ring, gx0, gy0, am, m.X, m.s);
+        if (act) acc = interp_marker<K>(p, cd, ring, gx0, gy0, zorg, am, m.X, m.s);
         double* dst = (act && m.q >= 0) ? p.Qout + ((int64_t)p.Q_depth * m.q + cd.qcomp) : p.sink + lane;
         *dst = acc;
     };
@@ -588,7 +625,7 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
 
 // Entries binned "outside" (no stencil point can reach any array): V = 0.
 __global__ __launch_bounds__(BLOCK) void k_interp_outside_col(Params p, int n) {
-    const int first = p.plane_start[p.cg.nbuckets];
+    const int first = p.plane_start[p.nbuckets_total];
     for (int e = first + blockIdx.x * BLOCK + threadIdx.x; e < n; e += gridDim.x * BLOCK) {
         const int s = p.qdst ? p.qdst[e] : p.sorted_s[e];
         if (s < 0) continue;
@@ -687,8 +724,8 @@ struct Cand {
 // so every point receives its contributions in a fixed order (bit-stable).
 template <int K>
 __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
-                                             bool act, int a, int X0, int Y0, int xlo, int xhi, int ylo, int yhi, int plo,
-                                             int phi, double inv_h3, const double* inv_d, Clk& clk) {
+                                             bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
+                                             int yhi, int plo, int phi, double inv_h3, const double* inv_d, Clk& clk) {
     using S = SSh<K>;
     constexpr int W = S::W, FAM = S::FAM, LO = S::LO, HI = S::HI, NS = S::NS, NSL = S::NSL;
     St<W> st[3];
@@ -699,7 +736,7 @@ __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd
         stencil1d<K, true>(cdat.X[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis,
                            p.K6, st[d], inv_d[d]);
     }
-    int ox = st[0].icl - X0, oy = st[1].icl - Y0, oz = st[2].icl - (p.cg.org[2] + a);
+    int ox = st[0].icl - X0, oy = st[1].icl - Y0, oz = st[2].icl - (zorg + a);
     bool ok = act;
     // binning invariant (and the memory bound of the spill: x in [-16, COLX + 15])
     if (act && (ox < -S::GUARD || ox > COLX + 15 - (W - 1) || oy < -60 || oy > 60 || oz < -60 || oz > 60)) {
@@ -776,25 +813,27 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     item_decode(p, it, c, si);
     const int col = si.col;
     const int lane = lane_id();
-    const int ncx = p.cg.ncx;
+    ColGeom cg;
+    CompDesc cd;
+    const int* bs;
+    item_patch(p, si, c, cg, cd, bs);
+    const int ncx = cg.ncx;
     const int cx = col % ncx, cy = col / ncx;
-    if (cx == 0 || cx == ncx - 1 || cy == 0 || cy == p.cg.ncy - 1) return;  // guard columns own no points
-    const CompDesc cd = p.comp[c];
-    const int X0 = p.cg.org[0] + cx * COLX, Y0 = p.cg.org[1] + cy * COLY;  // absolute
-    const int zorg = p.cg.org[2];
+    if (cx == 0 || cx == ncx - 1 || cy == 0 || cy == cg.ncy - 1) return;  // guard columns own no points
+    const int X0 = cg.org[0] + cx * COLX, Y0 = cg.org[1] + cy * COLY;  // absolute
+    const int zorg = cg.org[2];
     // owned, in-array ranges (column-local x/y, relative planes)
     const int xlo = max(cd.lo[0] - X0, 0), xhi = min(cd.hi[0] - X0, COLX - 1);
     const int ylo = max(cd.lo[1] - Y0, 0), yhi = min(cd.hi[1] - Y0, COLY - 1);
     const int plo = max(si.p0, cd.lo[2] - zorg), phi = min(si.p1 - 1, cd.hi[2] - zorg);
     if (xlo > xhi || ylo > yhi || plo > phi) return;
-    const int afirst = max(plo - HI, 0), alast = min(phi - LO, p.cg.nz - 1);
-    const int* bs = p.plane_start;
+    const int afirst = max(plo - HI, 0), alast = min(phi - LO, cg.nz - 1);
     const int col0 = (cy - 1) * ncx + (cx - 1);  // column (cx-1, cy-1)
     {
         bool any = false;  // no candidate reaches the item: u unchanged
         for (int a = afirst + lane; a <= alast; a += SW)
             for (int r = 0; r < 3; ++r)
-                any = any || bs[bucket(p, a, col0 + r * ncx, 3 * NBAND)] > bs[bucket(p, a, col0 + r * ncx, 0)];
+                any = any || bs[bucket(cg, a, col0 + r * ncx, 3 * NBAND)] > bs[bucket(cg, a, col0 + r * ncx, 0)];
         if (!__any(any)) return;
     }
     const int nlast = p.nsorted - 1;
@@ -818,7 +857,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // columns cx-1 .. cx+1), one entry per lane
     auto rows_load = [&](int a, int* rowv) {
 #pragma unroll
-        for (int r = 0; r < 3; ++r) rowv[r] = bs[bucket(p, a, col0 + r * ncx, 0) + min(lane, 27)];
+        for (int r = 0; r < 3; ++r) rowv[r] = bs[bucket(cg, a, col0 + r * ncx, 0) + min(lane, 27)];
     };
     // candidate data of sorted position e
     auto cand_at = [&](int e, Cand& d) {
@@ -844,8 +883,8 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         for (int k = 0; k < 3; ++k) d.X[k] = shfl_f64(mine.X[k], src);
         d.V = shfl_f64(mine.V, src);
         d.s = FAM == 2 ? __builtin_amdgcn_ds_bpermute(src << 2, mine.s) : 0;
-        spread_lanes<K>(p, cd, ring, d, src < n, src < r ? a - 1 : a, X0, Y0, xlo, xhi, ylo, yhi, plo, phi, inv_h3,
-                        inv_d, clk);
+        spread_lanes<K>(p, cd, ring, d, src < n, src < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi,
+                        inv_h3, inv_d, clk);
     };
     // plane z -> registers (the lane's NPL points); registers -> ring slot
     auto plane_load = [&](int z, double* v) {
@@ -982,36 +1021,71 @@ void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items) {
 // item of a sub-segment sums the markers anchored in its planes; the spread
 // item owns its planes and takes the candidates of the anchors reaching them
 // (NS - 1 extra anchor planes per cut).
+// (segment, column) pair j of the level -> its patch, column grid, segments
+__device__ __forceinline__ void job_patch(const Params& p, int j, int& q, ColGeom& cg, int& S, int& nseg, int& j0,
+                                          const int*& bs) {
+    if (!p.pd) {
+        q = 0;
+        cg = p.cg;
+        S = p.S;
+        nseg = p.nseg;
+        j0 = 0;
+        bs = p.plane_start;
+        return;
+    }
+    int lo = 0, hi = p.npatch - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (p.pd[mid].jbase <= j) lo = mid;
+        else hi = mid - 1;
+    }
+    const PatchDesc& P = p.pd[lo];
+    q = lo;
+    cg = P.cg;
+    S = P.S;
+    nseg = P.nseg;
+    j0 = P.jbase;
+    bs = p.plane_start + P.bucket_base;
+}
+
 template <int K>
 __global__ __launch_bounds__(BLOCK) void k_item_counts(Params p, int target, int* nsub) {
     constexpr int NS = KT<K>::HI - KT<K>::LO + 1;
     const int j = blockIdx.x * BLOCK + threadIdx.x;
-    if (j >= p.nseg * p.cg.ncol) return;
-    const int seg = j / p.cg.ncol, col = j - seg * p.cg.ncol;
-    const int a0 = seg * p.S, a1 = min(a0 + p.S, p.cg.nz);
-    const int* bs = p.plane_start;
+    if (j >= p.njobs) return;
+    int q, S, nseg, j0;
+    ColGeom cg;
+    const int* bs;
+    job_patch(p, j, q, cg, S, nseg, j0, bs);
+    const int jl = j - j0;
+    const int seg = jl / cg.ncol, col = jl - seg * cg.ncol;
+    const int a0 = seg * S, a1 = min(a0 + S, cg.nz);
     long load = 0;
-    for (int a = a0; a < a1; ++a) load += bs[bucket(p, a, col, NBAND)] - bs[bucket(p, a, col, 0)];
+    for (int a = a0; a < a1; ++a) load += bs[bucket(cg, a, col, NBAND)] - bs[bucket(cg, a, col, 0)];
     const int maxsub = max((a1 - a0) / max(NS, 8), 1);
     nsub[j] = (int)min((long)maxsub, max(1L, (load + target - 1) / target));
 }
 __global__ __launch_bounds__(BLOCK) void k_item_write(Params p, const int* nsub, const int* start, SweepItem* tab,
                                                       int* ntot) {
     const int j = blockIdx.x * BLOCK + threadIdx.x;
-    const int nj = p.nseg * p.cg.ncol;
-    if (j >= nj) return;
-    const int seg = j / p.cg.ncol, col = j - seg * p.cg.ncol;
-    const int a0 = seg * p.S, a1 = min(a0 + p.S, p.cg.nz), len = a1 - a0;
+    if (j >= p.njobs) return;
+    int q, S, nseg, j0;
+    ColGeom cg;
+    const int* bs;
+    job_patch(p, j, q, cg, S, nseg, j0, bs);
+    const int jl = j - j0;
+    const int seg = jl / cg.ncol, col = jl - seg * cg.ncol;
+    const int a0 = seg * S, a1 = min(a0 + S, cg.nz), len = a1 - a0;
     const int n = nsub[j], s0 = start[j];
-    for (int k = 0; k < n; ++k) tab[s0 + k] = SweepItem{col, a0 + (len * k) / n, a0 + (len * (k + 1)) / n};
-    if (j == nj - 1) *ntot = s0 + n;
+    for (int k = 0; k < n; ++k) tab[s0 + k] = SweepItem{col, a0 + (len * k) / n, a0 + (len * (k + 1)) / n, q};
+    if (j == p.njobs - 1) *ntot = s0 + n;
 }
 
 static int grid8(long items) { return (int)((items + 7) & ~7L); }
 
 template <int K> hipError_t launch_item_table_t(const Params& p, int target, int* nsub, int* start, SweepItem* tab,
                                                 int* ntot, void* temp, size_t temp_bytes, hipStream_t s) {
-    const int nj = p.nseg * p.cg.ncol;
+    const int nj = p.njobs;
     if (nj <= 0) return hipMemsetAsync(ntot, 0, sizeof(int), s);
     hipLaunchKernelGGL(k_item_counts<K>, dim3((nj + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, target, nsub);
     hipError_t e = launch_scan(temp, temp_bytes, nsub, start, nj, s);

@@ -242,6 +242,61 @@ def spread(ctx: Context, markers: Markers, kernel: str, centering: str, geom: Ge
                                         ctypes.byref(geom.c), arr, q_depth, _ptr(Q), Q_depth, _ptr(ds), _ptr(X)))
 
 
+class Level:
+    """A level of 3-D patches binned together (ibtk_le_level_bin): LDataManager's
+    patch loop (LDataManager.cpp:625-660, 763-807) as one launch per sweep.
+
+    geoms: the patches' Geometry (one dx); lists[q]: patch q's list, either None
+    (every marker) or (indices int32 device tensor, Xshift float64 device tensor
+    or None).  interp/spread take the arrays of every patch, patch by patch
+    (``arrays[q]`` = that patch's list of component arrays)."""
+
+    def __init__(self, ctx: Context, geoms: Sequence[Geometry], kernel: str, X: torch.Tensor, lists):
+        if len(geoms) != len(lists) or not geoms:
+            raise ValueError("one list per patch")
+        self.ctx, self.geoms, self.kernel = ctx, list(geoms), kernel
+        self.markers = Markers(ctx)
+        M = X.shape[0]
+        idx, xs, off = [], [], [0]
+        any_shift = any(l is not None and l[1] is not None for l in lists)
+        for l in lists:
+            if l is None:
+                i = torch.arange(M, dtype=torch.int32, device=X.device)
+                x = torch.zeros((M, 3), dtype=torch.float64, device=X.device)
+            else:
+                i = l[0].to(torch.int32)
+                x = l[1] if l[1] is not None else torch.zeros((i.numel(), 3), dtype=torch.float64, device=X.device)
+            idx.append(i)
+            xs.append(x)
+            off.append(off[-1] + i.numel())
+        self.indices = torch.cat(idx).contiguous()
+        self.xshift = torch.cat(xs).contiguous() if any_shift else None
+        G = (PatchGeom * len(geoms))(*[g.c for g in geoms])
+        O = (ctypes.c_int * len(off))(*off)
+        check(ctx.lib.ibtk_le_level_bin(ctx.h, self.markers.h, len(geoms), G, kernel_id(kernel), _ptr(X), O,
+                                        _ptr(self.indices), _ptr(self.xshift)))
+
+    def _arrays(self, arrays):
+        flat = [t for per in arrays for t in per]
+        return _ptr_array(flat)
+
+    def interp(self, centering: str, arrays, Q: torch.Tensor, X: torch.Tensor, q_depth: int = 1,
+               Q_depth: Optional[int] = None, axis: int = 0):
+        if Q_depth is None:
+            Q_depth = 3 if centering in ("side", "edge") else q_depth
+        check(self.ctx.lib.ibtk_le_level_interp(self.ctx.h, self.markers.h, kernel_id(self.kernel),
+                                                CENTERING[centering], axis, self._arrays(arrays), q_depth, _ptr(Q),
+                                                Q_depth, _ptr(X)))
+
+    def spread(self, centering: str, arrays, Q: torch.Tensor, X: torch.Tensor, q_depth: int = 1,
+               Q_depth: Optional[int] = None, axis: int = 0):
+        if Q_depth is None:
+            Q_depth = 3 if centering in ("side", "edge") else q_depth
+        check(self.ctx.lib.ibtk_le_level_spread(self.ctx.h, self.markers.h, kernel_id(self.kernel),
+                                                CENTERING[centering], axis, self._arrays(arrays), q_depth, _ptr(Q),
+                                                Q_depth, _ptr(X)))
+
+
 def _periodic_arg(periodic, ndim):
     if periodic is None:
         return None

@@ -151,6 +151,26 @@ int ibtk_le_spread_ds(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int center
                       const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
                       int Q_depth, const double* ds_dev, const double* X_dev);
 
+/* ---- a level of patches (3-D) ------------------------------------------------------
+ * LDataManager::spread / interp loop over the patches of a level, one LEInteractor
+ * call per patch (LDataManager.cpp:625-660, 763-807).  Here one launch per sweep
+ * covers every patch: the patches' lists are binned together (bucket ranges per
+ * patch, one device sort) and the sweep items of all patches form one table.
+ * geoms[q]: patch q's box, ghost width and geometry (one dx for the level);
+ * entry_offsets (host, npatch + 1): patch q's list is entries [off[q], off[q+1])
+ * of indices_dev / Xshift_dev (NULL/NULL: entry l is marker l, no shift) -- the
+ * interior list for interp, the ghost-box list for spread, as LDataManager uses.
+ * q_dev: the arrays of patch 0, then patch 1, ... (NDIM per patch for SIDE/EDGE,
+ * one for CELL/NODE).  Results equal the per-patch calls' (interp bit for bit;
+ * spread in each patch's own fixed order). */
+int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch, const ibtk_le_patch_geom* geoms, int kernel,
+                      const double* X_dev, const int* entry_offsets, const int* indices_dev,
+                      const double* Xshift_dev);
+int ibtk_le_level_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                         const double* const* q_dev, int q_depth, double* Q_dev, int Q_depth, const double* X_dev);
+int ibtk_le_level_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                         double* const* q_dev, int q_depth, const double* Q_dev, int Q_depth, const double* X_dev);
+
 /* ---- helpers for a single periodic patch (uniform finest level) -----------------
  * Fill the ghost layers of the arrays of `centering` from the periodic interior
  * (the RefineSchedule::fillData the caller runs before interp, LDataManager.cpp:750). */

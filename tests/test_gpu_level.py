@@ -1,0 +1,154 @@
+"""GPU: a level of patches in one launch per sweep (ibtk_le_level_*), against the
+per-patch calls and the oracle run patch by patch -- LDataManager::interp /
+spread's patch loop (LDataManager.cpp:625-660, 763-807; SURVEY.md 8(d) cfg5's
+multi-patch finest level).
+
+Each patch has its own ghosted side arrays, filled from one periodic field;
+interp takes the patch's interior list (markers whose cell is in the patch
+box), spread the patch's ghost-box list (the markers and periodic images whose
+cell is in the ghost box, as the index data's ghost box holds them), so every
+patch's interior is complete without a grid reduction.
+Interp must equal the per-patch result bit for bit, spread within 1e-12 of the
+oracle on each patch (the sweep sums each point in a fixed order), and both
+bit-stable run to run.
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+from oracle import oracle as ora
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+SPREAD_TOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def le():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ibamr_amd import le as _le
+    return _le
+
+
+@pytest.fixture(scope="module")
+def ctx(le):
+    return le.Context(0)
+
+
+def _patches(le, N, P, g):
+    n = N // P
+    dx = 1.0 / N
+    geoms = []
+    for k, j, i in itertools.product(range(P), repeat=3):
+        lo = [i * n, j * n, k * n]
+        geoms.append(le.Geometry(lo, [l + n - 1 for l in lo], g, [dx] * 3, [l * dx for l in lo]))
+    return geoms
+
+
+def _fill(geom, G, N):
+    """side arrays of the patch, values of the periodic field G[c] (z, y, x) at every point"""
+    out = []
+    for c in range(3):
+        shp = geom.array_shape("side", c)
+        zz = np.arange(shp[0]) + geom.ilower[2] - geom.gcw[2]
+        yy = np.arange(shp[1]) + geom.ilower[1] - geom.gcw[1]
+        xx = np.arange(shp[2]) + geom.ilower[0] - geom.gcw[0]
+        out.append(np.ascontiguousarray(G[c][np.ix_(zz % N, yy % N, xx % N)]))
+    return out
+
+
+def _lists(geom, X, N, g):
+    dx = 1.0 / N
+    c = np.floor(X / dx).astype(np.int64)
+    lo, hi = np.array(geom.ilower), np.array(geom.iupper)
+    inside = np.all((c >= lo) & (c <= hi), axis=1)
+    interior = np.nonzero(inside)[0].astype(np.int32)
+    idx, xs = [], []
+    for s in itertools.product((-1, 0, 1), repeat=3):
+        ci = c + np.array(s) * N
+        ok = np.all((ci >= lo - g) & (ci <= hi + g), axis=1)
+        sel = np.nonzero(ok)[0]
+        idx.append(sel)
+        xs.append(np.tile(np.array(s, np.float64), (sel.size, 1)))
+    idx = np.concatenate(idx).astype(np.int32)
+    xs = np.concatenate(xs)
+    o = np.argsort(idx, kind="stable")
+    return interior, idx[o], xs[o]
+
+
+@pytest.mark.parametrize("kernel,P,clustered", [("IB_4", 2, False), ("IB_6", 2, False), ("IB_4", 4, True),
+                                                ("BSPLINE_4", 2, True)])
+def test_level_matches_patch_by_patch(le, ctx, kernel, P, clustered):
+    N = 64 if P == 4 else 48
+    g = ora.min_ghost_width(kernel)
+    geoms = _patches(le, N, P, g)
+    rng = np.random.default_rng(3 + P)
+    M = 40_000
+    X = rng.uniform(0, 1, (M, 3))
+    if clustered:  # a sheet one cell thick and a fibre bundle along z
+        X[: M // 2, 2] = 0.5 + (rng.uniform(0, 1, M // 2) - 0.5) / N
+        r, t = 0.05 * np.sqrt(rng.uniform(0, 1, M // 4)), 2 * np.pi * rng.uniform(0, 1, M // 4)
+        X[M // 2: M // 2 + M // 4, 0] = 0.3 + r * np.cos(t)
+        X[M // 2: M // 2 + M // 4, 1] = 0.6 + r * np.sin(t)
+    F = rng.uniform(-1, 1, (M, 3))
+    G = [rng.uniform(-1, 1, (N, N, N)) for _ in range(3)]
+    Xd, Fd = torch.from_numpy(X).cuda(), torch.from_numpy(F).cuda()
+    lists_i, lists_s, host = [], [], []
+    for geom in geoms:
+        interior, idx, xs = _lists(geom, X, N, g)
+        host.append((interior, idx, xs))
+        lists_i.append((torch.from_numpy(interior).cuda(), None))
+        lists_s.append((torch.from_numpy(idx).cuda(), torch.from_numpy(xs).cuda()))
+    u = [[torch.from_numpy(a).cuda() for a in _fill(geom, G, N)] for geom in geoms]
+    # interp: one launch over the level
+    lvl_i = le.Level(ctx, geoms, kernel, Xd, lists_i)
+    U = torch.full((M, 3), np.nan, dtype=torch.float64, device="cuda")
+    lvl_i.interp("side", u, U, Xd)
+    # spread: one launch, twice (bit stability)
+    lvl_s = le.Level(ctx, geoms, kernel, Xd, lists_s)
+    outs = []
+    for rep in range(2):
+        f = [[torch.zeros_like(a) for a in per] for per in u]
+        lvl_s.spread("side", f, Fd, Xd)
+        outs.append(f)
+    ctx.synchronize()
+    Ug = U.cpu().numpy()
+    assert not np.isnan(Ug).any(), "every marker is interior to exactly one patch"
+    for q, geom in enumerate(geoms):
+        interior, idx, xs = host[q]
+        # the single-patch device call on the same list: interp bit for bit
+        m = le.Markers(ctx).bin(geom, kernel, Xd, torch.from_numpy(interior).cuda())
+        U1 = torch.zeros((M, 3), dtype=torch.float64, device="cuda")
+        le.interp(ctx, m, kernel, "side", geom, u[q], U1, Xd)
+        ctx.synchronize()
+        assert np.array_equal(Ug[interior], U1.cpu().numpy()[interior]), f"patch {q} interp"
+        # the oracle on the patch's ghost-box list
+        uo = [np.zeros(tuple(a.shape)) for a in u[q]]
+        ora.side_spread(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, uo, idx, xs, X, F)
+        for a in range(3):
+            got = outs[0][q][a].cpu().numpy()
+            assert np.array_equal(got, outs[1][q][a].cpu().numpy()), f"patch {q} comp {a} not bit-stable"
+            err = np.abs(got - uo[a]).max() / max(np.abs(uo[a]).max(), 1e-300)
+            assert err <= SPREAD_TOL, f"patch {q} comp {a} spread rel err {err:.2e}"
+    # the level's interiors are the periodic spread: conservation over unique points
+    h3 = geoms[0].dx[0] ** 3
+    for a in range(3):
+        tot = 0.0
+        for q, geom in enumerate(geoms):
+            n = geom.iupper[0] - geom.ilower[0] + 1
+            tot += outs[0][q][a][g:g + n, g:g + n, g:g + n].sum().item()
+        assert abs(tot * h3 - F[:, a].sum()) <= 1e-10 * np.abs(F[:, a]).sum()
+
+
+def test_level_rejects_single_patch_calls(le, ctx):
+    from ibamr_amd._lib import IBTKLEError
+    geoms = _patches(le, 32, 2, 3)
+    X = torch.rand((100, 3), dtype=torch.float64, device="cuda")
+    lvl = le.Level(ctx, geoms, "IB_4", X, [None] * len(geoms))
+    u = geoms[0].alloc("side")
+    Q = torch.zeros((100, 3), dtype=torch.float64, device="cuda")
+    with pytest.raises(IBTKLEError):
+        le.interp(ctx, lvl.markers, "IB_4", "side", geoms[0], u, Q, X)
