@@ -186,9 +186,10 @@ __device__ __forceinline__ int bucket(const ColGeom& cg, int a, int col, int ban
 }
 
 // The item's patch: its column grid, the component's array and its bucket table.
+template <bool LVL>
 __device__ __forceinline__ void item_patch(const Params& p, const SweepItem& si, int c, ColGeom& cg, CompDesc& cd,
                                            const int*& bs) {
-    if (p.pd) {
+    if constexpr (LVL) {
         const PatchDesc& P = p.pd[si.patch];
         cg = P.cg;
         cd = P.comp[c];
@@ -431,7 +432,7 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
 // pooled markers.  Points outside the component's array are staged as 0.  One
 // lane per marker sums its W^3 stencil from the ring (Fortran loop order,
 // bitwise the oracle's).
-template <int K>
+template <int K, bool LVL>
 __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     using S = ISh<K>;
     constexpr int LO = S::LO, HI = S::HI, RX = S::RX, NPT = S::NPT;
@@ -448,7 +449,7 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     ColGeom cg;
     CompDesc cd;
     const int* bs;
-    item_patch(p, si, c, cg, cd, bs);
+    item_patch<LVL>(p, si, c, cg, cd, bs);
     {
         bool any = false;  // the same answer in both waves
         for (int a = a0 + lane; a < a1; a += SW) any = any || bs[bucket(cg, a, col, NBAND)] > bs[bucket(cg, a, col, 0)];
@@ -800,7 +801,7 @@ __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd
 // ring holds planes a+LO..a+HI (u_old, then accumulating) plus a+HI+1 in
 // flight; plane a+LO is written back after anchor a and its slot takes plane
 // a+HI+2.  The candidates of anchor a+1 are staged while anchor a is added.
-template <int K>
+template <int K, bool LVL>
 __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     using S = SSh<K>;
     constexpr int LO = S::LO, HI = S::HI, NPL = S::NPL, FAM = S::FAM;
@@ -816,7 +817,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     ColGeom cg;
     CompDesc cd;
     const int* bs;
-    item_patch(p, si, c, cg, cd, bs);
+    item_patch<LVL>(p, si, c, cg, cd, bs);
     const int ncx = cg.ncx;
     const int cx = col % ncx, cy = col / ncx;
     if (cx == 0 || cx == ncx - 1 || cy == 0 || cy == cg.ncy - 1) return;  // guard columns own no points
@@ -1122,7 +1123,10 @@ template <int K>
 hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     if (ev0) (void)hipEventRecord(ev0, s);
     const long items = (long)p.item_bound * p.ncomp;
-    if (items > 0) hipLaunchKernelGGL(k_interp_sweep<K>, dim3(grid8(items)), dim3(SW * IWAVES), 0, s, p);
+    if (items > 0) {
+        if (p.pd) hipLaunchKernelGGL((k_interp_sweep<K, true>), dim3(grid8(items)), dim3(SW * IWAVES), 0, s, p);
+        else hipLaunchKernelGGL((k_interp_sweep<K, false>), dim3(grid8(items)), dim3(SW * IWAVES), 0, s, p);
+    }
     if (ev1) (void)hipEventRecord(ev1, s);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -1148,7 +1152,10 @@ template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s
                            const_cast<double*>(p.sorted_F));
     if (ev0) (void)hipEventRecord(ev0, s);  // the events bracket the sweep kernel alone
     const long items = (long)p.item_bound * p.ncomp;
-    if (items > 0) hipLaunchKernelGGL(k_spread_sweep<K>, dim3(grid8(items)), dim3(SW), 0, s, p);
+    if (items > 0) {
+        if (p.pd) hipLaunchKernelGGL((k_spread_sweep<K, true>), dim3(grid8(items)), dim3(SW), 0, s, p);
+        else hipLaunchKernelGGL((k_spread_sweep<K, false>), dim3(grid8(items)), dim3(SW), 0, s, p);
+    }
     if (ev1) (void)hipEventRecord(ev1, s);
     return hipGetLastError();
 }
