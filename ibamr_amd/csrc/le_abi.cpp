@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdlib>
 #include <cstdarg>
@@ -98,6 +99,7 @@ struct ibtk_le_ctx_s {
     hipStream_t stream = nullptr;
     DevBuf keys_in, vals_in, temp, counts, offsets, fbuf;
     DevBuf lst_idx, lst_xs, lst_key, lst_perm;  // index-list / node-distribution scratch
+    DevBuf lvl_tab;                             // level ghost fill tables
     DevBuf err;   // one int
     DevBuf sink;  // 64 doubles (Params::sink)
     DevBuf stamps;  // diagnostic phase clocks (IBTK_LE_STAMPS=1)
@@ -168,7 +170,8 @@ extern "C" int ibtk_le_ctx_destroy(ibtk_le_ctx ctx) {
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->keys_in, &ctx->vals_in, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->fbuf, &ctx->err, &ctx->sink,
-                       &ctx->stamps, &ctx->lst_idx, &ctx->lst_xs, &ctx->lst_key, &ctx->lst_perm})
+                       &ctx->stamps, &ctx->lst_idx, &ctx->lst_xs, &ctx->lst_key, &ctx->lst_perm,
+                       &ctx->lvl_tab})
         b->release();
     if (ctx->ev0) hipEventDestroy(ctx->ev0);
     if (ctx->ev1) hipEventDestroy(ctx->ev1);
@@ -1003,6 +1006,71 @@ extern "C" int ibtk_le_level_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kern
     ctx->ev_valid = false;
     HIP_TRY(launch_spread_sweep(kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
     if (t) ctx->ev_valid = true;
+    return IBTK_LE_OK;
+}
+
+// Ghost fill of a level of equal patches tiling a box (periodic in the flagged
+// dims): LDataManager::interp's fill schedule (LDataManager.cpp:748-751).
+// q_dev as for ibtk_le_level_interp.  The device tables live in the context
+// until the next call with another tiling.
+extern "C" int ibtk_le_level_fill_ghosts(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms,
+                                         int centering, double* const* q_dev, int q_depth, const int* periodic) {
+    if (!ctx || !geoms || !q_dev || npatch <= 0) return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: null argument");
+    if (centering != IBTK_LE_SIDE && centering != IBTK_LE_CELL)
+        return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: side or cell data");
+    LevelTiling t;
+    std::memset(&t, 0, sizeof(t));
+    int lo[3] = {INT_MAX, INT_MAX, INT_MAX}, hi[3] = {INT_MIN, INT_MIN, INT_MIN};
+    for (int q = 0; q < npatch; ++q) {
+        if (int rc = check_geom(&geoms[q])) return rc;
+        if (geoms[q].ndim != 3) return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: 3-D patches");
+        for (int d = 0; d < 3; ++d) {
+            const int n = geoms[q].iupper[d] - geoms[q].ilower[d] + 1;
+            if (q == 0) t.n[d] = n;
+            if (n != t.n[d] || geoms[q].gcw[d] != geoms[0].gcw[0])
+                return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: equal patches and ghost widths only");
+            lo[d] = std::min(lo[d], geoms[q].ilower[d]);
+            hi[d] = std::max(hi[d], geoms[q].iupper[d]);
+        }
+    }
+    t.g = geoms[0].gcw[0];
+    long long ntiles = 1;
+    for (int d = 0; d < 3; ++d) {
+        t.dom_lo[d] = lo[d];
+        t.ntile[d] = (hi[d] - lo[d] + 1) / t.n[d];
+        if (t.ntile[d] * t.n[d] != hi[d] - lo[d] + 1 || t.g > t.n[d])
+            return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: the patches must tile a box, ghost width <= patch size");
+        t.periodic[d] = periodic ? periodic[d] != 0 : 1;
+        ntiles *= t.ntile[d];
+    }
+    std::vector<int> tile_of(npatch), patch_of((size_t)ntiles, -1);
+    for (int q = 0; q < npatch; ++q) {
+        int tc[3];
+        for (int d = 0; d < 3; ++d) {
+            tc[d] = (geoms[q].ilower[d] - lo[d]) / t.n[d];
+            if ((geoms[q].ilower[d] - lo[d]) % t.n[d]) return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: unaligned patch");
+        }
+        tile_of[q] = tc[0] + t.ntile[0] * (tc[1] + t.ntile[1] * tc[2]);
+        if (patch_of[tile_of[q]] >= 0) return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: overlapping patches");
+        patch_of[tile_of[q]] = q;
+    }
+    t.side = centering == IBTK_LE_SIDE;
+    t.ncomp = t.side ? 3 : 1;
+    const size_t narr = (size_t)npatch * t.ncomp;
+    for (size_t i = 0; i < narr; ++i)
+        if (!q_dev[i]) return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: null array");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    const hipStream_t s = ctx->stream;
+    int rc;
+    if ((rc = ctx->lvl_tab.ensure(sizeof(int) * (size_t)(npatch + ntiles) + sizeof(double*) * narr + 64))) return rc;
+    char* base = ctx->lvl_tab.as<char>();
+    double** arr_d = reinterpret_cast<double**>(base);
+    int* tile_d = reinterpret_cast<int*>(base + sizeof(double*) * narr);
+    int* patch_d = tile_d + npatch;
+    HIP_TRY(hipMemcpyAsync(arr_d, q_dev, sizeof(double*) * narr, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(tile_d, tile_of.data(), sizeof(int) * (size_t)npatch, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(patch_d, patch_of.data(), sizeof(int) * (size_t)ntiles, hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_level_fill(t, npatch, tile_d, patch_d, arr_d, t.side ? 1 : q_depth, s));
     return IBTK_LE_OK;
 }
 

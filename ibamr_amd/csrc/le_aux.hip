@@ -208,6 +208,84 @@ hipError_t launch_zero_ghosts(int ndim, const GhostDesc* g, int n, hipStream_t s
 }
 
 // ---------------------------------------------------------------------------
+// level ghost fill: the RefineSchedule::fillData of LDataManager.cpp:748-751 on
+// a level of equal patches tiling a box.  Pass dreg covers the ghost layers of
+// dim dreg, the whole ghost extent of the dims below it and the unique points
+// of the dims above (the k_ghost regions): every ghost point once.  A point's
+// source is the patch owning its (wrapped) cell, at the same global index.
+// blockIdx.z = patch * ncomp + array; arrays[patch * ncomp + array] (depth
+// slices of a cell array are consecutive arrays of one allocation).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(BLOCK) void k_level_fill(LevelTiling t, int dreg, const int* tile_of_patch,
+                                                      const int* patch_of_tile, double* const* arrays, int depth) {
+    const int q = blockIdx.z / t.ncomp, a = blockIdx.z - q * t.ncomp;
+    const int tile = tile_of_patch[q];
+    const int tc[3] = {tile % t.ntile[0], (tile / t.ntile[0]) % t.ntile[1], tile / (t.ntile[0] * t.ntile[1])};
+    int ext[3], uni[3], lo[3];
+    for (int d = 0; d < 3; ++d) {
+        const int extra = (t.side && d == a) ? 1 : 0;
+        ext[d] = t.n[d] + 2 * t.g + extra;  // array extent
+        uni[d] = t.n[d];                     // unique points [g, g + n)
+        lo[d] = t.dom_lo[d] + tc[d] * t.n[d] - t.g;  // global index of array point 0
+    }
+    int rx[3];  // region extents of this pass
+    for (int d = 0; d < 3; ++d) rx[d] = d < dreg ? ext[d] : (d == dreg ? ext[d] - uni[d] : uni[d]);
+    const unsigned tid = blockIdx.x * BLOCK + threadIdx.x;
+    if (tid >= (unsigned)rx[0] * (unsigned)rx[1] || (int)blockIdx.y >= rx[2]) return;
+    const int r[3] = {(int)(tid % (unsigned)rx[0]), (int)(tid / (unsigned)rx[0]), (int)blockIdx.y};
+    int li[3];
+    for (int d = 0; d < 3; ++d) {
+        if (d < dreg) li[d] = r[d];
+        else if (d == dreg) li[d] = r[d] < t.g ? r[d] : t.g + uni[d] + (r[d] - t.g);
+        else li[d] = t.g + r[d];
+    }
+    int src_tile[3], sl[3];
+    for (int d = 0; d < 3; ++d) {
+        const int N = t.n[d] * t.ntile[d];
+        int gi = lo[d] + li[d] - t.dom_lo[d];
+        if (gi < 0 || gi >= N) {
+            if (!t.periodic[d]) return;  // a physical ghost: left to the boundary operators
+            gi = ((gi % N) + N) % N;
+        }
+        src_tile[d] = gi / t.n[d];
+        sl[d] = gi - src_tile[d] * t.n[d] + t.g;
+    }
+    const int sq = patch_of_tile[src_tile[0] + t.ntile[0] * (src_tile[1] + t.ntile[1] * src_tile[2])];
+    if (sq < 0) return;
+    const int64_t di = (int64_t)li[0] + (int64_t)ext[0] * (li[1] + (int64_t)ext[1] * li[2]);
+    const int64_t si = (int64_t)sl[0] + (int64_t)ext[0] * (sl[1] + (int64_t)ext[1] * sl[2]);
+    const int64_t vol = (int64_t)ext[0] * ext[1] * ext[2];
+    double* dst = arrays[(size_t)q * t.ncomp + a];
+    const double* src = arrays[(size_t)sq * t.ncomp + a];
+    for (int k = 0; k < depth; ++k) dst[k * vol + di] = src[k * vol + si];
+}
+
+hipError_t launch_level_fill(const LevelTiling& t, int npatch, const int* tile_of_patch, const int* patch_of_tile,
+                             double* const* arrays, int depth, hipStream_t s) {
+    for (int dreg = 0; dreg < 3; ++dreg) {
+        long long m01 = 0;
+        int m2 = 0;
+        for (int a = 0; a < t.ncomp; ++a) {
+            int rx[3];
+            for (int d = 0; d < 3; ++d) {
+                const int ext = t.n[d] + 2 * t.g + ((t.side && d == a) ? 1 : 0);
+                rx[d] = d < dreg ? ext : (d == dreg ? ext - t.n[d] : t.n[d]);
+            }
+            m01 = std::max(m01, (long long)rx[0] * rx[1]);
+            m2 = std::max(m2, rx[2]);
+        }
+        if (m01 <= 0 || m2 <= 0) continue;
+        const long long nz = (long long)npatch * t.ncomp;
+        if (m01 >= (1LL << 32) || m2 > 65535 || nz > 65535) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_level_fill, dim3((unsigned)((m01 + BLOCK - 1) / BLOCK), (unsigned)m2, (unsigned)nz),
+                           dim3(BLOCK), 0, s, t, dreg, tile_of_patch, patch_of_tile, arrays, depth);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------
 // periodic index lists (LIndexSetData::cacheLocalIndices for one periodic patch)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void cell_index(const ImageDesc& d, const double* X, int* c) {

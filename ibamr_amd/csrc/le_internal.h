@@ -241,6 +241,21 @@ hipError_t launch_unique_flags(const unsigned* skeys, const int* sorder, const i
 hipError_t launch_compact(const int* sorder, const int* flag, const int* pos, const unsigned* skeys,
                           unsigned local_end, unsigned ghost_end, int n, int* out, int* counts, hipStream_t s);
 
+// Ghost fill of a level of equal patches tiling a box (le_aux.hip): every ghost
+// point of every patch array takes the value of the patch that owns the point
+// (wrapped in periodic dims).
+struct LevelTiling {
+    int n[3];        // cells per patch and dim
+    int ntile[3];    // patches per dim
+    int dom_lo[3];   // lower cell of the tiled box
+    int g;           // ghost width
+    int periodic[3];
+    int ncomp;       // arrays per patch (side: 3, cell/node depth slices: 1)
+    int side;        // 1: side-centred (array a has one extra face along a)
+};
+hipError_t launch_level_fill(const LevelTiling& t, int npatch, const int* tile_of_patch, const int* patch_of_tile,
+                             double* const* arrays, int depth, hipStream_t s);
+
 // Physical-boundary ghost operators on one side-centred patch (le_bdry.hip)
 struct BdSide {
     double* u[3];

@@ -276,6 +276,13 @@ class Level:
         check(ctx.lib.ibtk_le_level_bin(ctx.h, self.markers.h, len(geoms), G, kernel_id(kernel), _ptr(X), O,
                                         _ptr(self.indices), _ptr(self.xshift)))
 
+    def fill_ghosts(self, centering: str, arrays, q_depth: int = 1, periodic=None):
+        """Ghost fill across the level's patches (ibtk_le_level_fill_ghosts)."""
+        G = (PatchGeom * len(self.geoms))(*[g.c for g in self.geoms])
+        pa = _periodic_arg(periodic, 3)
+        check(self.ctx.lib.ibtk_le_level_fill_ghosts(self.ctx.h, len(self.geoms), G, CENTERING[centering],
+                                                     self._arrays(arrays), q_depth, pa[0] if pa else None))
+
     def _arrays(self, arrays):
         flat = [t for per in arrays for t in per]
         return _ptr_array(flat)

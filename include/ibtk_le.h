@@ -170,6 +170,14 @@ int ibtk_le_level_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cen
                          const double* const* q_dev, int q_depth, double* Q_dev, int Q_depth, const double* X_dev);
 int ibtk_le_level_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                          double* const* q_dev, int q_depth, const double* Q_dev, int Q_depth, const double* X_dev);
+/* Ghost fill of a level of equal patches tiling a box, periodic in the dims
+ * periodic[d] != 0 (NULL: all): every ghost point of every patch array takes the
+ * value of the patch owning its (wrapped) index -- the RefineSchedule::fillData
+ * LDataManager::interp runs before interpolating (LDataManager.cpp:748-751).
+ * SIDE (NDIM arrays per patch; the face shared by two patches is the upper
+ * patch's) or CELL (one array of depth q_depth per patch). */
+int ibtk_le_level_fill_ghosts(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms, int centering,
+                              double* const* q_dev, int q_depth, const int* periodic);
 
 /* ---- helpers for a single periodic patch (uniform finest level) -----------------
  * Fill the ghost layers of the arrays of `centering` from the periodic interior

@@ -152,3 +152,30 @@ def test_level_rejects_single_patch_calls(le, ctx):
     Q = torch.zeros((100, 3), dtype=torch.float64, device="cuda")
     with pytest.raises(IBTKLEError):
         le.interp(ctx, lvl.markers, "IB_4", "side", geoms[0], u, Q, X)
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_level_fill_ghosts(le, ctx, P):
+    """Every ghost point of every patch takes the value of the patch owning it
+    (periodic wrap), the schedule fill before interp (LDataManager.cpp:748-751)."""
+    N, g = 32, 3
+    geoms = _patches(le, N, P, g)
+    rng = np.random.default_rng(P)
+    G = [rng.uniform(-1, 1, (N, N, N)) for _ in range(3)]
+    want = [_fill(geom, G, N) for geom in geoms]
+    n = N // P
+    arrays = []
+    for geom, w in zip(geoms, want):
+        per = []
+        for a in range(3):
+            t = torch.full(w[a].shape, np.nan, dtype=torch.float64, device="cuda")
+            t[g:g + n, g:g + n, g:g + n] = torch.from_numpy(w[a][g:g + n, g:g + n, g:g + n]).cuda()
+            per.append(t)
+        arrays.append(per)
+    X = torch.rand((10, 3), dtype=torch.float64, device="cuda")
+    lvl = le.Level(ctx, geoms, "IB_4", X, [None] * len(geoms))
+    lvl.fill_ghosts("side", arrays)
+    ctx.synchronize()
+    for q in range(len(geoms)):
+        for a in range(3):
+            assert np.array_equal(arrays[q][a].cpu().numpy(), want[q][a]), f"patch {q} comp {a}"
