@@ -41,8 +41,9 @@ CONFIGS = {
                  desc="cfg3: 512^3 periodic staggered grid, 1e7 uniform markers, IB_6"),
     "cfg4": dict(N=1024, M=100_000_000, kernel="IB_4", markers="uniform",
                  desc="cfg4: 1024^3 periodic staggered grid, 1e8 uniform markers (seed 1234), IB_4, z-slabs"),
-    "cfg5": dict(N=512, M=10_000_000, kernel="IB_4", markers="clustered",
-                 desc="cfg5: 512^3 periodic staggered grid, 1e7 markers in ~2% of cells (4 sheets + 2 bundles), IB_4"),
+    "cfg5": dict(N=512, M=10_000_000, kernel="IB_4", markers="clustered", patches=8,
+                 desc="cfg5: 512^3 multi-patch finest level (8^3 patches of 64^3), 1e7 markers in ~2% of cells "
+                      "(4 sheets + 2 bundles), IB_4"),
 }
 
 
@@ -181,6 +182,166 @@ def cpu_baseline(cfg, kernel, seconds_target=15.0):
                       f"{elapsed:.1f} s"}
 
 
+def level_lists(X, N, P, g):
+    """LIndexSetData's per-patch lists on a level of P^3 equal patches tiling a
+    periodic [0,1)^3 (device torch ops): the interior lists (markers whose cell is
+    in the patch box, for interp) and the ghost-box lists (the markers and their
+    periodic images whose cell is in the patch's ghost box, for spread,
+    LDataManager.cpp:634-654).  Returns flat (indices, Xshift, offsets) per kind,
+    patch-major; within a patch in marker order."""
+    import torch
+    n = N // P
+    c = torch.clamp((X * N).floor().long(), 0, N - 1)
+    t = c // n
+    pid = (t[:, 2] * P + t[:, 1]) * P + t[:, 0]
+    o = torch.argsort(pid, stable=True)
+    cnt = torch.bincount(pid, minlength=P ** 3)
+    off_i = [0] + torch.cumsum(cnt, 0).tolist()
+    interior = o.to(torch.int32)
+    ent_p, ent_s, ent_x = [], [], []
+    ar = torch.arange(X.shape[0], device=X.device)
+    for oz in (-1, 0, 1):
+        for oy in (-1, 0, 1):
+            for ox in (-1, 0, 1):
+                off = torch.tensor([ox, oy, oz], device=X.device)
+                tt = t + off                       # the tile whose ghost box may hold the cell
+                shift = torch.zeros_like(tt)
+                shift[tt < 0] = 1                  # tile -1 is tile P-1: the image X + L
+                shift[tt >= P] = -1                # tile P is tile 0: the image X - L
+                cimg = c + shift * N
+                tw = tt % P
+                ok = ((cimg >= tw * n - g) & (cimg <= tw * n + n - 1 + g)).all(dim=1)
+                sel = ar[ok]
+                ent_p.append(((tw[ok, 2] * P + tw[ok, 1]) * P + tw[ok, 0]))
+                ent_s.append(sel)
+                ent_x.append(shift[ok].to(torch.float64))
+    ep, es, ex = torch.cat(ent_p), torch.cat(ent_s), torch.cat(ent_x)
+    o2 = torch.argsort(ep * X.shape[0] + es)
+    cnt2 = torch.bincount(ep, minlength=P ** 3)
+    off_s = [0] + torch.cumsum(cnt2, 0).tolist()
+    return (interior, None, off_i), (es[o2].to(torch.int32).contiguous(), ex[o2].contiguous(), off_s)
+
+
+def run_level(args, cfg, kernel, dev):
+    """--config cfg5 (default): the clustered markers on a multi-patch finest level,
+    8^3 patches of 64^3, one launch per sweep over every patch.
+    One step = level ghost fill of u, bin of the interior lists, interp, bin of the
+    ghost-box lists, spread (the patches' interiors are complete: no reduction)."""
+    import torch
+    from ibamr_amd import le
+    N, P = cfg["N"], cfg.get("patches", 8)
+    n = N // P
+    ctx = le.Context(dev.index or 0)
+    g = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
+    dx = 1.0 / N
+    geoms = []
+    for k in range(P):
+        for j in range(P):
+            for i in range(P):
+                lo = [i * n, j * n, k * n]
+                geoms.append(le.Geometry(lo, [v + n - 1 for v in lo], g, [dx] * 3, [v * dx for v in lo]))
+    t_setup = time.perf_counter()
+    from ibamr_amd.slab import Slab
+    X = make_markers(cfg["markers"], cfg["M"], Slab([N, N, N], 1, 0, g), 1234, dev)
+    X = torch.remainder(X, 1.0).contiguous()
+    M = X.shape[0]
+    gen = torch.Generator(device=dev).manual_seed(4321)
+    F = torch.rand((M, 3), dtype=torch.float64, device=dev, generator=gen).mul_(2).sub_(1)
+    U = torch.zeros((M, 3), dtype=torch.float64, device=dev)
+    (ii, _, oi), (si, sx, os_) = level_lists(X, N, P, g)
+    lvl_i = le.Level.from_flat(ctx, geoms, kernel, X, ii, None, oi)
+    lvl_s = le.Level.from_flat(ctx, geoms, kernel, X, si, sx, os_)
+    u = [[a.uniform_(-1.0, 1.0, generator=gen) for a in geom.alloc("side", device=dev)] for geom in geoms]
+    f = [geom.alloc("side", device=dev) for geom in geoms]
+    # algorithmic bytes: the distinct points each patch's ghost-box stencils touch
+    S_touched = [0, 0, 0]
+    for q, geom in enumerate(geoms):
+        if os_[q + 1] == os_[q]:
+            continue
+        idx_q = si[os_[q]:os_[q + 1]].contiguous()
+        xs_q = sx[os_[q]:os_[q + 1]].contiguous()
+        mq = le.Markers(ctx).bin(geom, kernel, X, idx_q, xs_q)
+        for a, m in enumerate(le.mark_stencils(ctx, mq, kernel, "side", geom, X)):
+            S_touched[a] += int(m.sum(dtype=torch.int64).item())
+    torch.cuda.synchronize()
+    log(f"setup {time.perf_counter() - t_setup:.1f}s: level {P}^3 patches of {n}^3, markers {M}, "
+        f"interior entries {oi[-1]}, ghost-box entries {os_[-1]}")
+    E = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    acc = {"fill": [], "bin": [], "interp": [], "spread": []}
+
+    def step(record):
+        if record:
+            E[0].record()
+        lvl_i.fill_ghosts("side", u)
+        if record:
+            E[1].record()
+        lvl_i.bin(X)
+        lvl_s.bin(X)
+        if record:
+            E[2].record()
+        lvl_i.interp("side", u, U, X)
+        if record:
+            E[3].record()
+        for per in f:
+            for t in per:
+                t.zero_()
+        if record:
+            E[4].record()
+        lvl_s.spread("side", f, F, X)
+        if record:
+            E[5].record()
+
+    for _ in range(args.warmup):
+        step(False)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(False)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    for _ in range(max(3, min(args.steps, 10))):
+        step(True)
+        torch.cuda.synchronize()
+        acc["fill"].append(E[0].elapsed_time(E[1]))
+        acc["bin"].append(E[1].elapsed_time(E[2]))
+        acc["interp"].append(E[2].elapsed_time(E[3]))
+        acc["spread"].append(E[4].elapsed_time(E[5]))
+    ctx.enable_timing(True)
+    kt = {"interp": [], "spread": []}
+    for _ in range(3):
+        lvl_i.interp("side", u, U, X)
+        ctx.synchronize()
+        kt["interp"].append(ctx.last_kernel_ms())
+        lvl_s.spread("side", f, F, X)
+        ctx.synchronize()
+        kt["spread"].append(ctx.last_kernel_ms())
+    ctx.enable_timing(False)
+    mean = lambda v: sum(v) / len(v)
+    k_i, k_s = mean(kt["interp"]), mean(kt["spread"])
+    # per entry X and Q/F (24 + 24 B), per touched point 8 B (interp) or 16 B (spread);
+    # the touched points are those of the ghost-box lists (an upper bound for interp's)
+    B_i = M * 48 + 8 * sum(S_touched)
+    B_s = os_[-1] * 48 + 16 * sum(S_touched)
+    dominant = "spread" if k_s >= k_i else "interp"
+    achieved = (B_s / (k_s * 1e-3) if dominant == "spread" else B_i / (k_i * 1e-3)) / 1e9
+    return {
+        "metric": METRIC, "value": 2.0 * M * args.steps / elapsed, "unit": "marker-ops/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": cfg["desc"], "kernel": kernel, "grid": [N, N, N], "markers": M,
+                   "parallelism": "one GPU", "patches": [P, P, P], "patch_cells": [n, n, n], "ghost": g,
+                   "step": "level ghost fill + bin(interior lists) + bin(ghost-box lists) + interp(3 comps) + "
+                           "zero f + spread(3 comps), one launch per sweep over the 512 patches"},
+        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes": {"interp": B_i, "spread": B_s}, "kernel_ms": {"interp": k_i, "spread": k_s}},
+        "cpu_baseline": None,
+        "breakdown_ms": {k: mean(v) for k, v in acc.items()},
+        "touched_points": S_touched,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -195,6 +356,8 @@ def main():
                     help="storage order of the markers: 'cell' = sorted by cell (z, y, x), the order "
                          "LDataManager's local numbering gives after redistribution (SURVEY.md 8d); "
                          "'random' = generation order")
+    ap.add_argument("--single-patch", action="store_true",
+                    help="cfg5 on one 512^3 patch instead of the 8^3-patch level")
     ap.add_argument("--move", action="store_true",
                     help="a full explicit coupling step: interp, X += dt U (ibtk_le_position_update), "
                          "migrate the slab leavers (N > 1), re-bin, spread")
@@ -221,6 +384,16 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+
+    if cfg.get("patches") and not args.single_patch and world == 1:
+        out = run_level(args, cfg, kernel, dev)
+        if not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(cfg, kernel, args.cpu_seconds)
+            except Exception as e:  # the baseline must never hide the GPU result
+                out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        print(json.dumps(out), flush=True)
+        return
 
     from ibamr_amd import le
     from ibamr_amd.slab import Slab, SlabExchange, migrate

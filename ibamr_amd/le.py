@@ -271,16 +271,35 @@ class Level:
             off.append(off[-1] + i.numel())
         self.indices = torch.cat(idx).contiguous()
         self.xshift = torch.cat(xs).contiguous() if any_shift else None
-        G = (PatchGeom * len(geoms))(*[g.c for g in geoms])
-        O = (ctypes.c_int * len(off))(*off)
-        check(ctx.lib.ibtk_le_level_bin(ctx.h, self.markers.h, len(geoms), G, kernel_id(kernel), _ptr(X), O,
-                                        _ptr(self.indices), _ptr(self.xshift)))
+        self._G = (PatchGeom * len(geoms))(*[g.c for g in geoms])
+        self._O = (ctypes.c_int * len(off))(*off)
+        self.bin(X)
+
+    @classmethod
+    def from_flat(cls, ctx: Context, geoms: Sequence[Geometry], kernel: str, X: torch.Tensor, indices: torch.Tensor,
+                  xshift: Optional[torch.Tensor], offsets: Sequence[int]):
+        """A level from the concatenated lists: patch q's entries are [offsets[q], offsets[q+1])."""
+        self = cls.__new__(cls)
+        self.ctx, self.geoms, self.kernel = ctx, list(geoms), kernel
+        self.markers = Markers(ctx)
+        self.indices = indices.to(torch.int32).contiguous()
+        self.xshift = xshift.contiguous() if xshift is not None else None
+        self._G = (PatchGeom * len(geoms))(*[g.c for g in geoms])
+        self._O = (ctypes.c_int * len(offsets))(*[int(o) for o in offsets])
+        self.bin(X)
+        return self
+
+    def bin(self, X: torch.Tensor):
+        """(Re-)bin the level's lists at positions X (ibtk_le_level_bin)."""
+        check(self.ctx.lib.ibtk_le_level_bin(self.ctx.h, self.markers.h, len(self.geoms), self._G,
+                                             kernel_id(self.kernel), _ptr(X), self._O, _ptr(self.indices),
+                                             _ptr(self.xshift)))
+        return self
 
     def fill_ghosts(self, centering: str, arrays, q_depth: int = 1, periodic=None):
         """Ghost fill across the level's patches (ibtk_le_level_fill_ghosts)."""
-        G = (PatchGeom * len(self.geoms))(*[g.c for g in self.geoms])
         pa = _periodic_arg(periodic, 3)
-        check(self.ctx.lib.ibtk_le_level_fill_ghosts(self.ctx.h, len(self.geoms), G, CENTERING[centering],
+        check(self.ctx.lib.ibtk_le_level_fill_ghosts(self.ctx.h, len(self.geoms), self._G, CENTERING[centering],
                                                      self._arrays(arrays), q_depth, pa[0] if pa else None))
 
     def _arrays(self, arrays):
