@@ -100,6 +100,7 @@ struct ibtk_le_ctx_s {
     DevBuf keys_in, vals_in, temp, counts, offsets, fbuf;
     DevBuf lst_idx, lst_xs, lst_key, lst_perm;  // index-list / node-distribution scratch
     DevBuf lvl_tab;                             // level ghost fill tables
+    std::vector<char> lvl_host;                 // what lvl_tab holds
     DevBuf err;   // one int
     DevBuf sink;  // 64 doubles (Params::sink)
     DevBuf stamps;  // diagnostic phase clocks (IBTK_LE_STAMPS=1)
@@ -129,6 +130,8 @@ struct ibtk_le_markers_s {
     int npatch = 0;
     std::vector<ibtk_le_patch_geom> geoms;
     std::vector<PatchDesc> pdh;           // host copy of the patch table (comps filled per call)
+    std::vector<PatchDesc> pdh_dev;       // what the device table holds (uploads skipped when unchanged)
+    std::vector<int> off_dev;             // what entry_off holds
     DevBuf pd, entry_off;
     int nbuckets_total = 0, njobs = 0;
     bool has_indices = false, has_xshift = false;
@@ -797,6 +800,19 @@ static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cente
 // a level of patches: LDataManager::spread / interp's patch loop
 // (LDataManager.cpp:625-660, 763-807) as one launch per sweep
 // ---------------------------------------------------------------------------
+// The device patch table follows the host one; an upload (a pageable copy, which
+// waits for the stream) only when the content changed -- a level reused with the
+// same arrays uploads nothing per call.
+static int upload_patches(ibtk_le_ctx ctx, ibtk_le_markers m) {
+    const size_t bytes = sizeof(PatchDesc) * m->pdh.size();
+    if (m->pdh_dev.size() == m->pdh.size() && std::memcmp(m->pdh_dev.data(), m->pdh.data(), bytes) == 0)
+        return IBTK_LE_OK;
+    if (int rc = m->pd.ensure(bytes)) return rc;
+    m->pdh_dev = m->pdh;
+    HIP_TRY(hipMemcpyAsync(m->pd.p, m->pdh_dev.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+    return IBTK_LE_OK;
+}
+
 extern "C" int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch, const ibtk_le_patch_geom* geoms,
                                  int kernel, const double* X_dev, const int* entry_offsets, const int* indices_dev,
                                  const double* Xshift_dev) {
@@ -817,6 +833,8 @@ extern "C" int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch,
     const hipStream_t s = ctx->stream;
     m->npatch = npatch;
     m->geoms.assign(geoms, geoms + npatch);
+    std::vector<PatchDesc> prev;
+    prev.swap(m->pdh);
     m->pdh.assign((size_t)npatch, PatchDesc{});
     long long nb = 0, nj = 0;
     BinGeom bg0{};
@@ -835,6 +853,7 @@ extern "C" int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch,
             P.xlo[d] = geoms[q].x_lower[d];
             P.ilower[d] = geoms[q].ilower[d];
         }
+        if (prev.size() == (size_t)npatch) std::memcpy(P.comp, prev[q].comp, sizeof(P.comp));  // arrays of the last call
         nb += cg.nbuckets;
         nj += (long long)cg.ncol * P.nseg;
         if (nb + 1 >= (1LL << 31) || nj >= (1LL << 30)) return fail(IBTK_LE_ERR_RANGE, "level too large for 31-bit keys");
@@ -855,11 +874,14 @@ extern "C" int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch,
     m->dedup_done = false;
     m->has_dups = false;
     int rc;
-    if ((rc = m->pd.ensure(sizeof(PatchDesc) * (size_t)npatch))) return rc;
-    if ((rc = m->entry_off.ensure(sizeof(int) * (size_t)(npatch + 1)))) return rc;
-    HIP_TRY(hipMemcpyAsync(m->pd.p, m->pdh.data(), sizeof(PatchDesc) * (size_t)npatch, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(m->entry_off.p, entry_offsets, sizeof(int) * (size_t)(npatch + 1), hipMemcpyHostToDevice,
-                           s));
+    if ((rc = upload_patches(ctx, m))) return rc;
+    if (m->off_dev.size() != (size_t)(npatch + 1) ||
+        std::memcmp(m->off_dev.data(), entry_offsets, sizeof(int) * (size_t)(npatch + 1)) != 0) {
+        if ((rc = m->entry_off.ensure(sizeof(int) * (size_t)(npatch + 1)))) return rc;
+        m->off_dev.assign(entry_offsets, entry_offsets + npatch + 1);
+        HIP_TRY(hipMemcpyAsync(m->entry_off.p, m->off_dev.data(), sizeof(int) * (size_t)(npatch + 1),
+                               hipMemcpyHostToDevice, s));
+    }
     if ((rc = m->plane_start.ensure(sizeof(int) * (size_t)(nb + 1)))) return rc;
     if (n == 0) {
         HIP_TRY(hipMemsetAsync(m->plane_start.p, 0, sizeof(int) * (size_t)(nb + 1), s));
@@ -936,8 +958,7 @@ static int level_params(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cent
         if (q == 0) std::memcpy(p.comp, t.comp, sizeof(t.comp));
     }
     if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
-    HIP_TRY(hipMemcpyAsync(m->pd.p, m->pdh.data(), sizeof(PatchDesc) * (size_t)m->npatch, hipMemcpyHostToDevice,
-                           ctx->stream));
+    if (int rc = upload_patches(ctx, m)) return rc;
     p.ncomp = nc;
     p.bg = m->bg;
     p.cg = m->cg;
@@ -1067,9 +1088,16 @@ extern "C" int ibtk_le_level_fill_ghosts(ibtk_le_ctx ctx, int npatch, const ibtk
     double** arr_d = reinterpret_cast<double**>(base);
     int* tile_d = reinterpret_cast<int*>(base + sizeof(double*) * narr);
     int* patch_d = tile_d + npatch;
-    HIP_TRY(hipMemcpyAsync(arr_d, q_dev, sizeof(double*) * narr, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(tile_d, tile_of.data(), sizeof(int) * (size_t)npatch, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(patch_d, patch_of.data(), sizeof(int) * (size_t)ntiles, hipMemcpyHostToDevice, s));
+    // upload the tables only when they changed (a pageable copy waits for the stream)
+    std::vector<char> host(sizeof(double*) * narr + sizeof(int) * (size_t)(npatch + ntiles));
+    std::memcpy(host.data(), q_dev, sizeof(double*) * narr);
+    std::memcpy(host.data() + sizeof(double*) * narr, tile_of.data(), sizeof(int) * (size_t)npatch);
+    std::memcpy(host.data() + sizeof(double*) * narr + sizeof(int) * (size_t)npatch, patch_of.data(),
+                sizeof(int) * (size_t)ntiles);
+    if (ctx->lvl_host != host) {
+        ctx->lvl_host = host;
+        HIP_TRY(hipMemcpyAsync(base, ctx->lvl_host.data(), host.size(), hipMemcpyHostToDevice, s));
+    }
     HIP_TRY(launch_level_fill(t, npatch, tile_d, patch_d, arr_d, t.side ? 1 : q_depth, s));
     return IBTK_LE_OK;
 }

@@ -303,8 +303,16 @@ class Level:
                                                      self._arrays(arrays), q_depth, pa[0] if pa else None))
 
     def _arrays(self, arrays):
+        # the pointer table of a list of per-patch arrays, cached on the list object
+        # (a level reuses its u and f arrays step after step)
+        key = id(arrays)
+        hit = self.__dict__.setdefault("_ptr_cache", {}).get(key)
+        if hit is not None and hit[0] is arrays and hit[2] == arrays[0][0].data_ptr():
+            return hit[1]
         flat = [t for per in arrays for t in per]
-        return _ptr_array(flat)
+        tab = _ptr_array(flat)
+        self._ptr_cache[key] = (arrays, tab, arrays[0][0].data_ptr())
+        return tab
 
     def interp(self, centering: str, arrays, Q: torch.Tensor, X: torch.Tensor, q_depth: int = 1,
                Q_depth: Optional[int] = None, axis: int = 0):
