@@ -352,6 +352,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-rebin", action="store_true", help="bin once outside the timed loop")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N > 1: exchange the ghost planes before interp / after spread instead of overlapping "
+                         "them with the interior sweep items")
     ap.add_argument("--marker-order", default="cell", choices=["cell", "random"],
                     help="storage order of the markers: 'cell' = sorted by cell (z, y, x), the order "
                          "LDataManager's local numbering gives after redistribution (SURVEY.md 8d); "
@@ -422,6 +425,8 @@ def main():
     f = geom.alloc("side", device=dev)
     ex_u = SlabExchange(slab, u, ctx)
     ex_f = SlabExchange(slab, f, ctx)
+    if not args.no_overlap:
+        ex_u.cut_items()  # sweep items cut at the slab faces (N > 1)
     bins = le.Markers(ctx)
     bins.bin(geom, kernel, X)
     # exact algorithmic bytes: distinct side points touched by the clipped stencils
@@ -438,9 +443,26 @@ def main():
         f"slab z[{slab.z0},{slab.z1}), touched {S_touched}")
 
     E = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
-    acc = {"bin": [], "interp": [], "spread": [], "exchange": []}
+    acc = {"bin": [], "interp": [], "zero": [], "spread": []}
 
     dt_move = 0.05 * slab.dx[0]  # |U| <= ~1: markers move <= 1/20 cell per step
+
+    def interp_with_fill():
+        # N > 1: the interior sweep items run while the z ghost planes are in flight
+        if args.no_overlap:
+            ex_u.halo_fill()
+            le.interp(ctx, bins, kernel, "side", geom, u, U, X)
+        else:
+            ex_u.halo_fill(lambda: le.interp(ctx, bins, kernel, "side", geom, u, U, X))
+
+    def spread_with_sum():
+        # N > 1: the boundary items first, then the interior ones while the ghost
+        # planes are in flight
+        if args.no_overlap:
+            le.spread(ctx, bins, kernel, "side", geom, f, F, X)
+            ex_f.ghost_sum()
+        else:
+            ex_f.ghost_sum(lambda: le.spread(ctx, bins, kernel, "side", geom, f, F, X))
 
     def step_move(record):
         # interp -> X += dt U -> migrate -> bin -> spread: one bin per step, as in
@@ -448,8 +470,7 @@ def main():
         nonlocal X, F, U
         if record:
             E[0].record()
-        ex_u.halo_fill()
-        le.interp(ctx, bins, kernel, "side", geom, u, U, X)
+        interp_with_fill()
         if record:
             E[1].record()
         le.position_update(ctx, "euler", dt_move, X, U, out=X)
@@ -463,12 +484,9 @@ def main():
         le.zero_ghosts(ctx, geom, "side", f)
         if record:
             E[3].record()
-        le.spread(ctx, bins, kernel, "side", geom, f, F, X)
+        spread_with_sum()
         if record:
             E[4].record()
-        ex_f.ghost_sum()
-        if record:
-            E[5].record()
 
     def step(record):
         if args.move:
@@ -479,30 +497,27 @@ def main():
             bins.bin(geom, kernel, X)
         if record:
             E[1].record()
-        ex_u.halo_fill()
-        le.interp(ctx, bins, kernel, "side", geom, u, U, X)
+        interp_with_fill()
         if record:
             E[2].record()
         le.zero_ghosts(ctx, geom, "side", f)
         if record:
             E[3].record()
-        le.spread(ctx, bins, kernel, "side", geom, f, F, X)
+        spread_with_sum()
         if record:
             E[4].record()
-        ex_f.ghost_sum()
-        if record:
-            E[5].record()
 
     def collect():
+        # interp / spread include their ghost exchange (overlapped when N > 1)
         torch.cuda.synchronize()
-        if args.move:  # E0-E1 interp, E1-E2 update + migrate + bin
+        if args.move:  # E0-E1 fill + interp, E1-E2 update + migrate + bin
             acc["interp"].append(E[0].elapsed_time(E[1]))
             acc["bin"].append(E[1].elapsed_time(E[2]))
         else:
             acc["bin"].append(E[0].elapsed_time(E[1]))
             acc["interp"].append(E[1].elapsed_time(E[2]))
+        acc["zero"].append(E[2].elapsed_time(E[3]))
         acc["spread"].append(E[3].elapsed_time(E[4]))
-        acc["exchange"].append(E[2].elapsed_time(E[3]) + E[4].elapsed_time(E[5]))
 
     for _ in range(args.warmup):
         step(False)
@@ -587,7 +602,7 @@ def main():
         "data": "synthetic",
         "config": {"workload": cfg["desc"], "kernel": kernel, "grid": [N, N, N], "markers": M_total,
                    "parallelism": f"z-slab x{world}", "ghost": ghost, "marker_order": args.marker_order,
-                   "move": args.move,
+                   "move": args.move, "overlap": world > 1 and not args.no_overlap,
                    "step": ("ghost fill + interp(3 comps) + position update + migrate + bin + zero ghosts + "
                             "spread(3 comps) + ghost sum" if args.move else
                             "bin + ghost fill + interp(3 comps) + zero ghosts + spread(3 comps) + ghost sum")},

@@ -78,6 +78,7 @@ _SIGS = [
     ("ibtk_le_ctx_synchronize", c_int, [c_void_p]),
     ("ibtk_le_ctx_enable_timing", c_int, [c_void_p, c_int]),
     ("ibtk_le_ctx_tune", c_int, [c_void_p, ctypes.c_char_p, c_int]),
+    ("ibtk_le_ctx_set_plane_window", c_int, [c_void_p, c_int, c_int, c_int]),
     ("ibtk_le_ctx_last_kernel_ms", c_double, [c_void_p]),
     ("ibtk_le_markers_create", c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
     ("ibtk_le_markers_destroy", c_int, [c_void_p]),

@@ -107,6 +107,7 @@ struct ibtk_le_ctx_s {
     bool stamps_on = false;  // IBTK_LE_STAMPS=1, read once at ctx_create
     int dbg = 0;             // IBTK_LE_DBG, read once at ctx_create
     SweepTune tune;          // ibtk_le_ctx_tune (diagnostics)
+    int zmode = 0, zlo = 0, zhi = -1;  // ibtk_le_ctx_set_plane_window
     bool timing = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool ev_valid = false;
@@ -200,6 +201,15 @@ extern "C" int ibtk_le_ctx_synchronize(ibtk_le_ctx ctx) {
                     "device invariant failed (flag %d): a stencil left its staged region (1) or its bin bounds (2)",
                     flag);
     }
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_ctx_set_plane_window(ibtk_le_ctx ctx, int mode, int zlo, int zhi) {
+    if (!ctx) return fail(IBTK_LE_ERR_ARG, "null ctx");
+    if (mode < 0 || mode > 2) return fail(IBTK_LE_ERR_ARG, "plane window mode: 0 all, 1 inside, 2 outside");
+    ctx->zmode = mode;
+    ctx->zlo = zlo;
+    ctx->zhi = zhi;
     return IBTK_LE_OK;
 }
 
@@ -445,7 +455,21 @@ extern "C" int ibtk_le_markers_order(ibtk_le_markers m, const int** order_dev) {
 static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel) {
     const int nj = m->npatch ? m->njobs : m->cg.ncol * m->nseg;
     const int target = ctx->tune.split_target > 0 ? ctx->tune.split_target : IBTK_LE_SPLIT_TARGET;
-    const long long bound = (long long)nj + (long long)m->n / target + 1;
+    Params p;
+    std::memset(&p, 0, sizeof(p));
+    if (!m->npatch && ctx->zlo <= ctx->zhi) {
+        // cut the items at the plane window's edges, so that the items of a
+        // restricted call (ibtk_le_ctx_set_plane_window) are exactly the ones
+        // next to the window's faces: the anchors reading below zlo / above zhi
+        // (interp) and the planes outside [zlo, zhi] (spread)
+        const KernelInfo ki = kKernelInfo[kernel];
+        const int lo = ctx->zlo - m->cg.org[2], hi = ctx->zhi - m->cg.org[2];
+        int c[4] = {lo - ki.LO, lo, hi - ki.HI + 1, hi + 1};
+        std::sort(c, c + 4);
+        for (int i = 0; i < 4; ++i)
+            if (c[i] > 0 && c[i] < m->cg.nz && (p.ncut == 0 || p.cut[p.ncut - 1] != c[i])) p.cut[p.ncut++] = c[i];
+    }
+    const long long bound = (long long)nj + (long long)m->n / target + 1 + (long long)p.ncut * m->cg.ncol;
     if (bound * 3 >= (1LL << 31)) return fail(IBTK_LE_ERR_RANGE, "too many sweep items");
     m->item_bound = (int)bound;
     int rc;
@@ -453,8 +477,6 @@ static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel) {
     if ((rc = m->nsub.ensure(sizeof(int) * (size_t)std::max(nj, 1)))) return rc;
     if ((rc = m->isub.ensure(sizeof(int) * (size_t)std::max(nj, 1)))) return rc;
     if ((rc = m->nitems.ensure(sizeof(int)))) return rc;
-    Params p;
-    std::memset(&p, 0, sizeof(p));
     p.cg = m->cg;
     p.S = m->S;
     p.nseg = m->nseg;
@@ -610,6 +632,9 @@ static int prepare(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const ibtk_le
     p.err = ctx->err.as<int>();
     p.sink = ctx->sink.as<double>();
     p.tune = ctx->tune;
+    p.zmode = ctx->zmode;
+    p.zlo = ctx->zlo;
+    p.zhi = ctx->zhi;
     p.K6 = ib6_K();
     p.h3 = geom->ndim == 3 ? (geom->dx[0] * geom->dx[1]) * geom->dx[2] : geom->dx[0] * geom->dx[1];
     return IBTK_LE_OK;

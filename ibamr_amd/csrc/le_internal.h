@@ -130,6 +130,9 @@ struct Params {
     const int* entry_off;      // level: list entries of patch q are [entry_off[q], entry_off[q+1])
     int nbuckets_total;        // buckets of every patch (entries keyed >= it are outside)
     int njobs;                 // (segment, column) pairs of every patch
+    int ncut, cut[4];          // item table: extra cuts at these relative planes (the plane window's edges)
+    int zmode, zlo, zhi;       // plane window (ibtk_le_ctx_set_plane_window): 0 every item, 1 the items
+                               // whose planes lie in [zlo, zhi], 2 the others
     const SweepItem* items;    // 3-D sweep item table (k_item_write)
     const int* nitems;         // device: its length
     int item_bound;            // host: an upper bound of the length (the launch grid)

@@ -450,6 +450,10 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     CompDesc cd;
     const int* bs;
     item_patch<LVL>(p, si, c, cg, cd, bs);
+    if (p.zmode) {  // the planes the item reads: a0 + LO .. a1 - 1 + HI
+        const bool inner = cg.org[2] + a0 + LO >= p.zlo && cg.org[2] + a1 - 1 + HI <= p.zhi;
+        if (inner != (p.zmode == 1)) return;
+    }
     {
         bool any = false;  // the same answer in both waves
         for (int a = a0 + lane; a < a1; a += SW) any = any || bs[bucket(cg, a, col, NBAND)] > bs[bucket(cg, a, col, 0)];
@@ -828,6 +832,10 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     const int ylo = max(cd.lo[1] - Y0, 0), yhi = min(cd.hi[1] - Y0, COLY - 1);
     const int plo = max(si.p0, cd.lo[2] - zorg), phi = min(si.p1 - 1, cd.hi[2] - zorg);
     if (xlo > xhi || ylo > yhi || plo > phi) return;
+    if (p.zmode) {  // the planes the item owns (reads and writes)
+        const bool inner = zorg + plo >= p.zlo && zorg + phi <= p.zhi;
+        if (inner != (p.zmode == 1)) return;
+    }
     const int afirst = max(plo - HI, 0), alast = min(phi - LO, cg.nz - 1);
     const int col0 = (cy - 1) * ncx + (cx - 1);  // column (cx-1, cy-1)
     {
@@ -1049,25 +1057,24 @@ __device__ __forceinline__ void job_patch(const Params& p, int j, int& q, ColGeo
     bs = p.plane_start + P.bucket_base;
 }
 
+// load-based sub-segments of (column col, planes [a0, a1))
 template <int K>
-__global__ __launch_bounds__(BLOCK) void k_item_counts(Params p, int target, int* nsub) {
+__device__ __forceinline__ int load_split(const ColGeom& cg, const int* bs, int col, int a0, int a1, int target) {
     constexpr int NS = KT<K>::HI - KT<K>::LO + 1;
-    const int j = blockIdx.x * BLOCK + threadIdx.x;
-    if (j >= p.njobs) return;
-    int q, S, nseg, j0;
-    ColGeom cg;
-    const int* bs;
-    job_patch(p, j, q, cg, S, nseg, j0, bs);
-    const int jl = j - j0;
-    const int seg = jl / cg.ncol, col = jl - seg * cg.ncol;
-    const int a0 = seg * S, a1 = min(a0 + S, cg.nz);
     long load = 0;
     for (int a = a0; a < a1; ++a) load += bs[bucket(cg, a, col, NBAND)] - bs[bucket(cg, a, col, 0)];
     const int maxsub = max((a1 - a0) / max(NS, 8), 1);
-    nsub[j] = (int)min((long)maxsub, max(1L, (load + target - 1) / target));
+    return (int)min((long)maxsub, max(1L, (load + target - 1) / target));
 }
-__global__ __launch_bounds__(BLOCK) void k_item_write(Params p, const int* nsub, const int* start, SweepItem* tab,
-                                                      int* ntot) {
+// the plane cuts (ibtk_le_ctx_set_plane_window: sorted, relative) strictly inside (b0, b1)
+__device__ __forceinline__ int cuts_inside(const Params& p, int b0, int b1) {
+    int c = 0;
+    for (int i = 0; i < p.ncut; ++i) c += p.cut[i] > b0 && p.cut[i] < b1;
+    return c;
+}
+
+template <int K>
+__global__ __launch_bounds__(BLOCK) void k_item_counts(Params p, int target, int* nsub) {
     const int j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= p.njobs) return;
     int q, S, nseg, j0;
@@ -1077,9 +1084,37 @@ __global__ __launch_bounds__(BLOCK) void k_item_write(Params p, const int* nsub,
     const int jl = j - j0;
     const int seg = jl / cg.ncol, col = jl - seg * cg.ncol;
     const int a0 = seg * S, a1 = min(a0 + S, cg.nz), len = a1 - a0;
-    const int n = nsub[j], s0 = start[j];
-    for (int k = 0; k < n; ++k) tab[s0 + k] = SweepItem{col, a0 + (len * k) / n, a0 + (len * (k + 1)) / n, q};
-    if (j == p.njobs - 1) *ntot = s0 + n;
+    const int n = load_split<K>(cg, bs, col, a0, a1, target);
+    int pieces = n;
+    if (p.ncut)
+        for (int k = 0; k < n; ++k) pieces += cuts_inside(p, a0 + (len * k) / n, a0 + (len * (k + 1)) / n);
+    nsub[j] = pieces;
+}
+template <int K>
+__global__ __launch_bounds__(BLOCK) void k_item_write(Params p, int target, const int* nsub, const int* start,
+                                                      SweepItem* tab, int* ntot) {
+    const int j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= p.njobs) return;
+    int q, S, nseg, j0;
+    ColGeom cg;
+    const int* bs;
+    job_patch(p, j, q, cg, S, nseg, j0, bs);
+    const int jl = j - j0;
+    const int seg = jl / cg.ncol, col = jl - seg * cg.ncol;
+    const int a0 = seg * S, a1 = min(a0 + S, cg.nz), len = a1 - a0;
+    const int n = load_split<K>(cg, bs, col, a0, a1, target);
+    int w = start[j];
+    for (int k = 0; k < n; ++k) {
+        int b0 = a0 + (len * k) / n;
+        const int b1 = a0 + (len * (k + 1)) / n;
+        for (int i = 0; i < p.ncut; ++i)
+            if (p.cut[i] > b0 && p.cut[i] < b1) {
+                tab[w++] = SweepItem{col, b0, p.cut[i], q};
+                b0 = p.cut[i];
+            }
+        tab[w++] = SweepItem{col, b0, b1, q};
+    }
+    if (j == p.njobs - 1) *ntot = start[j] + nsub[j];
 }
 
 static int grid8(long items) { return (int)((items + 7) & ~7L); }
@@ -1091,7 +1126,8 @@ template <int K> hipError_t launch_item_table_t(const Params& p, int target, int
     hipLaunchKernelGGL(k_item_counts<K>, dim3((nj + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, target, nsub);
     hipError_t e = launch_scan(temp, temp_bytes, nsub, start, nj, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_item_write, dim3((nj + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, nsub, start, tab, ntot);
+    hipLaunchKernelGGL(k_item_write<K>, dim3((nj + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, target, nsub, start, tab,
+                       ntot);
     return hipGetLastError();
 }
 

@@ -112,6 +112,11 @@ class Context:
     def enable_timing(self, on=True):
         check(self.lib.ibtk_le_ctx_enable_timing(self.h, int(on)))
 
+    def set_plane_window(self, mode: int, zlo: int = 0, zhi: int = -1):
+        """Restrict the next 3-D sweeps to the items inside (1) / outside (2) the planes
+        [zlo, zhi]; 0 = every item (ibtk_le_ctx_set_plane_window)."""
+        check(self.lib.ibtk_le_ctx_set_plane_window(self.h, int(mode), int(zlo), int(zhi)))
+
     def tune(self, key: str, value: int):
         """Diagnostic overrides of the 3-D sweeps' work-item order (ibtk_le_ctx_tune)."""
         check(self.lib.ibtk_le_ctx_tune(self.h, key.encode(), int(value)))

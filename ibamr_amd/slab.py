@@ -105,7 +105,7 @@ class SlabExchange:
         le.fold_periodic_ghosts(self.ctx, self.geom, "side", self.arrays, periodic=periodic)
 
     # -- exchanges -------------------------------------------------------------------
-    def _p2p(self, sends, recvs):
+    def _p2p_start(self, sends, recvs):
         import torch.distributed as dist
         # gloo moves host memory only: device tensors are staged through the host
         # (the multi-rank rehearsal on one GPU; RCCL sends device memory directly)
@@ -121,17 +121,51 @@ class SlabExchange:
                 back.append((h, t))
                 t = h
             ops.append(dist.P2POp(dist.irecv, t, peer, group=self.group))
-        if ops:
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
+        # RCCL: the transfers run on the communicator's stream, ordered after the
+        # work already queued on the current stream; what is queued next overlaps
+        return (dist.batch_isend_irecv(ops) if ops else []), back
+
+    @staticmethod
+    def _p2p_wait(handle):
+        works, back = handle
+        for w in works:
+            w.wait()  # RCCL: the current stream waits for the transfers (no host block)
         for h, t in back:
             t.copy_(h)
 
-    def halo_fill(self):
-        """Every ghost point := its periodic interior value (before interpolation)."""
+    def _p2p(self, sends, recvs):
+        self._p2p_wait(self._p2p_start(sends, recvs))
+
+    def _windowed(self, work, mode):
+        """work() restricted to the sweep items inside (1) / outside (2) the rank's
+        own planes [z0, z1) (ibtk_le_ctx_set_plane_window); the two halves add up to
+        one unrestricted call bit for bit."""
+        s = self.slab
+        self.ctx.set_plane_window(mode, s.z0, s.z1 - 1)
+        try:
+            work()
+        finally:
+            self.ctx.set_plane_window(0, s.z0, s.z1 - 1)
+
+    def cut_items(self):
+        """Make the markers binned from now on on this context cut their sweep items
+        at the slab faces (ibtk_le_ctx_set_plane_window with mode 0), so the
+        boundary items of an overlapped call are only the few planes next to a face."""
+        if self.slab.P > 1 and self.ctx is not None:
+            self.ctx.set_plane_window(0, self.slab.z0, self.slab.z1 - 1)
+
+    def halo_fill(self, work=None):
+        """Every ghost point := its periodic interior value (before interpolation).
+
+        work: optional callable (the interpolation); it then runs in two halves,
+        the sweep items that read only the rank's own planes while the z planes
+        are in flight, and the items next to the slab faces after they land."""
         s = self.slab
         if s.P == 1:
-            return self.local_fill([1, 1, 1])
+            self.local_fill([1, 1, 1])
+            if work is not None:
+                work()
+            return
         self.local_fill([1, 1, 0])   # x/y ghosts of the interior planes
         sends, recvs = [], []
         for c, a in enumerate(self.arrays):
@@ -148,13 +182,26 @@ class SlabExchange:
             sends.append((a[b0:b1], s.down))    # my bottom planes -> down's upper ghosts
             recvs.append((a[lo0:lo1], s.down))  # down's top planes (its first send)
             recvs.append((a[hi0:hi1], s.up))    # up's bottom planes (its second send)
-        self._p2p(sends, recvs)
+        h = self._p2p_start(sends, recvs)
+        if work is not None:
+            self._windowed(work, 1)
+        self._p2p_wait(h)
+        if work is not None:
+            self._windowed(work, 2)
 
-    def ghost_sum(self):
-        """Fold every ghost value onto its owner's interior point (after spreading)."""
+    def ghost_sum(self, work=None):
+        """Fold every ghost value onto its owner's interior point (after spreading).
+
+        work: optional callable (the spreading into the zeroed-ghost arrays); it
+        then runs in two halves, the sweep items owning planes next to the slab
+        faces first, and the interior items while the ghost planes are in flight."""
         s = self.slab
         if s.P == 1:
+            if work is not None:
+                work()
             return self.local_fold([1, 1, 1])
+        if work is not None:
+            self._windowed(work, 2)
         sends, recvs = [], []
         for c, a in enumerate(self.arrays):
             b = s.blocks(c)
@@ -168,7 +215,10 @@ class SlabExchange:
             # send, my bottom planes)
             recvs.append((rlo, s.up))
             recvs.append((rhi, s.down))
-        self._p2p(sends, recvs)
+        h = self._p2p_start(sends, recvs)
+        if work is not None:
+            self._windowed(work, 1)
+        self._p2p_wait(h)
         for c, a in enumerate(self.arrays):
             b = s.blocks(c)
             rlo, rhi = self.bufs[c]
@@ -218,20 +268,21 @@ def migrate(slab: Slab, X: torch.Tensor, fields: Sequence[torch.Tensor] = (), gr
     order = torch.argsort(dest, stable=True)
     send = data[order].contiguous()
     send_counts = torch.bincount(dest, minlength=slab.P).to(torch.int64)
-    recv_counts = torch.empty_like(send_counts)
     if slab.P == 1:
-        recv, recv_counts = send, send_counts
+        recv = send
     else:
         # gloo moves host memory only (the one-GPU rehearsal): stage through the host
         host = dist.get_backend(group) == "gloo" and send.is_cuda
         sc = send_counts.cpu() if host else send_counts
         rc = torch.empty_like(sc)
         dist.all_to_all_single(rc, sc, group=group)
-        recv_counts = rc.to(send_counts.device)
+        # the split sizes must be host integers (all_to_all_single's signature):
+        # one device->host copy of both count vectors, the step's only host sync
+        counts = torch.stack([sc, rc]).cpu().tolist() if not host else [sc.tolist(), rc.tolist()]
         D = send.shape[1]
         sd = send.cpu() if host else send
-        recv = torch.empty((int(rc.sum().item()), D), dtype=send.dtype, device=sd.device)
-        dist.all_to_all_single(recv, sd, output_split_sizes=rc.tolist(), input_split_sizes=sc.tolist(), group=group)
+        recv = torch.empty((sum(counts[1]), D), dtype=send.dtype, device=sd.device)
+        dist.all_to_all_single(recv, sd, output_split_sizes=counts[1], input_split_sizes=counts[0], group=group)
         recv = recv.to(send.device)
     if stay is not None:
         recv = torch.cat([stay, recv], dim=0)

@@ -92,6 +92,18 @@ const char* ibtk_le_version(void);
 int ibtk_le_ctx_create(int device, void* stream, ibtk_le_ctx* out);
 int ibtk_le_ctx_destroy(ibtk_le_ctx ctx);
 int ibtk_le_ctx_set_stream(ibtk_le_ctx ctx, void* stream);
+/* Restricts the next 3-D interp / spread calls on this context to a subset of
+ * their work items (mode 1: the items whose planes -- interp: the planes it reads,
+ * spread: the planes it owns -- all lie in [zlo, zhi], absolute z indices; mode 2:
+ * the other items; mode 0: every item, the default).  A z-slab rank computes
+ * its interior items while the halo exchange is in flight and the boundary
+ * items after it; the two calls together equal one unrestricted call bit for
+ * bit (each grid point is owned by exactly one item).  While zlo <= zhi, the
+ * markers binned on this context (any mode) cut their sweep items at the
+ * window's edges, so the boundary items are only the planes next to them.
+ * 2-D calls ignore the window.  Replaces no reference entry point: the
+ * reference overlaps nothing (RefineSchedule::fillData, LDataManager.cpp:748). */
+int ibtk_le_ctx_set_plane_window(ibtk_le_ctx ctx, int mode, int zlo, int zhi);
 /* Waits for the context stream and reports device-side invariant failures
  * latched by earlier calls (IBTK_LE_ERR_INVARIANT), then clears them. */
 int ibtk_le_ctx_synchronize(ibtk_le_ctx ctx);

@@ -287,8 +287,10 @@ def _fill_interior(a, G, g, z0, nz, N):
     a[g:g + nz, g:g + N, g:g + N] = torch.from_numpy(G[z0:z0 + nz])
 
 
-def _slab_run(le, ctx, N, M, world, rank, kernel="IB_4", move=False):
-    """One rank's interp + spread on its slab; returns (ids, U, f interior planes)."""
+def _slab_run(le, ctx, N, M, world, rank, kernel="IB_4", move=False, overlap=False):
+    """One rank's interp + spread on its slab; returns (ids, U, f interior planes).
+    overlap: the sweep items cut at the slab faces, interp / spread in two halves
+    around the exchanges (SlabExchange.halo_fill(work) / ghost_sum(work))."""
     from ibamr_amd.slab import Slab, SlabExchange, migrate
     g = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
     slab = Slab([N, N, N], world, rank, g)
@@ -302,18 +304,30 @@ def _slab_run(le, ctx, N, M, world, rank, kernel="IB_4", move=False):
     u = geom.alloc("side")
     for c in range(3):
         _fill_interior(u[c], G[c], g, slab.z0, slab.nz, N)
-    SlabExchange(slab, u, ctx).halo_fill()
+    ex_u = SlabExchange(slab, u, ctx)
+    if overlap:
+        ex_u.cut_items()
+    else:
+        ctx.set_plane_window(0)  # no cuts
     m = le.Markers(ctx).bin(geom, kernel, X)
     U = torch.zeros_like(X)
-    le.interp(ctx, m, kernel, "side", geom, u, U, X)
+    if overlap:
+        ex_u.halo_fill(lambda: le.interp(ctx, m, kernel, "side", geom, u, U, X))
+    else:
+        ex_u.halo_fill()
+        le.interp(ctx, m, kernel, "side", geom, u, U, X)
     if move:
         le.position_update(ctx, "euler", 0.5 * slab.dx[0], X, U, out=X)
         X, (F, ids) = migrate(slab, X, [F, ids], cell_order=False)
         m = le.Markers(ctx).bin(geom, kernel, X)
     f = geom.alloc("side")
     le.zero_ghosts(ctx, geom, "side", f)
-    le.spread(ctx, m, kernel, "side", geom, f, F, X)
-    SlabExchange(slab, f, ctx).ghost_sum()
+    if overlap:
+        SlabExchange(slab, f, ctx).ghost_sum(lambda: le.spread(ctx, m, kernel, "side", geom, f, F, X))
+    else:
+        le.spread(ctx, m, kernel, "side", geom, f, F, X)
+        SlabExchange(slab, f, ctx).ghost_sum()
+    ctx.set_plane_window(0)
     ctx.synchronize()
     fin = [t[g:g + slab.nz, g:g + N, g:g + N].cpu().numpy().copy() for t in f]
     return mine, U.cpu().numpy(), fin, slab.z0, slab.nz
@@ -329,6 +343,13 @@ def _slab_worker(rank, world, port, N, M, move, out_q):
         from ibamr_amd import le
         ctx = le.Context(0)
         ids, U, fin, z0, nz = _slab_run(le, ctx, N, M, world, rank, move=move)
+        if not move:
+            # the overlapped form (cut items, two half-sweeps around each exchange)
+            # must give the same bits
+            ids2, U2, fin2, _, _ = _slab_run(le, ctx, N, M, world, rank, move=move, overlap=True)
+            assert np.array_equal(ids2, ids) and np.array_equal(U2, U), f"rank {rank}: overlapped interp differs"
+            for c in range(3):
+                assert np.array_equal(fin2[c], fin[c]), f"rank {rank}: overlapped spread comp {c} differs"
         out_q.put((rank, "ok", ids, U, fin, z0, nz))
         dist.barrier()
         dist.destroy_process_group()
