@@ -267,7 +267,7 @@ def run_level(args, cfg, kernel, dev):
     log(f"setup {time.perf_counter() - t_setup:.1f}s: level {P}^3 patches of {n}^3, markers {M}, "
         f"interior entries {oi[-1]}, ghost-box entries {os_[-1]}")
     E = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
-    acc = {"fill": [], "bin": [], "interp": [], "spread": []}
+    acc = {"fill": [], "bin": [], "interp": [], "zero": [], "spread": []}
 
     def step(record):
         if record:
@@ -282,9 +282,7 @@ def run_level(args, cfg, kernel, dev):
         lvl_i.interp("side", u, U, X)
         if record:
             E[3].record()
-        for per in f:
-            for t in per:
-                t.zero_()
+        lvl_s.zero("side", f)
         if record:
             E[4].record()
         lvl_s.spread("side", f, F, X)
@@ -306,6 +304,7 @@ def run_level(args, cfg, kernel, dev):
         acc["fill"].append(E[0].elapsed_time(E[1]))
         acc["bin"].append(E[1].elapsed_time(E[2]))
         acc["interp"].append(E[2].elapsed_time(E[3]))
+        acc["zero"].append(E[3].elapsed_time(E[4]))
         acc["spread"].append(E[4].elapsed_time(E[5]))
     ctx.enable_timing(True)
     kt = {"interp": [], "spread": []}

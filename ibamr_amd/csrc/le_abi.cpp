@@ -101,6 +101,8 @@ struct ibtk_le_ctx_s {
     DevBuf lst_idx, lst_xs, lst_key, lst_perm;  // index-list / node-distribution scratch
     DevBuf lvl_tab;                             // level ghost fill tables
     std::vector<char> lvl_host;                 // what lvl_tab holds
+    DevBuf zero_tab;                            // level zero tables
+    std::vector<char> zero_host;                // what zero_tab holds
     DevBuf err;   // one int
     DevBuf sink;  // 64 doubles (Params::sink)
     DevBuf stamps;  // diagnostic phase clocks (IBTK_LE_STAMPS=1)
@@ -175,7 +177,7 @@ extern "C" int ibtk_le_ctx_destroy(ibtk_le_ctx ctx) {
     hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->keys_in, &ctx->vals_in, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->fbuf, &ctx->err, &ctx->sink,
                        &ctx->stamps, &ctx->lst_idx, &ctx->lst_xs, &ctx->lst_key, &ctx->lst_perm,
-                       &ctx->lvl_tab})
+                       &ctx->lvl_tab, &ctx->zero_tab})
         b->release();
     if (ctx->ev0) hipEventDestroy(ctx->ev0);
     if (ctx->ev1) hipEventDestroy(ctx->ev1);
@@ -1124,6 +1126,55 @@ extern "C" int ibtk_le_level_fill_ghosts(ibtk_le_ctx ctx, int npatch, const ibtk
         HIP_TRY(hipMemcpyAsync(base, ctx->lvl_host.data(), host.size(), hipMemcpyHostToDevice, s));
     }
     HIP_TRY(launch_level_fill(t, npatch, tile_d, patch_d, arr_d, t.side ? 1 : q_depth, s));
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_level_zero(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms, int centering,
+                                  double* const* q_dev, int q_depth) {
+    if (!ctx || !geoms || !q_dev || npatch <= 0) return fail(IBTK_LE_ERR_ARG, "level_zero: null argument");
+    if (q_depth < 1) return fail(IBTK_LE_ERR_ARG, "level_zero: q_depth < 1");
+    const int nd = geoms[0].ndim;
+    const bool vec = centering == IBTK_LE_SIDE || centering == IBTK_LE_EDGE;
+    if (!vec && centering != IBTK_LE_CELL && centering != IBTK_LE_NODE)
+        return fail(IBTK_LE_ERR_ARG, "level_zero: unknown centering %d", centering);
+    const int per = vec ? nd : 1;
+    const size_t narr = (size_t)npatch * per;
+    if (narr > 65535) return fail(IBTK_LE_ERR_RANGE, "level_zero: more than 65535 arrays");
+    std::vector<long long> cnt(narr);
+    long long mx = 0;
+    for (int q = 0; q < npatch; ++q) {
+        if (int rc = check_geom(&geoms[q])) return rc;
+        if (geoms[q].ndim != nd) return fail(IBTK_LE_ERR_ARG, "level_zero: patches of one dimension");
+        for (int a = 0; a < per; ++a) {
+            long long n = vec ? 1 : q_depth;
+            for (int d = 0; d < nd; ++d) {
+                const int cells = geoms[q].iupper[d] - geoms[q].ilower[d] + 1;
+                int extra = 0;  // the extra point along the centring's dims
+                if (centering == IBTK_LE_NODE) extra = 1;
+                else if (centering == IBTK_LE_SIDE) extra = d == a;
+                else if (centering == IBTK_LE_EDGE) extra = d != a;
+                n *= cells + extra + 2 * geoms[q].gcw[d];
+            }
+            if (!q_dev[(size_t)q * per + a]) return fail(IBTK_LE_ERR_ARG, "level_zero: null array");
+            cnt[(size_t)q * per + a] = n;
+            mx = std::max(mx, n);
+        }
+    }
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    const size_t bytes = sizeof(double*) * narr + sizeof(long long) * narr;
+    int rc;
+    if ((rc = ctx->zero_tab.ensure(bytes))) return rc;
+    std::vector<char> host(bytes);
+    std::memcpy(host.data(), q_dev, sizeof(double*) * narr);
+    std::memcpy(host.data() + sizeof(double*) * narr, cnt.data(), sizeof(long long) * narr);
+    if (ctx->zero_host != host) {  // a pageable copy waits for the stream: only when changed
+        ctx->zero_host = host;
+        HIP_TRY(hipMemcpyAsync(ctx->zero_tab.p, ctx->zero_host.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+    }
+    char* base = ctx->zero_tab.as<char>();
+    HIP_TRY(launch_level_zero(reinterpret_cast<double* const*>(base),
+                              reinterpret_cast<const long long*>(base + sizeof(double*) * narr), (int)narr, mx,
+                              ctx->stream));
     return IBTK_LE_OK;
 }
 

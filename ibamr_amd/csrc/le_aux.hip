@@ -260,6 +260,30 @@ __global__ __launch_bounds__(BLOCK) void k_level_fill(LevelTiling t, int dreg, c
     for (int k = 0; k < depth; ++k) dst[k * vol + di] = src[k * vol + si];
 }
 
+// every element of narr arrays := 0 (array i: count[i] doubles, 16-byte aligned
+// when count is even), blockIdx.y = array: one launch for a level's patch arrays
+__global__ __launch_bounds__(BLOCK) void k_level_zero(double* const* arrays, const long long* count) {
+    double* a = arrays[blockIdx.y];
+    const long long n = count[blockIdx.y];
+    const bool vec = (reinterpret_cast<uintptr_t>(a) & 15) == 0;
+    const long long stride = (long long)gridDim.x * BLOCK;
+    if (vec) {
+        double2* a2 = reinterpret_cast<double2*>(a);
+        for (long long i = (long long)blockIdx.x * BLOCK + threadIdx.x; i < n / 2; i += stride) a2[i] = double2{0.0, 0.0};
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) a[n - 1] = 0.0;
+    } else {
+        for (long long i = (long long)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) a[i] = 0.0;
+    }
+}
+hipError_t launch_level_zero(double* const* arrays, const long long* count, int narr, long long max_count,
+                             hipStream_t s) {
+    if (narr <= 0 || max_count <= 0) return hipSuccess;
+    const long long want = (max_count / 2 + BLOCK - 1) / BLOCK;
+    const int gx = (int)std::max(1LL, std::min(want, 64LL));
+    hipLaunchKernelGGL(k_level_zero, dim3(gx, narr), dim3(BLOCK), 0, s, arrays, count);
+    return hipGetLastError();
+}
+
 hipError_t launch_level_fill(const LevelTiling& t, int npatch, const int* tile_of_patch, const int* patch_of_tile,
                              double* const* arrays, int depth, hipStream_t s) {
     for (int dreg = 0; dreg < 3; ++dreg) {
@@ -399,8 +423,8 @@ __global__ __launch_bounds__(BLOCK) void k_perm_list(const int* perm, const int*
 // patch-box linear index (local nodes, numbered first), then ncell + ghost-box
 // linear index (the nonlocal nodes in the ghost cells), 0xffffffff outside.
 __global__ __launch_bounds__(BLOCK) void k_node_keys(ImageDesc d, const double* X, int n, unsigned* keys) {
-    const int i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
+    const int i0 = blockIdx.x * BLOCK + threadIdx.x;
+    const int i = min(i0, n - 1);  // every lane reaches the wave count below
     int c[3] = {0, 0, 0};
     cell_index(d, X + (int64_t)d.ndim * i, c);
     bool in = true, ing = true;
@@ -427,15 +451,22 @@ __global__ __launch_bounds__(BLOCK) void k_unique_flags(const unsigned* skeys, c
     }
     flag[i] = first && skeys[i] != 0xffffffffu ? 1 : 0;
 }
+// counter += the wave's true predicates, one atomic from the wave (per-lane
+// atomics on one address serialise); every lane of the wave must call it
+__device__ __forceinline__ void wave_count(int* counter, bool pred) {
+    const unsigned long long m = __ballot(pred);
+    if (m && (threadIdx.x & 63) == 0) atomicAdd(counter, __popcll(m));
+}
+
 __global__ __launch_bounds__(BLOCK) void k_compact(const int* sorder, const int* flag, const int* pos,
                                                    const unsigned* skeys, unsigned local_end, unsigned ghost_end, int n,
                                                    int* out, int* counts) {
     const int i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    if (flag[i]) {
-        out[pos[i]] = sorder[i];
-        atomicAdd(counts + (skeys[i] < local_end ? 0 : 1), 1);
-    }
+    const bool f = i < n && flag[i];
+    const bool loc = f && skeys[i] < local_end;
+    if (f) out[pos[i]] = sorder[i];
+    wave_count(counts, loc);           // one atomic per wave and counter
+    wave_count(counts + 1, f && !loc);
 }
 hipError_t launch_iota(int* v, int n, hipStream_t s) {
     if (n <= 0) return hipSuccess;
@@ -483,8 +514,8 @@ hipError_t launch_compact(const int* sorder, const int* flag, const int* pos, co
 // so a stable sort keeps input order within a cell.
 __global__ __launch_bounds__(BLOCK) void k_cell_keys(ImageDesc d, const double* X, int n, unsigned ncells,
                                                      unsigned* keys, int* vals, int* inside) {
-    const int i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
+    const int i0 = blockIdx.x * BLOCK + threadIdx.x;
+    const int i = min(i0, n - 1);  // every lane reaches the wave count below
     int c[3] = {0, 0, 0};
     cell_index(d, X + (int64_t)d.ndim * i, c);
     unsigned key = 0, stride = 1;
@@ -494,9 +525,11 @@ __global__ __launch_bounds__(BLOCK) void k_cell_keys(ImageDesc d, const double* 
         key += (unsigned)(c[k] - d.ilo[k]) * stride;
         stride *= (unsigned)(d.ihi[k] - d.ilo[k] + 1);
     }
-    keys[i] = in ? key : ncells;
-    vals[i] = i;
-    if (in) atomicAdd(inside, 1);
+    if (i0 < n) {
+        keys[i] = in ? key : ncells;
+        vals[i] = i;
+    }
+    wave_count(inside, in && i0 < n);
 }
 
 hipError_t launch_cell_keys(const ImageDesc& d, const double* X, int n, unsigned ncells, unsigned* keys, int* vals,
@@ -527,11 +560,19 @@ hipError_t launch_image_write(const ImageDesc& d, const double* X, int n, const 
 // (lagrangian_interaction3d.f.m4:1366-1382).  qdst[e] = s for that entry, -1
 // for the earlier ones (their sums go to the sink).
 // ---------------------------------------------------------------------------
+// grid-stride max, reduced in the block: one atomic per block (one per wave on
+// a single address serialised 10M entries into 1.8 ms)
 __global__ __launch_bounds__(BLOCK) void k_max_index(const int* idx, int n, int* out) {
-    const int l = blockIdx.x * BLOCK + threadIdx.x;
-    int v = l < n ? idx[l] : -1;
+    __shared__ int wmax[BLOCK / 64];
+    int v = -1;
+    for (long l = (long)blockIdx.x * BLOCK + threadIdx.x; l < n; l += (long)gridDim.x * BLOCK) v = max(v, idx[l]);
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
-    if ((threadIdx.x & 63) == 0 && v >= 0) atomicMax(out, v);
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < BLOCK / 64; ++w) v = max(v, wmax[w]);
+        if (v >= 0) atomicMax(out, v);
+    }
 }
 __global__ __launch_bounds__(BLOCK) void k_last_entry(const int* idx, int n, int* last) {
     const int l = blockIdx.x * BLOCK + threadIdx.x;
@@ -548,7 +589,7 @@ __global__ __launch_bounds__(BLOCK) void k_qdst(const int* sorted_l, const int* 
 }
 hipError_t launch_max_index(const int* idx, int n, int* out, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_max_index, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, idx, n, out);
+    hipLaunchKernelGGL(k_max_index, dim3(std::min((n + BLOCK - 1) / BLOCK, 2048)), dim3(BLOCK), 0, s, idx, n, out);
     return hipGetLastError();
 }
 hipError_t launch_dedup(const int* indices, const int* sorted_l, const int* sorted_s, int n, int* last, int* qdst,

@@ -258,6 +258,8 @@ struct LevelTiling {
 };
 hipError_t launch_level_fill(const LevelTiling& t, int npatch, const int* tile_of_patch, const int* patch_of_tile,
                              double* const* arrays, int depth, hipStream_t s);
+hipError_t launch_level_zero(double* const* arrays, const long long* count, int narr, long long max_count,
+                             hipStream_t s);
 
 // Physical-boundary ghost operators on one side-centred patch (le_bdry.hip)
 struct BdSide {

@@ -111,6 +111,11 @@ __global__ __launch_bounds__(BLOCK) void k_bin_col(Params p, int n, unsigned* ke
     vals[i] = i;
 }
 
+// Buckets opened by one entry in k_gather_col; a longer run (the empty columns
+// and patches around clustered markers: a serial walk of millions of buckets by
+// one thread) is left to k_bucket_fix's binary searches.
+constexpr int GATHER_GAP = 32;
+
 // Per sorted entry e: the marker index and the shifted position (coalesced for
 // the sweeps), fused with the bucket starts: entry e > 0 opens every bucket in
 // (key[e-1], key[e]] (keys >= nbuckets: binned outside).  The buckets before
@@ -128,7 +133,8 @@ __global__ __launch_bounds__(BLOCK) void k_gather_col(Params p, int n, int* sort
         if (e > 0) {
             const int bi = (int)min(skeys[e], (unsigned)nbuckets);
             const int bp = (int)min(skeys[e - 1], (unsigned)nbuckets);
-            for (int b = bp + 1; b <= bi; ++b) bs[b] = e;
+            if (bi - bp <= GATHER_GAP)  // longer runs of empty buckets: k_bucket_fix
+                for (int b = bp + 1; b <= bi; ++b) bs[b] = e;
         }
         const int l = p.sorted_l[e];
         const int s = p.indices ? p.indices[l] : l;
@@ -1136,13 +1142,25 @@ template <int K> hipError_t launch_bin_col_t(const Params& p, int n, unsigned* k
     hipLaunchKernelGGL(k_bin_col<K>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, keys, vals);
     return hipGetLastError();
 }
-// bucket starts before the first and after the last sorted key
+// bucket starts before the first and after the last sorted key; -1 (k_bucket_fix)
+// in between
 __global__ __launch_bounds__(BLOCK) void k_bucket_ends(const unsigned* skeys, int n, int nbuckets, int* bs) {
     const int b = blockIdx.x * BLOCK + threadIdx.x;
     if (b > nbuckets) return;
     const int first = (int)min(skeys[0], (unsigned)nbuckets), last = (int)min(skeys[n - 1], (unsigned)nbuckets);
-    if (b <= first) bs[b] = 0;
-    else if (b > last) bs[b] = n;
+    bs[b] = b <= first ? 0 : (b > last ? n : -1);
+}
+// the buckets k_gather_col left (long empty runs): the first entry whose key >= b
+__global__ __launch_bounds__(BLOCK) void k_bucket_fix(const unsigned* skeys, int n, int nbuckets, int* bs) {
+    const int b = blockIdx.x * BLOCK + threadIdx.x;
+    if (b > nbuckets || bs[b] >= 0) return;
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int)min(skeys[mid], (unsigned)nbuckets) < b) lo = mid + 1;
+        else hi = mid;
+    }
+    bs[b] = lo;
 }
 
 template <int K>
@@ -1153,6 +1171,8 @@ hipError_t launch_gather_col_t(const Params& p, int n, int* ss, double* sx, cons
                        bs);
     hipLaunchKernelGGL(k_gather_col<K>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, ss, sx, skeys,
                        nbuckets, bs);
+    hipLaunchKernelGGL(k_bucket_fix, dim3((nbuckets + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, skeys, n, nbuckets,
+                       bs);
     return hipGetLastError();
 }
 template <int K>

@@ -307,6 +307,11 @@ class Level:
         check(self.ctx.lib.ibtk_le_level_fill_ghosts(self.ctx.h, len(self.geoms), self._G, CENTERING[centering],
                                                      self._arrays(arrays), q_depth, pa[0] if pa else None))
 
+    def zero(self, centering: str, arrays, q_depth: int = 1):
+        """Every patch array := 0, ghosts included, in one launch (ibtk_le_level_zero)."""
+        check(self.ctx.lib.ibtk_le_level_zero(self.ctx.h, len(self.geoms), self._G, CENTERING[centering],
+                                              self._arrays(arrays), q_depth))
+
     def _arrays(self, arrays):
         # the pointer table of a list of per-patch arrays, cached on the list object
         # (a level reuses its u and f arrays step after step)

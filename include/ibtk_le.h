@@ -182,6 +182,14 @@ int ibtk_le_level_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cen
                          const double* const* q_dev, int q_depth, double* Q_dev, int Q_depth, const double* X_dev);
 int ibtk_le_level_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                          double* const* q_dev, int q_depth, const double* Q_dev, int Q_depth, const double* X_dev);
+/* Zeroes every patch array of a level, ghosts included, in one launch: the
+ * f := 0 before LDataManager::spread accumulates into the level (its
+ * f_data_ops->setToScalar(f_data_idx, 0.0, interior_only = false),
+ * LDataManager.cpp:596).  q_dev as
+ * ibtk_le_level_fill_ghosts (NDIM arrays per patch for SIDE / EDGE; one array of
+ * depth q_depth for CELL / NODE), each contiguous. */
+int ibtk_le_level_zero(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms, int centering,
+                       double* const* q_dev, int q_depth);
 /* Ghost fill of a level of equal patches tiling a box, periodic in the dims
  * periodic[d] != 0 (NULL: all): every ghost point of every patch array takes the
  * value of the patch owning its (wrapped) index -- the RefineSchedule::fillData

@@ -305,10 +305,11 @@ def _slab_run(le, ctx, N, M, world, rank, kernel="IB_4", move=False, overlap=Fal
     for c in range(3):
         _fill_interior(u[c], G[c], g, slab.z0, slab.nz, N)
     ex_u = SlabExchange(slab, u, ctx)
-    if overlap:
-        ex_u.cut_items()
-    else:
-        ctx.set_plane_window(0)  # no cuts
+    # items cut at the slab faces (N > 1), overlapped or not: a different cut of
+    # the sweep items sums a point's spread contributions in another grouping
+    # (within SPREAD_TOL), the same cuts give the same bits
+    ctx.set_plane_window(0)
+    ex_u.cut_items()
     m = le.Markers(ctx).bin(geom, kernel, X)
     U = torch.zeros_like(X)
     if overlap:

@@ -179,3 +179,34 @@ def test_level_fill_ghosts(le, ctx, P):
     for q in range(len(geoms)):
         for a in range(3):
             assert np.array_equal(arrays[q][a].cpu().numpy(), want[q][a]), f"patch {q} comp {a}"
+
+
+@pytest.mark.parametrize("centering,depth", [("side", 1), ("cell", 1), ("cell", 2), ("node", 1)])
+def test_level_zero(le, ctx, centering, depth):
+    """ibtk_le_level_zero: every element of every patch array (ghosts included)
+    := 0, and nothing beyond the arrays (LDataManager.cpp:596's setToScalar)."""
+    geoms = _patches(le, 18, 2, 3)  # 9^3 patches: 15^3 cell arrays, an odd count
+    per = 3 if centering == "side" else 1
+    arrays, guards = [], []
+    for geom in geoms:
+        row = []
+        for a in range(per):
+            shp = geom.array_shape(centering, a, depth)
+            n = int(np.prod(shp))
+            buf = torch.full((n + 2,), np.nan, dtype=torch.float64, device="cuda")
+            row.append(buf[1:n + 1].view(shp))  # 8-byte aligned views: the scalar path
+            guards.append(buf)
+        arrays.append(row)
+    X = torch.rand((10, 3), dtype=torch.float64, device="cuda")
+    lvl = le.Level(ctx, geoms, "IB_4", X, [None] * len(geoms))
+    lvl.zero(centering, arrays, q_depth=depth)
+    ctx.synchronize()
+    for buf in guards:
+        b = buf.cpu().numpy()
+        assert np.isnan(b[0]) and np.isnan(b[-1]), "wrote outside the array"
+        assert not b[1:-1].any() and not np.isnan(b[1:-1]).any()
+    # 16-byte aligned arrays (the vector path)
+    f = [geom.alloc(centering, depth=depth, fill=float("nan")) for geom in geoms]
+    lvl.zero(centering, f, q_depth=depth)
+    ctx.synchronize()
+    assert all(not t.cpu().numpy().any() for row in f for t in row)
