@@ -1,20 +1,31 @@
 // LEInteractor.h -- C++ facade of IBTK::LEInteractor over the MI355X kernels.
 //
-// Mirrors the static interface of ibtk/include/ibtk/LEInteractor.h:100-993
-// (getStencilSize, getMinimumGhostWidth, interpolate/spread on Cell/Node/Side/
-// Edge data with an index set, a patch, a box, a periodic shift and the kernel
-// string; the raw double* overloads; the X-only overloads without index sets).
-// SAMRAI and PETSc are not part of this build, so the SAMRAI/PETSc objects are
-// replaced by light views that carry exactly what the reference reads from
-// them: the patch box and Cartesian geometry (CartesianPatchGeometry), the
-// ghosted arrays and their boxes (pdat::*Data), the marker arrays (LData's
-// ghosted Vec array) and the cached index lists of LIndexSetData
-// (LIndexSetData.cpp:83-169).  Every data pointer is a DEVICE pointer.
+// Mirrors the static interface of ibtk/include/ibtk/LEInteractor.h:100-993:
+// getStencilSize, getMinimumGhostWidth, and the 32 interpolate / spread
+// overloads -- on Cell / Node / Side / Edge data (overloaded by data type, as in
+// the reference), in four argument forms each:
+//   (a) LData Q and X with an index set, a box and a periodic shift
+//       (LEInteractor.h:146-224, 459-566);
+//   (b) raw Q / X arrays with an index set (:226-300, 571-684);
+//   (c) std::vector<double> Q / X, the markers whose cell lies in the box
+//       (:302-346, 690-796);
+//   (d) raw Q / X arrays with their sizes, likewise (:348-455, 798-993).
+// SAMRAI and PETSc are not part of this build, so their objects are replaced by
+// light views carrying exactly what the reference reads from them: the patch box
+// and Cartesian geometry (CartesianPatchGeometry), the ghosted arrays and their
+// boxes (pdat::*Data), the marker arrays (LData's ghosted Vec array) and the
+// cached index lists of LIndexSetData (LIndexSetData.cpp:83-169).
+//
+// Memory: the LData views, the raw-array overloads (b, d) and the data views
+// hold DEVICE pointers.  The std::vector overloads (c) take HOST vectors, as the
+// reference's do: X and Q are staged to the device and the interpolated Q is
+// copied back before the call returns.
 //
 // Errors: the reference aborts through TBOX_ERROR; the facade throws
-// IBTK::LEInteractorError carrying the same message.
+// IBTK::LEInteractorError carrying the same message and an IBTK_LE_ERR_* code.
 #pragma once
 
+#include <ostream>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -58,21 +69,29 @@ struct PatchView {
     bool touches_physical_bdry[3][2] = {{false, false}, {false, false}, {false, false}};  // getTouchesRegularBoundary
 };
 
-// pdat::{Cell,Node,Side,Edge}Data<NDIM,double>: ghosted Fortran-ordered arrays
-struct CellDataView {
-    double* ptr = nullptr;  // depth arrays, depth slowest
-    Box box;                // patch box (getBox())
+namespace detail {
+// pdat::CellData / NodeData<NDIM,double>: one ghosted Fortran-ordered array of
+// `depth` components (depth slowest).  The tag makes Cell and Node distinct types.
+template <int TAG>
+struct ScalarDataView {
+    double* ptr = nullptr;
+    Box box;  // patch box (getBox())
     int ghost[3] = {0, 0, 0};
     int depth = 1;
 };
-using NodeDataView = CellDataView;
-struct SideDataView {
-    double* ptr[3] = {nullptr, nullptr, nullptr};  // getPointer(axis)
+// pdat::SideData / EdgeData<NDIM,double>: NDIM ghosted arrays (getPointer(axis)).
+template <int TAG>
+struct VectorDataView {
+    double* ptr[3] = {nullptr, nullptr, nullptr};
     Box box;
     int ghost[3] = {0, 0, 0};
     int depth = 1;
 };
-using EdgeDataView = SideDataView;
+}  // namespace detail
+using CellDataView = detail::ScalarDataView<0>;
+using NodeDataView = detail::ScalarDataView<1>;
+using SideDataView = detail::VectorDataView<0>;
+using EdgeDataView = detail::VectorDataView<1>;
 
 // LData: ghosted blocked Vec array, AoS [local + ghost][depth]
 struct LDataView {
@@ -81,8 +100,10 @@ struct LDataView {
     int local_size = 0;  // number of local + ghost nodes
 };
 
-// LIndexSetData cached lists (LIndexSetData.cpp:83-169), device arrays
-struct LIndexSetView {
+// LIndexSetData<T> cached lists (LIndexSetData.cpp:83-169), device arrays in
+// the reference's order (ibtk_le_index_set_list builds them).  T is the node
+// type of the reference's template (LNode or LNodeIndex); the lists are the same.
+struct LIndexSetBase {
     Box ghost_box;                       // idx_data->getGhostBox()
     const int* local_indices = nullptr;  // all nodes in the ghost box
     const double* periodic_shifts = nullptr;
@@ -91,48 +112,128 @@ struct LIndexSetView {
     const double* interior_periodic_shifts = nullptr;
     int n_interior = 0;
 };
+struct LNode {};
+struct LNodeIndex {};
+template <class T = LNode>
+struct LIndexSetDataView : LIndexSetBase {};
+using LIndexSetView = LIndexSetDataView<LNode>;
 
 class LEInteractor {
 public:
+    static void setFromDatabase(const void* db = nullptr);  // no settable data (LEInteractor.cpp:654-658)
+    static void printClassData(std::ostream& os);
     static int getStencilSize(const std::string& kernel_fcn);
     static int getMinimumGhostWidth(const std::string& kernel_fcn);
 
-    // --- index-set overloads (LEInteractor.h:146-330, 557-760) -------------------
-    static void interpolate(LDataView Q_data, LDataView X_data, const LIndexSetView& idx_data,
+    // (a) LData + index set (LEInteractor.h:146-224) ------------------------------
+    static void interpolate(LDataView Q_data, LDataView X_data, const LIndexSetBase& idx_data,
                             const CellDataView& q_data, const PatchView& patch, const Box& interp_box,
                             const int* periodic_shift, const std::string& interp_fcn = "IB_4");
-    static void interpolate(LDataView Q_data, LDataView X_data, const LIndexSetView& idx_data,
+    static void interpolate(LDataView Q_data, LDataView X_data, const LIndexSetBase& idx_data,
+                            const NodeDataView& q_data, const PatchView& patch, const Box& interp_box,
+                            const int* periodic_shift, const std::string& interp_fcn = "IB_4");
+    static void interpolate(LDataView Q_data, LDataView X_data, const LIndexSetBase& idx_data,
                             const SideDataView& q_data, const PatchView& patch, const Box& interp_box,
                             const int* periodic_shift, const std::string& interp_fcn = "IB_4");
-    static void interpolateNode(LDataView Q_data, LDataView X_data, const LIndexSetView& idx_data,
-                                const NodeDataView& q_data, const PatchView& patch, const Box& interp_box,
-                                const int* periodic_shift, const std::string& interp_fcn = "IB_4");
-    static void interpolateEdge(LDataView Q_data, LDataView X_data, const LIndexSetView& idx_data,
-                                const EdgeDataView& q_data, const PatchView& patch, const Box& interp_box,
-                                const int* periodic_shift, const std::string& interp_fcn = "IB_4");
-
-    static void spread(const CellDataView& q_data, LDataView Q_data, LDataView X_data,
-                       const LIndexSetView& idx_data, const PatchView& patch, const Box& spread_box,
-                       const int* periodic_shift, const std::string& spread_fcn = "IB_4");
-    static void spread(const SideDataView& q_data, LDataView Q_data, LDataView X_data,
-                       const LIndexSetView& idx_data, const PatchView& patch, const Box& spread_box,
-                       const int* periodic_shift, const std::string& spread_fcn = "IB_4");
-    static void spreadNode(const NodeDataView& q_data, LDataView Q_data, LDataView X_data,
-                           const LIndexSetView& idx_data, const PatchView& patch, const Box& spread_box,
-                           const int* periodic_shift, const std::string& spread_fcn = "IB_4");
-    static void spreadEdge(const EdgeDataView& q_data, LDataView Q_data, LDataView X_data,
-                           const LIndexSetView& idx_data, const PatchView& patch, const Box& spread_box,
-                           const int* periodic_shift, const std::string& spread_fcn = "IB_4");
-
-    // --- X-only overloads without index sets (LEInteractor.cpp:3110-3139):
-    // every marker whose cell (IndexUtilities::getCellIndex) lies in `box`, no
-    // periodic shifts.  X_size is the number of doubles in X (nodes * NDIM).
-    static void interpolate(double* Q_data, int Q_depth, const double* X_data, int X_depth, int X_size,
+    static void interpolate(LDataView Q_data, LDataView X_data, const LIndexSetBase& idx_data,
+                            const EdgeDataView& q_data, const PatchView& patch, const Box& interp_box,
+                            const int* periodic_shift, const std::string& interp_fcn = "IB_4");
+    // (b) raw arrays + index set (:226-300) ---------------------------------------
+    static void interpolate(double* Q_data, int Q_depth, const double* X_data, int X_depth,
+                            const LIndexSetBase& idx_data, const CellDataView& q_data, const PatchView& patch,
+                            const Box& interp_box, const int* periodic_shift,
+                            const std::string& interp_fcn = "IB_4");
+    static void interpolate(double* Q_data, int Q_depth, const double* X_data, int X_depth,
+                            const LIndexSetBase& idx_data, const NodeDataView& q_data, const PatchView& patch,
+                            const Box& interp_box, const int* periodic_shift,
+                            const std::string& interp_fcn = "IB_4");
+    static void interpolate(double* Q_data, int Q_depth, const double* X_data, int X_depth,
+                            const LIndexSetBase& idx_data, const SideDataView& q_data, const PatchView& patch,
+                            const Box& interp_box, const int* periodic_shift,
+                            const std::string& interp_fcn = "IB_4");
+    static void interpolate(double* Q_data, int Q_depth, const double* X_data, int X_depth,
+                            const LIndexSetBase& idx_data, const EdgeDataView& q_data, const PatchView& patch,
+                            const Box& interp_box, const int* periodic_shift,
+                            const std::string& interp_fcn = "IB_4");
+    // (c) host vectors, the markers whose cell lies in the box (:302-346) ----------
+    static void interpolate(std::vector<double>& Q_data, int Q_depth, const std::vector<double>& X_data,
+                            int X_depth, const CellDataView& q_data, const PatchView& patch, const Box& interp_box,
+                            const std::string& interp_fcn = "IB_4");
+    static void interpolate(std::vector<double>& Q_data, int Q_depth, const std::vector<double>& X_data,
+                            int X_depth, const NodeDataView& q_data, const PatchView& patch, const Box& interp_box,
+                            const std::string& interp_fcn = "IB_4");
+    static void interpolate(std::vector<double>& Q_data, int Q_depth, const std::vector<double>& X_data,
+                            int X_depth, const SideDataView& q_data, const PatchView& patch, const Box& interp_box,
+                            const std::string& interp_fcn = "IB_4");
+    static void interpolate(std::vector<double>& Q_data, int Q_depth, const std::vector<double>& X_data,
+                            int X_depth, const EdgeDataView& q_data, const PatchView& patch, const Box& interp_box,
+                            const std::string& interp_fcn = "IB_4");
+    // (d) raw arrays with sizes, likewise (:348-455) --------------------------------
+    static void interpolate(double* Q_data, int Q_size, int Q_depth, const double* X_data, int X_size, int X_depth,
+                            const CellDataView& q_data, const PatchView& patch, const Box& interp_box,
+                            const std::string& interp_fcn = "IB_4");
+    static void interpolate(double* Q_data, int Q_size, int Q_depth, const double* X_data, int X_size, int X_depth,
+                            const NodeDataView& q_data, const PatchView& patch, const Box& interp_box,
+                            const std::string& interp_fcn = "IB_4");
+    static void interpolate(double* Q_data, int Q_size, int Q_depth, const double* X_data, int X_size, int X_depth,
                             const SideDataView& q_data, const PatchView& patch, const Box& interp_box,
                             const std::string& interp_fcn = "IB_4");
+    static void interpolate(double* Q_data, int Q_size, int Q_depth, const double* X_data, int X_size, int X_depth,
+                            const EdgeDataView& q_data, const PatchView& patch, const Box& interp_box,
+                            const std::string& interp_fcn = "IB_4");
+
+    // (a) LData + index set (LEInteractor.h:459-566) ------------------------------
+    static void spread(const CellDataView& q_data, LDataView Q_data, LDataView X_data,
+                       const LIndexSetBase& idx_data, const PatchView& patch, const Box& spread_box,
+                       const int* periodic_shift, const std::string& spread_fcn = "IB_4");
+    static void spread(const NodeDataView& q_data, LDataView Q_data, LDataView X_data,
+                       const LIndexSetBase& idx_data, const PatchView& patch, const Box& spread_box,
+                       const int* periodic_shift, const std::string& spread_fcn = "IB_4");
+    static void spread(const SideDataView& q_data, LDataView Q_data, LDataView X_data,
+                       const LIndexSetBase& idx_data, const PatchView& patch, const Box& spread_box,
+                       const int* periodic_shift, const std::string& spread_fcn = "IB_4");
+    static void spread(const EdgeDataView& q_data, LDataView Q_data, LDataView X_data,
+                       const LIndexSetBase& idx_data, const PatchView& patch, const Box& spread_box,
+                       const int* periodic_shift, const std::string& spread_fcn = "IB_4");
+    // (b) raw arrays + index set (:571-684) ---------------------------------------
+    static void spread(const CellDataView& q_data, const double* Q_data, int Q_depth, const double* X_data,
+                       int X_depth, const LIndexSetBase& idx_data, const PatchView& patch, const Box& spread_box,
+                       const int* periodic_shift, const std::string& spread_fcn = "IB_4");
+    static void spread(const NodeDataView& q_data, const double* Q_data, int Q_depth, const double* X_data,
+                       int X_depth, const LIndexSetBase& idx_data, const PatchView& patch, const Box& spread_box,
+                       const int* periodic_shift, const std::string& spread_fcn = "IB_4");
     static void spread(const SideDataView& q_data, const double* Q_data, int Q_depth, const double* X_data,
-                       int X_depth, int X_size, const PatchView& patch, const Box& spread_box,
-                       const std::string& spread_fcn = "IB_4");
+                       int X_depth, const LIndexSetBase& idx_data, const PatchView& patch, const Box& spread_box,
+                       const int* periodic_shift, const std::string& spread_fcn = "IB_4");
+    static void spread(const EdgeDataView& q_data, const double* Q_data, int Q_depth, const double* X_data,
+                       int X_depth, const LIndexSetBase& idx_data, const PatchView& patch, const Box& spread_box,
+                       const int* periodic_shift, const std::string& spread_fcn = "IB_4");
+    // (c) host vectors (:690-796) ----------------------------------------------------
+    static void spread(const CellDataView& q_data, const std::vector<double>& Q_data, int Q_depth,
+                       const std::vector<double>& X_data, int X_depth, const PatchView& patch,
+                       const Box& spread_box, const std::string& spread_fcn = "IB_4");
+    static void spread(const NodeDataView& q_data, const std::vector<double>& Q_data, int Q_depth,
+                       const std::vector<double>& X_data, int X_depth, const PatchView& patch,
+                       const Box& spread_box, const std::string& spread_fcn = "IB_4");
+    static void spread(const SideDataView& q_data, const std::vector<double>& Q_data, int Q_depth,
+                       const std::vector<double>& X_data, int X_depth, const PatchView& patch,
+                       const Box& spread_box, const std::string& spread_fcn = "IB_4");
+    static void spread(const EdgeDataView& q_data, const std::vector<double>& Q_data, int Q_depth,
+                       const std::vector<double>& X_data, int X_depth, const PatchView& patch,
+                       const Box& spread_box, const std::string& spread_fcn = "IB_4");
+    // (d) raw arrays with sizes (:798-993) -------------------------------------------
+    static void spread(const CellDataView& q_data, const double* Q_data, int Q_size, int Q_depth,
+                       const double* X_data, int X_size, int X_depth, const PatchView& patch,
+                       const Box& spread_box, const std::string& spread_fcn = "IB_4");
+    static void spread(const NodeDataView& q_data, const double* Q_data, int Q_size, int Q_depth,
+                       const double* X_data, int X_size, int X_depth, const PatchView& patch,
+                       const Box& spread_box, const std::string& spread_fcn = "IB_4");
+    static void spread(const SideDataView& q_data, const double* Q_data, int Q_size, int Q_depth,
+                       const double* X_data, int X_size, int X_depth, const PatchView& patch,
+                       const Box& spread_box, const std::string& spread_fcn = "IB_4");
+    static void spread(const EdgeDataView& q_data, const double* Q_data, int Q_size, int Q_depth,
+                       const double* X_data, int X_size, int X_depth, const PatchView& patch,
+                       const Box& spread_box, const std::string& spread_fcn = "IB_4");
 
     // Stream / device of the facade's context (default: device 0, null stream).
     static void setStream(int device, void* hip_stream);

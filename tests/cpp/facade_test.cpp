@@ -1,13 +1,21 @@
-// facade_test.cpp -- exercises the IBTK::LEInteractor C++ facade on the GPU the way
-// LDataManager drives LEInteractor (LDataManager.cpp:625-660, 763-807): side-centred
-// data on one periodic patch, interior index list for interpolation, ghost-box
-// list (with periodic images) for spreading.  Prints "FACADE OK" on success.
+// facade_test.cpp -- drives every overload form of the IBTK::LEInteractor C++ facade
+// (include/ibtk_le/LEInteractor.h) on the GPU, the way LDataManager drives
+// LEInteractor (LDataManager.cpp:625-660, 763-807), for Cell / Node / Side / Edge
+// data on one periodic 3-D patch.  tests/test_gpu_boundary.py::test_cpp_facade
+// writes the inputs (markers, fields, the index set's lists made by the oracle)
+// into a directory, runs this program on it and compares what it writes back
+// with the oracle.  Forms (LEInteractor.h:146-993):
+//   a  LData views + index set      (interior list for interp, ghost list for spread)
+//   b  raw device arrays + index set (same lists: must equal a bit for bit)
+//   c  host std::vector, box filter  (markers whose cell is in the patch box, no shifts)
+//   d  raw device arrays with sizes, box filter (must equal c bit for bit)
+// Prints "FACADE OK" after the error-convention checks.
 #include <hip/hip_runtime.h>
 
-#include <cmath>
 #include <cstdio>
 #include <cstdlib>
-#include <random>
+#include <string>
+#include <type_traits>
 #include <vector>
 
 #include "ibtk_le.h"
@@ -30,9 +38,129 @@ using namespace IBTK;
         }                                                                      \
     } while (0)
 
-int main() {
-    const int N = 16, g = 3, M = 500;
-    PatchView patch;
+static std::string D;
+
+template <class T>
+static std::vector<T> load(const std::string& name, size_t n) {
+    std::vector<T> v(n);
+    FILE* f = std::fopen((D + "/" + name).c_str(), "rb");
+    EXPECT(f, ("open " + name).c_str());
+    EXPECT(std::fread(v.data(), sizeof(T), n, f) == n, ("read " + name).c_str());
+    std::fclose(f);
+    return v;
+}
+template <class T>
+static void save(const std::string& name, const T* p, size_t n) {
+    FILE* f = std::fopen((D + "/" + name).c_str(), "wb");
+    EXPECT(f && std::fwrite(p, sizeof(T), n, f) == n, ("write " + name).c_str());
+    std::fclose(f);
+}
+template <class T>
+static T* upload(const std::vector<T>& h) {
+    T* d = nullptr;
+    HC(hipMalloc(&d, sizeof(T) * (h.size() ? h.size() : 1)));
+    if (!h.empty()) HC(hipMemcpy(d, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
+    return d;
+}
+static std::vector<double> download(const double* d, size_t n) {
+    std::vector<double> h(n);
+    HC(hipMemcpy(h.data(), d, sizeof(double) * n, hipMemcpyDeviceToHost));
+    return h;
+}
+
+int N, g, M, n_int, n_all, depth_c;
+PatchView patch;
+LIndexSetView idx;
+double *Xd, *Fd;
+std::vector<double> hX, hF;
+const int pshift[3] = {0, 0, 0};
+
+// array size of component a of a centering (ghosted), elements
+static size_t asize(const char* c, int a, int depth) {
+    size_t n = (size_t)depth;
+    for (int d = 0; d < 3; ++d) {
+        int e = N + 2 * g;
+        if (c[0] == 'n') e += 1;
+        if (c[0] == 's' && d == a) e += 1;
+        if (c[0] == 'e' && d != a) e += 1;
+        n *= (size_t)e;
+    }
+    return n;
+}
+
+// the four forms of interp and spread on one data view type
+template <class V>
+static void run(const char* cname, V& u, V& f, int ncomp, int depth, int Qdepth) {
+    auto fptr = [&](int a) -> double*& {
+        if constexpr (std::is_same_v<V, CellDataView> || std::is_same_v<V, NodeDataView>) return f.ptr;
+        else return f.ptr[a];
+    };
+    auto zero_f = [&]() {
+        for (int a = 0; a < ncomp; ++a) HC(hipMemset(fptr(a), 0, sizeof(double) * asize(cname, a, depth)));
+    };
+    auto save_f = [&](const std::string& form) {
+        for (int a = 0; a < ncomp; ++a) {
+            auto h = download(fptr(a), asize(cname, a, depth));
+            save(std::string("f_") + cname + "_" + form + "_" + std::to_string(a) + ".bin", h.data(), h.size());
+        }
+    };
+    const size_t nQ = (size_t)M * Qdepth;
+    std::vector<double> init(nQ, -7.0);
+    double* Qd = upload(init);
+    std::vector<double> hQ2(3 * (size_t)M);
+    for (int s = 0; s < M; ++s)
+        for (int k = 0; k < Qdepth; ++k) hQ2[(size_t)s * Qdepth + k] = hF[3 * (size_t)s + (k % 3)];
+    hQ2.resize(nQ);
+    double* Sd = upload(hQ2);  // the spread values, depth Qdepth
+    LDataView Qv{Qd, Qdepth, M}, Xv{Xd, 3, M}, Sv{Sd, Qdepth, M};
+    const Box ghost_box = idx.ghost_box;
+    // a: LData + index set
+    LEInteractor::interpolate(Qv, Xv, idx, u, patch, patch.box, pshift, "IB_4");
+    LEInteractor::synchronize();
+    auto h = download(Qd, nQ);
+    save(std::string("Q_") + cname + "_a.bin", h.data(), nQ);
+    zero_f();
+    LEInteractor::spread(f, Sv, Xv, idx, patch, ghost_box, pshift, "IB_4");
+    LEInteractor::synchronize();
+    save_f("a");
+    // b: raw arrays + index set
+    HC(hipMemcpy(Qd, init.data(), sizeof(double) * nQ, hipMemcpyHostToDevice));
+    LEInteractor::interpolate(Qd, Qdepth, Xd, 3, idx, u, patch, patch.box, pshift, "IB_4");
+    LEInteractor::synchronize();
+    h = download(Qd, nQ);
+    save(std::string("Q_") + cname + "_b.bin", h.data(), nQ);
+    zero_f();
+    LEInteractor::spread(f, Sd, Qdepth, Xd, 3, idx, patch, ghost_box, pshift, "IB_4");
+    LEInteractor::synchronize();
+    save_f("b");
+    // c: host vectors, the markers whose cell is in the patch box
+    std::vector<double> Qh(init);
+    LEInteractor::interpolate(Qh, Qdepth, hX, 3, u, patch, patch.box, "IB_4");
+    save(std::string("Q_") + cname + "_c.bin", Qh.data(), nQ);
+    zero_f();
+    LEInteractor::spread(f, hQ2, Qdepth, hX, 3, patch, patch.box, "IB_4");
+    LEInteractor::synchronize();
+    save_f("c");
+    // d: raw arrays with sizes
+    HC(hipMemcpy(Qd, init.data(), sizeof(double) * nQ, hipMemcpyHostToDevice));
+    LEInteractor::interpolate(Qd, (int)nQ, Qdepth, Xd, 3 * M, 3, u, patch, patch.box, "IB_4");
+    LEInteractor::synchronize();
+    h = download(Qd, nQ);
+    save(std::string("Q_") + cname + "_d.bin", h.data(), nQ);
+    zero_f();
+    LEInteractor::spread(f, Sd, (int)nQ, Qdepth, Xd, 3 * M, 3, patch, patch.box, "IB_4");
+    LEInteractor::synchronize();
+    save_f("d");
+    HC(hipFree(Qd));
+    HC(hipFree(Sd));
+}
+
+int main(int argc, char** argv) {
+    EXPECT(argc == 2, "usage: facade_test <dir>");
+    D = argv[1];
+    FILE* mf = std::fopen((D + "/meta.txt").c_str(), "r");
+    EXPECT(mf && std::fscanf(mf, "%d %d %d %d %d %d", &N, &g, &M, &n_int, &n_all, &depth_c) == 6, "meta");
+    std::fclose(mf);
     patch.box.ndim = 3;
     for (int d = 0; d < 3; ++d) {
         patch.box.lower[d] = 0;
@@ -41,112 +169,88 @@ int main() {
         patch.x_lower[d] = 0.0;
         patch.x_upper[d] = 1.0;
     }
-    SideDataView u, f;
-    u.box = f.box = patch.box;
-    size_t sz[3];
-    for (int a = 0; a < 3; ++a) {
-        sz[a] = 1;
-        for (int d = 0; d < 3; ++d) sz[a] *= (size_t)(N + 2 * g + (d == a));
-        HC(hipMalloc(&u.ptr[a], sz[a] * 8));
-        HC(hipMalloc(&f.ptr[a], sz[a] * 8));
-        std::vector<double> h(sz[a], 2.0 + a);
-        HC(hipMemcpy(u.ptr[a], h.data(), sz[a] * 8, hipMemcpyHostToDevice));
-        HC(hipMemset(f.ptr[a], 0, sz[a] * 8));
-    }
-    for (int d = 0; d < 3; ++d) u.ghost[d] = f.ghost[d] = g;
-    std::mt19937_64 rng(3);
-    std::uniform_real_distribution<double> U01(0.0, 1.0);
-    std::vector<double> hX(3 * M), hF(3 * M);
-    for (auto& v : hX) v = U01(rng);
-    for (auto& v : hF) v = U01(rng) - 0.5;
-    double *X, *Q, *Fd;
-    HC(hipMalloc(&X, 24 * M));
-    HC(hipMalloc(&Q, 24 * M));
-    HC(hipMalloc(&Fd, 24 * M));
-    HC(hipMemcpy(X, hX.data(), 24 * M, hipMemcpyHostToDevice));
-    HC(hipMemcpy(Fd, hF.data(), 24 * M, hipMemcpyHostToDevice));
-
-    // index set: interior = identity, ghost box = identity + periodic images
-    ibtk_le_ctx ctx;
-    EXPECT(ibtk_le_ctx_create(0, nullptr, &ctx) == 0, "ctx");
-    ibtk_le_patch_geom geom{};
-    geom.ndim = 3;
-    for (int d = 0; d < 3; ++d) {
-        geom.iupper[d] = N - 1;
-        geom.gcw[d] = g;
-        geom.dx[d] = 1.0 / N;
-        geom.x_upper[d] = 1.0;
-    }
-    int *idx_int, *idx_all;
-    double *xs_int, *xs_all;
-    HC(hipMalloc(&idx_int, 4 * M));
-    HC(hipMalloc(&xs_int, 24 * M));
-    HC(hipMalloc(&idx_all, 4 * 27 * M));
-    HC(hipMalloc(&xs_all, 24 * 27 * M));
-    int n_int = 0, n_all = 0;
-    EXPECT(ibtk_le_periodic_index_list(ctx, &geom, X, M, 0, nullptr, idx_int, xs_int, M, &n_int) == 0, "interior list");
-    EXPECT(ibtk_le_periodic_index_list(ctx, &geom, X, M, g, nullptr, idx_all, xs_all, 27 * M, &n_all) == 0, "ghost list");
-    EXPECT(n_int == M && n_all > M, "list sizes");
-    LIndexSetView idx;
+    hX = load<double>("X.bin", 3 * (size_t)M);
+    hF = load<double>("F.bin", 3 * (size_t)M);
+    Xd = upload(hX);
+    Fd = upload(hF);
     idx.ghost_box = patch.box.grow(g);
-    idx.local_indices = idx_all;
-    idx.periodic_shifts = xs_all;
-    idx.n = n_all;
-    idx.interior_local_indices = idx_int;
-    idx.interior_periodic_shifts = xs_int;
+    idx.interior_local_indices = upload(load<int>("idx_int.bin", n_int));
+    idx.interior_periodic_shifts = upload(load<double>("xs_int.bin", 3 * (size_t)n_int));
     idx.n_interior = n_int;
-    const int pshift[3] = {N, N, N};
+    idx.local_indices = upload(load<int>("idx_all.bin", n_all));
+    idx.periodic_shifts = upload(load<double>("xs_all.bin", 3 * (size_t)n_all));
+    idx.n = n_all;
 
     EXPECT(LEInteractor::getStencilSize("IB_4") == 4 && LEInteractor::getMinimumGhostWidth("IB_6") == 4, "stencil");
-    LDataView Qv{Q, 3, M}, Xv{X, 3, M}, Fv{Fd, 3, M};
-    LEInteractor::interpolate(Qv, Xv, idx, u, patch, patch.box, pshift, "IB_4");
-    LEInteractor::spread(f, Fv, Xv, idx, patch, idx.ghost_box, pshift, "IB_4");
-    LEInteractor::synchronize();
-    std::vector<double> hQ(3 * M);
-    HC(hipMemcpy(hQ.data(), Q, 24 * M, hipMemcpyDeviceToHost));
-    for (int s = 0; s < M; ++s)
-        for (int a = 0; a < 3; ++a) EXPECT(std::fabs(hQ[3 * s + a] - (2.0 + a)) < 1e-13, "interp of a constant");
-    // spreading with periodic images: the interior sum times h^3 equals sum F
+
+    CellDataView uc, fc;
+    uc.box = fc.box = patch.box;
+    uc.depth = fc.depth = depth_c;
+    NodeDataView un, fn;
+    un.box = fn.box = patch.box;
+    SideDataView us, fs;
+    us.box = fs.box = patch.box;
+    EdgeDataView ue, fe;
+    ue.box = fe.box = patch.box;
+    for (int d = 0; d < 3; ++d) uc.ghost[d] = fc.ghost[d] = un.ghost[d] = fn.ghost[d] = us.ghost[d] = fs.ghost[d] =
+        ue.ghost[d] = fe.ghost[d] = g;
+    uc.ptr = upload(load<double>("u_cell.bin", asize("cell", 0, depth_c)));
+    HC(hipMalloc(&fc.ptr, sizeof(double) * asize("cell", 0, depth_c)));
+    un.ptr = upload(load<double>("u_node.bin", asize("node", 0, 1)));
+    HC(hipMalloc(&fn.ptr, sizeof(double) * asize("node", 0, 1)));
     for (int a = 0; a < 3; ++a) {
-        std::vector<double> h(sz[a]);
-        HC(hipMemcpy(h.data(), f.ptr[a], sz[a] * 8, hipMemcpyDeviceToHost));
-        const int n0 = N + 2 * g + (a == 0), n1 = N + 2 * g + (a == 1);
-        double tot = 0.0, ref = 0.0;
-        for (int k = g; k < g + N; ++k)
-            for (int j = g; j < g + N; ++j)
-                for (int i = g; i < g + N; ++i) tot += h[(size_t)(k * n1 + j) * n0 + i];
-        for (int s = 0; s < M; ++s) ref += hF[3 * s + a];
-        EXPECT(std::fabs(tot / (N * N * N) - ref) < 1e-11, "spread conserves the total");
+        us.ptr[a] = upload(load<double>("u_side" + std::to_string(a) + ".bin", asize("side", a, 1)));
+        HC(hipMalloc(&fs.ptr[a], sizeof(double) * asize("side", a, 1)));
+        ue.ptr[a] = upload(load<double>("u_edge" + std::to_string(a) + ".bin", asize("edge", a, 1)));
+        HC(hipMalloc(&fe.ptr[a], sizeof(double) * asize("edge", a, 1)));
     }
-    // X-only overload over the patch box gives the same interpolant
-    HC(hipMemset(Q, 0, 24 * M));
-    LEInteractor::interpolate(Q, 3, X, 3, 3 * M, u, patch, patch.box, "IB_4");
-    LEInteractor::synchronize();
-    HC(hipMemcpy(hQ.data(), Q, 24 * M, hipMemcpyDeviceToHost));
-    for (int s = 0; s < M; ++s) EXPECT(std::fabs(hQ[3 * s] - 2.0) < 1e-13, "X-only interp");
-    // error conventions
+    run("cell", uc, fc, 1, depth_c, depth_c);
+    run("node", un, fn, 1, 1, 1);
+    run("side", us, fs, 3, 1, 3);
+    run("edge", ue, fe, 3, 1, 3);
+
+    // error conventions (TBOX_ERROR -> LEInteractorError with an IBTK_LE_ERR_* code)
+    double* Qd;
+    HC(hipMalloc(&Qd, 24 * (size_t)M));
+    LDataView Qv{Qd, 3, M}, Xv{Xd, 3, M};
     bool thrown = false;
     try {
-        LEInteractor::interpolate(Qv, Xv, idx, u, patch, patch.box, pshift, "NOT_A_KERNEL");
+        LEInteractor::interpolate(Qv, Xv, idx, us, patch, patch.box, pshift, "NOT_A_KERNEL");
     } catch (const LEInteractorError& e) {
         thrown = e.code == IBTK_LE_ERR_UNKNOWN_KERNEL;
     }
     EXPECT(thrown, "unknown kernel throws");
     thrown = false;
     try {
-        LEInteractor::interpolate(Qv, Xv, idx, u, patch, patch.box, pshift, "IB_6");  // needs 4 ghosts
+        LEInteractor::interpolate(Qv, Xv, idx, us, patch, patch.box, pshift, "IB_6");  // needs 4 ghosts
     } catch (const LEInteractorError& e) {
         thrown = e.code == IBTK_LE_ERR_GHOST_WIDTH;
     }
     EXPECT(thrown, "ghost width throws");
     thrown = false;
     try {
-        LDataView Q2{Q, 2, M};
-        LEInteractor::interpolate(Q2, Xv, idx, u, patch, patch.box, pshift, "IB_4");
+        LDataView Q2{Qd, 2, M};
+        LEInteractor::interpolate(Q2, Xv, idx, us, patch, patch.box, pshift, "IB_4");
     } catch (const LEInteractorError& e) {
         thrown = e.code == IBTK_LE_ERR_DEPTH;
     }
-    EXPECT(thrown, "depth mismatch throws");
+    EXPECT(thrown, "side depth mismatch throws");
+    thrown = false;
+    try {
+        LDataView Q2{Qd, 2, M};
+        LEInteractor::spread(fe, Q2, Xv, idx, patch, idx.ghost_box, pshift, "IB_4");
+    } catch (const LEInteractorError& e) {
+        thrown = e.code == IBTK_LE_ERR_DEPTH;
+    }
+    EXPECT(thrown, "edge depth mismatch throws");
+    thrown = false;
+    try {
+        Box other = patch.box.grow(1);
+        LEInteractor::interpolate(Qv, Xv, idx, us, patch, other, pshift, "IB_4");
+    } catch (const LEInteractorError& e) {
+        thrown = e.code == IBTK_LE_ERR_ARG;
+    }
+    EXPECT(thrown, "index-set box other than the patch / ghost box throws");
     std::printf("FACADE OK\n");
     return 0;
 }

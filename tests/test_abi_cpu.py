@@ -82,6 +82,15 @@ def test_cpp_facade_methods_exported(lib):
     assert {"interpolate", "spread", "getStencilSize", "getMinimumGhostWidth"} <= set(methods)
     for m in methods:
         assert f"IBTK::LEInteractor::{m}(" in out, m
+    # the reference's 16 interpolate and 16 spread overloads (LEInteractor.h:146-993):
+    # {LData + index set, raw + index set, std::vector, raw with sizes} x {Cell, Node,
+    # Side, Edge}, overloaded by data type
+    for m in ("interpolate", "spread"):
+        sigs = {ln for ln in out.splitlines() if f"IBTK::LEInteractor::{m}(" in ln}
+        assert len(sigs) == 16, (m, len(sigs))
+        # Cell / Node / Side / Edge = ScalarDataView<0>, <1>, VectorDataView<0>, <1>
+        for view in ("ScalarDataView<0>", "ScalarDataView<1>", "VectorDataView<0>", "VectorDataView<1>"):
+            assert sum(1 for ln in sigs if view in ln) == 4, (m, view)
 
 
 def test_argument_errors_before_any_device_call(lib):

@@ -89,11 +89,72 @@ def test_fortran_shims_match_oracle(lib, oracle, kernel, ndim):
     assert np.abs(ug - uo).max() <= 1e-12 * np.abs(uo).max()
 
 
-def test_cpp_facade():
+def _facade_exe():
     exe = ROOT / "ibamr_amd" / "lib" / "facade_test"
     src = ROOT / "tests" / "cpp" / "facade_test.cpp"
-    if not exe.exists() or exe.stat().st_mtime < src.stat().st_mtime:
+    hdr = ROOT / "include" / "ibtk_le" / "LEInteractor.h"
+    if not exe.exists() or exe.stat().st_mtime < max(src.stat().st_mtime, hdr.stat().st_mtime):
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", f"-I{ROOT / 'include'}",
                         str(src), f"-L{exe.parent}", "-libtk_le", "-Wl,-rpath,$ORIGIN", "-o", str(exe)], check=True)
-    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    return exe
+
+
+def test_cpp_facade(tmp_path):
+    """Every overload form of the C++ facade (include/ibtk_le/LEInteractor.h: LData +
+    index set, raw arrays + index set, std::vector and raw arrays with sizes, each on
+    Cell / Node / Side / Edge data) against the oracle on one periodic 16^3 patch:
+    interp of the index set's interior list and of the box-filtered markers within
+    1e-13 (the two index-set forms and the two box forms bit for bit alike), spread
+    of the ghost-box list (with periodic images) and of the box-filtered markers
+    within 1e-12 (LEInteractor.cpp:690-2397)."""
+    from oracle import oracle as ora
+    from test_gpu_parity import oracle_call
+
+    from ibamr_amd.le import Geometry
+    N, g, M, depth_c = 16, 3, 600, 2
+    geom = Geometry.periodic_unit([N, N, N], g)
+    rng = np.random.default_rng(17)
+    X = rng.uniform(0.0, 1.0, (M, 3))
+    X[:20] = np.floor(X[:20] * N) / N  # on cell faces
+    F = rng.uniform(-1, 1, (M, 3))
+    ii, xi, _ = ora.periodic_index_list(X, geom.x_lower, geom.x_upper, geom.dx, geom.ilower, geom.iupper, g,
+                                        which="interior")
+    ia, xa, _ = ora.periodic_index_list(X, geom.x_lower, geom.x_upper, geom.dx, geom.ilower, geom.iupper, g,
+                                        which="all")
+    # the box forms: the markers whose cell is in the patch box, no shifts
+    ib = np.arange(M, dtype=np.int32)
+    xb = np.zeros((M, 3))
+    u = {"cell": [rng.uniform(-1, 1, geom.array_shape("cell", 0, depth_c))],
+         "node": [rng.uniform(-1, 1, geom.array_shape("node", 0, 1))],
+         "side": [rng.uniform(-1, 1, geom.array_shape("side", a)) for a in range(3)],
+         "edge": [rng.uniform(-1, 1, geom.array_shape("edge", a)) for a in range(3)]}
+    (tmp_path / "meta.txt").write_text(f"{N} {g} {M} {ii.size} {ia.size} {depth_c}\n")
+    for name, arr in [("X", X), ("F", F), ("idx_int", ii.astype(np.int32)), ("xs_int", xi),
+                      ("idx_all", ia.astype(np.int32)), ("xs_all", xa), ("u_cell", u["cell"][0]),
+                      ("u_node", u["node"][0])] + [(f"u_side{a}", u["side"][a]) for a in range(3)] + \
+            [(f"u_edge{a}", u["edge"][a]) for a in range(3)]:
+        np.ascontiguousarray(arr).tofile(tmp_path / f"{name}.bin")
+    r = subprocess.run([str(_facade_exe()), str(tmp_path)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "FACADE OK" in r.stdout, r.stdout + r.stderr
+    for cent in ("cell", "node", "side", "edge"):
+        depth = depth_c if cent == "cell" else 1
+        Qd = 3 if cent in ("side", "edge") else depth
+        nc = len(u[cent])
+        Q = {f: np.fromfile(tmp_path / f"Q_{cent}_{f}.bin").reshape(M, Qd) for f in "abcd"}
+        fs = {f: [np.fromfile(tmp_path / f"f_{cent}_{f}_{a}.bin").reshape(u[cent][a].shape) for a in range(nc)]
+              for f in "abcd"}
+        assert np.array_equal(Q["a"], Q["b"]) and np.array_equal(Q["c"], Q["d"]), cent
+        for a in range(nc):
+            assert np.array_equal(fs["a"][a], fs["b"][a]) and np.array_equal(fs["c"][a], fs["d"][a]), cent
+        Sv = F[:, [k % 3 for k in range(Qd)]].copy()
+        for form, (idx, xs) in (("a", (ii, xi)), ("c", (ib, xb))):
+            Qo = np.full((M, Qd), -7.0)
+            oracle_call(ora, "interp", "IB_4", cent, geom, [x.copy() for x in u[cent]], idx, xs, X, Qo, depth)
+            scale = max(np.abs(Qo).max(), 1e-300)
+            assert np.abs(Q[form] - Qo).max() <= 1e-13 * scale, f"{cent} {form} interp"
+        for form, (idx, xs) in (("a", (ia, xa)), ("c", (ib, xb))):
+            fo = [np.zeros_like(x) for x in u[cent]]
+            oracle_call(ora, "spread", "IB_4", cent, geom, fo, idx, xs, X, Sv.copy(), depth)
+            for a in range(nc):
+                scale = max(np.abs(fo[a]).max(), 1e-300)
+                assert np.abs(fs[form][a] - fo[a]).max() <= 1e-12 * scale, f"{cent} {form} spread comp {a}"
