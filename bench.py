@@ -351,6 +351,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-rebin", action="store_true", help="bin once outside the timed loop")
+    ap.add_argument("--layout", default="packed", choices=["aligned", "packed"],
+                    help="Eulerian arrays: rows padded to 128 B (aligned) or SAMRAI's packed layout")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N > 1: exchange the ghost planes before interp / after spread instead of overlapping "
                          "them with the interior sweep items")
@@ -402,7 +404,7 @@ def main():
 
     N = cfg["N"]
     ghost = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
-    slab = Slab([N, N, N], world, rank, ghost)
+    slab = Slab([N, N, N], world, rank, ghost, align=16 if args.layout == "aligned" else 0)
     geom = slab.geometry()
     ctx = le.Context(local_dev)
 
@@ -600,7 +602,7 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {"workload": cfg["desc"], "kernel": kernel, "grid": [N, N, N], "markers": M_total,
-                   "parallelism": f"z-slab x{world}", "ghost": ghost, "marker_order": args.marker_order,
+                   "parallelism": f"z-slab x{world}", "ghost": ghost, "marker_order": args.marker_order, "layout": args.layout,
                    "move": args.move, "overlap": world > 1 and not args.no_overlap,
                    "step": ("ghost fill + interp(3 comps) + position update + migrate + bin + zero ghosts + "
                             "spread(3 comps) + ghost sum" if args.move else

@@ -41,10 +41,11 @@ class PatchGeom(ctypes.Structure):
         ("dx", c_double * 3),
         ("x_lower", c_double * 3),
         ("x_upper", c_double * 3),
+        ("pitch", c_int * 2),
     ]
 
     @classmethod
-    def make(cls, ilower, iupper, gcw, dx, x_lower, x_upper=None):
+    def make(cls, ilower, iupper, gcw, dx, x_lower, x_upper=None, pitch=None):
         nd = len(ilower)
         g = cls()
         g.ndim = nd
@@ -59,6 +60,8 @@ class PatchGeom(ctypes.Structure):
             g.dx[d] = float(dx[d])
             g.x_lower[d] = float(x_lower[d])
             g.x_upper[d] = float(x_upper[d])
+        if pitch is not None:
+            g.pitch[0], g.pitch[1] = int(pitch[0]), int(pitch[1])
         return g
 
 

@@ -250,7 +250,30 @@ static int check_geom(const ibtk_le_patch_geom* g) {
         if (g->gcw[d] < 0) return fail(IBTK_LE_ERR_ARG, "negative ghost width");
         if (!(g->dx[d] > 0.0)) return fail(IBTK_LE_ERR_ARG, "dx[%d] must be positive", d);
     }
+    if (g->pitch[0] || g->pitch[1]) {
+        if (g->ndim != 3) return fail(IBTK_LE_ERR_ARG, "an array pitch needs a 3-D patch");
+        // the widest array of any centering: the ghosted box + 1 (side / node)
+        const long long n0 = (long long)g->iupper[0] - g->ilower[0] + 2 + 2LL * g->gcw[0];
+        const long long n1 = (long long)g->iupper[1] - g->ilower[1] + 2 + 2LL * g->gcw[1];
+        if (g->pitch[0] < n0 || (g->pitch[1] != 0 && g->pitch[1] < n1))
+            return fail(IBTK_LE_ERR_ARG, "array pitch {%d, %d} below the ghosted extent {%lld, %lld} (+1 face)",
+                        g->pitch[0], g->pitch[1], n0, n1);
+    }
     return IBTK_LE_OK;
+}
+
+static bool packed(const ibtk_le_patch_geom* g) { return g->pitch[0] == 0 && g->pitch[1] == 0; }
+
+// Strides (elements) of an array of ghosted extents n: row s1, plane s2, depth sd.
+static void array_strides(const ibtk_le_patch_geom* g, const int64_t n[3], int64_t& s1, int64_t& s2, int64_t& sd) {
+    if (packed(g)) {
+        s1 = n[0];
+        s2 = n[0] * n[1];
+    } else {
+        s1 = g->pitch[0];
+        s2 = s1 * (g->pitch[1] ? g->pitch[1] : n[1]);
+    }
+    sd = s2 * n[2];
 }
 
 // Brick grid over key cells: every key whose stencil can touch any array of the
@@ -304,10 +327,16 @@ static int make_col_geom(const ibtk_le_patch_geom* g, int kernel, BinGeom& bg, C
         cg.org[d] = lo - ki.HI;
         cg.ext[d] = hi - ki.LO - cg.org[d] + 1;
     }
-    // one empty guard column / row on each side in x and y
-    cg.ncx = (cg.ext[0] + COLX - 1) / COLX + 2;
-    cg.ncy = (cg.ext[1] + COLY - 1) / COLY + 2;
+    // one empty guard column / row on each side in x and y.  The columns start
+    // at the arrays' first x index + a multiple of 16: with a pitched layout
+    // (ibtk_le_patch_geom::pitch) every 32-point row a sweep streams is then two
+    // whole 128-byte lines.
+    const int khi0 = cg.org[0] + cg.ext[0] - 1;  // last key cell in x
+    const int lo0 = g->ilower[0] - g->gcw[0];
     cg.org[0] -= COLX;
+    cg.org[0] -= ((cg.org[0] - lo0) % 16 + 16) % 16;
+    cg.ncx = (khi0 + 1 - cg.org[0] + COLX - 1) / COLX + 1;
+    cg.ncy = (cg.ext[1] + COLY - 1) / COLY + 2;
     cg.org[1] -= COLY;
     cg.ext[0] = cg.ncx * COLX;
     cg.ext[1] = cg.ncy * COLY;
@@ -385,9 +414,9 @@ static int make_comps(const ibtk_le_patch_geom* g, int centering, int axis, doub
                 cd.lo[d] = cd.hi[d] = 0;
             }
         }
-        cd.s1 = n[0];
-        cd.s2 = n[0] * n[1];
-        cd.u = base + (int64_t)depth_index * n[0] * n[1] * n[2];
+        int64_t sd;
+        array_strides(g, n, cd.s1, cd.s2, sd);
+        cd.u = base + (int64_t)depth_index * sd;
     }
     (void)q_depth;
     (void)Q_depth;
@@ -848,6 +877,7 @@ extern "C" int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch,
     if (kernel < 0 || kernel >= K_COUNT) return fail(IBTK_LE_ERR_UNKNOWN_KERNEL, "Unknown kernel function %d", kernel);
     for (int q = 0; q < npatch; ++q) {
         if (int rc = check_geom(&geoms[q])) return rc;
+        if (!packed(&geoms[q])) return fail(IBTK_LE_ERR_ARG, "level calls take packed arrays (pitch {0, 0})");
         if (geoms[q].ndim != 3) return fail(IBTK_LE_ERR_ARG, "level_bin: 3-D patches only");
         for (int d = 0; d < 3; ++d)
             if (geoms[q].dx[d] != geoms[0].dx[d]) return fail(IBTK_LE_ERR_ARG, "level_bin: patches of one level share dx");
@@ -1071,6 +1101,7 @@ extern "C" int ibtk_le_level_fill_ghosts(ibtk_le_ctx ctx, int npatch, const ibtk
     int lo[3] = {INT_MAX, INT_MAX, INT_MAX}, hi[3] = {INT_MIN, INT_MIN, INT_MIN};
     for (int q = 0; q < npatch; ++q) {
         if (int rc = check_geom(&geoms[q])) return rc;
+        if (!packed(&geoms[q])) return fail(IBTK_LE_ERR_ARG, "level calls take packed arrays (pitch {0, 0})");
         if (geoms[q].ndim != 3) return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: 3-D patches");
         for (int d = 0; d < 3; ++d) {
             const int n = geoms[q].iupper[d] - geoms[q].ilower[d] + 1;
@@ -1144,6 +1175,7 @@ extern "C" int ibtk_le_level_zero(ibtk_le_ctx ctx, int npatch, const ibtk_le_pat
     long long mx = 0;
     for (int q = 0; q < npatch; ++q) {
         if (int rc = check_geom(&geoms[q])) return rc;
+        if (!packed(&geoms[q])) return fail(IBTK_LE_ERR_ARG, "level calls take packed arrays (pitch {0, 0})");
         if (geoms[q].ndim != nd) return fail(IBTK_LE_ERR_ARG, "level_zero: patches of one dimension");
         for (int a = 0; a < per; ++a) {
             long long n = vec ? 1 : q_depth;
@@ -1212,12 +1244,12 @@ static int ghost_descs(const ibtk_le_patch_geom* g, int centering, double* const
             gd.ihi[d] = g->iupper[d];
             n[d] = gd.hi[d] - gd.lo[d] + 1;
         }
-        gd.s1 = n[0];
-        gd.s2 = n[0] * n[1];
+        int64_t sd;
+        array_strides(g, n, gd.s1, gd.s2, sd);
         for (int k = 0; k < depth; ++k) {
             if (narr >= 16) return fail(IBTK_LE_ERR_ARG, "too many arrays");
             out[narr] = gd;
-            out[narr].u = base + (int64_t)k * n[0] * n[1] * n[2];
+            out[narr].u = base + (int64_t)k * sd;
             ++narr;
         }
     }
@@ -1283,8 +1315,8 @@ extern "C" int ibtk_le_phys_bdry_side(ibtk_le_ctx ctx, const ibtk_le_patch_geom*
             P.lo[c][d] = P.ilo[d] - g;
             n[d] = (int64_t)(P.ihi[d] - P.ilo[d] + 1 + 2 * g + (d == c ? 1 : 0));
         }
-        P.s1[c] = n[0];
-        P.s2[c] = n[0] * n[1];
+        int64_t sd;
+        array_strides(geom, n, P.s1[c], P.s2[c], sd);
     }
     int phys[6] = {0, 0, 0, 0, 0, 0};
     BdCoef coef[18];
@@ -1565,7 +1597,9 @@ extern "C" int ibtk_le_mark_stencils(ibtk_le_ctx ctx, ibtk_le_markers m, int ker
     if (m->n == 0) return IBTK_LE_OK;
     if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
     std::vector<double*> dummy(nc, reinterpret_cast<double*>(16));
-    if (int rc = make_comps(geom, centering, axis, dummy.data(), q_depth, q_depth, 0, nc, p)) return rc;
+    ibtk_le_patch_geom gp = *geom;  // the masks are packed whatever the arrays' pitch
+    gp.pitch[0] = gp.pitch[1] = 0;
+    if (int rc = make_comps(&gp, centering, axis, dummy.data(), q_depth, q_depth, 0, nc, p)) return rc;
     unsigned char* mk[4] = {nullptr, nullptr, nullptr, nullptr};
     for (int c = 0; c < nc; ++c) {
         if (!masks_dev[c]) return fail(IBTK_LE_ERR_ARG, "null mask");

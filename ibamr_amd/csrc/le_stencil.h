@@ -102,13 +102,28 @@ template <int K> __device__ __forceinline__ int key_anchor(double X_o_dx) {
 //   IB_4_W8: lagrangian_interaction3d.f.m4:1594-1610
 //   IB_6:    lagrangian_interaction3d.f.m4:1914-1945
 //   BSPLINE_4: cubic B-spline on the IB_4 stencil (not in the reference)
-template <int KID> __device__ __forceinline__ int closed_weights(double X_o_dx, int ilower, double* w, double K6) {
+// sqrt(a) for a in [1, 2] (the IB_4 discriminant 1 + 4 r (1 - r), r in [0, 1]):
+// the hardware reciprocal square root and two Newton steps, within an ulp of the
+// correctly rounded root, no range scaling.  FAST closed weights only (the
+// spread, compared by tolerance); the interp keeps sqrt() for bitwise parity.
+__device__ __forceinline__ double sqrt_1_2(double a) {
+    const double y = __builtin_amdgcn_rsq(a);
+    double g = a * y, h = 0.5 * y;
+    const double r = __builtin_fma(-g, h, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    const double d = __builtin_fma(-g, g, a);
+    return __builtin_fma(d, h, g);
+}
+
+template <int KID, bool FAST = false>
+__device__ __forceinline__ int closed_weights(double X_o_dx, int ilower, double* w, double K6) {
     const int n = d_nint(X_o_dx);
     int ic_lower;
     if constexpr (KID == K_IB_4) {
         ic_lower = n + ilower - 2;
         const double r = X_o_dx - ((double)(ic_lower + 1 - ilower) + 0.5);
-        const double q = sqrt(1.0 + 4.0 * r * (1.0 - r));
+        const double q = FAST ? sqrt_1_2(1.0 + 4.0 * r * (1.0 - r)) : sqrt(1.0 + 4.0 * r * (1.0 - r));
         w[0] = 0.125 * (3.0 - 2.0 * r - q);
         w[1] = 0.125 * (3.0 - 2.0 * r + q);
         w[2] = 0.125 * (1.0 + 2.0 * r + q);
@@ -166,6 +181,9 @@ template <int KID> __device__ __forceinline__ int closed_weights(double X_o_dx, 
 //   MUL: X_o_dx by a multiply with inv_dx = 1/dx instead of the Fortran's
 //        division (closed-form kernels only): within an ulp of it, for the
 //        spread, whose sums are compared by tolerance, not bit for bit
+#ifndef IBTK_LE_FAST_SQRT
+#define IBTK_LE_FAST_SQRT 1
+#endif
 template <int K, bool MUL = false>
 __device__ __forceinline__ void stencil1d(double Xs, double Xraw, double xlo, double dx, int ilo, int glo, int ghi,
                                           bool axis_dim, double K6, St<KT<K>::W>& st, double inv_dx = 0.0) {
@@ -179,7 +197,7 @@ __device__ __forceinline__ void stencil1d(double Xs, double Xraw, double xlo, do
         // point that may then fall outside the key's bands carries a weight of
         // an ulp's order: within the spread's tolerance.
         const double X_o_dx = MUL ? (Xs - xlo) * inv_dx : (Xs - xlo) / dx;
-        st.icl = closed_weights<K>(X_o_dx, ilo, st.w, K6);
+        st.icl = closed_weights<K, MUL && IBTK_LE_FAST_SQRT>(X_o_dx, ilo, st.w, K6);
         const int icu = st.icl + (W - 1);
         st.ist = max(glo - st.icl, 0);
         st.isp = (W - 1) - max(icu - ghi, 0);

@@ -647,6 +647,12 @@ __global__ __launch_bounds__(BLOCK) void k_interp_outside_col(Params p, int n) {
 // ---------------------------------------------------------------------------
 // spreading
 // ---------------------------------------------------------------------------
+#ifndef IBTK_LE_SPREAD_DEAL
+#define IBTK_LE_SPREAD_DEAL 1  // 1: rank-dealt lanes by bank class; 0: none; 2: static stride-4
+#endif
+#ifndef IBTK_LE_SPREAD_ROT
+#define IBTK_LE_SPREAD_ROT 0  // measured 30 % slower on cfg4 (the spread is issue-bound)
+#endif
 template <int K> struct SSh {
     using T = KT<K>;
     static constexpr int W = T::W, LO = T::LO, HI = T::HI, FAM = T::FAM;
@@ -655,18 +661,30 @@ template <int K> struct SSh {
     static constexpr int PV = COLX * COLY;              // owned points per plane
     static constexpr int NPL = PV / SW;
     static constexpr int NR = 11;                       // candidate ranges per anchor plane
+    // Rotated adds (W = 4, spread_rot): ring rows of RS = 36 doubles (RS = 4 mod
+    // 16), so the 16 points (i0, i1) of a stencil plane fall in the 16 bank
+    // classes i0 + 4 i1 (+ the base's class), and a slot stride that is a
+    // multiple of 16 keeps a point's class independent of its plane.  A trash
+    // row of 16 doubles at the end of every slot takes the zero-weight adds of
+    // the clipped or not-owned points of that plane at their own class.
+    static constexpr bool ROT = IBTK_LE_SPREAD_ROT && W == 4 && (FAM == 0 || FAM == 2);
+    static constexpr int RS = ROT ? 36 : COLX;          // ring row stride
     // ring slot stride: a 16-double gap after each plane takes the spill of the
     // zero-weight adds of stencil columns that stick out of the column (x in
     // [-3, 34] of rows 0..COLY-1); a multiple of 16 keeps every point's bank
     // class = its x mod 16.  GUARD doubles before slot 0 take its low spill.
-    static constexpr int SLOT = PV + 16;
-    static constexpr int GUARD = 16;
+    static constexpr int TROW = (RS * COLY + 15) / 16 * 16;  // ROT: trash row of a slot
+    static constexpr int SLOT = ROT ? TROW + 16 : PV + 16;
+    static constexpr int GUARD = ROT ? 0 : 16;
     static_assert(NS <= 16, "plane field");
     static_assert(COLX == 32 && COLY >= 8, "32-point rows; bands need COLY >= 8");
 };
 
-// ring plane layout: row-major 32 x COLY (the bank of a point is x mod 32)
-__device__ __forceinline__ int swz(int x, int y) { return y * COLX + x; }
+// ring plane layout: row-major 32 x COLY, rows SSh::RS apart; q = the lane's
+// staged point (x = q mod 32, y = q / 32)
+template <int K> __device__ __forceinline__ int ring_index(int q) {
+    return (q >> 5) * SSh<K>::RS + (q & (COLX - 1));
+}
 
 template <int K> __device__ __forceinline__ int sslot(int prel) {
     using S = SSh<K>;
@@ -734,7 +752,7 @@ struct Cand {
 // Within one instruction the lanes that hit the same point add in lane order,
 // so every point receives its contributions in a fixed order (bit-stable).
 template <int K>
-__device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
+__device__ __forceinline__ void spread_lanes_rows(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
                                              bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
                                              int yhi, int plo, int phi, double inv_h3, const double* inv_d, Clk& clk) {
     using S = SSh<K>;
@@ -803,6 +821,173 @@ __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd
     }
     }
     clk.lap(3);
+}
+
+#ifndef IBTK_LE_SPREAD_FLAT
+#define IBTK_LE_SPREAD_FLAT 1
+#endif
+// spread_lanes with fewer instructions per chunk (the sweep is issue-bound):
+// every stencil row is added by every busy lane, a clipped or not-owned row
+// or plane with weight 0 at its row clamped into the column (a +0 on an owned
+// point), so there is no exec mask and branch per row -- one address add per
+// row instead; validity masks from clipped ranges; IB_4's square root by rsq
+// and Newton steps (the spread is compared by tolerance).
+template <int K>
+__device__ __forceinline__ void spread_lanes_flat(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
+                                                  bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
+                                                  int yhi, int plo, int phi, double inv_h3, const double* inv_d) {
+    using S = SSh<K>;
+    constexpr int W = S::W, FAM = S::FAM, NSL = S::NSL;
+    St<W> st[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const double Xraw = (FAM == 2) ? p.X[(int64_t)3 * cdat.s + d] : cdat.X[d];
+        stencil1d<K, true>(cdat.X[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis,
+                           p.K6, st[d], inv_d[d]);
+    }
+    const int ox = st[0].icl - X0, oy = st[1].icl - Y0, oz = st[2].icl - (zorg + a);
+    // binning invariant (and the memory bound of the x spill: ox in [-16, COLX + 15 - (W - 1)])
+    const bool bad = (unsigned)(ox + S::GUARD) > (unsigned)(COLX + 15 - (W - 1) + S::GUARD) ||
+                     (unsigned)(oy + 60) > 120u || (unsigned)(oz + 60) > 120u;
+    if (act && bad) atomicOr(p.err, 2);
+    if (!act || bad) return;  // idle lanes sit the adds out
+    // owned and clipped-in ranges of the stencil indices
+    const int x0 = max(st[0].ist, xlo - ox), x1 = min(st[0].isp, xhi - ox);
+    const int y0 = max(st[1].ist, ylo - oy), y1 = min(st[1].isp, yhi - oy);
+    const int z0 = max(st[2].ist, plo - (a + oz)), z1 = min(st[2].isp, phi - (a + oz));
+    double w0v[W], w1m[W], w2m[W];
+    int roff[W];  // byte offset of stencil row i1 (clamped into the column) from row 0 of the plane
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        w0v[i] = (i >= x0 && i <= x1) ? st[0].w[i] * cdat.V : 0.0;
+        w1m[i] = (i >= y0 && i <= y1) ? st[1].w[i] : 0.0;
+        w2m[i] = (i >= z0 && i <= z1) ? st[2].w[i] * inv_h3 : 0.0;
+        roff[i] = 8 * COLX * min(max(oy + i, 0), COLY - 1);
+    }
+    char* const base = reinterpret_cast<char*>(ring) + 8 * ox;
+    int sl = (int)((unsigned)(a + oz + 64 * NSL) % (unsigned)NSL);  // ring slot of plane i2 = 0
+#pragma unroll
+    for (int i2 = 0; i2 < W; ++i2) {
+        char* const plane = base + sl * (8 * S::SLOT);
+        sl = sl + 1 == NSL ? 0 : sl + 1;
+#pragma unroll
+        for (int i1 = 0; i1 < W; ++i1) {
+            const double t = w1m[i1] * w2m[i2];
+            double* const row = reinterpret_cast<double*>(plane + roff[i1]);
+#pragma unroll
+            for (int i0 = 0; i0 < W; ++i0)
+                __hip_atomic_fetch_add(row + i0, w0v[i0] * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
+                                             bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
+                                             int yhi, int plo, int phi, double inv_h3, const double* inv_d, Clk& clk) {
+    if constexpr (IBTK_LE_SPREAD_FLAT)
+        spread_lanes_flat<K>(p, cd, ring, cdat, act, a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi, inv_h3, inv_d);
+    else
+        spread_lanes_rows<K>(p, cd, ring, cdat, act, a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi, inv_h3, inv_d, clk);
+}
+
+// The adds of one staged candidate per lane for W = 4 kernels, conflict-free by
+// construction (SSh::ROT).  The 16 points (i0, i1) of a stencil plane sit at
+// ring offsets i0 + RS i1 with RS = 4 mod 16, so point k = i0 + 4 i1 has bank
+// class (B + k) mod 16, B the class of the stencil's first point.  At add step t
+// lane l adds point k = (t + rho) mod 16 with rho = (l - B) mod 16, i.e. the
+// point of class (l + t) mod 16: the 16 lanes of every ds_add_f64 lane group hit
+// 16 distinct classes, whatever the positions (no dealing, no conflicts).  Each
+// lane walks its own 16 points in a rotated order, plane by plane; the order
+// in which one grid point receives its contributions is still fixed by the
+// staging order and the lane order within an instruction (bit-stable).
+// Clipped and not-owned points get weight 0 and a trash address of the same
+// class; idle lanes sit the adds out.
+template <int K>
+__device__ __forceinline__ void spread_rot(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
+                                           bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
+                                           int yhi, int plo, int phi, double inv_h3, const double* inv_d) {
+    using S = SSh<K>;
+    constexpr int W = S::W, FAM = S::FAM, LO = S::LO, NS = S::NS, NSL = S::NSL, RS = S::RS;
+    static_assert(W == 4, "rotated adds: 16 points per stencil plane");
+    St<W> st[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const double Xraw = (FAM == 2) ? p.X[(int64_t)3 * cdat.s + d] : cdat.X[d];
+        stencil1d<K, true>(cdat.X[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis,
+                           p.K6, st[d], inv_d[d]);
+    }
+    int ox = st[0].icl - X0, oy = st[1].icl - Y0, oz = st[2].icl - (zorg + a);
+    bool ok = act;
+    // binning invariant (a net for binning errors: the owned points a lane adds
+    // lie in the column, and every address stays in the ring whatever it is):
+    // the stencil starts near the anchor's plane range and the column's reach
+    // bands (conservative: a stencil starting at -4 or at COLX / COLY reaches no
+    // owned point; the piecewise-cubic start moves up when it is clipped)
+    if (act && (ox < -8 || ox > COLX + 8 || oy < -8 || oy > COLY + 8 || oz < LO - 4 || oz > LO + NS)) {
+        atomicOr(p.err, 2);
+        ok = false;
+    }
+    if (!ok) return;  // idle lanes sit the adds out
+    double w0v[W], w1m[W], w2m[W];
+    unsigned xv = 0, yv = 0;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        const bool vx = i >= st[0].ist && i <= st[0].isp && ox + i >= xlo && ox + i <= xhi;
+        const bool vy = i >= st[1].ist && i <= st[1].isp && oy + i >= ylo && oy + i <= yhi;
+        const int pr = a + oz + i;  // relative plane
+        const bool vz = i >= st[2].ist && i <= st[2].isp && pr >= plo && pr <= phi;
+        xv |= vx ? 1u << i : 0u;
+        yv |= vy ? 1u << i : 0u;
+        w0v[i] = vx ? st[0].w[i] * cdat.V : 0.0;
+        w1m[i] = vy ? st[1].w[i] : 0.0;
+        w2m[i] = vz ? st[2].w[i] * inv_h3 : 0.0;
+    }
+    // byte offsets (in slot 0) of the 16 points of a stencil plane and their
+    // values before the z weight; not-owned points: the slot's trash row, same class
+    const unsigned rbase = (unsigned)(uintptr_t)ring;  // LDS byte address of the ring
+    const int b0 = ox + RS * oy;                          // ring index of point 0 (< 0 or past the column: spill)
+    const int B = (int)(((rbase >> 3) + (unsigned)b0) & 15u);
+    const int rho = (__lane_id() - B) & 15;
+    double P[16];
+    int A[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int i0 = k & 3, i1 = k >> 2;
+        const bool v = ((xv >> i0) & (yv >> i1) & 1u) != 0;
+        P[k] = w0v[i0] * w1m[i1];
+        A[k] = 8 * (v ? b0 + i0 + RS * i1 : S::TROW + ((B + k - (int)(rbase >> 3)) & 15));
+    }
+    // rotate left by rho: P'[t] = P[(t + rho) mod 16] (barrel, 4 stages)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int sh = 1 << b;
+        const bool on = (rho >> b) & 1;
+        double Pn[16];
+        int An[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            Pn[t] = on ? P[(t + sh) & 15] : P[t];
+            An[t] = on ? A[(t + sh) & 15] : A[t];
+        }
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            P[t] = Pn[t];
+            A[t] = An[t];
+        }
+    }
+    char* const rb = reinterpret_cast<char*>(ring);
+    int sl = (int)((unsigned)(a + oz + 64 * NSL) % (unsigned)NSL);  // ring slot of plane i2 = 0
+#pragma unroll
+    for (int i2 = 0; i2 < W; ++i2) {
+        const int poff = sl * (8 * S::SLOT);
+        sl = sl + 1 == NSL ? 0 : sl + 1;
+        const double wz = w2m[i2];
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+            __hip_atomic_fetch_add(reinterpret_cast<double*>(rb + A[t] + poff), P[t] * wz, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
 }
 
 // Spread work item = (segment, column, component).  Owned points: the column's
@@ -891,8 +1076,24 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // adds of the n <= 64 candidates held one per lane (lane j's anchor plane:
     // a - 1 for j < r, else a): dealt over the lanes by bank class, then spread
     auto process = [&](int a, int r, int n, const Cand& mine) {
+        if constexpr (S::ROT) {
+            spread_rot<K>(p, cd, ring, mine, lane < n, lane < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo,
+                          phi, inv_h3, inv_d);
+            return;
+        }
+#if IBTK_LE_SPREAD_DEAL == 1
         const int cls = lane < n ? ((int)floor((mine.X[0] - cd.xlo[0]) * inv_dx + 0.5) & 15) : 63;
         const int src = deal_lanes<4>(cls);
+#elif IBTK_LE_SPREAD_DEAL == 0
+        const int src = lane;
+        if (true) {
+            spread_lanes<K>(p, cd, ring, mine, src < n, src < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi,
+                            inv_h3, inv_d, clk);
+            return;
+        }
+#else
+        const int src = (lane & 3) * 16 + (lane >> 2);  // static: every 4th staged candidate per lane group
+#endif
         Cand d;
 #pragma unroll
         for (int k = 0; k < 3; ++k) d.X[k] = shfl_f64(mine.X[k], src);
@@ -910,7 +1111,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     auto plane_put = [&](int z, const double* v) {
         double* sl = ring + sslot<K>(z) * S::SLOT;
 #pragma unroll
-        for (int k = 0; k < NPL; ++k) sl[lane + k * SW] = v[k];
+        for (int k = 0; k < NPL; ++k) sl[ring_index<K>(lane + k * SW)] = v[k];
     };
     auto plane_writeback = [&](int z) {  // owned points of plane z, ring -> array
         if (z < plo || z > phi) return;
@@ -918,7 +1119,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         double* pb = const_cast<double*>(plane_ptr(z));
         double v[NPL];
 #pragma unroll
-        for (int k = 0; k < NPL; ++k) v[k] = sl[lane + k * SW];
+        for (int k = 0; k < NPL; ++k) v[k] = sl[ring_index<K>(lane + k * SW)];
 #pragma unroll
         for (int k = 0; k < NPL; ++k) {  // not-owned points store to the sink: no branch per store
             double* dst = ((okxy >> k) & 1u) ? pb + loff[k] : p.sink + lane;

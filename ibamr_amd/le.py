@@ -31,14 +31,20 @@ def _ptr(t: Optional[torch.Tensor]):
     return ctypes.c_void_p(t.data_ptr())
 
 
-def _ptr_array(ts: Sequence[torch.Tensor]):
+def _ptr_array(ts: Sequence[torch.Tensor], geom: Optional["Geometry"] = None):
+    """Pointer table of Eulerian arrays: contiguous, or laid out by ``geom``'s pitch."""
     arr = (ctypes.c_void_p * max(1, len(ts)))()
     for i, t in enumerate(ts):
         if t is None:
             arr[i] = None
             continue
-        if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous():
-            raise ValueError("Eulerian arrays must be contiguous float64 device tensors")
+        if t.dtype != torch.float64 or not t.is_cuda:
+            raise ValueError("Eulerian arrays must be float64 device tensors")
+        if geom is not None and geom.pitched:
+            if not geom.has_layout(t):
+                raise ValueError(f"array strides {t.stride()} do not follow the geometry's pitch {geom.pitch}")
+        elif not t.is_contiguous():
+            raise ValueError("Eulerian arrays must be contiguous (or follow the geometry's pitch)")
         arr[i] = t.data_ptr()
     return arr
 
@@ -53,6 +59,7 @@ class Geometry:
     dx: Sequence[float]
     x_lower: Sequence[float]
     x_upper: Optional[Sequence[float]] = None
+    pitch: Optional[Sequence[int]] = None  # (row, plane) pitch of the arrays in elements; None = packed
 
     def __post_init__(self):
         self.ndim = len(self.ilower)
@@ -61,7 +68,49 @@ class Geometry:
         if self.x_upper is None:
             self.x_upper = [self.x_lower[d] + (self.iupper[d] - self.ilower[d] + 1) * self.dx[d]
                             for d in range(self.ndim)]
-        self.c = PatchGeom.make(self.ilower, self.iupper, self.gcw, self.dx, self.x_lower, self.x_upper)
+        if self.pitch is not None:
+            self.pitch = (int(self.pitch[0]), int(self.pitch[1]))
+        self.c = PatchGeom.make(self.ilower, self.iupper, self.gcw, self.dx, self.x_lower, self.x_upper,
+                                self.pitch)
+
+    @property
+    def pitched(self) -> bool:
+        return self.pitch is not None and tuple(self.pitch) != (0, 0)
+
+    def aligned(self, align: int = 16) -> "Geometry":
+        """The same patch with its arrays' rows padded to a multiple of `align` elements
+        (ibtk_le_patch_geom::pitch): 128-byte rows for align 16 (3-D only)."""
+        if self.ndim != 3:
+            raise ValueError("a pitched layout needs a 3-D patch")
+        n0 = self.iupper[0] - self.ilower[0] + 2 + 2 * self.gcw[0]
+        n1 = self.iupper[1] - self.ilower[1] + 2 + 2 * self.gcw[1]
+        return Geometry(self.ilower, self.iupper, self.gcw, self.dx, self.x_lower, self.x_upper,
+                        ((n0 + align - 1) // align * align, n1))
+
+    def strides(self, centering: str, comp: int = 0, depth: int = 1):
+        """torch strides (elements) of component `comp`'s array."""
+        shape = self.array_shape(centering, comp, depth)
+        if not self.pitched:
+            st, acc = [], 1
+            for n in reversed(shape):
+                st.append(acc)
+                acc *= n
+            return tuple(reversed(st))
+        p0, p1 = self.pitch
+        n = list(reversed(shape[-3:]))  # (n0, n1, n2)
+        s2 = p0 * (p1 if p1 else n[1])
+        st = (s2, p0, 1)
+        return ((s2 * n[2],) + st) if len(shape) == 4 else st
+
+    def has_layout(self, t: torch.Tensor) -> bool:
+        """True if `t` is one of this geometry's arrays (shape and strides of some component)."""
+        for cen in ("side", "cell", "node", "edge"):
+            for c in range(self.ncomp(cen)):
+                shape = self.array_shape(cen, c, t.shape[0] if t.dim() == 4 else 1)
+                if tuple(t.shape) == tuple(shape) and tuple(t.stride()) == self.strides(cen, c, shape[0] if
+                                                                                        len(shape) == 4 else 1):
+                    return True
+        return False
 
     @staticmethod
     def periodic_unit(N: Sequence[int], ghost: int, x_lower=None, x_upper=None):
@@ -86,8 +135,17 @@ class Geometry:
         return self.ndim if centering in ("side", "edge") else 1
 
     def alloc(self, centering: str, depth: int = 1, device="cuda", fill=0.0):
-        return [torch.full(self.array_shape(centering, c, depth), fill, dtype=torch.float64, device=device)
-                for c in range(self.ncomp(centering))]
+        if not self.pitched:
+            return [torch.full(self.array_shape(centering, c, depth), fill, dtype=torch.float64, device=device)
+                    for c in range(self.ncomp(centering))]
+        out = []
+        for c in range(self.ncomp(centering)):
+            shape = self.array_shape(centering, c, depth)
+            st = self.strides(centering, c, depth)
+            size = 1 + sum((n - 1) * s for n, s in zip(shape, st))
+            buf = torch.full((size,), fill, dtype=torch.float64, device=device)  # allocator: 256-B aligned
+            out.append(torch.as_strided(buf, shape, st))
+        return out
 
 
 class Context:
@@ -222,7 +280,7 @@ def interp(ctx: Context, markers: Markers, kernel: str, centering: str, geom: Ge
     """Q(d, s) = sum w q  (LEInteractor::interpolate)."""
     if Q_depth is None:
         Q_depth = geom.ndim if centering in ("side", "edge") else q_depth
-    arr = _ptr_array(q)
+    arr = _ptr_array(q, geom)
     check(ctx.lib.ibtk_le_interp(ctx.h, markers.h, kernel_id(kernel), CENTERING[centering], axis,
                                  ctypes.byref(geom.c), arr, q_depth, _ptr(Q), Q_depth, _ptr(X)))
 
@@ -236,7 +294,7 @@ def spread(ctx: Context, markers: Markers, kernel: str, centering: str, geom: Ge
     LDataManager::spread (LDataManager.cpp:398-470)."""
     if Q_depth is None:
         Q_depth = geom.ndim if centering in ("side", "edge") else q_depth
-    arr = _ptr_array(q)
+    arr = _ptr_array(q, geom)
     if ds is None:
         check(ctx.lib.ibtk_le_spread(ctx.h, markers.h, kernel_id(kernel), CENTERING[centering], axis,
                                      ctypes.byref(geom.c), arr, q_depth, _ptr(Q), Q_depth, _ptr(X)))
@@ -350,18 +408,18 @@ def _periodic_arg(periodic, ndim):
 
 def fill_periodic_ghosts(ctx: Context, geom: Geometry, centering: str, q, q_depth=1, periodic=None):
     pa = _periodic_arg(periodic, geom.ndim)
-    check(ctx.lib.ibtk_le_fill_periodic_ghosts(ctx.h, ctypes.byref(geom.c), CENTERING[centering], _ptr_array(q),
+    check(ctx.lib.ibtk_le_fill_periodic_ghosts(ctx.h, ctypes.byref(geom.c), CENTERING[centering], _ptr_array(q, geom),
                                                q_depth, pa[0] if pa else None))
 
 
 def fold_periodic_ghosts(ctx: Context, geom: Geometry, centering: str, q, q_depth=1, periodic=None):
     pa = _periodic_arg(periodic, geom.ndim)
-    check(ctx.lib.ibtk_le_fold_periodic_ghosts(ctx.h, ctypes.byref(geom.c), CENTERING[centering], _ptr_array(q),
+    check(ctx.lib.ibtk_le_fold_periodic_ghosts(ctx.h, ctypes.byref(geom.c), CENTERING[centering], _ptr_array(q, geom),
                                                q_depth, pa[0] if pa else None))
 
 
 def zero_ghosts(ctx: Context, geom: Geometry, centering: str, q, q_depth=1):
-    check(ctx.lib.ibtk_le_zero_ghosts(ctx.h, ctypes.byref(geom.c), CENTERING[centering], _ptr_array(q), q_depth))
+    check(ctx.lib.ibtk_le_zero_ghosts(ctx.h, ctypes.byref(geom.c), CENTERING[centering], _ptr_array(q, geom), q_depth))
 
 
 def local_numbering(ctx: Context, geom: Geometry, X: torch.Tensor):
@@ -405,7 +463,7 @@ def phys_bdry_side(ctx: Context, geom: Geometry, u, physical, acoef, bcoef, gcoe
         a = np.ascontiguousarray(np.broadcast_to(np.asarray(c, np.float64), (nd, 2 * nd)))
         coefs.append(a)
     cp = [a.ctypes.data_as(ctypes.c_void_p) for a in coefs]
-    check(ctx.lib.ibtk_le_phys_bdry_side(ctx.h, ctypes.byref(geom.c), _ptr_array(u), ctypes.cast(phys, ctypes.c_void_p),
+    check(ctx.lib.ibtk_le_phys_bdry_side(ctx.h, ctypes.byref(geom.c), _ptr_array(u, geom), ctypes.cast(phys, ctypes.c_void_p),
                                          cp[0], cp[1], cp[2], int(bool(adjoint))))
 
 

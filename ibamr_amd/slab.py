@@ -41,6 +41,7 @@ class Slab:
     rank: int
     ghost: int
     L: Sequence[float] = (1.0, 1.0, 1.0)
+    align: int = 0        # > 0: the arrays' rows padded to a multiple of `align` (Geometry.aligned)
 
     def __post_init__(self):
         if self.N[2] % self.P:
@@ -56,9 +57,10 @@ class Slab:
 
     def geometry(self):
         from .le import Geometry
-        return Geometry([0, 0, self.z0], [self.N[0] - 1, self.N[1] - 1, self.z1 - 1], self.ghost, self.dx,
-                        [0.0, 0.0, self.z0 * self.dx[2]],
-                        [self.L[0], self.L[1], self.z1 * self.dx[2]])
+        g = Geometry([0, 0, self.z0], [self.N[0] - 1, self.N[1] - 1, self.z1 - 1], self.ghost, self.dx,
+                     [0.0, 0.0, self.z0 * self.dx[2]],
+                     [self.L[0], self.L[1], self.z1 * self.dx[2]])
+        return g.aligned(self.align) if self.align else g
 
     # plane blocks of one side component array (leading dim = z planes)
     def blocks(self, comp: int):
@@ -110,14 +112,22 @@ class SlabExchange:
         # gloo moves host memory only: device tensors are staged through the host
         # (the multi-rank rehearsal on one GPU; RCCL sends device memory directly)
         stage = dist.get_backend(self.group) == "gloo"
+        # plane blocks of pitched arrays (padded rows) are not contiguous: they are
+        # packed into / unpacked from contiguous buffers around the transfer
         ops, back = [], []
         for t, peer in sends:
             if stage and t.is_cuda:
                 t = t.cpu()
+            elif not t.is_contiguous():
+                t = t.contiguous()
             ops.append(dist.P2POp(dist.isend, t, peer, group=self.group))
         for t, peer in recvs:
             if stage and t.is_cuda:
                 h = torch.empty(t.shape, dtype=t.dtype)
+                back.append((h, t))
+                t = h
+            elif not t.is_contiguous():
+                h = torch.empty(t.shape, dtype=t.dtype, device=t.device)
                 back.append((h, t))
                 t = h
             ops.append(dist.P2POp(dist.irecv, t, peer, group=self.group))

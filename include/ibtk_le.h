@@ -62,7 +62,18 @@ typedef enum {
 } ibtk_le_centering;
 
 /* Patch geometry: the cell box, the ghost width of the Eulerian data and the
- * Cartesian patch geometry (CartesianPatchGeometry::getDx/getXLower/getXUpper). */
+ * Cartesian patch geometry (CartesianPatchGeometry::getDx/getXLower/getXUpper).
+ *
+ * pitch: the layout of the Eulerian arrays in device memory.  {0, 0} is SAMRAI's
+ * ArrayData layout, every array packed to its own ghosted extent (n0, n1, n2).
+ * Otherwise every array of the patch (each side axis, each depth) has row stride
+ * pitch[0] >= n0 and plane stride pitch[0] * pitch[1] (pitch[1] >= n1; 0 = n1);
+ * depth k of a cell/node array starts k * pitch[0] * pitch[1] * n2 elements in.
+ * With pitch[0] a multiple of 16 and 128-byte aligned array pointers, every
+ * 32-point column row the 3-D sweeps stream is two whole 128-byte lines (the
+ * sweeps' columns start at ilower - gcw + a multiple of 16 in x).  3-D single-
+ * patch calls honour it; the level calls, the 2-D calls, ibtk_le_mark_stencils'
+ * masks and the host Fortran shims take packed arrays only (pitch {0, 0}). */
 typedef struct {
     int ndim;          /* 2 or 3 */
     int ilower[3];     /* patch box lower (cell indices) */
@@ -71,6 +82,7 @@ typedef struct {
     double dx[3];
     double x_lower[3];
     double x_upper[3];
+    int pitch[2];      /* array row / plane pitch in elements; {0, 0} = packed */
 } ibtk_le_patch_geom;
 
 typedef struct ibtk_le_ctx_s* ibtk_le_ctx;
