@@ -232,6 +232,8 @@ def run_level(args, cfg, kernel, dev):
     N, P = cfg["N"], cfg.get("patches", 8)
     n = N // P
     ctx = le.Context(dev.index or 0)
+    for kv in args.tune:
+        ctx.tune(kv.split("=")[0], int(kv.split("=")[1]))
     g = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
     dx = 1.0 / N
     geoms = []
@@ -351,6 +353,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-rebin", action="store_true", help="bin once outside the timed loop")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="diagnostic sweep overrides (ibtk_le_ctx_tune: heavy, seg_items, split_target)")
     ap.add_argument("--layout", default="packed", choices=["aligned", "packed"],
                     help="Eulerian arrays: rows padded to 128 B (aligned) or SAMRAI's packed layout")
     ap.add_argument("--no-overlap", action="store_true",
@@ -407,6 +411,8 @@ def main():
     slab = Slab([N, N, N], world, rank, ghost, align=16 if args.layout == "aligned" else 0)
     geom = slab.geometry()
     ctx = le.Context(local_dev)
+    for kv in args.tune:
+        ctx.tune(kv.split("=")[0], int(kv.split("=")[1]))
 
     t_setup = time.perf_counter()
     X = make_markers(cfg["markers"], cfg["M"], slab, 1234, dev)
@@ -573,13 +579,24 @@ def main():
     dominant = "spread" if k_s >= k_i else "interp"
     achieved = (B_s / (k_s * 1e-3) if dominant == "spread" else B_i / (k_i * 1e-3)) / 1e9
     pair = (B_i + B_s) / ((t_i + t_s) * 1e-3) / 1e9
-    traffic = None
+    # HBM traffic per launch of the dominant kernel from the rocprofv3 PMC passes of
+    # tools/pmc_traffic.sh (2 x FETCH_SIZE + WRITE_SIZE: FETCH_SIZE counts half the
+    # bytes of 8- and 16-byte-per-lane reads on gfx950, profiles/r02b/
+    # fetch_calibration.json), used only if it profiled this very build
+    traffic, traffic_note = None, "no PMC profile of this build"
     pmc = ROOT / "profiles" / f"pmc_{args.config}_{kernel}_{world}gpu.json"
     if pmc.exists():
         try:
-            traffic = json.loads(pmc.read_text()).get("per_launch_bytes", {}).get(dominant)
-        except Exception:
-            traffic = None
+            from ibamr_amd.build import source_hash
+            rec = json.loads(pmc.read_text())
+            if rec.get("build") == source_hash():
+                traffic = rec.get("per_launch_bytes", {}).get(dominant)
+                traffic_note = (f"PMC {pmc.relative_to(ROOT)}: 2 x FETCH_SIZE + WRITE_SIZE per launch, "
+                                f"build {rec['build']}")
+            else:
+                traffic_note = f"PMC {pmc.relative_to(ROOT)} profiled build {rec.get('build')}, not this one"
+        except Exception as e:
+            traffic_note = f"PMC record unreadable: {e!r}"
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -608,7 +625,7 @@ def main():
                             "spread(3 comps) + ghost sum" if args.move else
                             "bin + ghost fill + interp(3 comps) + zero ghosts + spread(3 comps) + ghost sum")},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per launch (PMC)",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per launch (PMC)", "traffic_note": traffic_note,
                      "algorithmic_bytes": {"interp": B_i, "spread": B_s},
                      "kernel_ms": {"interp": k_i, "spread": k_s},
                      "pair_achieved": pair, "pair_frac": pair / HBM_PEAK_GBS},

@@ -45,6 +45,18 @@ def _stale(obj: Path, src: Path) -> bool:
     return any(p.stat().st_mtime > t for p in [src, *_headers(), Path(__file__)])
 
 
+def source_hash() -> str:
+    """sha256 (16 hex digits) of the sources and headers the library is built from:
+    ties a recorded profile (profiles/pmc_*.json) to the build it measured."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted([*(CSRC / n for n in SOURCES), *_headers()], key=lambda q: str(q.relative_to(ROOT))):
+        if f.exists():
+            h.update(str(f.relative_to(ROOT)).encode())
+            h.update(f.read_bytes())
+    return h.hexdigest()[:16]
+
+
 def build(verbose: bool = False) -> Path:
     OBJ.mkdir(parents=True, exist_ok=True)
     procs = []

@@ -221,6 +221,7 @@ extern "C" int ibtk_le_ctx_tune(ibtk_le_ctx ctx, const char* key, int value) {
     const std::string k = key;
     if (k == "seg_items") t.seg_items = value;
     else if (k == "split_target") t.split_target = value;
+    else if (k == "heavy") t.heavy = value;
     else return fail(IBTK_LE_ERR_ARG, "unknown tuning key %s", key);
     return IBTK_LE_OK;
 }
@@ -505,9 +506,9 @@ static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel) {
     m->item_bound = (int)bound;
     int rc;
     if ((rc = m->items.ensure(sizeof(SweepItem) * (size_t)bound))) return rc;
-    if ((rc = m->nsub.ensure(sizeof(int) * (size_t)std::max(nj, 1)))) return rc;
-    if ((rc = m->isub.ensure(sizeof(int) * (size_t)std::max(nj, 1)))) return rc;
-    if ((rc = m->nitems.ensure(sizeof(int)))) return rc;
+    if ((rc = m->nsub.ensure(2 * sizeof(int) * (size_t)std::max(nj, 1)))) return rc;
+    if ((rc = m->isub.ensure(2 * sizeof(int) * (size_t)std::max(nj, 1)))) return rc;
+    if ((rc = m->nitems.ensure(2 * sizeof(int)))) return rc;
     p.cg = m->cg;
     p.S = m->S;
     p.nseg = m->nseg;
@@ -520,8 +521,15 @@ static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel) {
     size_t tb = 0;
     HIP_TRY(launch_scan(nullptr, tb, m->nsub.as<int>(), m->isub.as<int>(), std::max(nj, 1), ctx->stream));
     if ((rc = ctx->temp.ensure(tb))) return rc;
-    HIP_TRY(launch_item_table(kernel, p, target, m->nsub.as<int>(), m->isub.as<int>(), m->items.as<SweepItem>(),
-                              m->nitems.as<int>(), ctx->temp.p, ctx->temp.cap, ctx->stream));
+    // heavy items (scheduled first): own markers per piece above 4x the mean per
+    // (column, segment) pair and above 2048 -- clustered markers; uniform ones
+    // never qualify
+    const long long mean = (long long)m->n / std::max(nj, 1);
+    int heavy = (int)std::min<long long>(std::max<long long>(4 * mean, 2048), INT_MAX / 2);
+    if (ctx->tune.heavy > 0) heavy = ctx->tune.heavy;
+    else if (ctx->tune.heavy < 0) heavy = INT_MAX / 2;  // off
+    HIP_TRY(launch_item_table(kernel, p, target, heavy, m->nsub.as<int>(), m->isub.as<int>(),
+                              m->items.as<SweepItem>(), m->nitems.as<int>(), ctx->temp.p, ctx->temp.cap, ctx->stream));
     return IBTK_LE_OK;
 }
 

@@ -102,6 +102,7 @@ struct ColGeom {
 struct SweepTune {
     int seg_items = 0;     // sweep_segments' item target
     int split_target = 0;  // own markers above which a (column, segment) is cut (k_item_counts)
+    int heavy = 0;         // own markers per piece above which an item is scheduled first (-1: never)
 };
 // One 3-D sweep item: a patch, a column and its owned planes [p0, p1) (relative
 // to the patch's cg.org[2]).
@@ -134,7 +135,7 @@ struct Params {
     int zmode, zlo, zhi;       // plane window (ibtk_le_ctx_set_plane_window): 0 every item, 1 the items
                                // whose planes lie in [zlo, zhi], 2 the others
     const SweepItem* items;    // 3-D sweep item table (k_item_write)
-    const int* nitems;         // device: its length
+    const int* nitems;         // device: its length, then the count of heavy items heading it
     int item_bound;            // host: an upper bound of the length (the launch grid)
     SweepTune tune;
     int ncomp;
@@ -191,7 +192,7 @@ hipError_t launch_gather_col(int kernel, const Params& p, int n, int* sorted_s, 
 hipError_t launch_interp_sweep(int kernel, const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_spread_sweep(int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items);
-hipError_t launch_item_table(int kernel, const Params& p, int target, int* nsub, int* start, SweepItem* tab, int* ntot,
+hipError_t launch_item_table(int kernel, const Params& p, int target, int heavy, int* nsub, int* start, SweepItem* tab, int* ntot,
                              void* temp, size_t temp_bytes, hipStream_t s);
 
 // Periodic helpers

@@ -166,13 +166,21 @@ __global__ __launch_bounds__(BLOCK) void k_gather_col(Params p, int n, int* sort
 // three components of a column and its x-neighbours run on one XCD at about the
 // same time and share marker data and halo planes through its L2.  The range
 // is cut from the table's actual length (read on the device; the grid is an
-// upper bound of it): an over-sized grid must not leave XCDs idle.
-__device__ __forceinline__ int sweep_item(int nitems) {
-    const int per = (nitems + 7) >> 3;
+// upper bound of it): an over-sized grid must not leave XCDs idle.  The heavy
+// items (k_item_counts: clustered markers, p.nitems[1] of them) head the table
+// and take the first blocks, dealt round-robin over the XCDs, so that they
+// start first and the light ones fill in around them.  The grid is 8 blocks
+// longer than the item bound (the heavy block count is rounded up to 8).
+__device__ __forceinline__ int sweep_item(const Params& p) {
+    const int nt = p.nitems[0] * p.ncomp, nh = p.nitems[1] * p.ncomp;
     const int b = blockIdx.x;
-    if ((b >> 3) >= per) return -1;
-    const int it = (b & 7) * per + (b >> 3);
-    return it < nitems ? it : -1;
+    const int h8 = (nh + 7) & ~7;
+    if (b < h8) return b < nh ? b : -1;
+    const int bl = b - h8, nl = nt - nh;
+    const int per = (nl + 7) >> 3;
+    if ((bl >> 3) >= per) return -1;
+    const int it = (bl & 7) * per + (bl >> 3);
+    return it < nl ? nh + it : -1;
 }
 
 // Work item -> (component c, table entry t): component fastest, so the three
@@ -443,7 +451,7 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     using S = ISh<K>;
     constexpr int LO = S::LO, HI = S::HI, RX = S::RX, NPT = S::NPT;
     __shared__ double ring[S::NSL * S::PVP];
-    const int it = sweep_item(*p.nitems * p.ncomp);
+    const int it = sweep_item(p);
     if (it < 0) return;
     int c;
     SweepItem si;
@@ -828,9 +836,9 @@ __device__ __forceinline__ void spread_lanes_rows(const Params& p, const CompDes
 #endif
 // spread_lanes with fewer instructions per chunk (the sweep is issue-bound):
 // every stencil row is added by every busy lane, a clipped or not-owned row
-// or plane with weight 0 at its row clamped into the column (a +0 on an owned
-// point), so there is no exec mask and branch per row -- one address add per
-// row instead; validity masks from clipped ranges; IB_4's square root by rsq
+// or plane with weight 0 at its row wrapped into the column (a +0 on an owned
+// point; clamping would pile the masked rows of dense chunks onto one row), so
+// there is no exec mask and branch per row -- one address add per row instead; validity masks from clipped ranges; IB_4's square root by rsq
 // and Newton steps (the spread is compared by tolerance).
 template <int K>
 __device__ __forceinline__ void spread_lanes_flat(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
@@ -856,13 +864,13 @@ __device__ __forceinline__ void spread_lanes_flat(const Params& p, const CompDes
     const int y0 = max(st[1].ist, ylo - oy), y1 = min(st[1].isp, yhi - oy);
     const int z0 = max(st[2].ist, plo - (a + oz)), z1 = min(st[2].isp, phi - (a + oz));
     double w0v[W], w1m[W], w2m[W];
-    int roff[W];  // byte offset of stencil row i1 (clamped into the column) from row 0 of the plane
+    int roff[W];  // byte offset of stencil row i1 (wrapped into the column) from row 0 of the plane
 #pragma unroll
     for (int i = 0; i < W; ++i) {
         w0v[i] = (i >= x0 && i <= x1) ? st[0].w[i] * cdat.V : 0.0;
         w1m[i] = (i >= y0 && i <= y1) ? st[1].w[i] : 0.0;
         w2m[i] = (i >= z0 && i <= z1) ? st[2].w[i] * inv_h3 : 0.0;
-        roff[i] = 8 * COLX * min(max(oy + i, 0), COLY - 1);
+        roff[i] = 8 * COLX * (((oy + i) % COLY + COLY) % COLY);  // masked rows wrap (no pile-up on one row)
     }
     char* const base = reinterpret_cast<char*>(ring) + 8 * ox;
     int sl = (int)((unsigned)(a + oz + 64 * NSL) % (unsigned)NSL);  // ring slot of plane i2 = 0
@@ -870,6 +878,9 @@ __device__ __forceinline__ void spread_lanes_flat(const Params& p, const CompDes
     for (int i2 = 0; i2 < W; ++i2) {
         char* const plane = base + sl * (8 * S::SLOT);
         sl = sl + 1 == NSL ? 0 : sl + 1;
+        // lanes whose plane is clipped or not owned sit it out (one exec mask per
+        // plane: the edge anchors of a short z-piece reach mostly unowned planes)
+        if (!(i2 >= z0 && i2 <= z1)) continue;
 #pragma unroll
         for (int i1 = 0; i1 < W; ++i1) {
             const double t = w1m[i1] * w2m[i2];
@@ -1002,7 +1013,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     constexpr int LO = S::LO, HI = S::HI, NPL = S::NPL, FAM = S::FAM;
     __shared__ double ring_mem[S::GUARD + S::NSL * S::SLOT];
     double* const ring = ring_mem + S::GUARD;
-    const int it = sweep_item(*p.nitems * p.ncomp);
+    const int it = sweep_item(p);
     if (it < 0) return;
     int c;
     SweepItem si;
@@ -1266,9 +1277,10 @@ __device__ __forceinline__ void job_patch(const Params& p, int j, int& q, ColGeo
 
 // load-based sub-segments of (column col, planes [a0, a1))
 template <int K>
-__device__ __forceinline__ int load_split(const ColGeom& cg, const int* bs, int col, int a0, int a1, int target) {
+__device__ __forceinline__ int load_split(const ColGeom& cg, const int* bs, int col, int a0, int a1, int target,
+                                          long& load) {
     constexpr int NS = KT<K>::HI - KT<K>::LO + 1;
-    long load = 0;
+    load = 0;
     for (int a = a0; a < a1; ++a) load += bs[bucket(cg, a, col, NBAND)] - bs[bucket(cg, a, col, 0)];
     const int maxsub = max((a1 - a0) / max(NS, 8), 1);
     return (int)min((long)maxsub, max(1L, (load + target - 1) / target));
@@ -1280,8 +1292,10 @@ __device__ __forceinline__ int cuts_inside(const Params& p, int b0, int b1) {
     return c;
 }
 
+// nsub[j]: the light pieces of job j, nsub[njobs + j]: its heavy pieces (own
+// markers per piece above `heavy`; they head the item table, see sweep_item)
 template <int K>
-__global__ __launch_bounds__(BLOCK) void k_item_counts(Params p, int target, int* nsub) {
+__global__ __launch_bounds__(BLOCK) void k_item_counts(Params p, int target, int heavy, int* nsub) {
     const int j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= p.njobs) return;
     int q, S, nseg, j0;
@@ -1291,15 +1305,18 @@ __global__ __launch_bounds__(BLOCK) void k_item_counts(Params p, int target, int
     const int jl = j - j0;
     const int seg = jl / cg.ncol, col = jl - seg * cg.ncol;
     const int a0 = seg * S, a1 = min(a0 + S, cg.nz), len = a1 - a0;
-    const int n = load_split<K>(cg, bs, col, a0, a1, target);
+    long load;
+    const int n = load_split<K>(cg, bs, col, a0, a1, target, load);
     int pieces = n;
     if (p.ncut)
         for (int k = 0; k < n; ++k) pieces += cuts_inside(p, a0 + (len * k) / n, a0 + (len * (k + 1)) / n);
-    nsub[j] = pieces;
+    const bool hv = load > (long)heavy * n;
+    nsub[j] = hv ? 0 : pieces;
+    nsub[p.njobs + j] = hv ? pieces : 0;
 }
 template <int K>
-__global__ __launch_bounds__(BLOCK) void k_item_write(Params p, int target, const int* nsub, const int* start,
-                                                      SweepItem* tab, int* ntot) {
+__global__ __launch_bounds__(BLOCK) void k_item_write(Params p, int target, int heavy, const int* nsub,
+                                                      const int* start, SweepItem* tab, int* ntot) {
     const int j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= p.njobs) return;
     int q, S, nseg, j0;
@@ -1309,8 +1326,12 @@ __global__ __launch_bounds__(BLOCK) void k_item_write(Params p, int target, cons
     const int jl = j - j0;
     const int seg = jl / cg.ncol, col = jl - seg * cg.ncol;
     const int a0 = seg * S, a1 = min(a0 + S, cg.nz), len = a1 - a0;
-    const int n = load_split<K>(cg, bs, col, a0, a1, target);
-    int w = start[j];
+    long load;
+    const int n = load_split<K>(cg, bs, col, a0, a1, target, load);
+    const int nj = p.njobs;
+    const int nheavy = start[2 * nj - 1] + nsub[2 * nj - 1];
+    const bool hv = load > (long)heavy * n;
+    int w = hv ? start[nj + j] : nheavy + start[j];
     for (int k = 0; k < n; ++k) {
         int b0 = a0 + (len * k) / n;
         const int b1 = a0 + (len * (k + 1)) / n;
@@ -1321,20 +1342,26 @@ __global__ __launch_bounds__(BLOCK) void k_item_write(Params p, int target, cons
             }
         tab[w++] = SweepItem{col, b0, b1, q};
     }
-    if (j == p.njobs - 1) *ntot = start[j] + nsub[j];
+    if (j == nj - 1) {
+        ntot[0] = nheavy + start[j] + nsub[j];
+        ntot[1] = nheavy;
+    }
 }
 
 static int grid8(long items) { return (int)((items + 7) & ~7L); }
 
-template <int K> hipError_t launch_item_table_t(const Params& p, int target, int* nsub, int* start, SweepItem* tab,
-                                                int* ntot, void* temp, size_t temp_bytes, hipStream_t s) {
+template <int K> hipError_t launch_item_table_t(const Params& p, int target, int heavy, int* nsub, int* start,
+                                                SweepItem* tab, int* ntot, void* temp, size_t temp_bytes,
+                                                hipStream_t s) {
     const int nj = p.njobs;
-    if (nj <= 0) return hipMemsetAsync(ntot, 0, sizeof(int), s);
-    hipLaunchKernelGGL(k_item_counts<K>, dim3((nj + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, target, nsub);
-    hipError_t e = launch_scan(temp, temp_bytes, nsub, start, nj, s);
+    if (nj <= 0) return hipMemsetAsync(ntot, 0, 2 * sizeof(int), s);
+    hipLaunchKernelGGL(k_item_counts<K>, dim3((nj + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, target, heavy, nsub);
+    hipError_t e = launch_scan(temp, temp_bytes, nsub, start, nj, s);  // light pieces
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_item_write<K>, dim3((nj + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, target, nsub, start, tab,
-                       ntot);
+    e = launch_scan(temp, temp_bytes, nsub + nj, start + nj, nj, s);   // heavy pieces
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_item_write<K>, dim3((nj + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, target, heavy, nsub,
+                       start, tab, ntot);
     return hipGetLastError();
 }
 
@@ -1381,8 +1408,8 @@ hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent
     if (ev0) (void)hipEventRecord(ev0, s);
     const long items = (long)p.item_bound * p.ncomp;
     if (items > 0) {
-        if (p.pd) hipLaunchKernelGGL((k_interp_sweep<K, true>), dim3(grid8(items)), dim3(SW * IWAVES), 0, s, p);
-        else hipLaunchKernelGGL((k_interp_sweep<K, false>), dim3(grid8(items)), dim3(SW * IWAVES), 0, s, p);
+        if (p.pd) hipLaunchKernelGGL((k_interp_sweep<K, true>), dim3(grid8(items + 8)), dim3(SW * IWAVES), 0, s, p);
+        else hipLaunchKernelGGL((k_interp_sweep<K, false>), dim3(grid8(items + 8)), dim3(SW * IWAVES), 0, s, p);
     }
     if (ev1) (void)hipEventRecord(ev1, s);
     hipError_t e = hipGetLastError();
@@ -1410,8 +1437,8 @@ template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s
     if (ev0) (void)hipEventRecord(ev0, s);  // the events bracket the sweep kernel alone
     const long items = (long)p.item_bound * p.ncomp;
     if (items > 0) {
-        if (p.pd) hipLaunchKernelGGL((k_spread_sweep<K, true>), dim3(grid8(items)), dim3(SW), 0, s, p);
-        else hipLaunchKernelGGL((k_spread_sweep<K, false>), dim3(grid8(items)), dim3(SW), 0, s, p);
+        if (p.pd) hipLaunchKernelGGL((k_spread_sweep<K, true>), dim3(grid8(items + 8)), dim3(SW), 0, s, p);
+        else hipLaunchKernelGGL((k_spread_sweep<K, false>), dim3(grid8(items + 8)), dim3(SW), 0, s, p);
     }
     if (ev1) (void)hipEventRecord(ev1, s);
     return hipGetLastError();
@@ -1431,12 +1458,12 @@ template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s
     default: return nullptr;                                         \
     }
 
-using ItemTabFn = hipError_t (*)(const Params&, int, int*, int*, SweepItem*, int*, void*, size_t, hipStream_t);
+using ItemTabFn = hipError_t (*)(const Params&, int, int, int*, int*, SweepItem*, int*, void*, size_t, hipStream_t);
 static ItemTabFn pick_item_table(int k) { IBTK_LE_DISPATCH_K(k, launch_item_table_t) }
-hipError_t launch_item_table(int kernel, const Params& p, int target, int* nsub, int* start, SweepItem* tab, int* ntot,
-                             void* temp, size_t temp_bytes, hipStream_t s) {
+hipError_t launch_item_table(int kernel, const Params& p, int target, int heavy, int* nsub, int* start, SweepItem* tab,
+                             int* ntot, void* temp, size_t temp_bytes, hipStream_t s) {
     ItemTabFn f = pick_item_table(kernel);
-    return f ? f(p, target, nsub, start, tab, ntot, temp, temp_bytes, s) : hipErrorInvalidValue;
+    return f ? f(p, target, heavy, nsub, start, tab, ntot, temp, temp_bytes, s) : hipErrorInvalidValue;
 }
 using BinColFn = hipError_t (*)(const Params&, int, unsigned*, int*, hipStream_t);
 using GatherColFn = hipError_t (*)(const Params&, int, int*, double*, const unsigned*, int, int*, hipStream_t);

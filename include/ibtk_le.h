@@ -318,7 +318,9 @@ int ibtk_le_mark_stencils(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int ce
  * measured with HIP events on the context stream when enabled). */
 int ibtk_le_ctx_enable_timing(ibtk_le_ctx ctx, int enable);
 /* Diagnostics: tuning overrides of the 3-D sweeps' work items (0 = default), both
- * taking effect at the next bin: "seg_items" (target number of (column, segment)
+ * taking effect at the next bin: "heavy" (own markers per item above which the
+ * item is scheduled first; -1 never; default 4x the mean, at least 2048),
+ * "seg_items" (target number of (column, segment)
  * items, which sets the segment length) and "split_target" (own markers above
  * which a (column, segment) is cut into sub-segments).  Results do not depend on
  * them (each grid point's order of contributions is fixed by the sorted list). */

@@ -1,12 +1,14 @@
 #!/bin/bash
 # HBM traffic of the sweep kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE, one
-# counter per pass (MI355X_MICROARCH.md, HBM section).  The guide's x2 FETCH_SIZE
-# correction is calibrated for 16-B-per-lane streaming reads only; the sweeps
-# load 8 B per lane, and their FETCH_SIZE matches the known byte count of the
-# Eulerian arrays they stream (interp: 3 x 1031 x 1030^2 x 8 B = 26.2 GB read,
-# FETCH_SIZE 25.7 GB), so it is taken at face value (calibration factor 1).
-# Writes <outdir>/pmc.json; copy it to profiles/pmc_<cfg>_<kernel>_1gpu.json,
-# which bench.py reads.
+# counter per pass (MI355X_MICROARCH.md, HBM section).  FETCH_SIZE is taken x2:
+# on gfx950 it reports half the bytes of 8-B-per-lane reads too, not only of the
+# guide's 16-B case (tools/ubench_fetch.hip + tools/calib_fetch.sh, result in
+# profiles/r02b/fetch_calibration.json: k_read8 and k_read16 both 0.50);
+# WRITE_SIZE is exact for contiguous stores (1.00) and counts whole 64-B pieces
+# for partial ones (24-B records written 8 B at a time: 3.00).
+# Writes <outdir>/pmc.json with the library's source hash; copy it to
+# profiles/pmc_<cfg>_<kernel>_1gpu.json, which bench.py reads when the hash
+# matches the build it runs.
 # Usage: tools/pmc_traffic.sh <outdir> [cfg] [kernel]
 out=$1; cfg=${2:-cfg4}; kern=${3:-IB_4}
 export TMPDIR=/tmp
@@ -28,9 +30,11 @@ for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             per[(r["Kernel_Name"].split("(")[0], r["Dispatch_Id"])] += float(r["Counter_Value"])
         for (k, _), v in per.items():
             vals[k][ctr].append(v)
-res = {"counters_kb": {}, "per_launch_bytes": {},
-       "note": "(FETCH_SIZE + WRITE_SIZE) KB x 1024 per launch, mean over launches; FETCH_SIZE calibration factor 1 "
-               "for the sweeps' 8-B-per-lane loads (see tools/pmc_traffic.sh)"}
+sys.path.insert(0, ".")
+from ibamr_amd.build import source_hash
+res = {"build": source_hash(), "counters_kb": {}, "per_launch_bytes": {}, "read_bytes": {}, "write_bytes": {},
+       "note": "(2 x FETCH_SIZE + WRITE_SIZE) KB x 1024 per launch, mean over launches; FETCH_SIZE x 2 per "
+               "profiles/r02b/fetch_calibration.json (8-B and 16-B-per-lane reads both report 0.50 of the bytes)"}
 for k, d in vals.items():
     name = "spread" if "k_spread_sweep" in k else "interp" if "k_interp_sweep" in k else None
     if name is None or not d.get("FETCH_SIZE") or not d.get("WRITE_SIZE"):
@@ -38,7 +42,9 @@ for k, d in vals.items():
     f = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"])
     w = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"])
     res["counters_kb"][name] = {"FETCH_SIZE": f, "WRITE_SIZE": w}
-    res["per_launch_bytes"][name] = (f + w) * 1024
+    res["per_launch_bytes"][name] = (2 * f + w) * 1024
+    res["read_bytes"][name] = 2 * f * 1024
+    res["write_bytes"][name] = w * 1024
 json.dump(res, open(f"{out}/pmc.json", "w"), indent=1)
 print(json.dumps(res))
 PY

@@ -52,8 +52,8 @@ def main():
     f = geom.alloc("side", device=dev)
     bins = le.Markers(ctx)
     settings = json.loads(args.settings)
-    keys = ["seg_items", "split_target"]
-    defaults = {"seg_items": 0, "split_target": 0}
+    keys = ["seg_items", "split_target", "heavy"]
+    defaults = {"seg_items": 0, "split_target": 0, "heavy": 0}
     Uref = fref = None
     for i, st in enumerate(settings):
         full = dict(defaults, **st)
