@@ -353,6 +353,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-rebin", action="store_true", help="bin once outside the timed loop")
+    ap.add_argument("--spread-mode", default="sum", choices=["sum", "markers"],
+                    help="N > 1: z ghost-region sum of the grid (sum) or the reference's ghost markers (markers)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="diagnostic sweep overrides (ibtk_le_ctx_tune: heavy, seg_items, split_target)")
     ap.add_argument("--layout", default="packed", choices=["aligned", "packed"],
@@ -404,7 +406,7 @@ def main():
         return
 
     from ibamr_amd import le
-    from ibamr_amd.slab import Slab, SlabExchange, migrate
+    from ibamr_amd.slab import GhostMarkers, Slab, SlabExchange, migrate
 
     N = cfg["N"]
     ghost = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
@@ -435,9 +437,24 @@ def main():
     if not args.no_overlap:
         ex_u.cut_items()  # sweep items cut at the slab faces (N > 1)
     bins = le.Markers(ctx)
-    bins.bin(geom, kernel, X)
+    gm = GhostMarkers(slab) if args.spread_mode == "markers" and world > 1 else None
+    # the binned list: own markers, or (ghost-marker mode) own + the neighbours'
+    # markers near the slab faces, exchanged with their forces every step
+    cur = {"X": X, "F": F, "U": U}
+
+    def bin_step():
+        if gm is None:
+            bins.bin(geom, kernel, X)
+            cur.update(X=X, F=F, U=U)
+            return
+        Xa, Fa, _ = gm.exchange(X, F)
+        bins.bin(geom, kernel, Xa)
+        Ua = cur["U"] if cur["U"].shape == Xa.shape else torch.empty_like(Xa)
+        cur.update(X=Xa, F=Fa, U=Ua)
+
+    bin_step()
     # exact algorithmic bytes: distinct side points touched by the clipped stencils
-    masks = le.mark_stencils(ctx, bins, kernel, "side", geom, X)
+    masks = le.mark_stencils(ctx, bins, kernel, "side", geom, cur["X"])
     S_touched = [int(m.sum(dtype=torch.int64).item()) for m in masks]
     del masks
     torch.cuda.synchronize()
@@ -456,20 +473,30 @@ def main():
 
     def interp_with_fill():
         # N > 1: the interior sweep items run while the z ghost planes are in flight
+        Xb, Ub = cur["X"], cur["U"]
         if args.no_overlap:
             ex_u.halo_fill()
-            le.interp(ctx, bins, kernel, "side", geom, u, U, X)
+            le.interp(ctx, bins, kernel, "side", geom, u, Ub, Xb)
         else:
-            ex_u.halo_fill(lambda: le.interp(ctx, bins, kernel, "side", geom, u, U, X))
+            ex_u.halo_fill(lambda: le.interp(ctx, bins, kernel, "side", geom, u, Ub, Xb))
+        if Ub is not U:
+            U.copy_(Ub[:U.shape[0]])  # the own markers' velocities (ghost markers' discarded)
 
     def spread_with_sum():
+        Xb, Fb = cur["X"], cur["F"]
+        if gm is not None:
+            # ghost markers: every rank spreads what reaches its own planes, no z
+            # exchange of the grid; x/y periodic ghosts fold locally
+            le.spread(ctx, bins, kernel, "side", geom, f, Fb, Xb)
+            ex_f.local_fold([1, 1, 0])
+            return
         # N > 1: the boundary items first, then the interior ones while the ghost
         # planes are in flight
         if args.no_overlap:
-            le.spread(ctx, bins, kernel, "side", geom, f, F, X)
+            le.spread(ctx, bins, kernel, "side", geom, f, Fb, Xb)
             ex_f.ghost_sum()
         else:
-            ex_f.ghost_sum(lambda: le.spread(ctx, bins, kernel, "side", geom, f, F, X))
+            ex_f.ghost_sum(lambda: le.spread(ctx, bins, kernel, "side", geom, f, Fb, Xb))
 
     def step_move(record):
         # interp -> X += dt U -> migrate -> bin -> spread: one bin per step, as in
@@ -485,7 +512,7 @@ def main():
             X, (F,) = migrate(slab, X, [F], cell_order=False)
             if U.shape != X.shape:
                 U = torch.empty_like(X)
-        bins.bin(geom, kernel, X)
+        bin_step()
         if record:
             E[2].record()
         le.zero_ghosts(ctx, geom, "side", f)
@@ -500,8 +527,8 @@ def main():
             return step_move(record)
         if record:
             E[0].record()
-        if not args.no_rebin:
-            bins.bin(geom, kernel, X)
+        if not args.no_rebin or gm is not None:
+            bin_step()
         if record:
             E[1].record()
         interp_with_fill()
@@ -557,11 +584,11 @@ def main():
     kt = {"interp": [], "spread": []}
     for _ in range(3):
         ex_u.halo_fill()
-        le.interp(ctx, bins, kernel, "side", geom, u, U, X)
+        le.interp(ctx, bins, kernel, "side", geom, u, cur["U"], cur["X"])
         ctx.synchronize()
         kt["interp"].append(ctx.last_kernel_ms())
         le.zero_ghosts(ctx, geom, "side", f)
-        le.spread(ctx, bins, kernel, "side", geom, f, F, X)
+        le.spread(ctx, bins, kernel, "side", geom, f, cur["F"], cur["X"])
         ctx.synchronize()
         kt["spread"].append(ctx.last_kernel_ms())
     ctx.enable_timing(False)
@@ -619,7 +646,7 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {"workload": cfg["desc"], "kernel": kernel, "grid": [N, N, N], "markers": M_total,
-                   "parallelism": f"z-slab x{world}", "ghost": ghost, "marker_order": args.marker_order, "layout": args.layout,
+                   "parallelism": f"z-slab x{world}", "ghost": ghost, "marker_order": args.marker_order, "layout": args.layout, "spread_mode": args.spread_mode if world > 1 else "one rank",
                    "move": args.move, "overlap": world > 1 and not args.no_overlap,
                    "step": ("ghost fill + interp(3 comps) + position update + migrate + bin + zero ghosts + "
                             "spread(3 comps) + ghost sum" if args.move else

@@ -171,8 +171,8 @@ __global__ __launch_bounds__(BLOCK) void k_gather_col(Params p, int n, int* sort
 // and take the first blocks, dealt round-robin over the XCDs, so that they
 // start first and the light ones fill in around them.  The grid is 8 blocks
 // longer than the item bound (the heavy block count is rounded up to 8).
-__device__ __forceinline__ int sweep_item(const Params& p) {
-    const int nt = p.nitems[0] * p.ncomp, nh = p.nitems[1] * p.ncomp;
+__device__ __forceinline__ int sweep_item(const Params& p, int per_entry) {
+    const int nt = p.nitems[0] * per_entry, nh = p.nitems[1] * per_entry;
     const int b = blockIdx.x;
     const int h8 = (nh + 7) & ~7;
     if (b < h8) return b < nh ? b : -1;
@@ -295,6 +295,9 @@ __device__ __forceinline__ double shfl_f64(double v, int src) {
 #define IBTK_LE_IWAVES 4
 #endif
 constexpr int IWAVES = IBTK_LE_IWAVES;  // waves per interp work item (one LDS ring)
+#ifndef IBTK_LE_ICW
+#define IBTK_LE_ICW 1  // 3: the three components of an item in one workgroup (measured 8 % slower on cfg4)
+#endif
 // 1: interp sums in the Fortran order, bitwise the oracle's (default);
 // 0: separable rows with FMAs, within tolerance (an experiment, not shipped)
 #ifndef IBTK_LE_IDEAL
@@ -446,20 +449,29 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
 // pooled markers.  Points outside the component's array are staged as 0.  One
 // lane per marker sums its W^3 stencil from the ring (Fortran loop order,
 // bitwise the oracle's).
-template <int K, bool LVL>
-__global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
+// ICW components per workgroup (ICW x IWAVES waves, one LDS ring per component):
+// the components of an item run side by side on one CU, in step (the group
+// barriers are the workgroup's), so they read the item's markers from L1/L2
+// once and their 8-byte Q stores to one AoS record land in L2 together (one
+// 24-byte record write-back instead of three partial-line ones).
+template <int K, bool LVL, int ICW>
+__global__ __launch_bounds__(SW * IWAVES * ICW) void k_interp_sweep(Params p) {
     using S = ISh<K>;
     constexpr int LO = S::LO, HI = S::HI, RX = S::RX, NPT = S::NPT;
-    __shared__ double ring[S::NSL * S::PVP];
-    const int it = sweep_item(p);
+    __shared__ double ring_all[ICW * S::NSL * S::PVP];
+    const int ng = (p.ncomp + ICW - 1) / ICW;  // component groups per table entry
+    const int it = sweep_item(p, ng);
     if (it < 0) return;
-    int c;
-    SweepItem si;
-    item_decode(p, it, c, si);
+    const int te = it / ng;
+    const int cw = ICW == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)threadIdx.x / (SW * IWAVES));
+    const int c = (it - te * ng) * ICW + cw;
+    if (c >= p.ncomp) return;  // an absent component: its waves leave, the barriers count the others
+    double* const ring = ring_all + cw * (S::NSL * S::PVP);
+    const SweepItem si = p.items[te];
     const int col = si.col;
     const int a0 = si.p0, a1 = si.p1;  // the item's anchor planes
     const int lane = lane_id();
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int w = __builtin_amdgcn_readfirstlane(((int)threadIdx.x >> 6) % IWAVES);
     ColGeom cg;
     CompDesc cd;
     const int* bs;
@@ -1013,7 +1025,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     constexpr int LO = S::LO, HI = S::HI, NPL = S::NPL, FAM = S::FAM;
     __shared__ double ring_mem[S::GUARD + S::NSL * S::SLOT];
     double* const ring = ring_mem + S::GUARD;
-    const int it = sweep_item(p);
+    const int it = sweep_item(p, p.ncomp);
     if (it < 0) return;
     int c;
     SweepItem si;
@@ -1244,7 +1256,12 @@ void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items) {
 // cut into sub-segments of its planes (at least NS planes each): a fibre bundle
 // along z is then many items instead of one wave's serial walk.  Sub-items own
 // disjoint planes, so every grid point still gets its contributions from one
-// item, in the same order: results do not depend on the split.  The interp
+// item.  The interp does not depend on the split (one lane sums a marker); the
+// spread adds a point's contributions anchor by anchor in sorted order, but two
+// candidates of one 64-lane chunk that hit the same point add in their dealt
+// lane order, and where the chunks start depends on the item's first anchor: so
+// a different split can round a spread sum differently (fixed settings are
+// bit-stable run to run; tests/test_gpu_items.py).  The interp
 // item of a sub-segment sums the markers anchored in its planes; the spread
 // item owns its planes and takes the candidates of the anchors reaching them
 // (NS - 1 extra anchor planes per cut).
@@ -1406,10 +1423,32 @@ hipError_t launch_gather_col_t(const Params& p, int n, int* ss, double* sx, cons
 template <int K>
 hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     if (ev0) (void)hipEventRecord(ev0, s);
-    const long items = (long)p.item_bound * p.ncomp;
-    if (items > 0) {
-        if (p.pd) hipLaunchKernelGGL((k_interp_sweep<K, true>), dim3(grid8(items + 8)), dim3(SW * IWAVES), 0, s, p);
-        else hipLaunchKernelGGL((k_interp_sweep<K, false>), dim3(grid8(items + 8)), dim3(SW * IWAVES), 0, s, p);
+    constexpr bool fits3 = 3 * ISh<K>::NSL * ISh<K>::PVP * 8 <= 160 * 1024;  // three rings in one CU's LDS
+    if constexpr (!fits3 || IBTK_LE_ICW != 3) {
+        const long items = (long)p.item_bound * p.ncomp;
+        if (items > 0) {
+            if (p.pd)
+                hipLaunchKernelGGL((k_interp_sweep<K, true, 1>), dim3(grid8(items + 8)), dim3(SW * IWAVES), 0, s, p);
+            else
+                hipLaunchKernelGGL((k_interp_sweep<K, false, 1>), dim3(grid8(items + 8)), dim3(SW * IWAVES), 0, s, p);
+        }
+    } else if (p.ncomp == 3) {  // the components of an item in one workgroup
+        const long items = (long)p.item_bound;
+        if (items > 0) {
+            if (p.pd)
+                hipLaunchKernelGGL((k_interp_sweep<K, true, 3>), dim3(grid8(items + 8)), dim3(SW * IWAVES * 3), 0, s, p);
+            else
+                hipLaunchKernelGGL((k_interp_sweep<K, false, 3>), dim3(grid8(items + 8)), dim3(SW * IWAVES * 3), 0, s,
+                                   p);
+        }
+    } else {
+        const long items = (long)p.item_bound * p.ncomp;
+        if (items > 0) {
+            if (p.pd)
+                hipLaunchKernelGGL((k_interp_sweep<K, true, 1>), dim3(grid8(items + 8)), dim3(SW * IWAVES), 0, s, p);
+            else
+                hipLaunchKernelGGL((k_interp_sweep<K, false, 1>), dim3(grid8(items + 8)), dim3(SW * IWAVES), 0, s, p);
+        }
     }
     if (ev1) (void)hipEventRecord(ev1, s);
     hipError_t e = hipGetLastError();

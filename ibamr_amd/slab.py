@@ -239,6 +239,90 @@ class SlabExchange:
         self.local_fold([1, 1, 0])
 
 
+class GhostMarkers:
+    """The reference's spread exchange: ghost markers instead of a grid reduction.
+
+    LDataManager::spread (LDataManager.cpp:555-675) spreads, per patch, the list of
+    every marker whose stencil can reach the patch -- its own and the ghost nodes a
+    neighbouring rank owns (LData ghost nodes, kept current by
+    LData::beginGhostUpdate) -- into the patch's ghosted data, and keeps the
+    interior: no ghost-region sum.  Here a rank sends the markers (position and
+    force) whose cell lies within ``ghost`` planes of a slab face to the
+    neighbour across it; each rank spreads its own plus the received markers and
+    keeps its own planes (the z ghost planes are left as they fall), then folds
+    x/y locally.  Markers crossing the periodic z wrap arrive shifted by -+L_z
+    (the periodic_shift of LIndexSetData's ghost lists).  One pair of
+    point-to-point messages per direction and step (the counts, then the data),
+    SURVEY.md 8(e) "reference mode": ~2 ghost/N_z of the markers move instead of
+    3 x ghost planes of grid per face.  Results match the grid-sum mode and one
+    rank within the spread tolerance, and are bit-stable run to run.
+    """
+
+    def __init__(self, slab: Slab, group=None):
+        self.slab = slab
+        self.group = group
+
+    def _p2p(self, sends, recvs):
+        import torch.distributed as dist
+        stage = dist.get_backend(self.group) == "gloo"
+        ops, back = [], []
+        for t, peer in sends:
+            ops.append(dist.P2POp(dist.isend, t.cpu() if stage and t.is_cuda else t, peer, group=self.group))
+        for t, peer in recvs:
+            if stage and t.is_cuda:
+                h = torch.empty(t.shape, dtype=t.dtype)
+                back.append((h, t))
+                t = h
+            ops.append(dist.P2POp(dist.irecv, t, peer, group=self.group))
+        for w in dist.batch_isend_irecv(ops) if ops else []:
+            w.wait()
+        for h, t in back:
+            t.copy_(h)
+
+    def select(self, X: torch.Tensor):
+        """(to_up, to_down): indices of the markers within `ghost` cells of the
+        upper / lower slab face (a marker can be in both when the slab is thin)."""
+        s = self.slab
+        cz = torch.clamp((X[:, 2] / s.dx[2]).floor().long(), 0, s.N[2] - 1)
+        up = (cz >= s.z1 - s.ghost).nonzero().squeeze(1)
+        down = (cz < s.z0 + s.ghost).nonzero().squeeze(1)
+        return up, down
+
+    def exchange(self, X: torch.Tensor, F: torch.Tensor):
+        """Own markers followed by the ghost markers from below, then from above:
+        (X_all, F_all, n_own).  X: (M, 3), F: (M, d) float64 of this rank."""
+        s = self.slab
+        if s.P == 1:
+            return X, F, X.shape[0]
+        up, down = self.select(X)
+        data = torch.cat([X, F.reshape(X.shape[0], -1).to(X.dtype)], dim=1)
+        send_up, send_down = data[up].contiguous(), data[down].contiguous()
+        # counts, then data; each peer's receives in the order it sends (RCCL
+        # matches a pair's messages in issue order; with P = 2 up == down):
+        # sends [to up, to down], receives [from down (its "to up"), from up]
+        dev = X.device
+        cu = torch.tensor([send_up.shape[0]], dtype=torch.int64, device=dev)
+        cd = torch.tensor([send_down.shape[0]], dtype=torch.int64, device=dev)
+        rd, ru = torch.empty_like(cu), torch.empty_like(cd)
+        self._p2p([(cu, s.up), (cd, s.down)], [(rd, s.down), (ru, s.up)])
+        nd, nu = (int(v) for v in torch.cat([rd, ru]).cpu().tolist())  # the step's one host sync
+        D = data.shape[1]
+        from_down = torch.empty((nd, D), dtype=data.dtype, device=dev)
+        from_up = torch.empty((nu, D), dtype=data.dtype, device=dev)
+        sends = [(t, peer) for t, peer in ((send_up, s.up), (send_down, s.down))]
+        recvs = [(t, peer) for t, peer in ((from_down, s.down), (from_up, s.up))]
+        self._p2p(sends, recvs)
+        Lz = s.L[2]
+        if s.rank == 0 and nd:
+            from_down[:, 2] -= Lz   # rank P-1's top planes sit below z = 0
+        if s.rank == s.P - 1 and nu:
+            from_up[:, 2] += Lz     # rank 0's bottom planes sit above z = L_z
+        allm = torch.cat([data, from_down, from_up], dim=0)
+        Xa = allm[:, :3].contiguous()
+        Fa = allm[:, 3:].reshape((allm.shape[0],) + tuple(F.shape[1:])).to(F.dtype).contiguous()
+        return Xa, Fa, X.shape[0]
+
+
 def migrate(slab: Slab, X: torch.Tensor, fields: Sequence[torch.Tensor] = (), group=None, cell_order: bool = True):
     """Move every marker to the rank whose slab holds its cell, after a position update.
 

@@ -322,8 +322,10 @@ int ibtk_le_ctx_enable_timing(ibtk_le_ctx ctx, int enable);
  * item is scheduled first; -1 never; default 4x the mean, at least 2048),
  * "seg_items" (target number of (column, segment)
  * items, which sets the segment length) and "split_target" (own markers above
- * which a (column, segment) is cut into sub-segments).  Results do not depend on
- * them (each grid point's order of contributions is fixed by the sorted list). */
+ * which a (column, segment) is cut into sub-segments).  Interp results do not
+ * depend on them; spread results are bit-stable for fixed settings and may differ
+ * in the last bits between settings (same-point adds within one 64-candidate
+ * chunk follow its lane order, and the chunk boundaries move with the items). */
 int ibtk_le_ctx_tune(ibtk_le_ctx ctx, const char* key, int value);
 double ibtk_le_ctx_last_kernel_ms(ibtk_le_ctx ctx);
 

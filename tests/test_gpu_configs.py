@@ -287,11 +287,11 @@ def _fill_interior(a, G, g, z0, nz, N):
     a[g:g + nz, g:g + N, g:g + N] = torch.from_numpy(G[z0:z0 + nz])
 
 
-def _slab_run(le, ctx, N, M, world, rank, kernel="IB_4", move=False, overlap=False):
+def _slab_run(le, ctx, N, M, world, rank, kernel="IB_4", move=False, overlap=False, mode="sum"):
     """One rank's interp + spread on its slab; returns (ids, U, f interior planes).
     overlap: the sweep items cut at the slab faces, interp / spread in two halves
     around the exchanges (SlabExchange.halo_fill(work) / ghost_sum(work))."""
-    from ibamr_amd.slab import Slab, SlabExchange, migrate
+    from ibamr_amd.slab import GhostMarkers, Slab, SlabExchange, migrate
     g = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
     slab = Slab([N, N, N], world, rank, g)
     geom = slab.geometry()
@@ -323,7 +323,13 @@ def _slab_run(le, ctx, N, M, world, rank, kernel="IB_4", move=False, overlap=Fal
         m = le.Markers(ctx).bin(geom, kernel, X)
     f = geom.alloc("side")
     le.zero_ghosts(ctx, geom, "side", f)
-    if overlap:
+    if mode == "markers" and world > 1:
+        # the reference's exchange: ghost markers in, the own planes kept, x/y folded
+        Xa, Fa, _ = GhostMarkers(slab).exchange(X, F)
+        ma = le.Markers(ctx).bin(geom, kernel, Xa)
+        le.spread(ctx, ma, kernel, "side", geom, f, Fa, Xa)
+        SlabExchange(slab, f, ctx).local_fold([1, 1, 0])
+    elif overlap:
         SlabExchange(slab, f, ctx).ghost_sum(lambda: le.spread(ctx, m, kernel, "side", geom, f, F, X))
     else:
         le.spread(ctx, m, kernel, "side", geom, f, F, X)
@@ -334,7 +340,7 @@ def _slab_run(le, ctx, N, M, world, rank, kernel="IB_4", move=False, overlap=Fal
     return mine, U.cpu().numpy(), fin, slab.z0, slab.nz
 
 
-def _slab_worker(rank, world, port, N, M, move, out_q):
+def _slab_worker(rank, world, port, N, M, move, out_q, mode="sum"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -343,8 +349,13 @@ def _slab_worker(rank, world, port, N, M, move, out_q):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from ibamr_amd import le
         ctx = le.Context(0)
-        ids, U, fin, z0, nz = _slab_run(le, ctx, N, M, world, rank, move=move)
-        if not move:
+        ids, U, fin, z0, nz = _slab_run(le, ctx, N, M, world, rank, move=move, mode=mode)
+        if mode == "markers":
+            # bit-stable on a repeat
+            ids2, U2, fin2, _, _ = _slab_run(le, ctx, N, M, world, rank, move=move, mode=mode)
+            for c in range(3):
+                assert np.array_equal(fin2[c], fin[c]), f"rank {rank}: ghost-marker spread comp {c} not bit-stable"
+        elif not move:
             # the overlapped form (cut items, two half-sweeps around each exchange)
             # must give the same bits
             ids2, U2, fin2, _, _ = _slab_run(le, ctx, N, M, world, rank, move=move, overlap=True)
@@ -359,15 +370,17 @@ def _slab_worker(rank, world, port, N, M, move, out_q):
         out_q.put((rank, traceback.format_exc(), None, None, None, 0, 0))
 
 
-@pytest.mark.parametrize("world,move", [(2, False), (4, False), (8, False), (2, True), (4, True)])
-def test_cfg4_slab_split_matches_one_rank(le, ctx, world, move):
+@pytest.mark.parametrize("world,move,mode", [(2, False, "sum"), (4, False, "sum"), (8, False, "sum"), (2, True, "sum"),
+                                             (4, True, "sum"), (2, False, "markers"), (4, False, "markers"),
+                                             (4, True, "markers")])
+def test_cfg4_slab_split_matches_one_rank(le, ctx, world, move, mode):
     import torch.multiprocessing as mp
     N, M = 64, 150_000
     ref_ids, ref_U, ref_f, _, _ = _slab_run(le, ctx, N, M, 1, 0, move=move)
     mpc = mp.get_context("spawn")
     q = mpc.Queue()
     port = _free_port()
-    procs = [mpc.Process(target=_slab_worker, args=(r, world, port, N, M, move, q)) for r in range(world)]
+    procs = [mpc.Process(target=_slab_worker, args=(r, world, port, N, M, move, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     res = []

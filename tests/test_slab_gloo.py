@@ -219,3 +219,81 @@ def test_marker_migration_gloo(world):
         for i, x, f in zip(idn, Xn, Fn):
             xb, fb = before[int(i)]
             assert np.allclose(x, xb, atol=1e-15, rtol=0) and np.array_equal(f, fb)
+
+
+def _ghost_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from ibamr_amd.slab import GhostMarkers, Slab
+        N, g = [16, 16, 32], 3
+        slab = Slab(N, world, rank, g)
+        rng = np.random.default_rng(7)
+        Xg = rng.uniform(0, 1, (3000, 3))
+        Fg = rng.standard_normal((3000, 3))
+        ids = np.arange(3000)
+        z = Xg[:, 2]
+        mine = (z >= slab.z0 * slab.dx[2]) & (z < slab.z1 * slab.dx[2])
+        X = torch.from_numpy(Xg[mine])
+        F = torch.from_numpy(np.column_stack([Fg[mine], ids[mine]]))  # the id rides along as a field
+        out = []
+        for rep in range(2):
+            Xa, Fa, n_own = GhostMarkers(slab).exchange(X, F)
+            out.append((Xa.numpy().copy(), Fa.numpy().copy(), n_own))
+        same = np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+        q.put((rank, "ok", slab.z0, slab.z1, out[0], same))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc(), 0, 0, None, False))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ghost_marker_exchange_gloo(world):
+    """Reference-mode spread exchange (GhostMarkers): each rank ends with its own
+    markers first, then exactly the other ranks' markers whose cell lies within
+    `ghost` planes beyond its faces (periodic in z, shifted by -+L_z across the
+    wrap), with their forces; deterministic on a repeat."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ghost_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    res.sort(key=lambda r: r[0])
+    bad = [r for r in res if r[1] != "ok"]
+    assert not bad, bad[0][1]
+    rng = np.random.default_rng(7)
+    Xg = rng.uniform(0, 1, (3000, 3))
+    Fg = rng.standard_normal((3000, 3))
+    Nz, g = 32, 3
+    dz = 1.0 / Nz
+    cz = np.clip(np.floor(Xg[:, 2] / dz).astype(int), 0, Nz - 1)
+    for rank, _, z0, z1, (Xa, Fa, n_own), same in res:
+        assert same
+        ids = Fa[:, 3].astype(int)
+        own = set(np.nonzero((cz >= z0) & (cz < z1))[0].tolist())
+        assert set(ids[:n_own].tolist()) == own and n_own == len(own)
+        # ghosts: cells in [z0 - g, z0) and [z1, z1 + g), wrapped
+        want = set()
+        for i in range(3000):
+            if i in own:
+                continue
+            for shift in (-Nz, 0, Nz):
+                c = cz[i] + shift
+                if z0 - g <= c < z0 or z1 <= c < z1 + g:
+                    want.add((i, shift))
+        got = set()
+        for k in range(n_own, len(ids)):
+            i = ids[k]
+            shift = int(round((Xa[k, 2] - Xg[i, 2]) / 1.0)) * Nz
+            assert np.array_equal(Xa[k, :2], Xg[i, :2]) and np.array_equal(Fa[k, :3], Fg[i])
+            assert abs(Xa[k, 2] - (Xg[i, 2] + shift / Nz)) < 1e-15
+            got.add((i, shift))
+        assert got == want, (rank, len(got), len(want))
+        assert len(ids) - n_own == len(want)
