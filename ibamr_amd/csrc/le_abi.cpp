@@ -137,6 +137,7 @@ struct ibtk_le_markers_s {
     std::vector<int> off_dev;             // what entry_off holds
     DevBuf pd, entry_off;
     int nbuckets_total = 0, njobs = 0;
+    int kbits = 0;  // class digit bits of the sorted 3-D keys
     bool has_indices = false, has_xshift = false;
     bool cand_valid = false;
     bool dedup_done = false, has_dups = false;
@@ -481,6 +482,9 @@ extern "C" int ibtk_le_markers_order(ibtk_le_markers m, const int** order_dev) {
 // (column, segment), heavy ones cut into sub-segments.  No host sync: the
 // sweeps launch over an upper bound of the item count and read the count on
 // the device.
+#ifndef IBTK_LE_KEY_CLASS_BITS
+#define IBTK_LE_KEY_CLASS_BITS 0  // 4: x mod 16 below the bucket (with static dealing: measured slower)
+#endif
 #ifndef IBTK_LE_SPLIT_TARGET
 #define IBTK_LE_SPLIT_TARGET 12288  // own markers per item above which it is cut (cfg4 items hold ~6.8K)
 #endif
@@ -598,11 +602,14 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     p.X = X_dev;
     p.indices = m->has_indices ? m->indices.as<int>() : nullptr;
     p.Xshift = m->has_xshift ? m->xshift.as<double>() : nullptr;
+    // the class digit below the bucket when the keys have room for it (k_bin_col)
+    p.kbits = cols && (((unsigned long long)cg.nbuckets + 1) << 4) < (1ULL << 32) ? IBTK_LE_KEY_CLASS_BITS : 0;
+    m->kbits = p.kbits;
     if (cols) HIP_TRY(launch_bin_col(kernel, p, n, ctx->keys_in.as<unsigned>(), ctx->vals_in.as<int>(), s));
     else HIP_TRY(launch_bin(geom->ndim, kernel, p, n, ctx->keys_in.as<unsigned>(), ctx->vals_in.as<int>(), s));
     int end_bit = 1;
     if (cols) {
-        while ((1ULL << end_bit) <= (unsigned long long)cg.nbuckets) ++end_bit;
+        while ((1ULL << end_bit) <= ((unsigned long long)cg.nbuckets << p.kbits)) ++end_bit;
     } else {
         end_bit = end_bit_for(bg);
     }
@@ -977,9 +984,11 @@ extern "C" int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch,
     p.X = X_dev;
     p.indices = m->has_indices ? m->indices.as<int>() : nullptr;
     p.Xshift = m->has_xshift ? m->xshift.as<double>() : nullptr;
+    p.kbits = (((unsigned long long)nb + 1) << 4) < (1ULL << 32) ? IBTK_LE_KEY_CLASS_BITS : 0;
+    m->kbits = p.kbits;
     HIP_TRY(launch_bin_col(kernel, p, n, ctx->keys_in.as<unsigned>(), ctx->vals_in.as<int>(), s));
     int end_bit = 1;
-    while ((1ULL << end_bit) <= (unsigned long long)nb) ++end_bit;
+    while ((1ULL << end_bit) <= ((unsigned long long)nb << p.kbits)) ++end_bit;
     size_t tb = 0;
     HIP_TRY(launch_sort(nullptr, tb, ctx->keys_in.as<unsigned>(), m->sorted_key.as<unsigned>(), ctx->vals_in.as<int>(),
                         m->sorted_l.as<int>(), n, end_bit, s));

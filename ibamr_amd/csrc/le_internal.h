@@ -130,6 +130,7 @@ struct Params {
     int npatch;
     const int* entry_off;      // level: list entries of patch q are [entry_off[q], entry_off[q+1])
     int nbuckets_total;        // buckets of every patch (entries keyed >= it are outside)
+    int kbits;                 // 3-D bin keys: class digit bits below the bucket (0 or 4)
     int njobs;                 // (segment, column) pairs of every patch
     int ncut, cut[4];          // item table: extra cuts at these relative planes (the plane window's edges)
     int zmode, zlo, zhi;       // plane window (ibtk_le_ctx_set_plane_window): 0 every item, 1 the items

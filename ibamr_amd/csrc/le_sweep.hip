@@ -96,16 +96,22 @@ __global__ __launch_bounds__(BLOCK) void k_bin_col(Params p, int n, unsigned* ke
 #pragma unroll
     for (int d = 0; d < 3; ++d) Xs[d] = p.X[(int64_t)3 * s + d] + (p.Xshift ? p.Xshift[(int64_t)3 * i + d] : 0.0);
     int ka[3];
-    unsigned key = (unsigned)p.nbuckets_total;
+    // key = bucket, then (p.kbits > 0) the key cell's x mod 16 as the lowest
+    // digit: within a bucket the entries follow their LDS bank class (x mod 16
+    // of a 32-wide ring row), so the spread deals a chunk's candidates over the
+    // ds_add_f64 lane groups by a fixed lane permutation instead of a ranking
+    unsigned key = (unsigned)p.nbuckets_total << p.kbits;
     if (p.pd) {  // a level: the entry's patch, its frame and its range of buckets
         const PatchDesc& P = p.pd[entry_patch(p, i)];
         if (col_key_cell<K>(P.xlo, p.bg.dx, P.ilower, P.cg, Xs, ka)) {
             const int col = (ka[1] / COLY) * P.cg.ncx + ka[0] / COLX;
-            key = (unsigned)(P.bucket_base + (ka[2] * P.cg.ncol + col) * NBAND + key_band<K>(ka[0], ka[1]));
+            const unsigned b = (unsigned)(P.bucket_base + (ka[2] * P.cg.ncol + col) * NBAND + key_band<K>(ka[0], ka[1]));
+            key = (b << p.kbits) | (((unsigned)ka[0] & 15u) >> (4 - p.kbits));
         }
     } else if (col_key_cell<K>(p.bg.xlo, p.bg.dx, p.bg.ilower, p.cg, Xs, ka)) {
         const int col = (ka[1] / COLY) * p.cg.ncx + ka[0] / COLX;
-        key = (unsigned)((ka[2] * p.cg.ncol + col) * NBAND + key_band<K>(ka[0], ka[1]));
+        const unsigned b = (unsigned)((ka[2] * p.cg.ncol + col) * NBAND + key_band<K>(ka[0], ka[1]));
+        key = (b << p.kbits) | (((unsigned)ka[0] & 15u) >> (4 - p.kbits));
     }
     keys[i] = key;
     vals[i] = i;
@@ -126,13 +132,14 @@ constexpr int GATHER_GAP = 32;
 template <int K>
 __global__ __launch_bounds__(BLOCK) void k_gather_col(Params p, int n, int* sorted_s, double* sorted_X,
                                                       const unsigned* skeys, int nbuckets, int* bs) {
+    const int kb = p.kbits;  // the key's class digit below the bucket
     __shared__ double sx[3 * BLOCK];
     const int e0 = blockIdx.x * BLOCK;
     const int e = e0 + threadIdx.x;
     if (e < n) {
         if (e > 0) {
-            const int bi = (int)min(skeys[e], (unsigned)nbuckets);
-            const int bp = (int)min(skeys[e - 1], (unsigned)nbuckets);
+            const int bi = (int)min(skeys[e] >> kb, (unsigned)nbuckets);
+            const int bp = (int)min(skeys[e - 1] >> kb, (unsigned)nbuckets);
             if (bi - bp <= GATHER_GAP)  // longer runs of empty buckets: k_bucket_fix
                 for (int b = bp + 1; b <= bi; ++b) bs[b] = e;
         }
@@ -278,6 +285,28 @@ __device__ __forceinline__ int deal_lanes(int cls) {  // cls in [0, 64); 63 = in
     const int k = __popcll(lt) + __popcll(eq & ((1ull << lane) - 1ull));  // rank
     const int t = (k % G) * (64 / G) + k / G;                              // dealt lane
     return __builtin_amdgcn_ds_permute(t << 2, lane);
+}
+
+// deal_lanes for 16 classes (cls in [0, 16); 16 = inactive): the rank is the
+// count of lanes of a lower class plus the lanes of the same class below this
+// one, from five ballots on 32-bit halves (about half deal_lanes' VALU work).
+template <int G = 4>
+__device__ __forceinline__ int deal_lanes16(int cls) {
+    unsigned elo = ~0u, ehi = ~0u, llo = 0u, lhi = 0u;  // same-class-so-far, lower-class lanes
+#pragma unroll
+    for (int b = 4; b >= 0; --b) {
+        const bool bit = (cls >> b) & 1;
+        const unsigned long long m = __ballot(bit);
+        const unsigned mlo = (unsigned)m, mhi = (unsigned)(m >> 32);
+        const unsigned slo = bit ? mlo : ~mlo, shi = bit ? mhi : ~mhi;
+        llo |= bit ? (elo & ~mlo) : 0u;
+        lhi |= bit ? (ehi & ~mhi) : 0u;
+        elo &= slo;
+        ehi &= shi;
+    }
+    const int k = __popc(llo) + __popc(lhi) + (int)__builtin_amdgcn_mbcnt_hi(ehi, __builtin_amdgcn_mbcnt_lo(elo, 0u));
+    const int t = (k % G) * (64 / G) + k / G;  // dealt lane
+    return __builtin_amdgcn_ds_permute(t << 2, __lane_id());
 }
 
 // value of lane `src` (ds_bpermute on the two halves)
@@ -668,7 +697,7 @@ __global__ __launch_bounds__(BLOCK) void k_interp_outside_col(Params p, int n) {
 // spreading
 // ---------------------------------------------------------------------------
 #ifndef IBTK_LE_SPREAD_DEAL
-#define IBTK_LE_SPREAD_DEAL 1  // 1: rank-dealt lanes by bank class; 0: none; 2: static stride-4
+#define IBTK_LE_SPREAD_DEAL 1  // 1: rank-dealt lanes by bank class; 0: none; 2: static blocks; 3: static stride 4
 #endif
 #ifndef IBTK_LE_SPREAD_ROT
 #define IBTK_LE_SPREAD_ROT 0  // measured 30 % slower on cfg4 (the spread is issue-bound)
@@ -1105,8 +1134,8 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
             return;
         }
 #if IBTK_LE_SPREAD_DEAL == 1
-        const int cls = lane < n ? ((int)floor((mine.X[0] - cd.xlo[0]) * inv_dx + 0.5) & 15) : 63;
-        const int src = deal_lanes<4>(cls);
+        const int cls = lane < n ? ((int)floor((mine.X[0] - cd.xlo[0]) * inv_dx + 0.5) & 15) : 16;
+        const int src = deal_lanes16<4>(cls);
 #elif IBTK_LE_SPREAD_DEAL == 0
         const int src = lane;
         if (true) {
@@ -1114,8 +1143,14 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
                             inv_h3, inv_d, clk);
             return;
         }
+#elif IBTK_LE_SPREAD_DEAL == 2
+        const int src = (lane & 3) * 16 + (lane >> 2);  // static: blocks of 4 staged candidates per lane group
 #else
-        const int src = (lane & 3) * 16 + (lane >> 2);  // static: every 4th staged candidate per lane group
+        // static stride 4: lane group g takes the staged candidates k = g mod 4.
+        // With the bin keys' class digit the candidates of a bucket come in bank
+        // class order, so every 4th one of a range steps the class by about one:
+        // the groups get spread classes without ranking them (DEAL 1's ballots)
+        const int src = 4 * (lane & 15) + (lane >> 4);
 #endif
         Cand d;
 #pragma unroll
@@ -1389,20 +1424,20 @@ template <int K> hipError_t launch_bin_col_t(const Params& p, int n, unsigned* k
 }
 // bucket starts before the first and after the last sorted key; -1 (k_bucket_fix)
 // in between
-__global__ __launch_bounds__(BLOCK) void k_bucket_ends(const unsigned* skeys, int n, int nbuckets, int* bs) {
+__global__ __launch_bounds__(BLOCK) void k_bucket_ends(const unsigned* skeys, int kb, int n, int nbuckets, int* bs) {
     const int b = blockIdx.x * BLOCK + threadIdx.x;
     if (b > nbuckets) return;
-    const int first = (int)min(skeys[0], (unsigned)nbuckets), last = (int)min(skeys[n - 1], (unsigned)nbuckets);
+    const int first = (int)min(skeys[0] >> kb, (unsigned)nbuckets), last = (int)min(skeys[n - 1] >> kb, (unsigned)nbuckets);
     bs[b] = b <= first ? 0 : (b > last ? n : -1);
 }
 // the buckets k_gather_col left (long empty runs): the first entry whose key >= b
-__global__ __launch_bounds__(BLOCK) void k_bucket_fix(const unsigned* skeys, int n, int nbuckets, int* bs) {
+__global__ __launch_bounds__(BLOCK) void k_bucket_fix(const unsigned* skeys, int kb, int n, int nbuckets, int* bs) {
     const int b = blockIdx.x * BLOCK + threadIdx.x;
     if (b > nbuckets || bs[b] >= 0) return;
     int lo = 0, hi = n;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if ((int)min(skeys[mid], (unsigned)nbuckets) < b) lo = mid + 1;
+        if ((int)min(skeys[mid] >> kb, (unsigned)nbuckets) < b) lo = mid + 1;
         else hi = mid;
     }
     bs[b] = lo;
@@ -1412,11 +1447,11 @@ template <int K>
 hipError_t launch_gather_col_t(const Params& p, int n, int* ss, double* sx, const unsigned* skeys, int nbuckets,
                                int* bs, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_bucket_ends, dim3((nbuckets + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, skeys, n, nbuckets,
+    hipLaunchKernelGGL(k_bucket_ends, dim3((nbuckets + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, skeys, p.kbits, n, nbuckets,
                        bs);
     hipLaunchKernelGGL(k_gather_col<K>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, ss, sx, skeys,
                        nbuckets, bs);
-    hipLaunchKernelGGL(k_bucket_fix, dim3((nbuckets + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, skeys, n, nbuckets,
+    hipLaunchKernelGGL(k_bucket_fix, dim3((nbuckets + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, skeys, p.kbits, n, nbuckets,
                        bs);
     return hipGetLastError();
 }

@@ -1,7 +1,10 @@
 #!/bin/bash
 # Round-end measurement of the default build: smoke, the default bench line (with
 # the CPU baseline), rocprofv3 kernel stats of the same workload, and the
-# FETCH_SIZE / WRITE_SIZE traffic passes.  Usage: tools/final_profile.sh <tag>
+# FETCH_SIZE / WRITE_SIZE traffic passes (tools/pmc_traffic.sh).  Copy
+# <out>/pmc/pmc.json to profiles/pmc_cfg4_IB_4_1gpu.json afterwards: bench.py
+# reports it as roofline.traffic while its build hash matches.
+# Usage: tools/final_profile.sh <tag>
 set -o pipefail
 out=gpurun_out/$1; mkdir -p $out
 export TMPDIR=/tmp
