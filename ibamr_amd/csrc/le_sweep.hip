@@ -627,8 +627,8 @@ __global__ __launch_bounds__(SW * IWAVES * ICW) void k_interp_sweep(Params p) {
         if constexpr (IBTK_LE_IDEAL) {
             const int kx = (int)floor((m0.X[0] - cd.xlo[0]) * inv_dx0);
             const int ky = (int)floor((m0.X[1] - cd.xlo[1]) * inv_dx1);
-            const int cls = act ? ((4 * ky + kx) & 15) : 63;
-            const int src = deal_lanes<4>(cls);
+            const int cls = act ? ((4 * ky + kx) & 15) : 16;
+            const int src = deal_lanes16<4>(cls);
             m.X[0] = shfl_f64(m0.X[0], src);
             m.X[1] = shfl_f64(m0.X[1], src);
             m.X[2] = shfl_f64(m0.X[2], src);
