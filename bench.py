@@ -406,7 +406,7 @@ def main():
         return
 
     from ibamr_amd import le
-    from ibamr_amd.slab import GhostMarkers, Slab, SlabExchange, migrate
+    from ibamr_amd.slab import GhostMarkers, Slab, SlabExchange, migrate, update_and_migrate
 
     N = cfg["N"]
     ghost = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
@@ -507,11 +507,14 @@ def main():
         interp_with_fill()
         if record:
             E[1].record()
-        le.position_update(ctx, "euler", dt_move, X, U, out=X)
         if world > 1:
-            X, (F,) = migrate(slab, X, [F], cell_order=False)
+            # fused on the device: update, wrap, owner classes, stable partition;
+            # the leavers to the z-neighbours (slab.update_and_migrate)
+            X, (F,) = update_and_migrate(slab, ctx, "euler", dt_move, X, U, [F])
             if U.shape != X.shape:
                 U = torch.empty_like(X)
+        else:
+            le.position_update(ctx, "euler", dt_move, X, U, out=X)
         bin_step()
         if record:
             E[2].record()

@@ -109,6 +109,9 @@ _SIGS = [
       c_int]),
     ("ibtk_le_position_update", c_int,
      [c_void_p, c_int, ctypes.c_longlong, c_double, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("ibtk_le_slab_update_partition", c_int,
+     [c_void_p, c_int, ctypes.c_longlong, c_double, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+      c_int, c_void_p, c_void_p]),
     ("ibtk_le_zero_ghosts", c_int, [c_void_p, ctypes.POINTER(PatchGeom), c_int, ctypes.POINTER(c_void_p), c_int]),
     ("ibtk_le_mark_stencils", c_int,
      [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_int,

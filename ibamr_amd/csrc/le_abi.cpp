@@ -106,6 +106,7 @@ struct ibtk_le_ctx_s {
     DevBuf err;   // one int
     DevBuf sink;  // 64 doubles (Params::sink)
     DevBuf stamps;  // diagnostic phase clocks (IBTK_LE_STAMPS=1)
+    DevBuf mig_cls, mig_cnt;  // ibtk_le_slab_update_partition scratch
     bool stamps_on = false;  // IBTK_LE_STAMPS=1, read once at ctx_create
     int dbg = 0;             // IBTK_LE_DBG, read once at ctx_create
     SweepTune tune;          // ibtk_le_ctx_tune (diagnostics)
@@ -178,7 +179,7 @@ extern "C" int ibtk_le_ctx_destroy(ibtk_le_ctx ctx) {
     hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->keys_in, &ctx->vals_in, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->fbuf, &ctx->err, &ctx->sink,
                        &ctx->stamps, &ctx->lst_idx, &ctx->lst_xs, &ctx->lst_key, &ctx->lst_perm,
-                       &ctx->lvl_tab, &ctx->zero_tab})
+                       &ctx->lvl_tab, &ctx->zero_tab, &ctx->mig_cls, &ctx->mig_cnt})
         b->release();
     if (ctx->ev0) hipEventDestroy(ctx->ev0);
     if (ctx->ev1) hipEventDestroy(ctx->ev1);
@@ -1353,6 +1354,50 @@ extern "C" int ibtk_le_position_update(ibtk_le_ctx ctx, int scheme, long long n,
         return fail(IBTK_LE_ERR_ARG, "null array");
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(launch_position_update(scheme, (long)n, dt, X_cur_dev, U0_dev, U1_dev, X_new_dev, ctx->stream));
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_slab_update_partition(ibtk_le_ctx ctx, int scheme, long long M, double dt,
+                                             const double* X_cur_dev, const double* U0_dev, const double* U1_dev,
+                                             double* X_new_dev, const double* L, int Nz, int nranks, int rank,
+                                             int* order_dev, int* counts_dev) {
+    if (!ctx) return fail(IBTK_LE_ERR_ARG, "null context");
+    if (scheme < IBTK_LE_EULER || scheme > IBTK_LE_TRAPEZOIDAL) return fail(IBTK_LE_ERR_ARG, "unknown update scheme");
+    if (M < 0 || M >= (1LL << 31)) return fail(IBTK_LE_ERR_ARG, "marker count out of range");
+    if (!L || !(L[0] > 0.0) || !(L[1] > 0.0) || !(L[2] > 0.0)) return fail(IBTK_LE_ERR_ARG, "domain lengths must be positive");
+    if (nranks < 1 || rank < 0 || rank >= nranks || Nz < nranks || Nz % nranks)
+        return fail(IBTK_LE_ERR_ARG, "slabs: %d ranks over %d planes (rank %d)", nranks, Nz, rank);
+    if (!counts_dev) return fail(IBTK_LE_ERR_ARG, "null counts");
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (M == 0) {
+        HIP_TRY(hipMemsetAsync(counts_dev, 0, 4 * sizeof(int), ctx->stream));
+        return IBTK_LE_OK;
+    }
+    if (!X_cur_dev || !U0_dev || !X_new_dev || !order_dev || (scheme == IBTK_LE_TRAPEZOIDAL && !U1_dev))
+        return fail(IBTK_LE_ERR_ARG, "null array");
+    if (X_new_dev == X_cur_dev) return fail(IBTK_LE_ERR_ARG, "X_new must not alias X_cur");
+    SlabMig g;
+    for (int d = 0; d < 3; ++d) g.L[d] = L[d];
+    g.Nz = Nz;
+    g.P = nranks;
+    g.nz = Nz / nranks;
+    g.rank = rank;
+    g.dz = L[2] / Nz;
+    const long nb = (long)((M + BLOCK - 1) / BLOCK);
+    int rc;
+    if ((rc = ctx->mig_cls.ensure((size_t)M))) return rc;
+    if ((rc = ctx->mig_cnt.ensure(sizeof(int) * 8 * (size_t)nb))) return rc;
+    int* bcount = ctx->mig_cnt.as<int>();
+    int* boff = bcount + 4 * nb;
+    size_t tb = 0;
+    HIP_TRY(launch_slab_update_partition(scheme, (long)M, dt, X_cur_dev, U0_dev, U1_dev, X_new_dev, g,
+                                         ctx->mig_cls.as<unsigned char>(), bcount, boff, nullptr, tb, order_dev,
+                                         counts_dev, ctx->stream));
+    if ((rc = ctx->temp.ensure(tb))) return rc;
+    tb = ctx->temp.cap;
+    HIP_TRY(launch_slab_update_partition(scheme, (long)M, dt, X_cur_dev, U0_dev, U1_dev, X_new_dev, g,
+                                         ctx->mig_cls.as<unsigned char>(), bcount, boff, ctx->temp.p, tb, order_dev,
+                                         counts_dev, ctx->stream));
     return IBTK_LE_OK;
 }
 

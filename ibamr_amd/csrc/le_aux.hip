@@ -663,3 +663,106 @@ hipError_t launch_position_update(int scheme, long n, double dt, const double* X
 }
 
 }  // namespace ibtk_le
+
+namespace ibtk_le {
+
+// ---------------------------------------------------------------------------
+// z-slab marker migration fused with the position update (the per-step
+// redistribution SURVEY.md 8(e) asks for; the reference's LDataManager.cpp:
+// 1504-1959 at regrid).  Pass 1 (k_slab_update): X_new = the update of
+// ibtk_le_position_update (same rounding), wrapped into [0, L) per dim exactly as
+// torch.remainder does it (fmod, then + L if negative, then - L if it reached L),
+// the owner of the wrapped z cell (IndexUtilities::getCellIndex, clamped), and
+// the class: 0 stays, 1 to the lower neighbour, 2 to the upper, 3 further; the
+// class counts per block.  Pass 2 (k_slab_partition), after an exclusive scan of
+// the class-major block counts: a stable partition of the marker indices,
+// [stay | down | up | far], each in input order.  Deterministic, no host sync.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double wrap_like_torch(double x, double L) {
+    double r = fmod(x, L);
+    if (r != 0.0 && r < 0.0) r = r + L;
+    if (r >= L) r = r - L;
+    return r;
+}
+
+template <int SCHEME>
+__global__ __launch_bounds__(BLOCK) void k_slab_update(long M, double dt, const double* X, const double* U0,
+                                                       const double* U1, double* Xn, SlabMig g, unsigned char* cls,
+                                                       int* bcount, int nb) {
+    __shared__ int cnt[4];
+    if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const long i = (long)blockIdx.x * BLOCK + threadIdx.x;
+    int c = -1;
+    if (i < M) {
+        double w[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const long k = 3 * i + d;
+            double x;
+            if constexpr (SCHEME == 2) {
+                const double h = 0.5 * dt;
+                x = (h * U0[k] + X[k]) + h * U1[k];
+            } else {
+                x = dt * U0[k] + X[k];
+            }
+            w[d] = wrap_like_torch(x, g.L[d]);
+            Xn[k] = w[d];
+        }
+        const long cz = min(max((long)floor(w[2] / g.dz), 0L), (long)g.Nz - 1);
+        const int owner = (int)(cz / g.nz);
+        const int down = (g.rank - 1 + g.P) % g.P, up = (g.rank + 1) % g.P;
+        c = owner == g.rank ? 0 : (owner == down ? 1 : (owner == up ? 2 : 3));
+        cls[i] = (unsigned char)c;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const unsigned long long b = __ballot(c == k);
+        if ((threadIdx.x & 63) == 0 && b) atomicAdd(&cnt[k], __popcll(b));
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) bcount[threadIdx.x * nb + blockIdx.x] = cnt[threadIdx.x];
+}
+
+__global__ __launch_bounds__(BLOCK) void k_slab_partition(long M, const unsigned char* cls, const int* bcount,
+                                                          const int* boff, int nb, int* order, int* counts) {
+    __shared__ int wcnt[BLOCK / 64][4];
+    const long i = (long)blockIdx.x * BLOCK + threadIdx.x;
+    const int c = i < M ? (int)cls[i] : -1;
+    const int w = threadIdx.x >> 6;
+    int rank = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const unsigned long long b = __ballot(c == k);
+        if (c == k) rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b, 0u));
+        if ((threadIdx.x & 63) == 0) wcnt[w][k] = __popcll(b);
+    }
+    __syncthreads();
+    if (c >= 0) {
+        int before = 0;
+        for (int v = 0; v < w; ++v) before += wcnt[v][c];
+        order[boff[c * nb + blockIdx.x] + before + rank] = (int)i;
+    }
+    if (blockIdx.x == nb - 1 && threadIdx.x < 4) {
+        const int k = threadIdx.x;
+        counts[k] = boff[k * nb + nb - 1] + bcount[k * nb + nb - 1] - boff[k * nb];
+    }
+}
+
+hipError_t launch_slab_update_partition(int scheme, long M, double dt, const double* X, const double* U0,
+                                        const double* U1, double* Xn, const SlabMig& g, unsigned char* cls,
+                                        int* bcount, int* boff, void* temp, size_t& temp_bytes, int* order,
+                                        int* counts, hipStream_t s) {
+    const int nb = (int)((M + BLOCK - 1) / BLOCK);
+    if (!temp) return launch_scan(nullptr, temp_bytes, bcount, boff, 4 * nb, s);  // size query
+    if (scheme == 2)
+        hipLaunchKernelGGL(k_slab_update<2>, dim3(nb), dim3(BLOCK), 0, s, M, dt, X, U0, U1, Xn, g, cls, bcount, nb);
+    else
+        hipLaunchKernelGGL(k_slab_update<0>, dim3(nb), dim3(BLOCK), 0, s, M, dt, X, U0, U1, Xn, g, cls, bcount, nb);
+    hipError_t e = launch_scan(temp, temp_bytes, bcount, boff, 4 * nb, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_slab_partition, dim3(nb), dim3(BLOCK), 0, s, M, cls, bcount, boff, nb, order, counts);
+    return hipGetLastError();
+}
+
+}  // namespace ibtk_le

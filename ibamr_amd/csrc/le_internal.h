@@ -186,6 +186,16 @@ hipError_t launch_scan(void* temp, size_t& temp_bytes, const int* in, int* out, 
 
 // 3-D column sweep (le_sweep.hip)
 hipError_t launch_bin_col(int kernel, const Params& p, int n, unsigned* keys, int* vals, hipStream_t s);
+// z-slab migration classes (le_aux.hip)
+struct SlabMig {
+    double L[3];
+    double dz;
+    int Nz, nz, P, rank;
+};
+hipError_t launch_slab_update_partition(int scheme, long M, double dt, const double* X, const double* U0,
+                                        const double* U1, double* Xn, const SlabMig& g, unsigned char* cls,
+                                        int* bcount, int* boff, void* temp, size_t& temp_bytes, int* order,
+                                        int* counts, hipStream_t s);
 hipError_t launch_position_update(int scheme, long n, double dt, const double* X, const double* U0, const double* U1,
                                   double* Xn, hipStream_t s);
 hipError_t launch_gather_col(int kernel, const Params& p, int n, int* sorted_s, double* sorted_X,

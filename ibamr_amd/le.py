@@ -494,6 +494,28 @@ def position_update(ctx: Context, scheme: str, dt: float, X: torch.Tensor, U0: t
     return out
 
 
+def slab_update_partition(ctx: Context, scheme: str, dt: float, X: torch.Tensor, U0: torch.Tensor, L, Nz: int,
+                          nranks: int, rank: int, U1: Optional[torch.Tensor] = None):
+    """Position update fused with the z-slab migration classes (ibtk_le_slab_update_partition):
+    (X_new wrapped into [0, L), order int32 [stay | to rank-1 | to rank+1 | further], counts
+    int32 device tensor of 4)."""
+    if scheme not in UPDATE_SCHEMES:
+        raise ValueError(f"unknown scheme {scheme!r}")
+    for t in [X, U0] + ([U1] if scheme == "trapezoidal" else []):
+        if t is None or t.dtype != torch.float64 or t.shape != X.shape or X.dim() != 2 or X.shape[1] != 3:
+            raise ValueError("X, U0, U1: (M, 3) float64 of one shape")
+    M = X.shape[0]
+    Xn = torch.empty_like(X)
+    order = torch.empty(max(M, 1), dtype=torch.int32, device=X.device)
+    counts = torch.zeros(4, dtype=torch.int32, device=X.device)
+    Ld = (ctypes.c_double * 3)(*[float(v) for v in L])
+    check(ctx.lib.ibtk_le_slab_update_partition(ctx.h, UPDATE_SCHEMES[scheme], M, float(dt), _ptr(X), _ptr(U0),
+                                                _ptr(U1) if scheme == "trapezoidal" else None, _ptr(Xn),
+                                                ctypes.cast(Ld, ctypes.c_void_p), int(Nz), int(nranks), int(rank),
+                                                _ptr(order), _ptr(counts)))
+    return Xn, order[:M], counts
+
+
 def index_set_list(ctx: Context, geom: Geometry, X: torch.Tensor, ghost: int, lag: Optional[torch.Tensor] = None,
                    periodic=None, which: str = "all"):
     """LIndexSetData::cacheLocalIndices' lists on the device (ibtk_le_index_set_list):

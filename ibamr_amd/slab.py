@@ -323,6 +323,60 @@ class GhostMarkers:
         return Xa, Fa, X.shape[0]
 
 
+def update_and_migrate(slab: Slab, ctx, scheme: str, dt: float, X: torch.Tensor, U0: torch.Tensor,
+                       fields: Sequence[torch.Tensor] = (), U1: Optional[torch.Tensor] = None, group=None):
+    """Position update and migration on the device (IBMethod's eulerStep/midpointStep/
+    trapezoidalStep, IBMethod.cpp:619-681, then the redistribution of
+    LDataManager.cpp:1504-1959 each step).
+
+    One fused HIP pass updates, wraps and classifies the markers and partitions them
+    stably (ibtk_le_slab_update_partition: [stay | down | up | further]); the leavers go
+    to the z-neighbours with two point-to-point messages each way (the counts, then the
+    rows).  A step moves markers by less than a slab, so "further" is empty; if a rank
+    finds it is not, every rank takes the all-to-all path of ``migrate`` (one max-reduce
+    of the flag decides, together with the counts).  The host syncs once, for the count
+    vector the receive buffers need.  Returns (X, fields): the stayers in their order,
+    then the arrivals from below, then from above (``migrate(cell_order=False)``'s
+    contract with a neighbour order)."""
+    import torch.distributed as dist
+    from . import le
+    M = X.shape[0]
+    Xn, order, counts = le.slab_update_partition(ctx, scheme, dt, X, U0, slab.L, slab.N[2], slab.P, slab.rank,
+                                                 U1=U1)
+    flat = [f.reshape(M, -1) for f in fields]
+    if slab.P == 1:
+        return Xn, list(fields)  # everything stays; the order is the input order
+    # counts to the neighbours and the global "further" flag
+    send_c = torch.stack([counts[1], counts[2]]).to(torch.int64)
+    far = counts[3:4].to(torch.int64).clone()
+    rc_down, rc_up = torch.empty(1, dtype=torch.int64, device=X.device), torch.empty(1, dtype=torch.int64,
+                                                                                    device=X.device)
+    gm = GhostMarkers(slab, group)
+    gm._p2p([(send_c[1:2], slab.up), (send_c[0:1], slab.down)], [(rc_down, slab.down), (rc_up, slab.up)])
+    dist.all_reduce(far, op=dist.ReduceOp.MAX, group=group)
+    host = torch.cat([counts.to(torch.int64), rc_down, rc_up, far]).cpu().tolist()  # the one host sync
+    n_stay, n_down, n_up, _, r_down, r_up, any_far = host
+    if any_far:
+        return migrate(slab, Xn, list(fields), group=group, cell_order=False)
+    data = torch.cat([Xn] + [f.to(Xn.dtype) for f in flat], dim=1)
+    stay = data[order[:n_stay].long()]
+    to_down = data[order[n_stay:n_stay + n_down].long()].contiguous()
+    to_up = data[order[n_stay + n_down:n_stay + n_down + n_up].long()].contiguous()
+    D = data.shape[1]
+    from_down = torch.empty((r_down, D), dtype=data.dtype, device=data.device)
+    from_up = torch.empty((r_up, D), dtype=data.dtype, device=data.device)
+    # each peer's receives in the order it sends (P = 2: up == down)
+    gm._p2p([(to_up, slab.up), (to_down, slab.down)], [(from_down, slab.down), (from_up, slab.up)])
+    allm = torch.cat([stay, from_down, from_up], dim=0)
+    Xo = allm[:, :3].contiguous()
+    outs, k = [], 3
+    for f, fl in zip(fields, flat):
+        w = fl.shape[1]
+        outs.append(allm[:, k:k + w].reshape((allm.shape[0],) + tuple(f.shape[1:])).to(f.dtype).contiguous())
+        k += w
+    return Xo, outs
+
+
 def migrate(slab: Slab, X: torch.Tensor, fields: Sequence[torch.Tensor] = (), group=None, cell_order: bool = True):
     """Move every marker to the rank whose slab holds its cell, after a position update.
 

@@ -306,6 +306,20 @@ enum { IBTK_LE_EULER = 0, IBTK_LE_MIDPOINT = 1, IBTK_LE_TRAPEZOIDAL = 2 };
 int ibtk_le_position_update(ibtk_le_ctx ctx, int scheme, long long n, double dt, const double* X_cur_dev,
                             const double* U0_dev, const double* U1_dev, double* X_new_dev);
 
+/* Position update fused with the z-slab migration classes (bench.py --move, ibamr_amd.slab.
+ * migrate_device): X_new = the ibtk_le_position_update of (X_cur, U0, U1), wrapped
+ * into [0, L) per dim as torch.remainder does; the markers' owners are the slabs of
+ * their wrapped z cells (IndexUtilities::getCellIndex, LDataManager.cpp:1446; Nz
+ * planes, nranks equal slabs).  order_dev (M ints) receives a stable partition of
+ * the marker indices [staying | to rank-1 | to rank+1 | further], each part in
+ * input order; counts_dev (4 ints, device) the part sizes.  Stream-ordered, no
+ * host sync (the redistribution LDataManager.cpp:1504-1959 runs at regrid; SURVEY.md
+ * 8(e) asks for it after every update).  X_new must not alias X_cur.  With two
+ * ranks both neighbours are one rank: every leaver is in the second part. */
+int ibtk_le_slab_update_partition(ibtk_le_ctx ctx, int scheme, long long M, double dt, const double* X_cur_dev,
+                                  const double* U0_dev, const double* U1_dev, double* X_new_dev, const double* L,
+                                  int Nz, int nranks, int rank, int* order_dev, int* counts_dev);
+
 /* Diagnostics: masks_dev[c] (one byte per point of component c's ghosted array,
  * same layout) gets 1 at every point some listed stencil touches after clipping.
  * bench.py sums the masks for the exact algorithmic byte count |S_a|. */

@@ -415,3 +415,79 @@ def test_cfg4_slab_split_matches_one_rank(le, ctx, world, move, mode):
     for rank, _, ids, U, fin, z0, nz in sorted(res, key=lambda r: r[0]):
         for c in range(3):
             assert rel_err(fin[c], ref_f[c][z0:z0 + nz]) <= SPREAD_TOL, f"rank {rank} comp {c}"
+
+
+# ---------------------------------------------------------------------------- device migration
+def _mig_worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from ibamr_amd import le
+        from ibamr_amd.slab import Slab, migrate, update_and_migrate
+        ctx = le.Context(0)
+        N = 48
+        slab = Slab([N, N, N], world, rank, 3)
+        rng = np.random.default_rng(100 + rank)
+        M = 20000
+        X = rng.uniform(0, 1, (M, 3))
+        X[:, 2] = (slab.z0 + rng.uniform(0, slab.nz, M)) * slab.dx[2]
+        # velocities that carry ~10 % of the markers across a slab face, some across the periodic wrap
+        U = rng.uniform(-1, 1, (M, 3))
+        ids = (rank * M + np.arange(M)).astype(np.float64)
+        F = rng.standard_normal((M, 3))
+        Xd, Ud = torch.from_numpy(X).cuda(), torch.from_numpy(U).cuda()
+        f = [torch.from_numpy(F).cuda(), torch.from_numpy(ids).cuda()]
+        dt = 1.5 * slab.dx[2]
+        # reference: the update, then the torch all-to-all migration
+        Xa = le.position_update(ctx, "euler", dt, Xd, Ud)
+        Xa, fa = migrate(slab, Xa, f, cell_order=False)
+        # device: fused update + classes + neighbour exchange
+        Xb, fb = update_and_migrate(slab, ctx, "euler", dt, Xd, Ud, f)
+        Xb2, fb2 = update_and_migrate(slab, ctx, "euler", dt, Xd, Ud, f)
+        ctx.synchronize()
+        same_repeat = torch.equal(Xb, Xb2) and all(torch.equal(a, b) for a, b in zip(fb, fb2))
+        oa = torch.argsort(fa[1]); ob = torch.argsort(fb[1])
+        ok = (torch.equal(fa[1][oa], fb[1][ob]) and torch.equal(Xa[oa], Xb[ob]) and torch.equal(fa[0][oa], fb[0][ob]))
+        # every marker is on the owner of its wrapped cell
+        cz = torch.clamp((Xb[:, 2] / slab.dx[2]).floor().long(), 0, N - 1)
+        owned = bool(((cz >= slab.z0) & (cz < slab.z1)).all())
+        inbox = bool(((Xb >= 0) & (Xb < 1)).all())
+        out_q.put((rank, "ok", ok, same_repeat, owned, inbox, int(Xb.shape[0])))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        out_q.put((rank, traceback.format_exc(), False, False, False, False, 0))
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_device_update_and_migrate(le, world):
+    """slab.update_and_migrate (ibtk_le_slab_update_partition + neighbour exchange) moves
+    the same markers with the same bits as the position update plus migrate(), leaves
+    every marker on the owner of its wrapped cell, and is deterministic."""
+    import torch.multiprocessing as mp
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_mig_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = []
+    for _ in range(world):
+        try:
+            res.append(q.get(timeout=240))
+        except Exception:
+            res.append((-1, "worker died: " + str([p.exitcode for p in procs]), False, False, False, False, 0))
+            break
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    bad = [r for r in res if r[1] != "ok"]
+    assert not bad, bad[0][1]
+    for rank, _, ok, rep, owned, inbox, n in res:
+        assert ok and rep and owned and inbox, (rank, ok, rep, owned, inbox)
+    assert sum(r[6] for r in res) == 20000 * world
