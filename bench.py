@@ -353,6 +353,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-rebin", action="store_true", help="bin once outside the timed loop")
+    ap.add_argument("--solo-slab", type=int, default=0, metavar="S",
+                    help="projection aid (one GPU, not a scaling measurement): run rank 0's slab of an S-way z "
+                         "split alone, its z ghosts wrapped locally instead of exchanged")
     ap.add_argument("--spread-mode", default="sum", choices=["sum", "markers"],
                     help="N > 1: z ghost-region sum of the grid (sum) or the reference's ghost markers (markers)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
@@ -411,6 +414,16 @@ def main():
     N = cfg["N"]
     ghost = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
     slab = Slab([N, N, N], world, rank, ghost, align=16 if args.layout == "aligned" else 0)
+    xslab = slab  # the slab the exchanges see
+    if args.solo_slab > 1:
+        if world > 1:
+            raise SystemExit("--solo-slab runs on one rank")
+        S = args.solo_slab
+        slab = Slab([N, N, N], S, 0, ghost, align=16 if args.layout == "aligned" else 0)
+        # the same planes, periodic in z on their own: the local fill / fold stand in for
+        # the exchange (same arrays, same passes); the RCCL transfers are not modelled
+        xslab = Slab([N, N, N // S], 1, 0, ghost, L=(1.0, 1.0, 1.0 / S),
+                     align=16 if args.layout == "aligned" else 0)
     geom = slab.geometry()
     ctx = le.Context(local_dev)
     for kv in args.tune:
@@ -432,8 +445,8 @@ def main():
     for a in u:
         a.uniform_(-1.0, 1.0, generator=gen)
     f = geom.alloc("side", device=dev)
-    ex_u = SlabExchange(slab, u, ctx)
-    ex_f = SlabExchange(slab, f, ctx)
+    ex_u = SlabExchange(xslab, u, ctx)
+    ex_f = SlabExchange(xslab, f, ctx)
     if not args.no_overlap:
         ex_u.cut_items()  # sweep items cut at the slab faces (N > 1)
     bins = le.Markers(ctx)
@@ -650,6 +663,7 @@ def main():
         "data": "synthetic",
         "config": {"workload": cfg["desc"], "kernel": kernel, "grid": [N, N, N], "markers": M_total,
                    "parallelism": f"z-slab x{world}", "ghost": ghost, "marker_order": args.marker_order, "layout": args.layout, "spread_mode": args.spread_mode if world > 1 else "one rank",
+                   "solo_slab": args.solo_slab or None,
                    "move": args.move, "overlap": world > 1 and not args.no_overlap,
                    "step": ("ghost fill + interp(3 comps) + position update + migrate + bin + zero ghosts + "
                             "spread(3 comps) + ghost sum" if args.move else
@@ -663,6 +677,10 @@ def main():
         "breakdown_ms": {k: mean(v) for k, v in acc.items()},
         "touched_points": S_touched,
     }
+    if args.solo_slab > 1:  # a projection aid, never the metric
+        out["projection"] = {"slabs": args.solo_slab, "per_rank_value": value,
+                             "value_if_exchanges_hidden": value * args.solo_slab,
+                             "note": "rank 0's slab alone on one GPU, z ghosts wrapped locally; RCCL not modelled"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -699,6 +699,9 @@ __global__ __launch_bounds__(BLOCK) void k_interp_outside_col(Params p, int n) {
 #ifndef IBTK_LE_SPREAD_DEAL
 #define IBTK_LE_SPREAD_DEAL 1  // 1: rank-dealt lanes by bank class; 0: none; 2: static blocks; 3: static stride 4
 #endif
+#ifndef IBTK_LE_SPREAD_EARLY
+#define IBTK_LE_SPREAD_EARLY 0
+#endif
 #ifndef IBTK_LE_SPREAD_ROT
 #define IBTK_LE_SPREAD_ROT 0  // measured 30 % slower on cfg4 (the spread is issue-bound)
 #endif
@@ -1224,6 +1227,11 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         const int nmid = (tCur - h) / SW;       // full middle chunks
         const int r_a = (tCur - h) % SW;        // carried into a+1
         clk.lap(1);
+#if IBTK_LE_SPREAD_EARLY
+        // the adds of chunk 1 first: they drain through the LDS while the prefetch
+        // below computes (the next writeback waits for them)
+        if (cur_n > 0) process(a, cur_r, cur_n, cur);
+#endif
         // prefetch for a+1: its ranges, its chunk 1, plane a+HI+1, the rows of a+2
         if (a + 1 <= alast) {
             make_ranges_lanes(rowv, rg);
@@ -1237,7 +1245,9 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
             plane_load(a + HI + 1, pv);
             if (a + 2 <= alast) rows_load(a + 2, rowv);
         }
+#if !IBTK_LE_SPREAD_EARLY
         if (cur_n > 0) process(a, cur_r, cur_n, cur);
+#endif
         if (nmid > 0) {  // dense planes: the full middle chunks (ranges of a rebuilt)
             int rowm[3];
             rows_load(a, rowm);
@@ -1277,9 +1287,19 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
 #ifndef IBTK_LE_SEG_ITEMS
 #define IBTK_LE_SEG_ITEMS 16384
 #endif
+// Segments shorter than MIN_SEG planes are not cut: a segment re-reads HI - LO
+// planes of z halo (interp) or anchors (spread), so a thin z-slab (8 GPUs: 139
+// planes) keeps two segments of ~70 planes rather than five of 32 -- measured
+// on rank 0's slab of an 8-way cfg4 split, 6.2 -> 5.5 ms per step
+// (bench.py --solo-slab 8, profiles/r02v).
+constexpr int MIN_SEG = 64;
 void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items) {
     long long want = seg_items > 0 ? seg_items : IBTK_LE_SEG_ITEMS;
     long long s = ((long long)cg.nz * cg.ncol + want - 1) / want;
+    if (s < MIN_SEG && seg_items <= 0) {
+        const long long ns = cg.nz / MIN_SEG > 1 ? cg.nz / MIN_SEG : 1;  // equal segments of >= MIN_SEG planes
+        s = (cg.nz + ns - 1) / ns;
+    }
     if (s < 32) s = 32;
     if (s > cg.nz) s = cg.nz;
     if (s < 1) s = 1;
