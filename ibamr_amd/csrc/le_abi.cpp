@@ -224,6 +224,7 @@ extern "C" int ibtk_le_ctx_tune(ibtk_le_ctx ctx, const char* key, int value) {
     if (k == "seg_items") t.seg_items = value;
     else if (k == "split_target") t.split_target = value;
     else if (k == "heavy") t.heavy = value;
+    else if (k == "strip") t.strip = value;
     else return fail(IBTK_LE_ERR_ARG, "unknown tuning key %s", key);
     return IBTK_LE_OK;
 }
@@ -483,6 +484,9 @@ extern "C" int ibtk_le_markers_order(ibtk_le_markers m, const int** order_dev) {
 // (column, segment), heavy ones cut into sub-segments.  No host sync: the
 // sweeps launch over an upper bound of the item count and read the count on
 // the device.
+#ifndef IBTK_LE_STRIP
+#define IBTK_LE_STRIP 1  // column rows per strip of the sweep item order (job_column)
+#endif
 #ifndef IBTK_LE_KEY_CLASS_BITS
 #define IBTK_LE_KEY_CLASS_BITS 0  // 4: x mod 16 below the bucket (with static dealing: measured slower)
 #endif
@@ -518,6 +522,7 @@ static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel) {
     p.S = m->S;
     p.nseg = m->nseg;
     p.njobs = nj;
+    p.strip = ctx->tune.strip > 0 ? ctx->tune.strip : IBTK_LE_STRIP;
     p.plane_start = m->plane_start.as<int>();
     if (m->npatch) {
         p.pd = m->pd.as<PatchDesc>();

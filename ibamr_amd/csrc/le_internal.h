@@ -103,6 +103,7 @@ struct SweepTune {
     int seg_items = 0;     // sweep_segments' item target
     int split_target = 0;  // own markers above which a (column, segment) is cut (k_item_counts)
     int heavy = 0;         // own markers per piece above which an item is scheduled first (-1: never)
+    int strip = 0;         // column rows per strip of the item order (0: default)
 };
 // One 3-D sweep item: a patch, a column and its owned planes [p0, p1) (relative
 // to the patch's cg.org[2]).
@@ -132,6 +133,7 @@ struct Params {
     int nbuckets_total;        // buckets of every patch (entries keyed >= it are outside)
     int kbits;                 // 3-D bin keys: class digit bits below the bucket (0 or 4)
     int njobs;                 // (segment, column) pairs of every patch
+    int strip;                 // item order: column rows per strip (job_column)
     int ncut, cut[4];          // item table: extra cuts at these relative planes (the plane window's edges)
     int zmode, zlo, zhi;       // plane window (ibtk_le_ctx_set_plane_window): 0 every item, 1 the items
                                // whose planes lie in [zlo, zhi], 2 the others

@@ -887,7 +887,8 @@ __device__ __forceinline__ void spread_lanes_rows(const Params& p, const CompDes
 template <int K>
 __device__ __forceinline__ void spread_lanes_flat(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
                                                   bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
-                                                  int yhi, int plo, int phi, double inv_h3, const double* inv_d) {
+                                                  int yhi, int plo, int phi, double inv_h3, const double* inv_d,
+                                                  Clk& clk) {
     using S = SSh<K>;
     constexpr int W = S::W, FAM = S::FAM, NSL = S::NSL;
     St<W> st[3];
@@ -918,6 +919,7 @@ __device__ __forceinline__ void spread_lanes_flat(const Params& p, const CompDes
     }
     char* const base = reinterpret_cast<char*>(ring) + 8 * ox;
     int sl = (int)((unsigned)(a + oz + 64 * NSL) % (unsigned)NSL);  // ring slot of plane i2 = 0
+    clk.lap(2);
 #pragma unroll
     for (int i2 = 0; i2 < W; ++i2) {
         char* const plane = base + sl * (8 * S::SLOT);
@@ -934,6 +936,7 @@ __device__ __forceinline__ void spread_lanes_flat(const Params& p, const CompDes
                 __hip_atomic_fetch_add(row + i0, w0v[i0] * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
+    clk.lap(3);
 }
 
 template <int K>
@@ -941,7 +944,7 @@ __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd
                                              bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
                                              int yhi, int plo, int phi, double inv_h3, const double* inv_d, Clk& clk) {
     if constexpr (IBTK_LE_SPREAD_FLAT)
-        spread_lanes_flat<K>(p, cd, ring, cdat, act, a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi, inv_h3, inv_d);
+        spread_lanes_flat<K>(p, cd, ring, cdat, act, a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi, inv_h3, inv_d, clk);
     else
         spread_lanes_rows<K>(p, cd, ring, cdat, act, a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi, inv_h3, inv_d, clk);
 }
@@ -1347,6 +1350,19 @@ __device__ __forceinline__ void job_patch(const Params& p, int j, int& q, ColGeo
     bs = p.plane_start + P.bucket_base;
 }
 
+// The column of the i-th job of a segment: rows of columns in strips of `strip`
+// (>= 1) column rows, x-major within a strip, so that the jobs that run together
+// on an XCD include y-neighbours as well as x-neighbours (their shared halo rows
+// and candidate ranges then come from L2); strip 1 is plain row-major order.
+__device__ __forceinline__ int job_column(const ColGeom& cg, int i, int strip) {
+    if (strip <= 1) return i;
+    const int band = strip * cg.ncx;            // jobs per full strip
+    const int sb = i / band, w = i - sb * band;
+    const int rows = min(strip, cg.ncy - sb * strip);  // the last strip may be shorter
+    const int cx = w / rows, cy = sb * strip + (w - cx * rows);
+    return cy * cg.ncx + cx;
+}
+
 // load-based sub-segments of (column col, planes [a0, a1))
 template <int K>
 __device__ __forceinline__ int load_split(const ColGeom& cg, const int* bs, int col, int a0, int a1, int target,
@@ -1375,7 +1391,7 @@ __global__ __launch_bounds__(BLOCK) void k_item_counts(Params p, int target, int
     const int* bs;
     job_patch(p, j, q, cg, S, nseg, j0, bs);
     const int jl = j - j0;
-    const int seg = jl / cg.ncol, col = jl - seg * cg.ncol;
+    const int seg = jl / cg.ncol, col = job_column(cg, jl - seg * cg.ncol, p.strip);
     const int a0 = seg * S, a1 = min(a0 + S, cg.nz), len = a1 - a0;
     long load;
     const int n = load_split<K>(cg, bs, col, a0, a1, target, load);
@@ -1396,7 +1412,7 @@ __global__ __launch_bounds__(BLOCK) void k_item_write(Params p, int target, int 
     const int* bs;
     job_patch(p, j, q, cg, S, nseg, j0, bs);
     const int jl = j - j0;
-    const int seg = jl / cg.ncol, col = jl - seg * cg.ncol;
+    const int seg = jl / cg.ncol, col = job_column(cg, jl - seg * cg.ncol, p.strip);
     const int a0 = seg * S, a1 = min(a0 + S, cg.nz), len = a1 - a0;
     long load;
     const int n = load_split<K>(cg, bs, col, a0, a1, target, load);
