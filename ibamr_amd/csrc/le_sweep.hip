@@ -335,6 +335,9 @@ constexpr int IWAVES = IBTK_LE_IWAVES;  // waves per interp work item (one LDS r
 #ifndef IBTK_LE_IBLOCK
 #define IBTK_LE_IBLOCK 1  // interp: read blocks of stencil rows before summing them
 #endif
+#ifndef IBTK_LE_IPF
+#define IBTK_LE_IPF 1  // interp: plane prefetch depth in groups (1 or 2)
+#endif
 #ifndef IBTK_LE_INTERP_EXACT
 #define IBTK_LE_INTERP_EXACT 1
 #endif
@@ -399,7 +402,9 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
             // to back before the block is summed, so one LDS latency is exposed
             // per block rather than one per pair of reads (the sum itself stays
             // the Fortran's sequential chain).
-            constexpr int R = !IBTK_LE_IBLOCK ? 1 : (W <= 4 ? W : (W <= 6 ? 3 : 2));  // rows per block; divides W
+            constexpr int R = !IBTK_LE_IBLOCK ? 1
+                            : IBTK_LE_IBLOCK == 2 ? (W % 2 == 0 ? 2 : 1)
+                                                  : (W <= 4 ? W : (W <= 6 ? 3 : 2));  // rows per block; divides W
 #pragma unroll
             for (int i2 = 0; i2 < W; ++i2) {
                 const double* pl = base + islot<K>(oz + i2) * PV;
@@ -483,8 +488,13 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
 // barriers are the workgroup's), so they read the item's markers from L1/L2
 // once and their 8-byte Q stores to one AoS record land in L2 together (one
 // 24-byte record write-back instead of three partial-line ones).
+#ifdef IBTK_LE_IVGPR
+#define IBTK_LE_IVGPR_ATTR __attribute__((amdgpu_waves_per_eu(IBTK_LE_IVGPR)))
+#else
+#define IBTK_LE_IVGPR_ATTR
+#endif
 template <int K, bool LVL, int ICW>
-__global__ __launch_bounds__(SW * IWAVES * ICW) void k_interp_sweep(Params p) {
+__global__ __launch_bounds__(SW * IWAVES * ICW) IBTK_LE_IVGPR_ATTR void k_interp_sweep(Params p) {
     using S = ISh<K>;
     constexpr int LO = S::LO, HI = S::HI, RX = S::RX, NPT = S::NPT;
     __shared__ double ring_all[ICW * S::NSL * S::PVP];
@@ -648,6 +658,8 @@ __global__ __launch_bounds__(SW * IWAVES * ICW) void k_interp_sweep(Params p) {
         plane_put(z, pv);
     }
     plane_load(a0 + w + HI, pv);
+    double pv2[IBTK_LE_IPF >= 2 ? NPT : 1];
+    if constexpr (IBTK_LE_IPF >= 2) plane_load(a0 + w + IWAVES + HI, pv2);
     GSpan gs;
     gspan_get(a0, gspan_load(a0), gs);
     Mk nxt;
@@ -667,7 +679,13 @@ __global__ __launch_bounds__(SW * IWAVES * ICW) void k_interp_sweep(Params p) {
         gspan_get(a + IWAVES, vsp1, gs);
         chunk_load(gs, a + IWAVES, w, nxt, anx);
         vsp1 = gspan_load(a + 2 * IWAVES);
-        plane_load(my + IWAVES + HI, pv);
+        if constexpr (IBTK_LE_IPF >= 2) {  // planes two groups ahead
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) pv[k] = pv2[k];
+            plane_load(my + 2 * IWAVES + HI, pv2);
+        } else {
+            plane_load(my + IWAVES + HI, pv);
+        }
         const int tot = gc.pre[IWAVES];
         if (SW * w < tot) {
             // dense groups: the wave's next chunk loads while this one is summed
@@ -1284,11 +1302,19 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
 // ---------------------------------------------------------------------------
 // Segment length: about IBTK_LE_SEG_ITEMS (column, segment) items over the
 // patch, but no segment shorter than 32 planes (the z halo of a segment is HI-LO
-// planes).  16384 is measured (cfg4: S = 141, 8 segments): both sweeps ran
-// 10-12 % faster than at 8192 (S = 281); 4096, 12288, 17952, 20480, 24576 and
-// 32768 were all slower than 16384.
+// planes), and the patch's planes cut into segments of equal length (+-1).
+// Equal lengths matter more than the length: sweep_item gives each XCD an equal
+// share of the items, contiguous in (segment, column) order, so a short last
+// segment leaves the last XCD idle while the others carry its planes -- cfg4 at
+// S = 128 (8 x 128 + 11 planes) and S = 141 (7 x 141 + 48) ran the sweeps 9-11 %
+// slower than at S = 149 (6 x 149 + 141), the round-1 "narrow optimum"
+// (profiles/r02seg).  With equal segments the count hardly matters (5-14
+// segments within a few per cent, profiles/r02seg2).
 #ifndef IBTK_LE_SEG_ITEMS
 #define IBTK_LE_SEG_ITEMS 16384
+#endif
+#ifndef IBTK_LE_SEG_EQUAL
+#define IBTK_LE_SEG_EQUAL 1  // 0: segments of the target length and a shorter last one (round 1)
 #endif
 // Segments shorter than MIN_SEG planes are not cut: a segment re-reads HI - LO
 // planes of z halo (interp) or anchors (spread), so a thin z-slab (8 GPUs: 139
@@ -1300,12 +1326,16 @@ void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items) {
     long long want = seg_items > 0 ? seg_items : IBTK_LE_SEG_ITEMS;
     long long s = ((long long)cg.nz * cg.ncol + want - 1) / want;
     if (s < MIN_SEG && seg_items <= 0) {
-        const long long ns = cg.nz / MIN_SEG > 1 ? cg.nz / MIN_SEG : 1;  // equal segments of >= MIN_SEG planes
+        const long long ns = cg.nz / MIN_SEG > 1 ? cg.nz / MIN_SEG : 1;  // segments of >= MIN_SEG planes
         s = (cg.nz + ns - 1) / ns;
     }
     if (s < 32) s = 32;
     if (s > cg.nz) s = cg.nz;
     if (s < 1) s = 1;
+    if (IBTK_LE_SEG_EQUAL) {
+        const long long ns = (cg.nz + s - 1) / s;  // segments of about s planes, equal (+-1)
+        s = (cg.nz + ns - 1) / ns;
+    }
     S = (int)s;
     nseg = (cg.nz + S - 1) / S;
 }
