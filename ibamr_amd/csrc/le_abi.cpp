@@ -225,6 +225,7 @@ extern "C" int ibtk_le_ctx_tune(ibtk_le_ctx ctx, const char* key, int value) {
     else if (k == "split_target") t.split_target = value;
     else if (k == "heavy") t.heavy = value;
     else if (k == "strip") t.strip = value;
+    else if (k == "interp_planes") t.interp_planes = value;
     else return fail(IBTK_LE_ERR_ARG, "unknown tuning key %s", key);
     return IBTK_LE_OK;
 }
@@ -684,6 +685,7 @@ static int prepare(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const ibtk_le
     p.err = ctx->err.as<int>();
     p.sink = ctx->sink.as<double>();
     p.tune = ctx->tune;
+    p.ipl_frames = -1;
     p.zmode = ctx->zmode;
     p.zlo = ctx->zlo;
     p.zhi = ctx->zhi;
@@ -1036,7 +1038,10 @@ static int level_params(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cent
         if (int rc = make_comps(&g, centering, axis, q_dev + (size_t)q * per, q_depth, Q_depth, 0, nc, t)) return rc;
         std::memcpy(m->pdh[q].comp, t.comp, sizeof(t.comp));
         if (q == 0) std::memcpy(p.comp, t.comp, sizeof(t.comp));
+        if (q == 0) p.ipl_frames = 1;
+        if (!interp_plane_frames(t.comp, nc)) p.ipl_frames = 0;
     }
+    p.tune = ctx->tune;
     if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
     if (int rc = upload_patches(ctx, m)) return rc;
     p.ncomp = nc;

@@ -104,6 +104,7 @@ struct SweepTune {
     int split_target = 0;  // own markers above which a (column, segment) is cut (k_item_counts)
     int heavy = 0;         // own markers per piece above which an item is scheduled first (-1: never)
     int strip = 0;         // column rows per strip of the item order (0: default)
+    int interp_planes = 0; // 1: the plane interp sweep (k_interp_planes) where it applies (slower: DESIGN.md)
 };
 // One 3-D sweep item: a patch, a column and its owned planes [p0, p1) (relative
 // to the patch's cg.org[2]).
@@ -170,6 +171,8 @@ struct Params {
     double* sink;              // 64 doubles: the store target of masked-off lanes (branch-free stores)
     unsigned long long* stamps;  // diagnostic phase clocks (nullptr: off)
     int dbg;                     // diagnostic switches (0: off)
+    int ipl_frames;              // 3-D interp: 1 = the components' frames allow the plane sweep (two frames
+                                 // per axis, k_interp_planes), 0 = they do not, -1 = check p.comp
 };
 
 // Host-side launchers (le_kernels.hip).
@@ -188,6 +191,9 @@ hipError_t launch_scan(void* temp, size_t& temp_bytes, const int* in, int* out, 
 
 // 3-D column sweep (le_sweep.hip)
 hipError_t launch_bin_col(int kernel, const Params& p, int n, unsigned* keys, int* vals, hipStream_t s);
+// the components' frames allow the plane interp sweep: in every axis d the
+// components other than d share one frame (side, edge, cell, node data do)
+bool interp_plane_frames(const CompDesc* comp, int nc);
 // z-slab migration classes (le_aux.hip)
 struct SlabMig {
     double L[3];

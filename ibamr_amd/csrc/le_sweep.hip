@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 
@@ -337,6 +338,12 @@ constexpr int IWAVES = IBTK_LE_IWAVES;  // waves per interp work item (one LDS r
 #endif
 #ifndef IBTK_LE_IPF
 #define IBTK_LE_IPF 1  // interp: plane prefetch depth in groups (1 or 2)
+#endif
+#ifndef IBTK_LE_DIAG_INTERP_NOCHUNK
+#define IBTK_LE_DIAG_INTERP_NOCHUNK 0  // diagnostic: the plane stream alone (no marker chunks)
+#endif
+#ifndef IBTK_LE_DIAG_INTERP_NOMATH
+#define IBTK_LE_DIAG_INTERP_NOMATH 0
 #endif
 #ifndef IBTK_LE_INTERP_EXACT
 #define IBTK_LE_INTERP_EXACT 1
@@ -648,7 +655,11 @@ __global__ __launch_bounds__(SW * IWAVES * ICW) IBTK_LE_IVGPR_ATTR void k_interp
             act = src < n;
         }
         double acc = 0.0;
+#if IBTK_LE_DIAG_INTERP_NOMATH  // diagnostic: markers and planes stream, no stencil sums
+        if (act) acc = m.X[0] + m.X[1] + m.X[2];
+#else
         if (act) acc = interp_marker<K>(p, cd, ring, gx0, gy0, zorg, am, m.X, m.s);
+#endif
         double* dst = (act && m.q >= 0) ? p.Qout + ((int64_t)p.Q_depth * m.q + cd.qcomp) : p.sink + lane;
         *dst = acc;
     };
@@ -687,7 +698,7 @@ __global__ __launch_bounds__(SW * IWAVES * ICW) IBTK_LE_IVGPR_ATTR void k_interp
             plane_load(my + IWAVES + HI, pv);
         }
         const int tot = gc.pre[IWAVES];
-        if (SW * w < tot) {
+        if (!IBTK_LE_DIAG_INTERP_NOCHUNK && SW * w < tot) {
             // dense groups: the wave's next chunk loads while this one is summed
             Mk m = cur;
             int am = acur;
@@ -712,6 +723,317 @@ __global__ __launch_bounds__(BLOCK) void k_interp_outside_col(Params p, int n) {
 }
 
 // ---------------------------------------------------------------------------
+// interpolation, one plane at a time (FAM 0 kernels: IB_4, BSPLINE_4, IB_6,
+// IB_4_W8), every component of an item in one workgroup
+// ---------------------------------------------------------------------------
+// Work item = (column, owned anchor planes [a0, a1)), all NC components.  The
+// workgroup has NS = HI - LO + 1 waves; wave w takes the anchor planes
+// a = a0 + w (mod NS).  An anchor plane's markers read planes a+LO .. a+HI, so
+// with the workgroup stepping through the item's planes one per step, every
+// wave has exactly one anchor plane in flight, at stage s = p - (a + LO), and
+// the LDS holds one plane per component (column + stencil halo) plus the next
+// one being put: 2 NC planes instead of k_interp_sweep's ring of NS + 3 planes
+// per component, which is what lets one workgroup take every component.
+// A lane keeps its marker's 1-D weights and partial sums in registers across
+// the NS steps and adds plane i2 = s - dz of its stencil at stage s: each sum
+// runs in the Fortran order (i2, i1, i0; f.m4:1366-1382), so Q is bitwise the
+// oracle's.  The markers are read once for all components, and each Q record
+// is written whole by one lane.
+// More than 64 markers on one anchor plane: the first 64 are register-resident;
+// the others are re-staged at every stage (weights recomputed, bit for bit the
+// same) with their partial sums kept in Q itself (each Q entry has one writer).
+// Weights: two frames per axis, frame 1 = component d's own in axis d, frame
+// 0 = the one the other components share (interp_plane_frames checks it).
+template <int K> struct IPl {
+    using T = KT<K>;
+    static constexpr int W = T::W, LO = T::LO, HI = T::HI;
+    static constexpr int NS = HI - LO + 1;  // planes an anchor plane's markers read; waves per workgroup
+    static constexpr int NT = SW * NS;
+    static constexpr int RX = COLX + HI - LO, RY = COLY + HI - LO;  // staged plane: column + stencil halo
+    static constexpr int PV = RX * RY;
+    static constexpr int PVP = (PV + 31) / 32 * 32;
+    static constexpr int NPC = (PV + NT - 1) / NT;  // staged points per thread, component and plane
+};
+
+// frame of component c in axis d; the component whose frame is frame f of axis d
+template <int NC> __device__ __forceinline__ constexpr int ipl_fr(int c, int d) { return NC == 1 ? 0 : (c == d ? 1 : 0); }
+template <int NC> __device__ __forceinline__ constexpr int ipl_fc(int d, int f) {
+    return NC == 1 ? 0 : (f ? d : (d == 0 ? 1 : 0));
+}
+
+template <int W, int NC> struct IMk {
+    static constexpr int NF = NC == 1 ? 1 : 2;
+    double wt[3][NF][W];  // 1-D weights [axis][frame][i]
+    int o[3][NF];         // stencil starts: x, y in the staged region, z from the anchor's first plane
+    unsigned okc;         // bit c: component c's stencil lies in the staged region
+};
+
+template <int I, int N, class F> __device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+// 1-D stencils of one marker (shifted position Xs); za = the anchor's first plane
+template <int K, int NC>
+__device__ __forceinline__ void ipl_weights(const Params& p, const CompDesc* cdv, const double* Xs, int gx0, int gy0,
+                                            int za, IMk<KT<K>::W, NC>& m) {
+    using S = IPl<K>;
+    constexpr int W = S::W, NF = IMk<W, NC>::NF;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            const CompDesc& cd = cdv[ipl_fc<NC>(d, f)];
+            St<W> st;
+            stencil1d<K>(Xs[d], Xs[d], cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis, p.K6, st);
+#pragma unroll
+            for (int i = 0; i < W; ++i) m.wt[d][f][i] = st.w[i];
+            m.o[d][f] = st.icl - (d == 0 ? gx0 : (d == 1 ? gy0 : za));
+        }
+    }
+    m.okc = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int ox = m.o[0][ipl_fr<NC>(c, 0)], oy = m.o[1][ipl_fr<NC>(c, 1)], oz = m.o[2][ipl_fr<NC>(c, 2)];
+        // binning invariant: the stencil lies in the staged region and the anchor's planes
+        if (ox >= 0 && ox + W <= S::RX && oy >= 0 && oy + W <= S::RY && oz >= 0 && oz + W <= S::NS) m.okc |= 1u << c;
+    }
+}
+
+// Stage s of one marker: plane i2 = s - dz of each component's stencil, read
+// from the current LDS planes pl[c] and added to acc[c] in the Fortran order.
+template <int K, int NC, int s>
+__device__ __forceinline__ void ipl_stage(const IMk<KT<K>::W, NC>& m, const double* const* pl, double* acc) {
+    using S = IPl<K>;
+    constexpr int W = S::W, RX = S::RX;
+    constexpr int jlo = s - (S::NS - W) > 0 ? s - (S::NS - W) : 0;  // the stencil planes stage s can be
+    constexpr int jhi = s < W - 1 ? s : W - 1;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int fx = ipl_fr<NC>(c, 0), fy = ipl_fr<NC>(c, 1), fz = ipl_fr<NC>(c, 2);
+        const int i2 = s - m.o[2][fz];
+        if (!((m.okc >> c) & 1u) || i2 < jlo || i2 > jhi) continue;  // not a plane of this stencil
+        double wz = m.wt[2][fz][jlo];
+#pragma unroll
+        for (int j = jlo + 1; j <= jhi; ++j) wz = i2 == j ? m.wt[2][fz][j] : wz;
+        const double* base = pl[c] + m.o[1][fy] * RX + m.o[0][fx];
+        double a = acc[c];
+#pragma unroll
+        for (int i1 = 0; i1 < W; ++i1) {
+            double v[W];
+#pragma unroll
+            for (int i0 = 0; i0 < W; ++i0) v[i0] = base[i1 * RX + i0];
+            const double wyz = m.wt[1][fy][i1] * wz;  // f.m4:1349-1353
+#pragma unroll
+            for (int i0 = 0; i0 < W; ++i0) {
+                const double wt = m.wt[0][fx][i0] * wyz;
+                a = a + wt * v[i0];  // f.m4:1375
+            }
+        }
+        acc[c] = a;
+    }
+}
+
+#ifndef IBTK_LE_IPL_WAVES
+#define IBTK_LE_IPL_WAVES 4  // waves per SIMD the plane interp is compiled for (VGPR budget 512 / this)
+#endif
+template <int K, bool LVL, int NC>
+__global__ __launch_bounds__(IPl<K>::NT) __attribute__((amdgpu_waves_per_eu(IBTK_LE_IPL_WAVES)))
+void k_interp_planes(Params p) {
+    using S = IPl<K>;
+    constexpr int W = S::W, LO = S::LO, HI = S::HI, NS = S::NS, NT = S::NT, NPC = S::NPC, RX = S::RX, PVP = S::PVP;
+    __shared__ double ring[2 * NC * PVP];
+    const int it = sweep_item(p, 1);
+    if (it < 0) return;
+    const SweepItem si = p.items[it];
+    const int col = si.col, a0 = si.p0, a1 = si.p1;
+    ColGeom cg;
+    CompDesc cd0;
+    const int* bs;
+    item_patch<LVL>(p, si, 0, cg, cd0, bs);
+    CompDesc cdv[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) cdv[c] = LVL ? p.pd[si.patch].comp[c] : p.comp[c];
+    const int tid = threadIdx.x, lane = lane_id();
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (p.zmode) {  // the planes the item reads: a0 + LO .. a1 - 1 + HI
+        const bool inner = cg.org[2] + a0 + LO >= p.zlo && cg.org[2] + a1 - 1 + HI <= p.zhi;
+        if (inner != (p.zmode == 1)) return;
+    }
+    {
+        bool any = false;  // the same answer in every wave
+        for (int a = a0 + lane; a < a1; a += SW) any = any || bs[bucket(cg, a, col, NBAND)] > bs[bucket(cg, a, col, 0)];
+        if (!__any(any)) return;
+    }
+    const int cx = col % cg.ncx, cy = col / cg.ncx;
+    const int gx0 = cg.org[0] + cx * COLX + LO, gy0 = cg.org[1] + cy * COLY + LO;
+    const int zorg = cg.org[2];
+    const int nlast = p.nsorted - 1;
+    // the thread's staged points q = tid + NT k of each component: array
+    // offsets (clamped) and in-array bits
+    int poff[NC][NPC];
+    unsigned okm = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+#pragma unroll
+        for (int k = 0; k < NPC; ++k) {
+            const int q = min(tid + NT * k, S::PV - 1);
+            const int gxu = gx0 + q % RX, gyu = gy0 + q / RX;
+            const int gx = min(max(gxu, cdv[c].lo[0]), cdv[c].hi[0]), gy = min(max(gyu, cdv[c].lo[1]), cdv[c].hi[1]);
+            poff[c][k] = (gx - cdv[c].lo[0]) + (gy - cdv[c].lo[1]) * (int)cdv[c].s1;
+            if (gx == gxu && gy == gyu) okm |= 1u << (c * NPC + k);
+        }
+    }
+    const int P0 = a0 + LO, plast = a1 - 1 + HI;
+    const int T = plast - P0 + 1;  // steps: one per plane the item reads
+    // relative plane zr -> registers: unconditional loads at clamped addresses
+    // (points outside the array are zeroed when the plane is put)
+    auto plane_load = [&](int zr, double (&v)[NC][NPC]) {
+        const int z = zorg + min(zr, plast);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int zc = min(max(z, cdv[c].lo[2]), cdv[c].hi[2]);
+            const double* pb = cdv[c].u + (int64_t)(zc - cdv[c].lo[2]) * cdv[c].s2;
+#pragma unroll
+            for (int k = 0; k < NPC; ++k) v[c][k] = pb[poff[c][k]];
+        }
+    };
+    auto plane_put = [&](int zr, const double (&v)[NC][NPC]) {  // into slot zr mod 2
+        const int z = zorg + min(zr, plast);
+        double* sl = ring + (zr & 1) * (NC * PVP);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const bool zin = z >= cdv[c].lo[2] && z <= cdv[c].hi[2];
+#pragma unroll
+            for (int k = 0; k < NPC; ++k)
+                if (S::PV % NT == 0 || k < NPC - 1 || tid + NT * k < S::PV)
+                    sl[c * PVP + tid + NT * k] = (zin && ((okm >> (c * NPC + k)) & 1u)) ? v[c][k] : 0.0;
+        }
+    };
+    auto lds_barrier = [&]() {  // LDS barrier; global loads in flight stay in flight
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    // anchor plane a's sorted entries: lane 0 its first, lane 1 its end (readlane)
+    auto span_load = [&](int a) {
+        const int ac = max(min(min(a, a1 - 1), cg.nz - 1), 0);
+        return bs[bucket(cg, ac, col, lane == 1 ? NBAND : 0)];
+    };
+    auto mk_load = [&](int e, double* X, int& q, bool act) {
+        e = min(e, nlast);
+        const double* xs = p.sorted_X + (int64_t)3 * e;
+        X[0] = xs[0];
+        X[1] = xs[1];
+        X[2] = xs[2];
+        const int qq = p.qdst ? p.qdst[e] : p.sorted_s[e];
+        q = act ? qq : -1;
+    };
+    auto qaddr = [&](int q, int c) { return p.Qout + ((int64_t)p.Q_depth * q + cdv[c].qcomp); };
+
+    double pv[NC][NPC];
+    plane_load(P0, pv);
+    plane_put(P0, pv);
+    plane_load(P0 + 1, pv);
+    // this wave's first anchor plane: its span and its first 64 markers
+    int beg, nA, nq;
+    double nX[3];
+    {
+        const int a = a0 + w;
+        const int v = span_load(a);
+        beg = __builtin_amdgcn_readlane(v, 0);
+        nA = a < a1 ? __builtin_amdgcn_readlane(v, 1) - beg : 0;
+        mk_load(beg + lane, nX, nq, lane < nA);
+    }
+    lds_barrier();
+    auto step_begin = [&](int tt) {  // plane P0+tt+1 into its slot, plane P0+tt+2 into registers
+        plane_put(P0 + tt + 1, pv);
+        plane_load(P0 + tt + 2, pv);
+    };
+    int t = 0;
+    for (; t < w && t < T; ++t) {  // wave w starts its first anchor plane at step w
+        step_begin(t);
+        lds_barrier();
+    }
+    IMk<W, NC> m;
+    double acc[NC];
+    int q = -1, nCur = 0, begCur = 0, vsp = 0;
+    for (int a = a0 + w; t < T; a += NS) {
+        static_for<0, NS>([&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            if (t >= T) return;
+            step_begin(t);
+            if (a < a1) {
+                if constexpr (s == 0) {  // the anchor plane's first 64 markers: weights into registers
+                    nCur = nA;
+                    begCur = beg;
+                    q = nq;
+                    ipl_weights<K, NC>(p, cdv, nX, gx0, gy0, zorg + a + LO, m);
+                    if (lane < nCur && m.okc != (1u << NC) - 1u) atomicOr(p.err, 1);
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) acc[c] = 0.0;
+                    vsp = span_load(a + NS);  // this wave's next anchor plane
+                }
+                if constexpr (s == 2) {
+                    beg = __builtin_amdgcn_readlane(vsp, 0);
+                    nA = a + NS < a1 ? __builtin_amdgcn_readlane(vsp, 1) - beg : 0;
+                    mk_load(beg + lane, nX, nq, lane < nA);
+                }
+                const double* pl[NC];
+#pragma unroll
+                for (int c = 0; c < NC; ++c) pl[c] = ring + ((P0 + t) & 1) * (NC * PVP) + c * PVP;
+                if (lane < nCur) ipl_stage<K, NC, s>(m, pl, acc);
+                // markers past the first 64: staged again at every stage, partial
+                // sums in Q (each entry written by one lane only)
+                for (int k = 1; SW * k < nCur; ++k) {
+                    const int nk = min(SW, nCur - SW * k);
+                    double Xo[3];
+                    int qo;
+                    mk_load(begCur + SW * k + lane, Xo, qo, lane < nk);
+                    if (qo >= 0) {
+                        // one component at a time (one marker state's registers)
+#pragma unroll
+                        for (int c = 0; c < NC; ++c) {
+                            IMk<W, 1> mo;
+                            ipl_weights<K, 1>(p, cdv + c, Xo, gx0, gy0, zorg + a + LO, mo);
+                            if constexpr (s == 0)
+                                if (mo.okc != 1u) atomicOr(p.err, 1);
+                            double ao = s == 0 ? 0.0 : *qaddr(qo, c);
+                            ipl_stage<K, 1, s>(mo, pl + c, &ao);
+                            *qaddr(qo, c) = ao;
+                        }
+                    }
+                }
+                if constexpr (s == NS - 1) {
+                    if (lane < nCur && q >= 0) {
+#pragma unroll
+                        for (int c = 0; c < NC; ++c) *qaddr(q, c) = acc[c];
+                    }
+                }
+            }
+            lds_barrier();
+            ++t;
+        });
+    }
+}
+
+// Two frames per axis: in every axis d the components other than d share one.
+bool interp_plane_frames(const CompDesc* comp, int nc) {
+    if (nc == 1) return true;
+    if (nc != 3) return false;
+    for (int d = 0; d < 3; ++d) {
+        const int a = d == 0 ? 1 : 0, b = d == 2 ? 1 : 2;  // the components other than d
+        const CompDesc &A = comp[a], &B = comp[b];
+        if (A.xlo[d] != B.xlo[d] || A.ilower[d] != B.ilower[d] || A.lo[d] != B.lo[d] || A.hi[d] != B.hi[d] ||
+            (A.axis == d) != (B.axis == d))
+            return false;
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------------------
 // spreading
 // ---------------------------------------------------------------------------
 #ifndef IBTK_LE_SPREAD_DEAL
@@ -719,6 +1041,17 @@ __global__ __launch_bounds__(BLOCK) void k_interp_outside_col(Params p, int n) {
 #endif
 #ifndef IBTK_LE_SPREAD_EARLY
 #define IBTK_LE_SPREAD_EARLY 0
+#endif
+// diagnostics (variant builds only): spread without reading u_old / without
+// the LDS adds; interp without the stencil sums
+#ifndef IBTK_LE_DIAG_SPREAD_NOLOAD
+#define IBTK_LE_DIAG_SPREAD_NOLOAD 0
+#endif
+#ifndef IBTK_LE_DIAG_SPREAD_NOPROC
+#define IBTK_LE_DIAG_SPREAD_NOPROC 0
+#endif
+#ifndef IBTK_LE_DIAG_SPREAD_NOADD
+#define IBTK_LE_DIAG_SPREAD_NOADD 0
 #endif
 #ifndef IBTK_LE_SPREAD_ROT
 #define IBTK_LE_SPREAD_ROT 0  // measured 30 % slower on cfg4 (the spread is issue-bound)
@@ -938,6 +1271,9 @@ __device__ __forceinline__ void spread_lanes_flat(const Params& p, const CompDes
     char* const base = reinterpret_cast<char*>(ring) + 8 * ox;
     int sl = (int)((unsigned)(a + oz + 64 * NSL) % (unsigned)NSL);  // ring slot of plane i2 = 0
     clk.lap(2);
+#if IBTK_LE_DIAG_SPREAD_NOADD
+    double diag = 0.0;
+#endif
 #pragma unroll
     for (int i2 = 0; i2 < W; ++i2) {
         char* const plane = base + sl * (8 * S::SLOT);
@@ -950,10 +1286,18 @@ __device__ __forceinline__ void spread_lanes_flat(const Params& p, const CompDes
             const double t = w1m[i1] * w2m[i2];
             double* const row = reinterpret_cast<double*>(plane + roff[i1]);
 #pragma unroll
-            for (int i0 = 0; i0 < W; ++i0)
+            for (int i0 = 0; i0 < W; ++i0) {
+#if IBTK_LE_DIAG_SPREAD_NOADD  // diagnostic: the weights and addresses without the LDS adds
+                diag = diag + w0v[i0] * t + (double)(reinterpret_cast<uintptr_t>(row + i0) & 1);
+#else
                 __hip_atomic_fetch_add(row + i0, w0v[i0] * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+            }
         }
     }
+#if IBTK_LE_DIAG_SPREAD_NOADD
+    __hip_atomic_fetch_add(reinterpret_cast<double*>(base), diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
     clk.lap(3);
 }
 
@@ -1152,6 +1496,10 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // adds of the n <= 64 candidates held one per lane (lane j's anchor plane:
     // a - 1 for j < r, else a): dealt over the lanes by bank class, then spread
     auto process = [&](int a, int r, int n, const Cand& mine) {
+        if constexpr (IBTK_LE_DIAG_SPREAD_NOPROC) {  // diagnostic: the plane and candidate streams alone
+            if (mine.V == 12345.0) atomicOr(p.err, 8);
+            return;
+        }
         if constexpr (S::ROT) {
             spread_rot<K>(p, cd, ring, mine, lane < n, lane < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo,
                           phi, inv_h3, inv_d);
@@ -1188,7 +1536,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     auto plane_load = [&](int z, double* v) {
         const double* pb = plane_ptr(z);
 #pragma unroll
-        for (int k = 0; k < NPL; ++k) v[k] = pb[loff[k]];
+        for (int k = 0; k < NPL; ++k) v[k] = IBTK_LE_DIAG_SPREAD_NOLOAD ? 0.0 : pb[loff[k]];
     };
     auto plane_put = [&](int z, const double* v) {
         double* sl = ring + sslot<K>(z) * S::SLOT;
@@ -1525,7 +1873,28 @@ template <int K>
 hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     if (ev0) (void)hipEventRecord(ev0, s);
     constexpr bool fits3 = 3 * ISh<K>::NSL * ISh<K>::PVP * 8 <= 160 * 1024;  // three rings in one CU's LDS
-    if constexpr (!fits3 || IBTK_LE_ICW != 3) {
+    bool planes = false;  // the plane sweep (k_interp_planes): closed-form kernels, 1 or 3 components
+    if constexpr (KT<K>::FAM == 0) {
+        const bool frames = p.ipl_frames < 0 ? interp_plane_frames(p.comp, p.ncomp) : p.ipl_frames == 1;
+        planes = p.tune.interp_planes == 1 && frames && (p.ncomp == 3 || p.ncomp == 1);
+    }
+    if constexpr (KT<K>::FAM == 0) {
+        if (planes) {
+            const long items = (long)p.item_bound;
+            const dim3 g(grid8(items + 8)), b(IPl<K>::NT);
+            if (items > 0) {
+                if (p.ncomp == 3) {
+                    if (p.pd) hipLaunchKernelGGL((k_interp_planes<K, true, 3>), g, b, 0, s, p);
+                    else hipLaunchKernelGGL((k_interp_planes<K, false, 3>), g, b, 0, s, p);
+                } else {
+                    if (p.pd) hipLaunchKernelGGL((k_interp_planes<K, true, 1>), g, b, 0, s, p);
+                    else hipLaunchKernelGGL((k_interp_planes<K, false, 1>), g, b, 0, s, p);
+                }
+            }
+        }
+    }
+    if (planes) {
+    } else if constexpr (!fits3 || IBTK_LE_ICW != 3) {
         const long items = (long)p.item_bound * p.ncomp;
         if (items > 0) {
             if (p.pd)
