@@ -726,6 +726,45 @@ static int build_dedup(ibtk_le_ctx ctx, ibtk_le_markers m) {
     return IBTK_LE_OK;
 }
 
+// Diagnostic phase clocks of the spread sweep (IBTK_LE_STAMPS=1 with a
+// -DIBTK_LE_CLOCKS=1 build): per-item cycle totals, summarised on stderr.
+static int stamps_begin(ibtk_le_ctx ctx, size_t nst, Params& p) {
+    if (!ctx->stamps_on) return IBTK_LE_OK;
+    if (int rc = ctx->stamps.ensure(nst * sizeof(unsigned long long))) return rc;
+    HIP_TRY(hipMemsetAsync(ctx->stamps.p, 0, nst * sizeof(unsigned long long), ctx->stream));
+    p.stamps = ctx->stamps.as<unsigned long long>();
+    return IBTK_LE_OK;
+}
+static int stamps_report(ibtk_le_ctx ctx, size_t nst, Params& p) {
+    if (!p.stamps) return IBTK_LE_OK;
+    std::vector<unsigned long long> h(nst);
+    HIP_TRY(hipMemcpyAsync(h.data(), p.stamps, nst * sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    double tot[6] = {0, 0, 0, 0, 0, 0};
+    long items = 0;
+    std::vector<unsigned long long> sums;
+    for (size_t i = 0; i < nst / 8; ++i) {
+        unsigned long long sum = 0;
+        for (int k = 0; k < 6; ++k) sum += h[i * 8 + k];
+        if (!sum) continue;
+        ++items;
+        sums.push_back(sum);
+        for (int k = 0; k < 6; ++k) tot[k] += (double)h[i * 8 + k];
+    }
+    std::sort(sums.begin(), sums.end());
+    const double q99 = sums.empty() ? 0.0 : (double)sums[(size_t)(0.99 * (sums.size() - 1))];
+    const double mx = sums.empty() ? 0.0 : (double)sums.back();
+    double all = 0.0;
+    for (unsigned long long v : sums) all += (double)v;
+    const long n = items > 0 ? items : 1;
+    fprintf(stderr,
+            "spread stamps: %ld items; mean cycles/item: prologue %.0f writeback+put %.0f prefetch+deal+weights %.0f "
+            "adds %.0f rest %.0f epilogue %.0f; item total mean %.0f p99 %.0f max %.0f; sum over items %.3e\n",
+            items, tot[0] / n, tot[1] / n, tot[2] / n, tot[3] / n, tot[4] / n, tot[5] / n, all / n, q99, mx, all);
+    p.stamps = nullptr;
+    return IBTK_LE_OK;
+}
+
 int ibtk_le::interp_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis, const void* geomv,
                          const double* const* q_dev, int q_depth, double* Q_dev, int Q_depth, const double* X_dev,
                          bool check_ghosts) {
@@ -838,38 +877,13 @@ static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cente
         const bool t = ctx->timing && first == 0;
         p.dbg = ctx->dbg;  // diagnostics: variants of the add loop
         const size_t nst = (size_t)m->item_bound * cnt * 8;
-        if (geom->ndim == 3 && ctx->stamps_on) {
-            if (int rc = ctx->stamps.ensure(nst * sizeof(unsigned long long))) return rc;
-            HIP_TRY(hipMemsetAsync(ctx->stamps.p, 0, nst * sizeof(unsigned long long), ctx->stream));
-            p.stamps = ctx->stamps.as<unsigned long long>();
-        }
+        if (geom->ndim == 3)
+            if (int rc = stamps_begin(ctx, nst, p)) return rc;
         if (geom->ndim == 3)
             HIP_TRY(launch_spread_sweep(kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
         else
             HIP_TRY(launch_spread(geom->ndim, kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
-        if (p.stamps) {  // per-phase cycle totals over the work items (diagnostics only)
-            std::vector<unsigned long long> h(nst);
-            HIP_TRY(hipMemcpyAsync(h.data(), p.stamps, nst * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                                   ctx->stream));
-            HIP_TRY(hipStreamSynchronize(ctx->stream));
-            double tot[6] = {0, 0, 0, 0, 0, 0};
-            long items = 0;
-            std::vector<unsigned long long> sums;
-            for (size_t i = 0; i < nst / 8; ++i) {
-                unsigned long long sum = 0;
-                for (int k = 0; k < 6; ++k) sum += h[i * 8 + k];
-                if (!sum) continue;
-                ++items;
-                sums.push_back(sum);
-                for (int k = 0; k < 6; ++k) tot[k] += (double)h[i * 8 + k];
-            }
-            std::sort(sums.begin(), sums.end());
-            const double q99 = sums.empty() ? 0.0 : (double)sums[(size_t)(0.99 * (sums.size() - 1))];
-            const double mx = sums.empty() ? 0.0 : (double)sums.back();
-            fprintf(stderr, "spread stamps: %ld items; mean cycles/item: prologue %.0f wait %.0f chunk0 %.0f dense %.0f tail %.0f drain %.0f; item total p99 %.0f max %.0f\n",
-                    items, tot[0] / items, tot[1] / items, tot[2] / items, tot[3] / items, tot[4] / items, tot[5] / items, q99, mx);
-            p.stamps = nullptr;
-        }
+        if (int rc = stamps_report(ctx, nst, p)) return rc;
         if (t) ctx->ev_valid = true;
     }
     return IBTK_LE_OK;
@@ -1110,7 +1124,10 @@ extern "C" int ibtk_le_level_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kern
     p.sorted_F = ctx->fbuf.as<double>();
     const bool t = ctx->timing;
     ctx->ev_valid = false;
+    const size_t nst = (size_t)m->item_bound * nc * 8;
+    if (int rc = stamps_begin(ctx, nst, p)) return rc;
     HIP_TRY(launch_spread_sweep(kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
+    if (int rc = stamps_report(ctx, nst, p)) return rc;
     if (t) ctx->ev_valid = true;
     return IBTK_LE_OK;
 }

@@ -42,6 +42,12 @@ constexpr int SW = 64;  // one wavefront per work item
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// three consecutive doubles (a position record) as one 24-byte load (dwordx4 + dwordx2)
+struct D3 {
+    double v[3];
+};
+__device__ __forceinline__ D3 ld3(const double* q) { return *reinterpret_cast<const D3*>(q); }
+
 // ---------------------------------------------------------------------------
 // binning
 // ---------------------------------------------------------------------------
@@ -147,9 +153,12 @@ __global__ __launch_bounds__(BLOCK) void k_gather_col(Params p, int n, int* sort
         const int l = p.sorted_l[e];
         const int s = p.indices ? p.indices[l] : l;
         sorted_s[e] = s;
+        struct R3 {
+            double v[3];
+        };
+        const R3 x = *reinterpret_cast<const R3*>(p.X + (int64_t)3 * s);  // one 24-byte record per lane
 #pragma unroll
-        for (int d = 0; d < 3; ++d)
-            sx[3 * threadIdx.x + d] = p.X[(int64_t)3 * s + d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
+        for (int d = 0; d < 3; ++d) sx[3 * threadIdx.x + d] = x.v[d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
     }
     __syncthreads();
     const int cnt = 3 * min(BLOCK, n - e0);  // doubles this block writes
@@ -622,10 +631,10 @@ __global__ __launch_bounds__(SW * IWAVES * ICW) IBTK_LE_IVGPR_ATTR void k_interp
         e = min(e, nlast);
         m.s = p.sorted_s[e];
         m.q = p.qdst ? p.qdst[e] : m.s;
-        const double* xs = p.sorted_X + (int64_t)3 * e;
-        m.X[0] = xs[0];
-        m.X[1] = xs[1];
-        m.X[2] = xs[2];
+        const D3 xs = ld3(p.sorted_X + (int64_t)3 * e);
+        m.X[0] = xs.v[0];
+        m.X[1] = xs.v[1];
+        m.X[2] = xs.v[2];
     };
     // one chunk of n <= 64 markers held one per lane: summed, stored.  (Dealing
     // the markers over the two 32-lane halves of a ds_read_b64 by bank class,
@@ -1046,6 +1055,9 @@ bool interp_plane_frames(const CompDesc* comp, int nc) {
 // the LDS adds; interp without the stencil sums
 #ifndef IBTK_LE_DIAG_SPREAD_NOLOAD
 #define IBTK_LE_DIAG_SPREAD_NOLOAD 0
+#endif
+#ifndef IBTK_LE_SPF
+#define IBTK_LE_SPF 1  // spread: plane prefetch depth in anchor steps (1 or 2)
 #endif
 #ifndef IBTK_LE_SPREAD_PIPE
 #define IBTK_LE_SPREAD_PIPE 0  // 1: k_spread_pipe (dealing and writeback one chunk ahead of the adds)
@@ -1489,10 +1501,10 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // candidate data of sorted position e
     auto cand_at = [&](int e, Cand& d) {
         e = min(e, nlast);
-        const double* xs = p.sorted_X + (int64_t)3 * e;
-        d.X[0] = xs[0];
-        d.X[1] = xs[1];
-        d.X[2] = xs[2];
+        const D3 xs = ld3(p.sorted_X + (int64_t)3 * e);
+        d.X[0] = xs.v[0];
+        d.X[1] = xs.v[1];
+        d.X[2] = xs.v[2];
         if constexpr (IBTK_LE_SPREAD_FDIRECT) {  // F(s, c) through the sorted marker index (no gather pass)
             const int sm = p.sorted_s[e];
             const double v = p.Qin[(int64_t)p.Q_depth * sm + cd.qcomp];
@@ -1585,6 +1597,8 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         plane_put(z, pv);
     }
     plane_load(afirst + HI, pv);
+    double pv2[IBTK_LE_SPF >= 2 ? NPL : 1];  // SPF 2: the plane after it, loaded a step earlier
+    if constexpr (IBTK_LE_SPF >= 2) plane_load(afirst + HI + 1, pv2);
     int rowv[3];
     rows_load(afirst, rowv);
     Ranges rg;  // ranges of the anchor whose chunk 1 is prefetched (wave-uniform)
@@ -1625,7 +1639,13 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
             etail = range_pos(rg, max(tA - SW + lane, 0));
             n1 = r_a + min(SW - r_a, tA);
             r_prev = r_a;
-            plane_load(a + HI + 1, pv);
+            if constexpr (IBTK_LE_SPF >= 2) {
+#pragma unroll
+                for (int k = 0; k < NPL; ++k) pv[k] = pv2[k];
+                plane_load(a + HI + 2, pv2);
+            } else {
+                plane_load(a + HI + 1, pv);
+            }
             if (a + 2 <= alast) rows_load(a + 2, rowv);
         }
 #if !IBTK_LE_SPREAD_EARLY
@@ -1820,10 +1840,10 @@ __global__ __launch_bounds__(SW) void k_spread_pipe(Params p) {
     };
     auto cand_at = [&](int e, Cand& d) {
         e = min(max(e, 0), nlast);
-        const double* xs = p.sorted_X + (int64_t)3 * e;
-        d.X[0] = xs[0];
-        d.X[1] = xs[1];
-        d.X[2] = xs[2];
+        const D3 xs = ld3(p.sorted_X + (int64_t)3 * e);
+        d.X[0] = xs.v[0];
+        d.X[1] = xs.v[1];
+        d.X[2] = xs.v[2];
         d.V = p.sorted_F[(int64_t)c * p.nsorted + e];
         d.s = FAM == 2 ? p.sorted_s[e] : 0;
     };
@@ -2267,23 +2287,39 @@ hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent
     if (n > 0) hipLaunchKernelGGL(k_interp_outside_col, dim3(64), dim3(BLOCK), 0, s, p, n);
     return hipGetLastError();
 }
-// sorted_F[c * n + e] = Q(qcomp_c, s(e)): the spread values in sorted order
+// sorted_F[c * n + e] = Q(qcomp_c, s(e)): the spread values in sorted order.
+// REC3: three components that are a whole 24-byte Q record (Q_depth 3, qcomp
+// 0, 1, 2: the side-centred force), read as one record per lane.
+struct Rec3 {
+    double v[3];
+};
+template <bool REC3>
 __global__ __launch_bounds__(BLOCK) void k_gather_F_col(Params p, int n, double* out) {
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     if (e >= n) return;
     const int s = p.sorted_s[e];
     // density-weighted spread: F ds rounded once, as LDataManager.cpp:446-451 forms it
     const double w = p.ds ? p.ds[s] : 1.0;
-    for (int c = 0; c < p.ncomp; ++c) {
-        const double v = p.Qin[(int64_t)p.Q_depth * s + p.comp[c].qcomp];
-        out[(int64_t)c * n + e] = p.ds ? v * w : v;
+    if constexpr (REC3) {
+        const Rec3 r = *reinterpret_cast<const Rec3*>(p.Qin + (int64_t)3 * s);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) out[(int64_t)c * n + e] = p.ds ? r.v[c] * w : r.v[c];
+    } else {
+        for (int c = 0; c < p.ncomp; ++c) {
+            const double v = p.Qin[(int64_t)p.Q_depth * s + p.comp[c].qcomp];
+            out[(int64_t)c * n + e] = p.ds ? v * w : v;
+        }
     }
 }
 
 template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-    if (!IBTK_LE_SPREAD_FDIRECT && p.nsorted > 0)
-        hipLaunchKernelGGL(k_gather_F_col, dim3((p.nsorted + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, p.nsorted,
-                           const_cast<double*>(p.sorted_F));
+    if (!IBTK_LE_SPREAD_FDIRECT && p.nsorted > 0) {
+        const bool rec3 = p.ncomp == 3 && p.Q_depth == 3 && p.comp[0].qcomp == 0 && p.comp[1].qcomp == 1 &&
+                          p.comp[2].qcomp == 2;
+        const dim3 g((p.nsorted + BLOCK - 1) / BLOCK), b(BLOCK);
+        if (rec3) hipLaunchKernelGGL(k_gather_F_col<true>, g, b, 0, s, p, p.nsorted, const_cast<double*>(p.sorted_F));
+        else hipLaunchKernelGGL(k_gather_F_col<false>, g, b, 0, s, p, p.nsorted, const_cast<double*>(p.sorted_F));
+    }
     if (ev0) (void)hipEventRecord(ev0, s);  // the events bracket the sweep kernel alone
     const long items = (long)p.item_bound * p.ncomp;
     if (items > 0) {
