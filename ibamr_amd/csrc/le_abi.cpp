@@ -226,6 +226,7 @@ extern "C" int ibtk_le_ctx_tune(ibtk_le_ctx ctx, const char* key, int value) {
     else if (k == "heavy") t.heavy = value;
     else if (k == "strip") t.strip = value;
     else if (k == "interp_planes") t.interp_planes = value;
+    else if (k == "xcd_block") t.xcd_block = value;
     else return fail(IBTK_LE_ERR_ARG, "unknown tuning key %s", key);
     return IBTK_LE_OK;
 }

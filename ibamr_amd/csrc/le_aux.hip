@@ -218,46 +218,54 @@ hipError_t launch_zero_ghosts(int ndim, const GhostDesc* g, int n, hipStream_t s
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(BLOCK) void k_level_fill(LevelTiling t, int dreg, const int* tile_of_patch,
                                                       const int* patch_of_tile, double* const* arrays, int depth) {
+    // The source of a ghost point is the neighbouring tile in direction dir (per dim
+    // -1, 0, +1) at local index li - dir n: the 27 neighbours' arrays are looked up
+    // once per workgroup (the tiles are equal, so a ghost layer no wider than a
+    // patch reaches only them; wrapped in the periodic dims, none across a
+    // physical boundary -- left to the boundary operators).
     const int q = blockIdx.z / t.ncomp, a = blockIdx.z - q * t.ncomp;
-    const int tile = tile_of_patch[q];
-    const int tc[3] = {tile % t.ntile[0], (tile / t.ntile[0]) % t.ntile[1], tile / (t.ntile[0] * t.ntile[1])};
-    int ext[3], uni[3], lo[3];
-    for (int d = 0; d < 3; ++d) {
-        const int extra = (t.side && d == a) ? 1 : 0;
-        ext[d] = t.n[d] + 2 * t.g + extra;  // array extent
-        uni[d] = t.n[d];                     // unique points [g, g + n)
-        lo[d] = t.dom_lo[d] + tc[d] * t.n[d] - t.g;  // global index of array point 0
+    __shared__ const double* nbr[27];
+    if (threadIdx.x < 27) {
+        const int tile = tile_of_patch[q];
+        const int tc[3] = {tile % t.ntile[0], (tile / t.ntile[0]) % t.ntile[1], tile / (t.ntile[0] * t.ntile[1])};
+        const int dir[3] = {(int)threadIdx.x % 3 - 1, ((int)threadIdx.x / 3) % 3 - 1, (int)threadIdx.x / 9 - 1};
+        int nt[3];
+        bool ok = true;
+        for (int d = 0; d < 3; ++d) {
+            nt[d] = tc[d] + dir[d];
+            if (nt[d] < 0 || nt[d] >= t.ntile[d]) {
+                if (!t.periodic[d]) ok = false;
+                nt[d] = (nt[d] + t.ntile[d]) % t.ntile[d];
+            }
+        }
+        const int sq = ok ? patch_of_tile[nt[0] + t.ntile[0] * (nt[1] + t.ntile[1] * nt[2])] : -1;
+        nbr[threadIdx.x] = sq >= 0 ? arrays[(size_t)sq * t.ncomp + a] : nullptr;
     }
-    int rx[3];  // region extents of this pass
-    for (int d = 0; d < 3; ++d) rx[d] = d < dreg ? ext[d] : (d == dreg ? ext[d] - uni[d] : uni[d]);
+    __syncthreads();
+    int ext[3];
+    for (int d = 0; d < 3; ++d) ext[d] = t.n[d] + 2 * t.g + ((t.side && d == a) ? 1 : 0);  // array extent
+    int rx[3];  // region extents of this pass: ghost layers in dreg, all below it, unique points above
+    for (int d = 0; d < 3; ++d) rx[d] = d < dreg ? ext[d] : (d == dreg ? ext[d] - t.n[d] : t.n[d]);
     const unsigned tid = blockIdx.x * BLOCK + threadIdx.x;
     if (tid >= (unsigned)rx[0] * (unsigned)rx[1] || (int)blockIdx.y >= rx[2]) return;
     const int r[3] = {(int)(tid % (unsigned)rx[0]), (int)(tid / (unsigned)rx[0]), (int)blockIdx.y};
-    int li[3];
+    int li[3], sl[3], k = 0, mul = 1;
     for (int d = 0; d < 3; ++d) {
         if (d < dreg) li[d] = r[d];
-        else if (d == dreg) li[d] = r[d] < t.g ? r[d] : t.g + uni[d] + (r[d] - t.g);
+        else if (d == dreg) li[d] = r[d] < t.g ? r[d] : t.g + t.n[d] + (r[d] - t.g);
         else li[d] = t.g + r[d];
+        const int dir = li[d] < t.g ? -1 : (li[d] >= t.g + t.n[d] ? 1 : 0);
+        sl[d] = li[d] - dir * t.n[d];
+        k += (dir + 1) * mul;
+        mul *= 3;
     }
-    int src_tile[3], sl[3];
-    for (int d = 0; d < 3; ++d) {
-        const int N = t.n[d] * t.ntile[d];
-        int gi = lo[d] + li[d] - t.dom_lo[d];
-        if (gi < 0 || gi >= N) {
-            if (!t.periodic[d]) return;  // a physical ghost: left to the boundary operators
-            gi = ((gi % N) + N) % N;
-        }
-        src_tile[d] = gi / t.n[d];
-        sl[d] = gi - src_tile[d] * t.n[d] + t.g;
-    }
-    const int sq = patch_of_tile[src_tile[0] + t.ntile[0] * (src_tile[1] + t.ntile[1] * src_tile[2])];
-    if (sq < 0) return;
+    const double* src = nbr[k];
+    if (!src) return;
     const int64_t di = (int64_t)li[0] + (int64_t)ext[0] * (li[1] + (int64_t)ext[1] * li[2]);
     const int64_t si = (int64_t)sl[0] + (int64_t)ext[0] * (sl[1] + (int64_t)ext[1] * sl[2]);
     const int64_t vol = (int64_t)ext[0] * ext[1] * ext[2];
     double* dst = arrays[(size_t)q * t.ncomp + a];
-    const double* src = arrays[(size_t)sq * t.ncomp + a];
-    for (int k = 0; k < depth; ++k) dst[k * vol + di] = src[k * vol + si];
+    for (int j = 0; j < depth; ++j) dst[j * vol + di] = src[j * vol + si];
 }
 
 // every element of narr arrays := 0 (array i: count[i] doubles, 16-byte aligned

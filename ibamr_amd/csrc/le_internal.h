@@ -105,6 +105,8 @@ struct SweepTune {
     int heavy = 0;         // own markers per piece above which an item is scheduled first (-1: never)
     int strip = 0;         // column rows per strip of the item order (0: default)
     int interp_planes = 0; // 1: the plane interp sweep (k_interp_planes) where it applies (slower: DESIGN.md)
+    int xcd_block = 0;     // light sweep items over the XCDs in blocks of this many table entries (1:
+                           // round-robin; -1: one contiguous range per XCD; 0: the default, 8)
 };
 // One 3-D sweep item: a patch, a column and its owned planes [p0, p1) (relative
 // to the patch's cg.org[2]).

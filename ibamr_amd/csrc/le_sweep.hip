@@ -188,12 +188,27 @@ __global__ __launch_bounds__(BLOCK) void k_gather_col(Params p, int n, int* sort
 // and take the first blocks, dealt round-robin over the XCDs, so that they
 // start first and the light ones fill in around them.  The grid is 8 blocks
 // longer than the item bound (the heavy block count is rounded up to 8).
+constexpr int XCD_BLOCK = 8;  // table entries per block of items dealt to one XCD
 __device__ __forceinline__ int sweep_item(const Params& p, int per_entry) {
     const int nt = p.nitems[0] * per_entry, nh = p.nitems[1] * per_entry;
     const int b = blockIdx.x;
     const int h8 = (nh + 7) & ~7;
     if (b < h8) return b < nh ? b : -1;
     const int bl = b - h8, nl = nt - nh;
+    // Light items over the XCDs in blocks of B table entries, block j to XCD
+    // j mod 8 (ctx_tune xcd_block; 1 = round-robin, -1 = one contiguous range per
+    // XCD, the round-1 order).  Contiguous ranges give one XCD a whole z-layer of
+    // a level's patches -- a sheet of markers: blocks take cfg5 from 1.74e9 to
+    // 1.96e9 marker-ops/s (spread sweep 4.32 -> 3.41 ms); on cfg4 blocks of 8
+    // keep the x-neighbour columns' shared halo lines in one L2 (interp 10.8 ms;
+    // round-robin 11.1, ranges 11.0, blocks of 34 11.0; profiles/r02z).
+    const int B = p.tune.xcd_block != 0 ? p.tune.xcd_block : XCD_BLOCK;
+    if (B > 0) {
+        const int Bi = B * per_entry;  // items per block
+        const int k = bl >> 3, x = bl & 7;
+        const int it = ((k / Bi) * 8 + x) * Bi + (k % Bi);
+        return it < nl ? nh + it : -1;
+    }
     const int per = (nl + 7) >> 3;
     if ((bl >> 3) >= per) return -1;
     const int it = (bl & 7) * per + (bl >> 3);
@@ -2176,6 +2191,13 @@ __global__ __launch_bounds__(BLOCK) void k_item_write(Params p, int target, int 
 }
 
 static int grid8(long items) { return (int)((items + 7) & ~7L); }
+// a sweep's grid: the items, the heavy items' rounding to 8 (sweep_item), and with
+// block dealing over the XCDs (xcd_block > 0) a block of slack per XCD
+static int sweep_grid(const Params& p, long items) {
+    const int B = p.tune.xcd_block != 0 ? p.tune.xcd_block : XCD_BLOCK;
+    const long per = p.item_bound > 0 ? items / p.item_bound : 1;
+    return grid8(items + 8 + (B > 0 ? 8L * B * per : 0));
+}
 
 template <int K> hipError_t launch_item_table_t(const Params& p, int target, int heavy, int* nsub, int* start,
                                                 SweepItem* tab, int* ntot, void* temp, size_t temp_bytes,
@@ -2242,7 +2264,7 @@ hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent
     if constexpr (KT<K>::FAM == 0) {
         if (planes) {
             const long items = (long)p.item_bound;
-            const dim3 g(grid8(items + 8)), b(IPl<K>::NT);
+            const dim3 g(sweep_grid(p, items)), b(IPl<K>::NT);
             if (items > 0) {
                 if (p.ncomp == 3) {
                     if (p.pd) hipLaunchKernelGGL((k_interp_planes<K, true, 3>), g, b, 0, s, p);
@@ -2259,26 +2281,26 @@ hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent
         const long items = (long)p.item_bound * p.ncomp;
         if (items > 0) {
             if (p.pd)
-                hipLaunchKernelGGL((k_interp_sweep<K, true, 1>), dim3(grid8(items + 8)), dim3(SW * IWAVES), 0, s, p);
+                hipLaunchKernelGGL((k_interp_sweep<K, true, 1>), dim3(sweep_grid(p, items)), dim3(SW * IWAVES), 0, s, p);
             else
-                hipLaunchKernelGGL((k_interp_sweep<K, false, 1>), dim3(grid8(items + 8)), dim3(SW * IWAVES), 0, s, p);
+                hipLaunchKernelGGL((k_interp_sweep<K, false, 1>), dim3(sweep_grid(p, items)), dim3(SW * IWAVES), 0, s, p);
         }
     } else if (p.ncomp == 3) {  // the components of an item in one workgroup
         const long items = (long)p.item_bound;
         if (items > 0) {
             if (p.pd)
-                hipLaunchKernelGGL((k_interp_sweep<K, true, 3>), dim3(grid8(items + 8)), dim3(SW * IWAVES * 3), 0, s, p);
+                hipLaunchKernelGGL((k_interp_sweep<K, true, 3>), dim3(sweep_grid(p, items)), dim3(SW * IWAVES * 3), 0, s, p);
             else
-                hipLaunchKernelGGL((k_interp_sweep<K, false, 3>), dim3(grid8(items + 8)), dim3(SW * IWAVES * 3), 0, s,
+                hipLaunchKernelGGL((k_interp_sweep<K, false, 3>), dim3(sweep_grid(p, items)), dim3(SW * IWAVES * 3), 0, s,
                                    p);
         }
     } else {
         const long items = (long)p.item_bound * p.ncomp;
         if (items > 0) {
             if (p.pd)
-                hipLaunchKernelGGL((k_interp_sweep<K, true, 1>), dim3(grid8(items + 8)), dim3(SW * IWAVES), 0, s, p);
+                hipLaunchKernelGGL((k_interp_sweep<K, true, 1>), dim3(sweep_grid(p, items)), dim3(SW * IWAVES), 0, s, p);
             else
-                hipLaunchKernelGGL((k_interp_sweep<K, false, 1>), dim3(grid8(items + 8)), dim3(SW * IWAVES), 0, s, p);
+                hipLaunchKernelGGL((k_interp_sweep<K, false, 1>), dim3(sweep_grid(p, items)), dim3(SW * IWAVES), 0, s, p);
         }
     }
     if (ev1) (void)hipEventRecord(ev1, s);
@@ -2324,11 +2346,11 @@ template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s
     const long items = (long)p.item_bound * p.ncomp;
     if (items > 0) {
         if (IBTK_LE_SPREAD_PIPE && !S_ROT<K>) {
-            if (p.pd) hipLaunchKernelGGL((k_spread_pipe<K, true>), dim3(grid8(items + 8)), dim3(SW), 0, s, p);
-            else hipLaunchKernelGGL((k_spread_pipe<K, false>), dim3(grid8(items + 8)), dim3(SW), 0, s, p);
+            if (p.pd) hipLaunchKernelGGL((k_spread_pipe<K, true>), dim3(sweep_grid(p, items)), dim3(SW), 0, s, p);
+            else hipLaunchKernelGGL((k_spread_pipe<K, false>), dim3(sweep_grid(p, items)), dim3(SW), 0, s, p);
         } else {
-            if (p.pd) hipLaunchKernelGGL((k_spread_sweep<K, true>), dim3(grid8(items + 8)), dim3(SW), 0, s, p);
-            else hipLaunchKernelGGL((k_spread_sweep<K, false>), dim3(grid8(items + 8)), dim3(SW), 0, s, p);
+            if (p.pd) hipLaunchKernelGGL((k_spread_sweep<K, true>), dim3(sweep_grid(p, items)), dim3(SW), 0, s, p);
+            else hipLaunchKernelGGL((k_spread_sweep<K, false>), dim3(sweep_grid(p, items)), dim3(SW), 0, s, p);
         }
     }
     if (ev1) (void)hipEventRecord(ev1, s);

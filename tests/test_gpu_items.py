@@ -24,6 +24,9 @@ SETTINGS = [
     {"seg_items": 2000, "split_target": 300},             # many load splits
     {"seg_items": 3000, "split_target": 500, "heavy": 1}, # every item heavy (scheduled first)
     {"heavy": -1},                                        # no heavy-first ordering
+    {"xcd_block": 1},                                     # light items round-robin over the XCDs
+    {"xcd_block": 3},                                     # ... in blocks of 3 table entries
+    {"interp_planes": 1},                                 # the plane-at-a-time interp sweep
 ]
 
 
