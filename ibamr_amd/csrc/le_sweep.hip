@@ -1074,9 +1074,6 @@ bool interp_plane_frames(const CompDesc* comp, int nc) {
 #ifndef IBTK_LE_SPF
 #define IBTK_LE_SPF 1  // spread: plane prefetch depth in anchor steps (1 or 2)
 #endif
-#ifndef IBTK_LE_SPREAD_PIPE
-#define IBTK_LE_SPREAD_PIPE 0  // 1: k_spread_pipe (dealing and writeback one chunk ahead of the adds)
-#endif
 #ifndef IBTK_LE_SPREAD_FDIRECT
 #define IBTK_LE_SPREAD_FDIRECT 0  // 1: candidates read F through sorted_s (no k_gather_F_col pass)
 #endif
@@ -1118,7 +1115,6 @@ template <int K> struct SSh {
 
 // ring plane layout: row-major 32 x COLY, rows SSh::RS apart; q = the lane's
 // staged point (x = q mod 32, y = q / 32)
-template <int K> constexpr bool S_ROT = SSh<K>::ROT;
 template <int K> __device__ __forceinline__ int ring_index(int q) {
     return (q >> 5) * SSh<K>::RS + (q & (COLX - 1));
 }
@@ -1695,333 +1691,6 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
 }
 
 // ---------------------------------------------------------------------------
-// spreading, software-pipelined by one chunk (IBTK_LE_SPREAD_PIPE)
-// ---------------------------------------------------------------------------
-// k_spread_sweep's work in another order.  A wave's LDS operations complete in
-// issue order, so any LDS result it waits for -- the bank-class dealing's
-// ds_bpermute, the writeback's ring reads -- waits for every ds_add_f64 it
-// issued before (measured: 20 % of the sweep in the writeback wait, part of
-// another 34 % in the dealing).  Here each chunk's candidates are dealt one
-// chunk ahead, and the LDS section of a step (writeback, put, the next chunk's
-// dealing) comes after the current chunk's weights are computed: the previous
-// chunk's adds drain while the VALU works.  Per anchor plane a:
-//   1. weights of chunk 1 of a (dealt during step a-1)           VALU
-//   2. writeback of plane a-2+LO, put of plane a+HI, dealing of
-//      chunk 1 of a+1 (loaded during step a-1)                   LDS
-//   3. the adds of chunk 1 of a                                  LDS atomics
-//   4. loads for a+2 (ranges from rows loaded during a-1, chunk 1's
-//      candidates with the carried positions of a+1), plane a+1+HI, rows of a+3
-//   5. a's full middle chunks, pipelined the same way; at the last anchor
-//      plane, its carried candidates
-// The chunks, their lanes, the points and the order of the adds are those of
-// k_spread_sweep: the results are the same bit for bit.
-
-// one dealt candidate's stencil, ready for its adds (spread_lanes_flat split in two)
-template <int W> struct SPrep {
-    double w0v[W], w1m[W], w2m[W];
-    int roff[W];
-    int base;  // byte offset of the stencil's x start in a ring plane
-    int sl;    // ring slot of stencil plane i2 = 0
-    int z0, z1;
-    bool on;
-};
-
-template <int K>
-__device__ __forceinline__ void spread_prep(const Params& p, const CompDesc& cd, const Cand& cdat, bool act, int a,
-                                            int X0, int Y0, int zorg, int xlo, int xhi, int ylo, int yhi, int plo,
-                                            int phi, double inv_h3, const double* inv_d, SPrep<KT<K>::W>& r) {
-    using S = SSh<K>;
-    constexpr int W = S::W, FAM = S::FAM, NSL = S::NSL;
-    St<W> st[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        const double Xraw = (FAM == 2) ? p.X[(int64_t)3 * cdat.s + d] : cdat.X[d];
-        stencil1d<K, true>(cdat.X[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis,
-                           p.K6, st[d], inv_d[d]);
-    }
-    const int ox = st[0].icl - X0, oy = st[1].icl - Y0, oz = st[2].icl - (zorg + a);
-    const bool bad = (unsigned)(ox + S::GUARD) > (unsigned)(COLX + 15 - (W - 1) + S::GUARD) ||
-                     (unsigned)(oy + 60) > 120u || (unsigned)(oz + 60) > 120u;
-    if (act && bad) atomicOr(p.err, 2);
-    r.on = act && !bad;
-    const int x0 = max(st[0].ist, xlo - ox), x1 = min(st[0].isp, xhi - ox);
-    const int y0 = max(st[1].ist, ylo - oy), y1 = min(st[1].isp, yhi - oy);
-    r.z0 = max(st[2].ist, plo - (a + oz));
-    r.z1 = min(st[2].isp, phi - (a + oz));
-#pragma unroll
-    for (int i = 0; i < W; ++i) {
-        r.w0v[i] = (i >= x0 && i <= x1) ? st[0].w[i] * cdat.V : 0.0;
-        r.w1m[i] = (i >= y0 && i <= y1) ? st[1].w[i] : 0.0;
-        r.w2m[i] = (i >= r.z0 && i <= r.z1) ? st[2].w[i] * inv_h3 : 0.0;
-        r.roff[i] = 8 * COLX * (((oy + i) % COLY + COLY) % COLY);  // masked rows wrap (no pile-up on one row)
-    }
-    r.base = 8 * ox;
-    r.sl = (int)((unsigned)(a + oz + 64 * NSL) % (unsigned)NSL);
-}
-
-// an empty asm on every field: the weights are computed here, not sunk into
-// the adds' branch past the LDS section (the point of the pipelining)
-template <int W> __device__ __forceinline__ void spread_pin(SPrep<W>& r) {
-#pragma unroll
-    for (int i = 0; i < W; ++i) {
-        asm volatile("" : "+v"(r.w0v[i]), "+v"(r.w1m[i]), "+v"(r.w2m[i]), "+v"(r.roff[i]));
-    }
-    int on = r.on;
-    asm volatile("" : "+v"(r.base), "+v"(r.sl), "+v"(r.z0), "+v"(r.z1), "+v"(on));
-    r.on = on;
-}
-
-template <int K>
-__device__ __forceinline__ void spread_adds(double* ring, const SPrep<KT<K>::W>& r) {
-    using S = SSh<K>;
-    constexpr int W = S::W, NSL = S::NSL;
-    if (!r.on) return;  // idle lanes sit the adds out
-    char* const base = reinterpret_cast<char*>(ring) + r.base;
-    int sl = r.sl;
-#pragma unroll
-    for (int i2 = 0; i2 < W; ++i2) {
-        char* const plane = base + sl * (8 * S::SLOT);
-        sl = sl + 1 == NSL ? 0 : sl + 1;
-        if (!(i2 >= r.z0 && i2 <= r.z1)) continue;  // one exec mask per plane
-#pragma unroll
-        for (int i1 = 0; i1 < W; ++i1) {
-            const double t = r.w1m[i1] * r.w2m[i2];
-            double* const row = reinterpret_cast<double*>(plane + r.roff[i1]);
-#pragma unroll
-            for (int i0 = 0; i0 < W; ++i0)
-                __hip_atomic_fetch_add(row + i0, r.w0v[i0] * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-    }
-}
-
-template <int K, bool LVL>
-__global__ __launch_bounds__(SW) void k_spread_pipe(Params p) {
-    using S = SSh<K>;
-    constexpr int LO = S::LO, HI = S::HI, NPL = S::NPL, FAM = S::FAM, W = S::W;
-    __shared__ double ring_mem[S::GUARD + S::NSL * S::SLOT];
-    double* const ring = ring_mem + S::GUARD;
-    const int it = sweep_item(p, p.ncomp);
-    if (it < 0) return;
-    int c;
-    SweepItem si;
-    item_decode(p, it, c, si);
-    const int col = si.col;
-    const int lane = lane_id();
-    ColGeom cg;
-    CompDesc cd;
-    const int* bs;
-    item_patch<LVL>(p, si, c, cg, cd, bs);
-    const int ncx = cg.ncx;
-    const int cx = col % ncx, cy = col / ncx;
-    if (cx == 0 || cx == ncx - 1 || cy == 0 || cy == cg.ncy - 1) return;  // guard columns own no points
-    const int X0 = cg.org[0] + cx * COLX, Y0 = cg.org[1] + cy * COLY;
-    const int zorg = cg.org[2];
-    const int xlo = max(cd.lo[0] - X0, 0), xhi = min(cd.hi[0] - X0, COLX - 1);
-    const int ylo = max(cd.lo[1] - Y0, 0), yhi = min(cd.hi[1] - Y0, COLY - 1);
-    const int plo = max(si.p0, cd.lo[2] - zorg), phi = min(si.p1 - 1, cd.hi[2] - zorg);
-    if (xlo > xhi || ylo > yhi || plo > phi) return;
-    if (p.zmode) {
-        const bool inner = zorg + plo >= p.zlo && zorg + phi <= p.zhi;
-        if (inner != (p.zmode == 1)) return;
-    }
-    const int afirst = max(plo - HI, 0), alast = min(phi - LO, cg.nz - 1);
-    const int col0 = (cy - 1) * ncx + (cx - 1);
-    {
-        bool any = false;
-        for (int a = afirst + lane; a <= alast; a += SW)
-            for (int r = 0; r < 3; ++r)
-                any = any || bs[bucket(cg, a, col0 + r * ncx, 3 * NBAND)] > bs[bucket(cg, a, col0 + r * ncx, 0)];
-        if (!__any(any)) return;
-    }
-    const int nlast = p.nsorted - 1;
-    int loff[NPL];
-    unsigned okxy = 0;
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-        const int q = lane + k * SW;
-        const int xl = q & (COLX - 1), yl = q / COLX;
-        if (xl >= xlo && xl <= xhi && yl >= ylo && yl <= yhi) okxy |= 1u << k;
-        const int x = min(max(X0 + xl, cd.lo[0]), cd.hi[0]), y = min(max(Y0 + yl, cd.lo[1]), cd.hi[1]);
-        loff[k] = (x - cd.lo[0]) + (y - cd.lo[1]) * (int)cd.s1;
-    }
-    auto plane_ptr = [&](int z) {
-        const int zc = min(max(zorg + z, cd.lo[2]), cd.hi[2]);
-        return cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2;
-    };
-    auto rows_load = [&](int a, int* rowv) {
-        const int ac = min(a, alast);
-#pragma unroll
-        for (int r = 0; r < 3; ++r) rowv[r] = bs[bucket(cg, ac, col0 + r * ncx, 0) + min(lane, 27)];
-    };
-    auto cand_at = [&](int e, Cand& d) {
-        e = min(max(e, 0), nlast);
-        const D3 xs = ld3(p.sorted_X + (int64_t)3 * e);
-        d.X[0] = xs.v[0];
-        d.X[1] = xs.v[1];
-        d.X[2] = xs.v[2];
-        d.V = p.sorted_F[(int64_t)c * p.nsorted + e];
-        d.s = FAM == 2 ? p.sorted_s[e] : 0;
-    };
-    const double inv_dx = 1.0 / p.bg.dx[0];
-    const double inv_h3 = 1.0 / p.h3;
-    const double inv_d[3] = {1.0 / p.bg.dx[0], 1.0 / p.bg.dx[1], 1.0 / p.bg.dx[2]};
-    // bank-class dealing of a raw chunk of n lanes: the dealt candidate and its source lane
-    auto deal = [&](const Cand& raw, int n, Cand& d, int& src) {
-        const int cls = lane < n ? ((int)floor((raw.X[0] - cd.xlo[0]) * inv_dx + 0.5) & 15) : 16;
-        src = deal_lanes16<4>(cls);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) d.X[k] = shfl_f64(raw.X[k], src);
-        d.V = shfl_f64(raw.V, src);
-        d.s = FAM == 2 ? __builtin_amdgcn_ds_bpermute(src << 2, raw.s) : 0;
-    };
-    // weights of a dealt chunk: lane anchor a - 1 for the r carried ones
-    auto prep = [&](const Cand& d, int src, int n, int r, int a, SPrep<W>& sp) {
-        spread_prep<K>(p, cd, d, src < n, src < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi, inv_h3,
-                       inv_d, sp);
-    };
-    auto plane_load = [&](int z, double* v) {
-        const double* pb = plane_ptr(z);
-#pragma unroll
-        for (int k = 0; k < NPL; ++k) v[k] = pb[loff[k]];
-    };
-    auto plane_put = [&](int z, const double* v) {
-        double* sl = ring + sslot<K>(z) * S::SLOT;
-#pragma unroll
-        for (int k = 0; k < NPL; ++k) sl[ring_index<K>(lane + k * SW)] = v[k];
-    };
-    auto plane_writeback = [&](int z) {
-        if (z < plo || z > phi) return;
-        const double* sl = ring + sslot<K>(z) * S::SLOT;
-        double* pb = const_cast<double*>(plane_ptr(z));
-        double v[NPL];
-#pragma unroll
-        for (int k = 0; k < NPL; ++k) v[k] = sl[ring_index<K>(lane + k * SW)];
-#pragma unroll
-        for (int k = 0; k < NPL; ++k) {
-            double* dst = ((okxy >> k) & 1u) ? pb + loff[k] : p.sink + lane;
-            *dst = v[k];
-        }
-    };
-    // Per anchor plane b: tot (candidates), h (in its chunk 1 after the r_{b-1}
-    // carried ones), r_b (its last ones, carried into chunk 1 of b+1), and the
-    // sorted positions of those carried ones (lane k < r_b: the k-th).
-    struct An {
-        int tot, h, r, n1;  // n1: lanes of chunk 1 of b (r_{b-1} + h)
-    };
-    auto anchor_info = [&](const Ranges& rg, int rprev, An& A, int& ecar) {
-        A.tot = rg.pre[S::NR];
-        A.h = min(SW - rprev, A.tot);
-        A.r = (A.tot - A.h) % SW;
-        A.n1 = rprev + A.h;
-        ecar = range_pos(rg, max(A.tot - A.r + lane, 0));
-    };
-    // raw chunk 1 of anchor b: the r_{b-1} carried positions (lanes < rprev), then b's first
-    auto chunk1_load = [&](const Ranges& rg, int rprev, int ecar_prev, const An& A, Cand& raw) {
-        const int pos = lane < rprev ? ecar_prev : range_pos(rg, min(max(lane - rprev, 0), max(A.tot - 1, 0)));
-        cand_at(pos, raw);
-    };
-
-    // prologue: planes afirst+LO .. afirst+HI-1 into the ring, plane afirst+HI in
-    // registers; chunk 1 of afirst dealt, chunk 1 of afirst+1 loaded, rows of afirst+2
-    double pv[NPL];
-    for (int z = afirst + LO; z < afirst + HI; ++z) {
-        plane_load(z, pv);
-        plane_put(z, pv);
-    }
-    plane_load(afirst + HI, pv);
-    int rowv[3];
-    Ranges rg;
-    An A0, A1;      // anchors a and a+1
-    int E0, E1;     // carried positions of a and a+1
-    Cand rawA, rawB;
-    rows_load(afirst, rowv);
-    make_ranges_lanes(rowv, rg);
-    anchor_info(rg, 0, A0, E0);
-    chunk1_load(rg, 0, 0, A0, rawA);
-    if (afirst + 1 <= alast) {
-        rows_load(afirst + 1, rowv);
-        make_ranges_lanes(rowv, rg);
-        anchor_info(rg, A0.r, A1, E1);
-        chunk1_load(rg, A0.r, E0, A1, rawB);
-        rows_load(afirst + 2, rowv);
-    } else {
-        A1 = {0, 0, 0, 0};
-        E1 = 0;
-    }
-    int rprev = 0;  // r_{a-1}: lanes of chunk 1 of a that belong to a-1
-    Cand dc;
-    int dsrc;
-    deal(rawA, A0.n1, dc, dsrc);
-    for (int a = afirst; a <= alast; ++a) {
-        // 1. weights of chunk 1 of a
-        SPrep<W> sp;
-        prep(dc, dsrc, A0.n1, rprev, a, sp);
-        spread_pin(sp);
-        __builtin_amdgcn_sched_barrier(0);  // keep the weights' VALU ahead of the LDS waits below
-        // 2. LDS section: writeback, put, dealing of chunk 1 of a+1
-        if (a >= afirst + 2) plane_writeback(a - 2 + LO);
-        plane_put(a + HI, pv);
-        Cand dn;
-        int nsrc = 0;
-        if (a + 1 <= alast) deal(rawB, A1.n1, dn, nsrc);
-        // 3. the adds of chunk 1 of a
-        spread_adds<K>(ring, sp);
-        // 4. loads for a+2: its chunk 1, the carried positions; plane a+1+HI; rows of a+3
-        An A2 = {0, 0, 0, 0};
-        int E2 = 0;
-        Cand rawC;
-        if (a + 2 <= alast) {
-            make_ranges_lanes(rowv, rg);
-            anchor_info(rg, A1.r, A2, E2);
-            chunk1_load(rg, A1.r, E1, A2, rawC);
-        }
-        if (a + 1 <= alast) plane_load(a + 1 + HI, pv);
-        if (a + 3 <= alast) rows_load(a + 3, rowv);
-        // 5. a's full middle chunks (dense planes), pipelined by one chunk
-        const int nmid = (A0.tot - A0.h) / SW;
-        if (nmid > 0) {
-            int rowm[3];
-            rows_load(a, rowm);
-            Ranges rgm;
-            make_ranges_lanes(rowm, rgm);
-            Cand raw, dm;
-            int msrc;
-            cand_at(range_pos(rgm, A0.h + lane), raw);
-            deal(raw, SW, dm, msrc);
-            for (int k = 0; k < nmid; ++k) {
-                if (k + 1 < nmid) cand_at(range_pos(rgm, A0.h + SW * (k + 1) + lane), raw);
-                SPrep<W> mp;
-                prep(dm, msrc, SW, 0, a, mp);
-                spread_pin(mp);
-                __builtin_amdgcn_sched_barrier(0);
-                if (k + 1 < nmid) deal(raw, SW, dm, msrc);
-                spread_adds<K>(ring, mp);
-            }
-        }
-        if (a == alast && A0.r > 0) {  // the last anchor plane's carried candidates
-            Cand raw, dl;
-            int lsrc;
-            cand_at(E0, raw);
-            deal(raw, A0.r, dl, lsrc);
-            SPrep<W> lp;
-            prep(dl, lsrc, A0.r, 0, a, lp);
-            spread_adds<K>(ring, lp);
-        }
-        // shift the pipeline
-        rprev = A0.r;
-        A0 = A1;
-        A1 = A2;
-        E0 = E1;
-        E1 = E2;
-        rawB = rawC;
-        dc = dn;
-        dsrc = nsrc;
-    }
-    plane_writeback(alast - 1 + LO);
-    plane_writeback(alast + LO);
-}
-
-// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 // Segment length: about IBTK_LE_SEG_ITEMS (column, segment) items over the
@@ -2345,13 +2014,8 @@ template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s
     if (ev0) (void)hipEventRecord(ev0, s);  // the events bracket the sweep kernel alone
     const long items = (long)p.item_bound * p.ncomp;
     if (items > 0) {
-        if (IBTK_LE_SPREAD_PIPE && !S_ROT<K>) {
-            if (p.pd) hipLaunchKernelGGL((k_spread_pipe<K, true>), dim3(sweep_grid(p, items)), dim3(SW), 0, s, p);
-            else hipLaunchKernelGGL((k_spread_pipe<K, false>), dim3(sweep_grid(p, items)), dim3(SW), 0, s, p);
-        } else {
-            if (p.pd) hipLaunchKernelGGL((k_spread_sweep<K, true>), dim3(sweep_grid(p, items)), dim3(SW), 0, s, p);
-            else hipLaunchKernelGGL((k_spread_sweep<K, false>), dim3(sweep_grid(p, items)), dim3(SW), 0, s, p);
-        }
+        if (p.pd) hipLaunchKernelGGL((k_spread_sweep<K, true>), dim3(sweep_grid(p, items)), dim3(SW), 0, s, p);
+        else hipLaunchKernelGGL((k_spread_sweep<K, false>), dim3(sweep_grid(p, items)), dim3(SW), 0, s, p);
     }
     if (ev1) (void)hipEventRecord(ev1, s);
     return hipGetLastError();
