@@ -115,22 +115,8 @@ __device__ __forceinline__ int wrap(int i, int lo, int n) {
 // mode 0: fill (ghost <- its image with every periodic dim wrapped at once)
 // mode 1: fold dim dreg (interior-in-dreg point += ghost point), one source per destination
 // mode 2: zero
-__global__ __launch_bounds__(BLOCK) void k_ghost(GhostSet gs, int ndim, int dreg, int mode, int p0, int p1, int p2) {
-    const GhostDesc& g = gs.g[blockIdx.z];
-    const int per[3] = {p0, p1, p2};
-    int ext[3];
-    ghost_ext(g, ndim, dreg, per, ext);
-    const unsigned t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t >= (unsigned)ext[0] * (unsigned)ext[1] || (int)blockIdx.y >= ext[2]) return;
-    const int q[3] = {(int)(t % (unsigned)ext[0]), (int)(t / (unsigned)ext[0]), (int)blockIdx.y};
-    int pt[3] = {0, 0, 0};
-    for (int d = 0; d < ndim; ++d) {
-        if (d == dreg) {
-            const int nlo = g.ilo[d] - g.lo[d];
-            pt[d] = q[d] < nlo ? g.lo[d] + q[d] : g.ihi[d] + 1 + (q[d] - nlo);
-        } else if (full_dim(d, dreg, per)) pt[d] = g.lo[d] + q[d];
-        else pt[d] = g.ilo[d] + q[d];
-    }
+__device__ __forceinline__ void ghost_point(const GhostDesc& g, int ndim, int dreg, int mode, const int* per,
+                                            const int* pt) {
     if (mode == 2) {
         g.u[goff(g, ndim, pt)] = 0.0;
         return;
@@ -155,6 +141,36 @@ __global__ __launch_bounds__(BLOCK) void k_ghost(GhostSet gs, int ndim, int dreg
     g.u[od] = g.u[od] + g.u[os];
 }
 
+// VX points of dim 0 per thread (q0 + v ex0: each instruction coalesced) in the
+// passes where dim 0 is long (dreg > 0: its whole ghost box or interior): VX
+// independent loads in flight per thread instead of one.
+template <int VX>
+__global__ __launch_bounds__(BLOCK) void k_ghost(GhostSet gs, int ndim, int dreg, int mode, int p0, int p1, int p2) {
+    const GhostDesc& g = gs.g[blockIdx.z];
+    const int per[3] = {p0, p1, p2};
+    int ext[3];
+    ghost_ext(g, ndim, dreg, per, ext);
+    const unsigned ex0 = (unsigned)(ext[0] + VX - 1) / VX;  // thread columns along dim 0
+    const unsigned t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= ex0 * (unsigned)ext[1] || (int)blockIdx.y >= ext[2]) return;
+    const int q0 = (int)(t % ex0), q[2] = {(int)(t / ex0), (int)blockIdx.y};  // points q0 + v ex0 (coalesced per v)
+    int base[3] = {0, 0, 0};
+    for (int d = 0; d < ndim; ++d) {
+        const int qd = d == 0 ? q0 : q[d - 1];
+        if (d == dreg) {
+            const int nlo = g.ilo[d] - g.lo[d];
+            base[d] = qd < nlo ? g.lo[d] + qd : g.ihi[d] + 1 + (qd - nlo);
+        } else if (full_dim(d, dreg, per)) base[d] = g.lo[d] + qd;
+        else base[d] = g.ilo[d] + qd;
+    }
+#pragma unroll
+    for (int v = 0; v < VX; ++v) {
+        if (q0 + v * (int)ex0 >= ext[0]) break;
+        const int pt[3] = {base[0] + v * (int)ex0, base[1], base[2]};  // dreg > 0 when VX > 1: dim 0 is contiguous
+        ghost_point(g, ndim, dreg, mode, per, pt);
+    }
+}
+
 static hipError_t ghost_pass(const GhostDesc* gds, int n, int ndim, int dreg, int mode, const int* per,
                              hipStream_t s) {
     for (int first = 0; first < n; first += GSET) {
@@ -172,8 +188,19 @@ static hipError_t ghost_pass(const GhostDesc* gds, int n, int ndim, int dreg, in
         }
         if (m01 <= 0 || m2 <= 0) continue;
         if (m01 >= (1LL << 32) || m2 > 65535) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_ghost, dim3((unsigned)((m01 + BLOCK - 1) / BLOCK), (unsigned)m2, (unsigned)cnt),
-                           dim3(BLOCK), 0, s, gs, ndim, dreg, mode, per[0], per[1], ndim > 2 ? per[2] : 0);
+        if (dreg > 0) {  // dim 0 long and contiguous: 4 points a thread
+            long long mv = 0;
+            for (int i = 0; i < cnt; ++i) {
+                int ext[3];
+                ghost_ext(gs.g[i], ndim, dreg, per, ext);
+                mv = std::max(mv, (long long)((ext[0] + 3) / 4) * ext[1]);
+            }
+            hipLaunchKernelGGL(k_ghost<4>, dim3((unsigned)((mv + BLOCK - 1) / BLOCK), (unsigned)m2, (unsigned)cnt),
+                               dim3(BLOCK), 0, s, gs, ndim, dreg, mode, per[0], per[1], ndim > 2 ? per[2] : 0);
+        } else {
+            hipLaunchKernelGGL(k_ghost<1>, dim3((unsigned)((m01 + BLOCK - 1) / BLOCK), (unsigned)m2, (unsigned)cnt),
+                               dim3(BLOCK), 0, s, gs, ndim, dreg, mode, per[0], per[1], ndim > 2 ? per[2] : 0);
+        }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
