@@ -420,6 +420,7 @@ static int make_comps(const ibtk_le_patch_geom* g, int centering, int axis, doub
                 cd.lo[d] = cd.hi[d] = 0;
             }
         }
+        cd.zcell = (nd == 3 && !((shift_mask >> 2) & 1)) ? 1 : 0;
         int64_t sd;
         array_strides(g, n, cd.s1, cd.s2, sd);
         cd.u = base + (int64_t)depth_index * sd;

@@ -55,6 +55,7 @@ struct CompDesc {
     double xlo[3];   // the "x_lower" argument the Fortran receives (frame shift applied)
     int qcomp;       // which AoS component of Q this array pairs with
     int axis;        // `axis` argument (DISCONTINUOUS_LINEAR)
+    int zcell;       // 3-D: the z frame is the cell frame of the bin keys (not shifted by dx/2)
     int64_t s1, s2;  // strides of dims 1 and 2 (elements)
 };
 
@@ -173,6 +174,8 @@ struct Params {
     double* sink;              // 64 doubles: the store target of masked-off lanes (branch-free stores)
     unsigned long long* stamps;  // diagnostic phase clocks (nullptr: off)
     int dbg;                     // diagnostic switches (0: off)
+    int fcomp[MAXC];             // 3-D spread: component c of this launch is component fcomp[c] of the call
+                                 // (comp[], sorted_F rows, the level's patch table); set by the launcher
     int ipl_frames;              // 3-D interp: 1 = the components' frames allow the plane sweep (two frames
                                  // per axis, k_interp_planes), 0 = they do not, -1 = check p.comp
 };

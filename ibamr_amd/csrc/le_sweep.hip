@@ -1077,6 +1077,12 @@ bool interp_plane_frames(const CompDesc* comp, int nc) {
 #ifndef IBTK_LE_SPREAD_FDIRECT
 #define IBTK_LE_SPREAD_FDIRECT 0  // 1: candidates read F through sorted_s (no k_gather_F_col pass)
 #endif
+#ifndef IBTK_LE_SPREAD_ZLOW
+#define IBTK_LE_SPREAD_ZLOW 0  // 1: cell-frame-in-z components with a ring one slot shorter (a launch of their own)
+#endif
+#ifndef IBTK_LE_DIAG_SPREAD_LDSPAD
+#define IBTK_LE_DIAG_SPREAD_LDSPAD 0  // diagnostic: extra doubles of LDS per spread wave (occupancy probe)
+#endif
 #ifndef IBTK_LE_DIAG_SPREAD_NOPROC
 #define IBTK_LE_DIAG_SPREAD_NOPROC 0
 #endif
@@ -1086,9 +1092,14 @@ bool interp_plane_frames(const CompDesc* comp, int nc) {
 #ifndef IBTK_LE_SPREAD_ROT
 #define IBTK_LE_SPREAD_ROT 0  // measured 30 % slower on cfg4 (the spread is issue-bound)
 #endif
-template <int K> struct SSh {
+// ZH: the highest stencil plane relative to the anchor plane that the item's
+// component reaches -- KT::HI in general, HI - 1 for a closed-form kernel whose
+// component has the bin keys' own z frame (cell-like in z: its stencil starts at
+// NINT - W/2, e.g. IB_4 a-2 .. a+1), one ring slot less: 5 slots instead of 6
+// for IB_4, 7 spread waves per CU instead of 6 (spread_zhi).
+template <int K, int ZH = KT<K>::HI> struct SSh {
     using T = KT<K>;
-    static constexpr int W = T::W, LO = T::LO, HI = T::HI, FAM = T::FAM;
+    static constexpr int W = T::W, LO = T::LO, HI = ZH, FAM = T::FAM;
     static constexpr int NS = HI - LO + 1;              // planes an anchor plane reaches
     static constexpr int NSL = NS + 1;                  // ring slots: the planes two anchors reach
     static constexpr int PV = COLX * COLY;              // owned points per plane
@@ -1119,8 +1130,8 @@ template <int K> __device__ __forceinline__ int ring_index(int q) {
     return (q >> 5) * SSh<K>::RS + (q & (COLX - 1));
 }
 
-template <int K> __device__ __forceinline__ int sslot(int prel) {
-    using S = SSh<K>;
+template <int K, int ZH = KT<K>::HI> __device__ __forceinline__ int sslot(int prel) {
+    using S = SSh<K, ZH>;
     return (int)((unsigned)(prel + 16 * S::NSL) % (unsigned)S::NSL);  // prel >= -HI + LO > -16*NSL
 }
 
@@ -1184,11 +1195,11 @@ struct Cand {
 // lanes dealt to distinct bank classes stay conflict-free for all W^3 adds.
 // Within one instruction the lanes that hit the same point add in lane order,
 // so every point receives its contributions in a fixed order (bit-stable).
-template <int K>
+template <int K, int ZH>
 __device__ __forceinline__ void spread_lanes_rows(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
                                              bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
                                              int yhi, int plo, int phi, double inv_h3, const double* inv_d, Clk& clk) {
-    using S = SSh<K>;
+    using S = SSh<K, ZH>;
     constexpr int W = S::W, FAM = S::FAM, LO = S::LO, HI = S::HI, NS = S::NS, NSL = S::NSL;
     St<W> st[3];
 #pragma unroll
@@ -1265,12 +1276,12 @@ __device__ __forceinline__ void spread_lanes_rows(const Params& p, const CompDes
 // point; clamping would pile the masked rows of dense chunks onto one row), so
 // there is no exec mask and branch per row -- one address add per row instead; validity masks from clipped ranges; IB_4's square root by rsq
 // and Newton steps (the spread is compared by tolerance).
-template <int K>
+template <int K, int ZH>
 __device__ __forceinline__ void spread_lanes_flat(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
                                                   bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
                                                   int yhi, int plo, int phi, double inv_h3, const double* inv_d,
                                                   Clk& clk) {
-    using S = SSh<K>;
+    using S = SSh<K, ZH>;
     constexpr int W = S::W, FAM = S::FAM, NSL = S::NSL;
     St<W> st[3];
 #pragma unroll
@@ -1288,7 +1299,10 @@ __device__ __forceinline__ void spread_lanes_flat(const Params& p, const CompDes
     // owned and clipped-in ranges of the stencil indices
     const int x0 = max(st[0].ist, xlo - ox), x1 = min(st[0].isp, xhi - ox);
     const int y0 = max(st[1].ist, ylo - oy), y1 = min(st[1].isp, yhi - oy);
-    const int z0 = max(st[2].ist, plo - (a + oz)), z1 = min(st[2].isp, phi - (a + oz));
+    // planes within the ring's reach of the lane's anchor, [LO, ZH] (a stencil moved
+    // by a NINT tie of the multiply -- a weight of an ulp's order -- is cut there)
+    const int z0 = max(max(st[2].ist, plo - (a + oz)), S::LO - oz);
+    const int z1 = min(min(st[2].isp, phi - (a + oz)), S::HI - oz);
     double w0v[W], w1m[W], w2m[W];
     int roff[W];  // byte offset of stencil row i1 (wrapped into the column) from row 0 of the plane
 #pragma unroll
@@ -1331,14 +1345,14 @@ __device__ __forceinline__ void spread_lanes_flat(const Params& p, const CompDes
     clk.lap(3);
 }
 
-template <int K>
+template <int K, int ZH>
 __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
                                              bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
                                              int yhi, int plo, int phi, double inv_h3, const double* inv_d, Clk& clk) {
     if constexpr (IBTK_LE_SPREAD_FLAT)
-        spread_lanes_flat<K>(p, cd, ring, cdat, act, a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi, inv_h3, inv_d, clk);
+        spread_lanes_flat<K, ZH>(p, cd, ring, cdat, act, a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi, inv_h3, inv_d, clk);
     else
-        spread_lanes_rows<K>(p, cd, ring, cdat, act, a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi, inv_h3, inv_d, clk);
+        spread_lanes_rows<K, ZH>(p, cd, ring, cdat, act, a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi, inv_h3, inv_d, clk);
 }
 
 // The adds of one staged candidate per lane for W = 4 kernels, conflict-free by
@@ -1353,11 +1367,11 @@ __device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd
 // staging order and the lane order within an instruction (bit-stable).
 // Clipped and not-owned points get weight 0 and a trash address of the same
 // class; idle lanes sit the adds out.
-template <int K>
+template <int K, int ZH>
 __device__ __forceinline__ void spread_rot(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
                                            bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
                                            int yhi, int plo, int phi, double inv_h3, const double* inv_d) {
-    using S = SSh<K>;
+    using S = SSh<K, ZH>;
     constexpr int W = S::W, FAM = S::FAM, LO = S::LO, NS = S::NS, NSL = S::NSL, RS = S::RS;
     static_assert(W == 4, "rotated adds: 16 points per stencil plane");
     St<W> st[3];
@@ -1446,17 +1460,20 @@ __device__ __forceinline__ void spread_rot(const Params& p, const CompDesc& cd, 
 // ring holds planes a+LO..a+HI (u_old, then accumulating) plus a+HI+1 in
 // flight; plane a+LO is written back after anchor a and its slot takes plane
 // a+HI+2.  The candidates of anchor a+1 are staged while anchor a is added.
-template <int K, bool LVL>
+template <int K, bool LVL, int ZH>
 __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
-    using S = SSh<K>;
+    using S = SSh<K, ZH>;
     constexpr int LO = S::LO, HI = S::HI, NPL = S::NPL, FAM = S::FAM;
-    __shared__ double ring_mem[S::GUARD + S::NSL * S::SLOT];
+    __shared__ double ring_mem[S::GUARD + S::NSL * S::SLOT + IBTK_LE_DIAG_SPREAD_LDSPAD];
     double* const ring = ring_mem + S::GUARD;
+    if constexpr (IBTK_LE_DIAG_SPREAD_LDSPAD > 0)  // diagnostic: occupancy probe (keep the pad allocated)
+        if (p.dbg == 12345) ring_mem[S::GUARD + S::NSL * S::SLOT] = 0.0;
     const int it = sweep_item(p, p.ncomp);
     if (it < 0) return;
     int c;
     SweepItem si;
     item_decode(p, it, c, si);
+    c = p.fcomp[c];  // this launch's component c is the call's component fcomp[c]
     const int col = si.col;
     const int lane = lane_id();
     ColGeom cg;
@@ -1538,7 +1555,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
             return;
         }
         if constexpr (S::ROT) {
-            spread_rot<K>(p, cd, ring, mine, lane < n, lane < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo,
+            spread_rot<K, ZH>(p, cd, ring, mine, lane < n, lane < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo,
                           phi, inv_h3, inv_d);
             return;
         }
@@ -1548,7 +1565,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
 #elif IBTK_LE_SPREAD_DEAL == 0
         const int src = lane;
         if (true) {
-            spread_lanes<K>(p, cd, ring, mine, src < n, src < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi,
+            spread_lanes<K, ZH>(p, cd, ring, mine, src < n, src < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi,
                             inv_h3, inv_d, clk);
             return;
         }
@@ -1566,7 +1583,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         for (int k = 0; k < 3; ++k) d.X[k] = shfl_f64(mine.X[k], src);
         d.V = shfl_f64(mine.V, src);
         d.s = FAM == 2 ? __builtin_amdgcn_ds_bpermute(src << 2, mine.s) : 0;
-        spread_lanes<K>(p, cd, ring, d, src < n, src < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi,
+        spread_lanes<K, ZH>(p, cd, ring, d, src < n, src < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi,
                         inv_h3, inv_d, clk);
     };
     // plane z -> registers (the lane's NPL points); registers -> ring slot
@@ -1576,13 +1593,13 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         for (int k = 0; k < NPL; ++k) v[k] = IBTK_LE_DIAG_SPREAD_NOLOAD ? 0.0 : pb[loff[k]];
     };
     auto plane_put = [&](int z, const double* v) {
-        double* sl = ring + sslot<K>(z) * S::SLOT;
+        double* sl = ring + sslot<K, ZH>(z) * S::SLOT;
 #pragma unroll
         for (int k = 0; k < NPL; ++k) sl[ring_index<K>(lane + k * SW)] = v[k];
     };
     auto plane_writeback = [&](int z) {  // owned points of plane z, ring -> array
         if (z < plo || z > phi) return;
-        const double* sl = ring + sslot<K>(z) * S::SLOT;
+        const double* sl = ring + sslot<K, ZH>(z) * S::SLOT;
         double* pb = const_cast<double*>(plane_ptr(z));
         double v[NPL];
 #pragma unroll
@@ -2011,12 +2028,29 @@ template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s
         if (rec3) hipLaunchKernelGGL(k_gather_F_col<true>, g, b, 0, s, p, p.nsorted, const_cast<double*>(p.sorted_F));
         else hipLaunchKernelGGL(k_gather_F_col<false>, g, b, 0, s, p, p.nsorted, const_cast<double*>(p.sorted_F));
     }
-    if (ev0) (void)hipEventRecord(ev0, s);  // the events bracket the sweep kernel alone
-    const long items = (long)p.item_bound * p.ncomp;
-    if (items > 0) {
-        if (p.pd) hipLaunchKernelGGL((k_spread_sweep<K, true>), dim3(sweep_grid(p, items)), dim3(SW), 0, s, p);
-        else hipLaunchKernelGGL((k_spread_sweep<K, false>), dim3(sweep_grid(p, items)), dim3(SW), 0, s, p);
+    if (ev0) (void)hipEventRecord(ev0, s);  // the events bracket the sweep kernels alone
+    // IBTK_LE_SPREAD_ZLOW: components whose z frame is the bin keys' cell frame
+    // take a ring one slot shorter (SSh's ZH: 7 waves per CU instead of 6 for
+    // IB_4), as a launch of their own.  Measured (profiles/r02z/zlow): cfg4
+    // spread 17.3 ms against 17.6 with the groups side by side on two streams,
+    // 17.3 one after the other; cfg5 3.7 / 4.1 against 3.4 (two launches, two
+    // tails).  Off: one launch, every component with the full ring.
+    Params q[2] = {p, p};
+    for (int g = 0; g < 2; ++g) q[g].ncomp = 0;
+    for (int c = 0; c < p.ncomp; ++c) {
+        const bool low = KT<K>::FAM == 0 && !SSh<K>::ROT && p.comp[c].zcell && IBTK_LE_SPREAD_ZLOW;
+        Params& g = q[low ? 0 : 1];
+        g.fcomp[g.ncomp++] = c;
     }
+    auto launch = [&](const Params& g, auto zh) {
+        constexpr int ZH = decltype(zh)::value;
+        const long items = (long)g.item_bound * g.ncomp;
+        if (items <= 0) return;
+        if (g.pd) hipLaunchKernelGGL((k_spread_sweep<K, true, ZH>), dim3(sweep_grid(g, items)), dim3(SW), 0, s, g);
+        else hipLaunchKernelGGL((k_spread_sweep<K, false, ZH>), dim3(sweep_grid(g, items)), dim3(SW), 0, s, g);
+    };
+    if constexpr (IBTK_LE_SPREAD_ZLOW) launch(q[0], std::integral_constant<int, KT<K>::HI - 1>{});
+    launch(q[1], std::integral_constant<int, KT<K>::HI>{});
     if (ev1) (void)hipEventRecord(ev1, s);
     return hipGetLastError();
 }
