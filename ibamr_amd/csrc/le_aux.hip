@@ -243,13 +243,15 @@ hipError_t launch_zero_ghosts(int ndim, const GhostDesc* g, int n, hipStream_t s
 // blockIdx.z = patch * ncomp + array; arrays[patch * ncomp + array] (depth
 // slices of a cell array are consecutive arrays of one allocation).
 // ---------------------------------------------------------------------------
+template <int VX>
 __global__ __launch_bounds__(BLOCK) void k_level_fill(LevelTiling t, int dreg, const int* tile_of_patch,
                                                       const int* patch_of_tile, double* const* arrays, int depth) {
     // The source of a ghost point is the neighbouring tile in direction dir (per dim
     // -1, 0, +1) at local index li - dir n: the 27 neighbours' arrays are looked up
     // once per workgroup (the tiles are equal, so a ghost layer no wider than a
     // patch reaches only them; wrapped in the periodic dims, none across a
-    // physical boundary -- left to the boundary operators).
+    // physical boundary -- left to the boundary operators).  VX points of dim 0
+    // per thread (q0 + v ex0) where dim 0 is long (dreg > 0).
     const int q = blockIdx.z / t.ncomp, a = blockIdx.z - q * t.ncomp;
     __shared__ const double* nbr[27];
     if (threadIdx.x < 27) {
@@ -273,26 +275,32 @@ __global__ __launch_bounds__(BLOCK) void k_level_fill(LevelTiling t, int dreg, c
     for (int d = 0; d < 3; ++d) ext[d] = t.n[d] + 2 * t.g + ((t.side && d == a) ? 1 : 0);  // array extent
     int rx[3];  // region extents of this pass: ghost layers in dreg, all below it, unique points above
     for (int d = 0; d < 3; ++d) rx[d] = d < dreg ? ext[d] : (d == dreg ? ext[d] - t.n[d] : t.n[d]);
+    const unsigned ex0 = (unsigned)(rx[0] + VX - 1) / VX;
     const unsigned tid = blockIdx.x * BLOCK + threadIdx.x;
-    if (tid >= (unsigned)rx[0] * (unsigned)rx[1] || (int)blockIdx.y >= rx[2]) return;
-    const int r[3] = {(int)(tid % (unsigned)rx[0]), (int)(tid / (unsigned)rx[0]), (int)blockIdx.y};
-    int li[3], sl[3], k = 0, mul = 1;
-    for (int d = 0; d < 3; ++d) {
-        if (d < dreg) li[d] = r[d];
-        else if (d == dreg) li[d] = r[d] < t.g ? r[d] : t.g + t.n[d] + (r[d] - t.g);
-        else li[d] = t.g + r[d];
-        const int dir = li[d] < t.g ? -1 : (li[d] >= t.g + t.n[d] ? 1 : 0);
-        sl[d] = li[d] - dir * t.n[d];
-        k += (dir + 1) * mul;
-        mul *= 3;
-    }
-    const double* src = nbr[k];
-    if (!src) return;
-    const int64_t di = (int64_t)li[0] + (int64_t)ext[0] * (li[1] + (int64_t)ext[1] * li[2]);
-    const int64_t si = (int64_t)sl[0] + (int64_t)ext[0] * (sl[1] + (int64_t)ext[1] * sl[2]);
+    if (tid >= ex0 * (unsigned)rx[1] || (int)blockIdx.y >= rx[2]) return;
+    const int q0 = (int)(tid % ex0), r1 = (int)(tid / ex0), r2 = (int)blockIdx.y;
     const int64_t vol = (int64_t)ext[0] * ext[1] * ext[2];
     double* dst = arrays[(size_t)q * t.ncomp + a];
-    for (int j = 0; j < depth; ++j) dst[j * vol + di] = src[j * vol + si];
+#pragma unroll
+    for (int v = 0; v < VX; ++v) {
+        const int r[3] = {q0 + v * (int)ex0, r1, r2};
+        if (r[0] >= rx[0]) break;
+        int li[3], sl[3], k = 0, mul = 1;
+        for (int d = 0; d < 3; ++d) {
+            if (d < dreg) li[d] = r[d];
+            else if (d == dreg) li[d] = r[d] < t.g ? r[d] : t.g + t.n[d] + (r[d] - t.g);
+            else li[d] = t.g + r[d];
+            const int dir = li[d] < t.g ? -1 : (li[d] >= t.g + t.n[d] ? 1 : 0);
+            sl[d] = li[d] - dir * t.n[d];
+            k += (dir + 1) * mul;
+            mul *= 3;
+        }
+        const double* src = nbr[k];
+        if (!src) continue;
+        const int64_t di = (int64_t)li[0] + (int64_t)ext[0] * (li[1] + (int64_t)ext[1] * li[2]);
+        const int64_t si = (int64_t)sl[0] + (int64_t)ext[0] * (sl[1] + (int64_t)ext[1] * sl[2]);
+        for (int j = 0; j < depth; ++j) dst[j * vol + di] = src[j * vol + si];
+    }
 }
 
 // every element of narr arrays := 0 (array i: count[i] doubles, 16-byte aligned
@@ -336,8 +344,20 @@ hipError_t launch_level_fill(const LevelTiling& t, int npatch, const int* tile_o
         if (m01 <= 0 || m2 <= 0) continue;
         const long long nz = (long long)npatch * t.ncomp;
         if (m01 >= (1LL << 32) || m2 > 65535 || nz > 65535) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_level_fill, dim3((unsigned)((m01 + BLOCK - 1) / BLOCK), (unsigned)m2, (unsigned)nz),
-                           dim3(BLOCK), 0, s, t, dreg, tile_of_patch, patch_of_tile, arrays, depth);
+        if (dreg > 0) {  // dim 0 long: 4 points a thread
+            long long mv = 0;
+            for (int a = 0; a < t.ncomp; ++a) {
+                const int ext0 = t.n[0] + 2 * t.g + ((t.side && a == 0) ? 1 : 0);
+                const int ext1 = t.n[1] + 2 * t.g + ((t.side && a == 1) ? 1 : 0);
+                const int rx1 = dreg == 1 ? ext1 - t.n[1] : ext1;
+                mv = std::max(mv, (long long)((ext0 + 3) / 4) * rx1);
+            }
+            hipLaunchKernelGGL(k_level_fill<4>, dim3((unsigned)((mv + BLOCK - 1) / BLOCK), (unsigned)m2, (unsigned)nz),
+                               dim3(BLOCK), 0, s, t, dreg, tile_of_patch, patch_of_tile, arrays, depth);
+        } else {
+            hipLaunchKernelGGL(k_level_fill<1>, dim3((unsigned)((m01 + BLOCK - 1) / BLOCK), (unsigned)m2, (unsigned)nz),
+                               dim3(BLOCK), 0, s, t, dreg, tile_of_patch, patch_of_tile, arrays, depth);
+        }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
