@@ -572,7 +572,7 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     m->cg = cg;
     m->npatch = 0;
     m->nbuckets_total = cg.nbuckets;
-    if (cols) sweep_segments(cg, m->S, m->nseg, ctx->tune.seg_items);
+    if (cols) sweep_segments(cg, m->S, m->nseg, ctx->tune.seg_items, false);
     m->geom = *geom;
     m->has_indices = indices_dev != nullptr;
     m->has_xshift = Xshift_dev != nullptr;
@@ -944,7 +944,7 @@ extern "C" int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch,
         P.cg = cg;
         P.bucket_base = (int)nb;
         P.jbase = (int)nj;
-        sweep_segments(cg, P.S, P.nseg, ctx->tune.seg_items);
+        sweep_segments(cg, P.S, P.nseg, ctx->tune.seg_items, true);
         for (int d = 0; d < 3; ++d) {
             P.xlo[d] = geoms[q].x_lower[d];
             P.ilower[d] = geoms[q].ilower[d];

@@ -215,7 +215,7 @@ hipError_t launch_gather_col(int kernel, const Params& p, int n, int* sorted_s, 
                              const unsigned* sorted_key, int nbuckets, int* bucket_start, hipStream_t s);
 hipError_t launch_interp_sweep(int kernel, const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_spread_sweep(int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
-void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items);
+void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items, bool level);
 hipError_t launch_item_table(int kernel, const Params& p, int target, int heavy, int* nsub, int* start, SweepItem* tab, int* ntot,
                              void* temp, size_t temp_bytes, hipStream_t s);
 

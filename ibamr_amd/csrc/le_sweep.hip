@@ -1731,12 +1731,16 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
 // planes) keeps two segments of ~70 planes rather than five of 32 -- measured
 // on rank 0's slab of an 8-way cfg4 split, 6.2 -> 5.5 ms per step
 // (bench.py --solo-slab 8, profiles/r02v).
-constexpr int MIN_SEG = 64;
-void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items) {
+// A level's patches (64^3 on cfg5) take segments down to 32 planes: two per patch
+// instead of one gives the clustered level twice the items to balance (cfg5
+// 2.00e9 -> 2.14e9 marker-ops/s, spread sweep 3.41 -> 3.08 ms, profiles/r02z).
+constexpr int MIN_SEG = 64, MIN_SEG_LEVEL = 32;
+void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items, bool level) {
+    const int min_seg = level ? MIN_SEG_LEVEL : MIN_SEG;
     long long want = seg_items > 0 ? seg_items : IBTK_LE_SEG_ITEMS;
     long long s = ((long long)cg.nz * cg.ncol + want - 1) / want;
-    if (s < MIN_SEG && seg_items <= 0) {
-        const long long ns = cg.nz / MIN_SEG > 1 ? cg.nz / MIN_SEG : 1;  // segments of >= MIN_SEG planes
+    if (s < min_seg && seg_items <= 0) {
+        const long long ns = cg.nz / min_seg > 1 ? cg.nz / min_seg : 1;  // segments of >= min_seg planes
         s = (cg.nz + ns - 1) / ns;
     }
     if (s < 32) s = 32;
