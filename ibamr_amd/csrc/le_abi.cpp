@@ -138,7 +138,6 @@ struct ibtk_le_markers_s {
     std::vector<int> off_dev;             // what entry_off holds
     DevBuf pd, entry_off;
     int nbuckets_total = 0, njobs = 0;
-    int kbits = 0;  // class digit bits of the sorted 3-D keys
     bool has_indices = false, has_xshift = false;
     bool cand_valid = false;
     bool dedup_done = false, has_dups = false;
@@ -225,7 +224,6 @@ extern "C" int ibtk_le_ctx_tune(ibtk_le_ctx ctx, const char* key, int value) {
     else if (k == "split_target") t.split_target = value;
     else if (k == "heavy") t.heavy = value;
     else if (k == "strip") t.strip = value;
-    else if (k == "interp_planes") t.interp_planes = value;
     else if (k == "xcd_block") t.xcd_block = value;
     else return fail(IBTK_LE_ERR_ARG, "unknown tuning key %s", key);
     return IBTK_LE_OK;
@@ -490,9 +488,6 @@ extern "C" int ibtk_le_markers_order(ibtk_le_markers m, const int** order_dev) {
 #ifndef IBTK_LE_STRIP
 #define IBTK_LE_STRIP 1  // column rows per strip of the sweep item order (job_column)
 #endif
-#ifndef IBTK_LE_KEY_CLASS_BITS
-#define IBTK_LE_KEY_CLASS_BITS 0  // 4: x mod 16 below the bucket (with static dealing: measured slower)
-#endif
 #ifndef IBTK_LE_SPLIT_TARGET
 #define IBTK_LE_SPLIT_TARGET 12288  // own markers per item above which it is cut (cfg4 items hold ~6.8K)
 #endif
@@ -611,14 +606,11 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     p.X = X_dev;
     p.indices = m->has_indices ? m->indices.as<int>() : nullptr;
     p.Xshift = m->has_xshift ? m->xshift.as<double>() : nullptr;
-    // the class digit below the bucket when the keys have room for it (k_bin_col)
-    p.kbits = cols && (((unsigned long long)cg.nbuckets + 1) << 4) < (1ULL << 32) ? IBTK_LE_KEY_CLASS_BITS : 0;
-    m->kbits = p.kbits;
     if (cols) HIP_TRY(launch_bin_col(kernel, p, n, ctx->keys_in.as<unsigned>(), ctx->vals_in.as<int>(), s));
     else HIP_TRY(launch_bin(geom->ndim, kernel, p, n, ctx->keys_in.as<unsigned>(), ctx->vals_in.as<int>(), s));
     int end_bit = 1;
     if (cols) {
-        while ((1ULL << end_bit) <= ((unsigned long long)cg.nbuckets << p.kbits)) ++end_bit;
+        while ((1ULL << end_bit) <= (unsigned long long)cg.nbuckets) ++end_bit;
     } else {
         end_bit = end_bit_for(bg);
     }
@@ -687,7 +679,6 @@ static int prepare(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const ibtk_le
     p.err = ctx->err.as<int>();
     p.sink = ctx->sink.as<double>();
     p.tune = ctx->tune;
-    p.ipl_frames = -1;
     p.zmode = ctx->zmode;
     p.zlo = ctx->zlo;
     p.zhi = ctx->zhi;
@@ -1008,11 +999,9 @@ extern "C" int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch,
     p.X = X_dev;
     p.indices = m->has_indices ? m->indices.as<int>() : nullptr;
     p.Xshift = m->has_xshift ? m->xshift.as<double>() : nullptr;
-    p.kbits = (((unsigned long long)nb + 1) << 4) < (1ULL << 32) ? IBTK_LE_KEY_CLASS_BITS : 0;
-    m->kbits = p.kbits;
     HIP_TRY(launch_bin_col(kernel, p, n, ctx->keys_in.as<unsigned>(), ctx->vals_in.as<int>(), s));
     int end_bit = 1;
-    while ((1ULL << end_bit) <= ((unsigned long long)nb << p.kbits)) ++end_bit;
+    while ((1ULL << end_bit) <= (unsigned long long)nb) ++end_bit;
     size_t tb = 0;
     HIP_TRY(launch_sort(nullptr, tb, ctx->keys_in.as<unsigned>(), m->sorted_key.as<unsigned>(), ctx->vals_in.as<int>(),
                         m->sorted_l.as<int>(), n, end_bit, s));
@@ -1054,8 +1043,6 @@ static int level_params(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cent
         if (int rc = make_comps(&g, centering, axis, q_dev + (size_t)q * per, q_depth, Q_depth, 0, nc, t)) return rc;
         std::memcpy(m->pdh[q].comp, t.comp, sizeof(t.comp));
         if (q == 0) std::memcpy(p.comp, t.comp, sizeof(t.comp));
-        if (q == 0) p.ipl_frames = 1;
-        if (!interp_plane_frames(t.comp, nc)) p.ipl_frames = 0;
     }
     p.tune = ctx->tune;
     if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;

@@ -352,110 +352,10 @@ __global__ __launch_bounds__(BLOCK) void k_interp_outside(Params p, int n) {
     }
 }
 
-// Direct form: one thread per sorted entry, every component, stencil values read
-// straight from HBM/L2 (no staging).  Neighbouring threads hold neighbouring
-// markers, so a wave's loads hit a compact set of lines.  Entries binned
-// "outside" get V = 0 (their clipped stencil is empty).
-template <int NDIM, int K>
-__global__ __launch_bounds__(BLOCK) void k_interp_direct(Params p, int n) {
-    using T = KT<K>;
-    constexpr int W = T::W, FAM = T::FAM;
-    const int blk = xcd_item(0, gridDim.x, blockIdx.x);
-    const int e = blk * BLOCK + threadIdx.x;
-    if (e >= n) return;
-    const unsigned key = p.sorted_key[e];
-    const int s = p.sorted_s[e];
-    double Xs[NDIM];
-#pragma unroll
-    for (int d = 0; d < NDIM; ++d) Xs[d] = p.sorted_X[(int64_t)NDIM * e + d];
-    const bool out = (key >> BrickT<NDIM>::SHIFT) >= (unsigned)p.bg.nbricks;
-    for (int c = 0; c < p.ncomp; ++c) {
-        const CompDesc& cd = p.comp[c];
-        double acc = 0.0;
-        if (!out) {
-            St<W> st[NDIM];
-            marker_stencils_x<NDIM, K>(p, cd, Xs, s, st);
-            if constexpr (FAM == 3) {
-                bool nonempty = true;
-#pragma unroll
-                for (int d = 0; d < NDIM; ++d) nonempty = nonempty && (st[d].ist <= st[d].isp);
-                if (nonempty)
-                    acc = cd.u[(int64_t)(st[0].icl - cd.lo[0]) + (int64_t)(st[1].icl - cd.lo[1]) * cd.s1 +
-                               (NDIM == 3 ? (int64_t)(st[2 % NDIM].icl - cd.lo[2]) * cd.s2 : 0)];
-            } else {
-                // clipped entries: weight 0 at a clamped (in-array) index, acc + 0 == acc
-                double w[NDIM][W];
-                int64_t o[NDIM][W];
-#pragma unroll
-                for (int d = 0; d < NDIM; ++d) {
-                    const int64_t stride = d == 0 ? 1 : (d == 1 ? cd.s1 : cd.s2);
-#pragma unroll
-                    for (int i = 0; i < W; ++i) {
-                        const bool in = i >= st[d].ist && i <= st[d].isp;
-                        w[d][i] = in ? st[d].w[i] : 0.0;
-                        o[d][i] = (int64_t)(min(max(st[d].icl + i, cd.lo[d]), cd.hi[d]) - cd.lo[d]) * stride;
-                    }
-                }
-                if constexpr (NDIM == 3) {
-#pragma unroll
-                    for (int i2 = 0; i2 < W; ++i2) {
-#pragma unroll
-                        for (int i1 = 0; i1 < W; ++i1) {
-                            const double* row = cd.u + o[1][i1] + o[2][i2];
-                            if constexpr (FAM == 0) {
-                                const double wyz = w[1][i1] * w[2][i2];  // f.m4:1349-1353
-#pragma unroll
-                                for (int i0 = 0; i0 < W; ++i0) {
-                                    const double wt = w[0][i0] * wyz;
-                                    acc = acc + wt * row[o[0][i0]];  // f.m4:1375
-                                }
-                            } else {
-#pragma unroll
-                                for (int i0 = 0; i0 < W; ++i0)
-                                    acc = acc + w[0][i0] * w[1][i1] * w[2][i2] * row[o[0][i0]];  // f.m4:545-548
-                            }
-                        }
-                    }
-                } else {
-#pragma unroll
-                    for (int i1 = 0; i1 < W; ++i1) {
-                        const double* row = cd.u + o[1][i1];
-#pragma unroll
-                        for (int i0 = 0; i0 < W; ++i0) {
-                            if constexpr (FAM == 0) {
-                                const double wt = w[0][i0] * w[1][i1];
-                                acc = acc + wt * row[o[0][i0]];
-                            } else {
-                                acc = acc + w[0][i0] * w[1][i1] * row[o[0][i0]];
-                            }
-                        }
-                    }
-                }
-            }
-        }
-        const int sq = p.qdst ? p.qdst[e] : s;
-        if (sq >= 0) p.Qout[(int64_t)p.Q_depth * sq + cd.qcomp] = acc;
-    }
-}
-
-static int interp_mode() {
-    static int mode = -1;
-    if (mode < 0) {
-        const char* v = getenv("IBTK_LE_INTERP");
-        mode = (v && v[0] == 'd') ? 1 : 0;  // 0 staged, 1 direct
-    }
-    return mode;
-}
-
 template <int NDIM, int K>
 hipError_t launch_interp_t(const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     using S = IShape<NDIM, K>;
     if (ev0) (void)hipEventRecord(ev0, s);
-    if (interp_mode() == 1) {
-        if (n > 0) hipLaunchKernelGGL((k_interp_direct<NDIM, K>), dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n);
-        if (ev1) (void)hipEventRecord(ev1, s);
-        return hipGetLastError();
-    }
     const long items = (long)(p.bg.nbricks / S::GB);
     hipLaunchKernelGGL((k_interp<NDIM, K>), dim3(grid_for(items, 64)), dim3(BLOCK), 0, s, p);
     if (ev1) (void)hipEventRecord(ev1, s);

@@ -105,7 +105,6 @@ struct SweepTune {
     int split_target = 0;  // own markers above which a (column, segment) is cut (k_item_counts)
     int heavy = 0;         // own markers per piece above which an item is scheduled first (-1: never)
     int strip = 0;         // column rows per strip of the item order (0: default)
-    int interp_planes = 0; // 1: the plane interp sweep (k_interp_planes) where it applies (slower: DESIGN.md)
     int xcd_block = 0;     // light sweep items over the XCDs in blocks of this many table entries (1:
                            // round-robin; -1: one contiguous range per XCD; 0: the default, 8)
 };
@@ -135,7 +134,6 @@ struct Params {
     int npatch;
     const int* entry_off;      // level: list entries of patch q are [entry_off[q], entry_off[q+1])
     int nbuckets_total;        // buckets of every patch (entries keyed >= it are outside)
-    int kbits;                 // 3-D bin keys: class digit bits below the bucket (0 or 4)
     int njobs;                 // (segment, column) pairs of every patch
     int strip;                 // item order: column rows per strip (job_column)
     int ncut, cut[4];          // item table: extra cuts at these relative planes (the plane window's edges)
@@ -174,10 +172,6 @@ struct Params {
     double* sink;              // 64 doubles: the store target of masked-off lanes (branch-free stores)
     unsigned long long* stamps;  // diagnostic phase clocks (nullptr: off)
     int dbg;                     // diagnostic switches (0: off)
-    int fcomp[MAXC];             // 3-D spread: component c of this launch is component fcomp[c] of the call
-                                 // (comp[], sorted_F rows, the level's patch table); set by the launcher
-    int ipl_frames;              // 3-D interp: 1 = the components' frames allow the plane sweep (two frames
-                                 // per axis, k_interp_planes), 0 = they do not, -1 = check p.comp
 };
 
 // Host-side launchers (le_kernels.hip).
@@ -196,9 +190,6 @@ hipError_t launch_scan(void* temp, size_t& temp_bytes, const int* in, int* out, 
 
 // 3-D column sweep (le_sweep.hip)
 hipError_t launch_bin_col(int kernel, const Params& p, int n, unsigned* keys, int* vals, hipStream_t s);
-// the components' frames allow the plane interp sweep: in every axis d the
-// components other than d share one frame (side, edge, cell, node data do)
-bool interp_plane_frames(const CompDesc* comp, int nc);
 // z-slab migration classes (le_aux.hip)
 struct SlabMig {
     double L[3];

@@ -16,16 +16,18 @@
 //    (column + stencil halo) and take alternate anchor planes.  One lane per
 //    marker sums its W^3 stencil from the ring in the Fortran loop order (i2,
 //    i1, i0), so the value is bitwise the oracle's.
-//  * spread: one wave per item owns the column's points in its z-segment.
-//    Planes are loaded (u_old) when the first anchor plane that reaches them
-//    comes up and written back when the last one has passed.  The candidates
-//    (markers of the 3x3 neighbouring buckets whose stencil reaches the column:
-//    11 contiguous ranges of the sorted list, by band) stream through full
-//    64-lane chunks across anchor planes; each lane computes its candidate's
-//    1-D weights in registers and issues its W^3 adds as LDS f64 atomics
-//    (ds_add_f64).  Every grid point receives its contributions in a fixed
-//    order (staging order, lane order within an instruction): bit-stable from
-//    run to run, within rounding of the oracle's sequential l-loop.
+//  * spread: one wave per item owns the column's points in its z-segment, held
+//    in an LDS ring of 4 x 4 point tiles.  Planes are loaded (u_old) when the
+//    first anchor plane that reaches them comes up and written back when the
+//    last one has passed.  The candidates (markers of the 3x3 neighbouring
+//    buckets whose stencil reaches the column: 11 contiguous ranges of the
+//    sorted list, by band) stream through full 64-lane chunks across anchor
+//    planes; each lane computes its candidate's 1-D weights in registers and
+//    issues its W^3 adds as LDS f64 atomics (ds_add_f64) in a lane-rotated
+//    order that keeps every instruction free of bank conflicts.  Every grid
+//    point receives its contributions in a fixed order (staging order, step
+//    order, lane order within an instruction): bit-stable from run to run,
+//    within rounding of the oracle's sequential l-loop.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -103,22 +105,16 @@ __global__ __launch_bounds__(BLOCK) void k_bin_col(Params p, int n, unsigned* ke
 #pragma unroll
     for (int d = 0; d < 3; ++d) Xs[d] = p.X[(int64_t)3 * s + d] + (p.Xshift ? p.Xshift[(int64_t)3 * i + d] : 0.0);
     int ka[3];
-    // key = bucket, then (p.kbits > 0) the key cell's x mod 16 as the lowest
-    // digit: within a bucket the entries follow their LDS bank class (x mod 16
-    // of a 32-wide ring row), so the spread deals a chunk's candidates over the
-    // ds_add_f64 lane groups by a fixed lane permutation instead of a ranking
-    unsigned key = (unsigned)p.nbuckets_total << p.kbits;
+    unsigned key = (unsigned)p.nbuckets_total;  // outside
     if (p.pd) {  // a level: the entry's patch, its frame and its range of buckets
         const PatchDesc& P = p.pd[entry_patch(p, i)];
         if (col_key_cell<K>(P.xlo, p.bg.dx, P.ilower, P.cg, Xs, ka)) {
             const int col = (ka[1] / COLY) * P.cg.ncx + ka[0] / COLX;
-            const unsigned b = (unsigned)(P.bucket_base + (ka[2] * P.cg.ncol + col) * NBAND + key_band<K>(ka[0], ka[1]));
-            key = (b << p.kbits) | (((unsigned)ka[0] & 15u) >> (4 - p.kbits));
+            key = (unsigned)(P.bucket_base + (ka[2] * P.cg.ncol + col) * NBAND + key_band<K>(ka[0], ka[1]));
         }
     } else if (col_key_cell<K>(p.bg.xlo, p.bg.dx, p.bg.ilower, p.cg, Xs, ka)) {
         const int col = (ka[1] / COLY) * p.cg.ncx + ka[0] / COLX;
-        const unsigned b = (unsigned)((ka[2] * p.cg.ncol + col) * NBAND + key_band<K>(ka[0], ka[1]));
-        key = (b << p.kbits) | (((unsigned)ka[0] & 15u) >> (4 - p.kbits));
+        key = (unsigned)((ka[2] * p.cg.ncol + col) * NBAND + key_band<K>(ka[0], ka[1]));
     }
     keys[i] = key;
     vals[i] = i;
@@ -139,24 +135,20 @@ constexpr int GATHER_GAP = 32;
 template <int K>
 __global__ __launch_bounds__(BLOCK) void k_gather_col(Params p, int n, int* sorted_s, double* sorted_X,
                                                       const unsigned* skeys, int nbuckets, int* bs) {
-    const int kb = p.kbits;  // the key's class digit below the bucket
     __shared__ double sx[3 * BLOCK];
     const int e0 = blockIdx.x * BLOCK;
     const int e = e0 + threadIdx.x;
     if (e < n) {
         if (e > 0) {
-            const int bi = (int)min(skeys[e] >> kb, (unsigned)nbuckets);
-            const int bp = (int)min(skeys[e - 1] >> kb, (unsigned)nbuckets);
+            const int bi = (int)min(skeys[e], (unsigned)nbuckets);
+            const int bp = (int)min(skeys[e - 1], (unsigned)nbuckets);
             if (bi - bp <= GATHER_GAP)  // longer runs of empty buckets: k_bucket_fix
                 for (int b = bp + 1; b <= bi; ++b) bs[b] = e;
         }
         const int l = p.sorted_l[e];
         const int s = p.indices ? p.indices[l] : l;
         sorted_s[e] = s;
-        struct R3 {
-            double v[3];
-        };
-        const R3 x = *reinterpret_cast<const R3*>(p.X + (int64_t)3 * s);  // one 24-byte record per lane
+        const D3 x = ld3(p.X + (int64_t)3 * s);  // one 24-byte record per lane
 #pragma unroll
         for (int d = 0; d < 3; ++d) sx[3 * threadIdx.x + d] = x.v[d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
     }
@@ -178,16 +170,14 @@ __global__ __launch_bounds__(BLOCK) void k_gather_col(Params p, int n, int* sort
 // ---------------------------------------------------------------------------
 // work items
 // ---------------------------------------------------------------------------
-// Items are (segment, column, component), component fastest; blocks are dealt
-// round-robin over the 8 XCDs, so give XCD x a contiguous range of items: the
-// three components of a column and its x-neighbours run on one XCD at about the
-// same time and share marker data and halo planes through its L2.  The range
-// is cut from the table's actual length (read on the device; the grid is an
-// upper bound of it): an over-sized grid must not leave XCDs idle.  The heavy
-// items (k_item_counts: clustered markers, p.nitems[1] of them) head the table
-// and take the first blocks, dealt round-robin over the XCDs, so that they
-// start first and the light ones fill in around them.  The grid is 8 blocks
-// longer than the item bound (the heavy block count is rounded up to 8).
+// Items are (segment, column, component), component fastest.  The heavy items
+// (k_item_counts: clustered markers, p.nitems[1] of them) head the table and
+// take the first blocks, dealt round-robin over the XCDs, so that they start
+// first and the light ones fill in around them.  The light items go to the XCDs
+// in blocks of B table entries (block j to XCD j mod 8), so the three
+// components of a column and its x-neighbours run on one XCD at about the same
+// time and share marker data and halo planes through its L2.  The item count
+// is read on the device (the grid is an upper bound of it).
 constexpr int XCD_BLOCK = 8;  // table entries per block of items dealt to one XCD
 __device__ __forceinline__ int sweep_item(const Params& p, int per_entry) {
     const int nt = p.nitems[0] * per_entry, nh = p.nitems[1] * per_entry;
@@ -195,13 +185,11 @@ __device__ __forceinline__ int sweep_item(const Params& p, int per_entry) {
     const int h8 = (nh + 7) & ~7;
     if (b < h8) return b < nh ? b : -1;
     const int bl = b - h8, nl = nt - nh;
-    // Light items over the XCDs in blocks of B table entries, block j to XCD
-    // j mod 8 (ctx_tune xcd_block; 1 = round-robin, -1 = one contiguous range per
-    // XCD, the round-1 order).  Contiguous ranges give one XCD a whole z-layer of
-    // a level's patches -- a sheet of markers: blocks take cfg5 from 1.74e9 to
+    // ctx_tune xcd_block: 1 = round-robin, -1 = one contiguous range per XCD (the
+    // round-1 order).  Contiguous ranges give one XCD a whole z-layer of a
+    // level's patches -- a sheet of markers: blocks take cfg5 from 1.74e9 to
     // 1.96e9 marker-ops/s (spread sweep 4.32 -> 3.41 ms); on cfg4 blocks of 8
-    // keep the x-neighbour columns' shared halo lines in one L2 (interp 10.8 ms;
-    // round-robin 11.1, ranges 11.0, blocks of 34 11.0; profiles/r02z).
+    // keep the x-neighbour columns' shared halo lines in one L2 (profiles/r02z).
     const int B = p.tune.xcd_block != 0 ? p.tune.xcd_block : XCD_BLOCK;
     if (B > 0) {
         const int Bi = B * per_entry;  // items per block
@@ -217,8 +205,7 @@ __device__ __forceinline__ int sweep_item(const Params& p, int per_entry) {
 
 // Work item -> (component c, table entry t): component fastest, so the three
 // components of a column run on one XCD at about the same time (their Q
-// stores fill the same AoS lines; tools/tune_sweep.py measured the component-
-// major and column-tiled orders slower).  The table (k_item_write) lists the
+// stores fill the same AoS lines).  The table (k_item_write) lists the
 // (column, owned planes [p0, p1)) of every item, segment-major.
 __device__ __forceinline__ void item_decode(const Params& p, int it, int& c, SweepItem& si) {
     const int t = it / p.ncomp;
@@ -247,13 +234,9 @@ __device__ __forceinline__ void item_patch(const Params& p, const SweepItem& si,
     }
 }
 
-
 // ---------------------------------------------------------------------------
 // diagnostics
 // ---------------------------------------------------------------------------
-
-// Diagnostic phase clocks (Params::stamps != nullptr): per work item, cycles
-// spent per phase, accumulated in registers and written once at the end.
 // Phase clocks (s_memtime per work item, IBTK_LE_STAMPS=1 at run time) exist
 // only in builds with -DIBTK_LE_CLOCKS=1: their 64-bit accumulators would
 // otherwise hold 14 SGPRs through the sweep loop.
@@ -288,90 +271,10 @@ struct Clk {
 };
 #endif
 
-// Lane assignment of staged markers by LDS bank class.  An LDS instruction runs
-// as G lane groups, each costing about the largest number of its lanes that
-// share a bank: ds_add_f64 as 4 x 16 lanes, bank class = f64 index mod 16
-// (tools/ubench_lds2.hip; the microarchitecture guide's ds_write_b64 row);
-// ds_read_b64 as 2 x 32 lanes, class = f64 index mod 32.  The markers are
-// ranked by class (stable in staging order; idle lanes, class 63, last) and
-// dealt round-robin over the groups, so the markers of one class land in
-// different groups.  Returns the staged index this lane processes.
-template <int G = 4>  // lane groups: 4 x 16 (ds_add_f64, ds_write_b64) or 2 x 32 (ds_read_b64)
-__device__ __forceinline__ int deal_lanes(int cls) {  // cls in [0, 64); 63 = inactive
-    const int lane = __lane_id();
-    unsigned long long eq = ~0ull, lt = 0ull;
-#pragma unroll
-    for (int b = 5; b >= 0; --b) {
-        const bool bit = (cls >> b) & 1;
-        const unsigned long long m = __ballot(bit);
-        lt |= bit ? (eq & ~m) : 0ull;
-        eq &= bit ? m : ~m;
-    }
-    const int k = __popcll(lt) + __popcll(eq & ((1ull << lane) - 1ull));  // rank
-    const int t = (k % G) * (64 / G) + k / G;                              // dealt lane
-    return __builtin_amdgcn_ds_permute(t << 2, lane);
-}
-
-// deal_lanes for 16 classes (cls in [0, 16); 16 = inactive): the rank is the
-// count of lanes of a lower class plus the lanes of the same class below this
-// one, from five ballots on 32-bit halves (about half deal_lanes' VALU work).
-template <int G = 4>
-__device__ __forceinline__ int deal_lanes16(int cls) {
-    unsigned elo = ~0u, ehi = ~0u, llo = 0u, lhi = 0u;  // same-class-so-far, lower-class lanes
-#pragma unroll
-    for (int b = 4; b >= 0; --b) {
-        const bool bit = (cls >> b) & 1;
-        const unsigned long long m = __ballot(bit);
-        const unsigned mlo = (unsigned)m, mhi = (unsigned)(m >> 32);
-        const unsigned slo = bit ? mlo : ~mlo, shi = bit ? mhi : ~mhi;
-        llo |= bit ? (elo & ~mlo) : 0u;
-        lhi |= bit ? (ehi & ~mhi) : 0u;
-        elo &= slo;
-        ehi &= shi;
-    }
-    const int k = __popc(llo) + __popc(lhi) + (int)__builtin_amdgcn_mbcnt_hi(ehi, __builtin_amdgcn_mbcnt_lo(elo, 0u));
-    const int t = (k % G) * (64 / G) + k / G;  // dealt lane
-    return __builtin_amdgcn_ds_permute(t << 2, __lane_id());
-}
-
-// value of lane `src` (ds_bpermute on the two halves)
-__device__ __forceinline__ double shfl_f64(double v, int src) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b & 0xffffffffll));
-    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b >> 32));
-    return __hiloint2double(hi, lo);
-}
-
 // ---------------------------------------------------------------------------
 // interpolation
 // ---------------------------------------------------------------------------
-#ifndef IBTK_LE_IWAVES
-#define IBTK_LE_IWAVES 4
-#endif
-constexpr int IWAVES = IBTK_LE_IWAVES;  // waves per interp work item (one LDS ring)
-#ifndef IBTK_LE_ICW
-#define IBTK_LE_ICW 1  // 3: the three components of an item in one workgroup (measured 8 % slower on cfg4)
-#endif
-// 1: interp sums in the Fortran order, bitwise the oracle's (default);
-// 0: separable rows with FMAs, within tolerance (an experiment, not shipped)
-#ifndef IBTK_LE_IDEAL
-#define IBTK_LE_IDEAL 0  // interp: deal markers over lanes by LDS bank class (measured slower: off)
-#endif
-#ifndef IBTK_LE_IBLOCK
-#define IBTK_LE_IBLOCK 1  // interp: read blocks of stencil rows before summing them
-#endif
-#ifndef IBTK_LE_IPF
-#define IBTK_LE_IPF 1  // interp: plane prefetch depth in groups (1 or 2)
-#endif
-#ifndef IBTK_LE_DIAG_INTERP_NOCHUNK
-#define IBTK_LE_DIAG_INTERP_NOCHUNK 0  // diagnostic: the plane stream alone (no marker chunks)
-#endif
-#ifndef IBTK_LE_DIAG_INTERP_NOMATH
-#define IBTK_LE_DIAG_INTERP_NOMATH 0
-#endif
-#ifndef IBTK_LE_INTERP_EXACT
-#define IBTK_LE_INTERP_EXACT 1
-#endif
+constexpr int IWAVES = 4;  // waves per interp work item (one LDS ring)
 
 template <int K> struct ISh {
     using T = KT<K>;
@@ -426,52 +329,31 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
     } else if constexpr (FAM == 0) {
         // Clipped points (outside the ghost box) are staged as 0: acc + (w*wyz)*0
         // == acc bit for bit (acc is never -0), so the clipped sum of
-        // f.m4:1366-1382 needs no per-point branch.
+        // f.m4:1366-1382 needs no per-point branch.  The reads of a block of R
+        // stencil rows (R W ~ 16 values) go out back to back before the block is
+        // summed, so one LDS latency is exposed per block rather than one per
+        // pair of reads (the sum itself stays the Fortran's sequential chain).
         const double* base = ring + oy * RX + ox;
-        if constexpr (IBTK_LE_INTERP_EXACT) {
-            // The reads of a block of R stencil rows (R W ~ 16 values) go out back
-            // to back before the block is summed, so one LDS latency is exposed
-            // per block rather than one per pair of reads (the sum itself stays
-            // the Fortran's sequential chain).
-            constexpr int R = !IBTK_LE_IBLOCK ? 1
-                            : IBTK_LE_IBLOCK == 2 ? (W % 2 == 0 ? 2 : 1)
-                                                  : (W <= 4 ? W : (W <= 6 ? 3 : 2));  // rows per block; divides W
+        constexpr int R = W <= 4 ? W : (W <= 6 ? 3 : 2);  // rows per block; divides W
 #pragma unroll
-            for (int i2 = 0; i2 < W; ++i2) {
-                const double* pl = base + islot<K>(oz + i2) * PV;
+        for (int i2 = 0; i2 < W; ++i2) {
+            const double* pl = base + islot<K>(oz + i2) * PV;
 #pragma unroll
-                for (int r0 = 0; r0 < W; r0 += R) {
-                    double v[R * W];
+            for (int r0 = 0; r0 < W; r0 += R) {
+                double v[R * W];
 #pragma unroll
-                    for (int r = 0; r < R; ++r)
+                for (int r = 0; r < R; ++r)
 #pragma unroll
-                        for (int i0 = 0; i0 < W; ++i0) v[r * W + i0] = pl[(r0 + r) * RX + i0];
+                    for (int i0 = 0; i0 < W; ++i0) v[r * W + i0] = pl[(r0 + r) * RX + i0];
 #pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        const double wyz = st[1].w[r0 + r] * st[2].w[i2];  // f.m4:1349-1353
+                for (int r = 0; r < R; ++r) {
+                    const double wyz = st[1].w[r0 + r] * st[2].w[i2];  // f.m4:1349-1353
 #pragma unroll
-                        for (int i0 = 0; i0 < W; ++i0) {
-                            const double wt = st[0].w[i0] * wyz;
-                            acc = acc + wt * v[r * W + i0];  // f.m4:1375
-                        }
+                    for (int i0 = 0; i0 < W; ++i0) {
+                        const double wt = st[0].w[i0] * wyz;
+                        acc = acc + wt * v[r * W + i0];  // f.m4:1375
                     }
                 }
-            }
-        } else {
-            // separable rows with fused multiply-adds: within a few ulp of the
-            // Fortran order, not bitwise (a tolerance build)
-#pragma unroll
-            for (int i2 = 0; i2 < W; ++i2) {
-                const double* pl = base + islot<K>(oz + i2) * PV;
-                double az = 0.0;
-#pragma unroll
-                for (int i1 = 0; i1 < W; ++i1) {
-                    double r = st[0].w[0] * pl[i1 * RX];
-#pragma unroll
-                    for (int i0 = 1; i0 < W; ++i0) r = __builtin_fma(st[0].w[i0], pl[i1 * RX + i0], r);
-                    az = __builtin_fma(st[1].w[i1], r, az);
-                }
-                acc = __builtin_fma(st[2].w[i2], az, acc);
             }
         }
     } else {
@@ -502,7 +384,6 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
     return acc;
 }
 
-
 // Interpolation work item = (segment, column, component), one workgroup of
 // IWAVES waves sharing one LDS ring (more waves per CU for the same LDS: the
 // per-marker sum is a dependent chain in the Fortran order, so the latency
@@ -514,34 +395,20 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
 // pooled markers.  Points outside the component's array are staged as 0.  One
 // lane per marker sums its W^3 stencil from the ring (Fortran loop order,
 // bitwise the oracle's).
-// ICW components per workgroup (ICW x IWAVES waves, one LDS ring per component):
-// the components of an item run side by side on one CU, in step (the group
-// barriers are the workgroup's), so they read the item's markers from L1/L2
-// once and their 8-byte Q stores to one AoS record land in L2 together (one
-// 24-byte record write-back instead of three partial-line ones).
-#ifdef IBTK_LE_IVGPR
-#define IBTK_LE_IVGPR_ATTR __attribute__((amdgpu_waves_per_eu(IBTK_LE_IVGPR)))
-#else
-#define IBTK_LE_IVGPR_ATTR
-#endif
-template <int K, bool LVL, int ICW>
-__global__ __launch_bounds__(SW * IWAVES * ICW) IBTK_LE_IVGPR_ATTR void k_interp_sweep(Params p) {
+template <int K, bool LVL>
+__global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     using S = ISh<K>;
     constexpr int LO = S::LO, HI = S::HI, RX = S::RX, NPT = S::NPT;
-    __shared__ double ring_all[ICW * S::NSL * S::PVP];
-    const int ng = (p.ncomp + ICW - 1) / ICW;  // component groups per table entry
-    const int it = sweep_item(p, ng);
+    __shared__ double ring[S::NSL * S::PVP];
+    const int it = sweep_item(p, p.ncomp);
     if (it < 0) return;
-    const int te = it / ng;
-    const int cw = ICW == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)threadIdx.x / (SW * IWAVES));
-    const int c = (it - te * ng) * ICW + cw;
-    if (c >= p.ncomp) return;  // an absent component: its waves leave, the barriers count the others
-    double* const ring = ring_all + cw * (S::NSL * S::PVP);
-    const SweepItem si = p.items[te];
+    int c;
+    SweepItem si;
+    item_decode(p, it, c, si);
     const int col = si.col;
     const int a0 = si.p0, a1 = si.p1;  // the item's anchor planes
     const int lane = lane_id();
-    const int w = __builtin_amdgcn_readfirstlane(((int)threadIdx.x >> 6) % IWAVES);
+    const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     ColGeom cg;
     CompDesc cd;
     const int* bs;
@@ -551,7 +418,7 @@ __global__ __launch_bounds__(SW * IWAVES * ICW) IBTK_LE_IVGPR_ATTR void k_interp
         if (inner != (p.zmode == 1)) return;
     }
     {
-        bool any = false;  // the same answer in both waves
+        bool any = false;  // the same answer in every wave
         for (int a = a0 + lane; a < a1; a += SW) any = any || bs[bucket(cg, a, col, NBAND)] > bs[bucket(cg, a, col, 0)];
         if (!__any(any)) return;
     }
@@ -596,7 +463,7 @@ __global__ __launch_bounds__(SW * IWAVES * ICW) IBTK_LE_IVGPR_ATTR void k_interp
         int q;  // the marker whose Q this entry writes (-1: a later duplicate entry does)
         double X[3];
     };
-    // LDS barrier of the two waves; global loads in flight stay in flight
+    // LDS barrier of the waves; global loads in flight stay in flight
     auto lds_barrier = [&]() {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -651,39 +518,11 @@ __global__ __launch_bounds__(SW * IWAVES * ICW) IBTK_LE_IVGPR_ATTR void k_interp
         m.X[1] = xs.v[1];
         m.X[2] = xs.v[2];
     };
-    // one chunk of n <= 64 markers held one per lane: summed, stored.  (Dealing
-    // the markers over the two 32-lane halves of a ds_read_b64 by bank class,
-    // as the spread does for its adds, measured 10 % slower: the ranking costs
-    // more than the reads' bank conflicts.)
-    // The markers are dealt over the lanes by the LDS bank class of their
-    // stencil start (deal_lanes: ds_read2_b64 serves 4 groups of 16 lanes, a
-    // group conflict-free when its f64 indices differ mod 16; the ring row
-    // stride RX = 36 = 4 mod 16 gives class (4 y + x) mod 16, the same for
-    // every read of the stencil).  IBTK_LE_IDEAL=0 turns it off.
-    const double inv_dx0 = 1.0 / p.bg.dx[0], inv_dx1 = 1.0 / p.bg.dx[1];
-    auto process_pool = [&](int n, const Mk& m0, int am0) {
-        Mk m = m0;
-        int am = am0;
-        bool act = lane < n;
-        if constexpr (IBTK_LE_IDEAL) {
-            const int kx = (int)floor((m0.X[0] - cd.xlo[0]) * inv_dx0);
-            const int ky = (int)floor((m0.X[1] - cd.xlo[1]) * inv_dx1);
-            const int cls = act ? ((4 * ky + kx) & 15) : 16;
-            const int src = deal_lanes16<4>(cls);
-            m.X[0] = shfl_f64(m0.X[0], src);
-            m.X[1] = shfl_f64(m0.X[1], src);
-            m.X[2] = shfl_f64(m0.X[2], src);
-            m.s = __builtin_amdgcn_ds_bpermute(src << 2, m0.s);
-            m.q = __builtin_amdgcn_ds_bpermute(src << 2, m0.q);
-            am = __builtin_amdgcn_ds_bpermute(src << 2, am0);
-            act = src < n;
-        }
+    // one chunk of n <= 64 markers held one per lane: summed, stored
+    auto process_pool = [&](int n, const Mk& m, int am) {
+        const bool act = lane < n;
         double acc = 0.0;
-#if IBTK_LE_DIAG_INTERP_NOMATH  // diagnostic: markers and planes stream, no stencil sums
-        if (act) acc = m.X[0] + m.X[1] + m.X[2];
-#else
         if (act) acc = interp_marker<K>(p, cd, ring, gx0, gy0, zorg, am, m.X, m.s);
-#endif
         double* dst = (act && m.q >= 0) ? p.Qout + ((int64_t)p.Q_depth * m.q + cd.qcomp) : p.sink + lane;
         *dst = acc;
     };
@@ -693,8 +532,6 @@ __global__ __launch_bounds__(SW * IWAVES * ICW) IBTK_LE_IVGPR_ATTR void k_interp
         plane_put(z, pv);
     }
     plane_load(a0 + w + HI, pv);
-    double pv2[IBTK_LE_IPF >= 2 ? NPT : 1];
-    if constexpr (IBTK_LE_IPF >= 2) plane_load(a0 + w + IWAVES + HI, pv2);
     GSpan gs;
     gspan_get(a0, gspan_load(a0), gs);
     Mk nxt;
@@ -714,15 +551,9 @@ __global__ __launch_bounds__(SW * IWAVES * ICW) IBTK_LE_IVGPR_ATTR void k_interp
         gspan_get(a + IWAVES, vsp1, gs);
         chunk_load(gs, a + IWAVES, w, nxt, anx);
         vsp1 = gspan_load(a + 2 * IWAVES);
-        if constexpr (IBTK_LE_IPF >= 2) {  // planes two groups ahead
-#pragma unroll
-            for (int k = 0; k < NPT; ++k) pv[k] = pv2[k];
-            plane_load(my + 2 * IWAVES + HI, pv2);
-        } else {
-            plane_load(my + IWAVES + HI, pv);
-        }
+        plane_load(my + IWAVES + HI, pv);
         const int tot = gc.pre[IWAVES];
-        if (!IBTK_LE_DIAG_INTERP_NOCHUNK && SW * w < tot) {
+        if (SW * w < tot) {
             // dense groups: the wave's next chunk loads while this one is summed
             Mk m = cur;
             int am = acur;
@@ -747,395 +578,48 @@ __global__ __launch_bounds__(BLOCK) void k_interp_outside_col(Params p, int n) {
 }
 
 // ---------------------------------------------------------------------------
-// interpolation, one plane at a time (FAM 0 kernels: IB_4, BSPLINE_4, IB_6,
-// IB_4_W8), every component of an item in one workgroup
-// ---------------------------------------------------------------------------
-// Work item = (column, owned anchor planes [a0, a1)), all NC components.  The
-// workgroup has NS = HI - LO + 1 waves; wave w takes the anchor planes
-// a = a0 + w (mod NS).  An anchor plane's markers read planes a+LO .. a+HI, so
-// with the workgroup stepping through the item's planes one per step, every
-// wave has exactly one anchor plane in flight, at stage s = p - (a + LO), and
-// the LDS holds one plane per component (column + stencil halo) plus the next
-// one being put: 2 NC planes instead of k_interp_sweep's ring of NS + 3 planes
-// per component, which is what lets one workgroup take every component.
-// A lane keeps its marker's 1-D weights and partial sums in registers across
-// the NS steps and adds plane i2 = s - dz of its stencil at stage s: each sum
-// runs in the Fortran order (i2, i1, i0; f.m4:1366-1382), so Q is bitwise the
-// oracle's.  The markers are read once for all components, and each Q record
-// is written whole by one lane.
-// More than 64 markers on one anchor plane: the first 64 are register-resident;
-// the others are re-staged at every stage (weights recomputed, bit for bit the
-// same) with their partial sums kept in Q itself (each Q entry has one writer).
-// Weights: two frames per axis, frame 1 = component d's own in axis d, frame
-// 0 = the one the other components share (interp_plane_frames checks it).
-template <int K> struct IPl {
-    using T = KT<K>;
-    static constexpr int W = T::W, LO = T::LO, HI = T::HI;
-    static constexpr int NS = HI - LO + 1;  // planes an anchor plane's markers read; waves per workgroup
-    static constexpr int NT = SW * NS;
-    static constexpr int RX = COLX + HI - LO, RY = COLY + HI - LO;  // staged plane: column + stencil halo
-    static constexpr int PV = RX * RY;
-    static constexpr int PVP = (PV + 31) / 32 * 32;
-    static constexpr int NPC = (PV + NT - 1) / NT;  // staged points per thread, component and plane
-};
-
-// frame of component c in axis d; the component whose frame is frame f of axis d
-template <int NC> __device__ __forceinline__ constexpr int ipl_fr(int c, int d) { return NC == 1 ? 0 : (c == d ? 1 : 0); }
-template <int NC> __device__ __forceinline__ constexpr int ipl_fc(int d, int f) {
-    return NC == 1 ? 0 : (f ? d : (d == 0 ? 1 : 0));
-}
-
-template <int W, int NC> struct IMk {
-    static constexpr int NF = NC == 1 ? 1 : 2;
-    double wt[3][NF][W];  // 1-D weights [axis][frame][i]
-    int o[3][NF];         // stencil starts: x, y in the staged region, z from the anchor's first plane
-    unsigned okc;         // bit c: component c's stencil lies in the staged region
-};
-
-template <int I, int N, class F> __device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        static_for<I + 1, N>(f);
-    }
-}
-
-// 1-D stencils of one marker (shifted position Xs); za = the anchor's first plane
-template <int K, int NC>
-__device__ __forceinline__ void ipl_weights(const Params& p, const CompDesc* cdv, const double* Xs, int gx0, int gy0,
-                                            int za, IMk<KT<K>::W, NC>& m) {
-    using S = IPl<K>;
-    constexpr int W = S::W, NF = IMk<W, NC>::NF;
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-#pragma unroll
-        for (int f = 0; f < NF; ++f) {
-            const CompDesc& cd = cdv[ipl_fc<NC>(d, f)];
-            St<W> st;
-            stencil1d<K>(Xs[d], Xs[d], cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis, p.K6, st);
-#pragma unroll
-            for (int i = 0; i < W; ++i) m.wt[d][f][i] = st.w[i];
-            m.o[d][f] = st.icl - (d == 0 ? gx0 : (d == 1 ? gy0 : za));
-        }
-    }
-    m.okc = 0;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-        const int ox = m.o[0][ipl_fr<NC>(c, 0)], oy = m.o[1][ipl_fr<NC>(c, 1)], oz = m.o[2][ipl_fr<NC>(c, 2)];
-        // binning invariant: the stencil lies in the staged region and the anchor's planes
-        if (ox >= 0 && ox + W <= S::RX && oy >= 0 && oy + W <= S::RY && oz >= 0 && oz + W <= S::NS) m.okc |= 1u << c;
-    }
-}
-
-// Stage s of one marker: plane i2 = s - dz of each component's stencil, read
-// from the current LDS planes pl[c] and added to acc[c] in the Fortran order.
-template <int K, int NC, int s>
-__device__ __forceinline__ void ipl_stage(const IMk<KT<K>::W, NC>& m, const double* const* pl, double* acc) {
-    using S = IPl<K>;
-    constexpr int W = S::W, RX = S::RX;
-    constexpr int jlo = s - (S::NS - W) > 0 ? s - (S::NS - W) : 0;  // the stencil planes stage s can be
-    constexpr int jhi = s < W - 1 ? s : W - 1;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-        const int fx = ipl_fr<NC>(c, 0), fy = ipl_fr<NC>(c, 1), fz = ipl_fr<NC>(c, 2);
-        const int i2 = s - m.o[2][fz];
-        if (!((m.okc >> c) & 1u) || i2 < jlo || i2 > jhi) continue;  // not a plane of this stencil
-        double wz = m.wt[2][fz][jlo];
-#pragma unroll
-        for (int j = jlo + 1; j <= jhi; ++j) wz = i2 == j ? m.wt[2][fz][j] : wz;
-        const double* base = pl[c] + m.o[1][fy] * RX + m.o[0][fx];
-        double a = acc[c];
-#pragma unroll
-        for (int i1 = 0; i1 < W; ++i1) {
-            double v[W];
-#pragma unroll
-            for (int i0 = 0; i0 < W; ++i0) v[i0] = base[i1 * RX + i0];
-            const double wyz = m.wt[1][fy][i1] * wz;  // f.m4:1349-1353
-#pragma unroll
-            for (int i0 = 0; i0 < W; ++i0) {
-                const double wt = m.wt[0][fx][i0] * wyz;
-                a = a + wt * v[i0];  // f.m4:1375
-            }
-        }
-        acc[c] = a;
-    }
-}
-
-#ifndef IBTK_LE_IPL_WAVES
-#define IBTK_LE_IPL_WAVES 4  // waves per SIMD the plane interp is compiled for (VGPR budget 512 / this)
-#endif
-template <int K, bool LVL, int NC>
-__global__ __launch_bounds__(IPl<K>::NT) __attribute__((amdgpu_waves_per_eu(IBTK_LE_IPL_WAVES)))
-void k_interp_planes(Params p) {
-    using S = IPl<K>;
-    constexpr int W = S::W, LO = S::LO, HI = S::HI, NS = S::NS, NT = S::NT, NPC = S::NPC, RX = S::RX, PVP = S::PVP;
-    __shared__ double ring[2 * NC * PVP];
-    const int it = sweep_item(p, 1);
-    if (it < 0) return;
-    const SweepItem si = p.items[it];
-    const int col = si.col, a0 = si.p0, a1 = si.p1;
-    ColGeom cg;
-    CompDesc cd0;
-    const int* bs;
-    item_patch<LVL>(p, si, 0, cg, cd0, bs);
-    CompDesc cdv[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) cdv[c] = LVL ? p.pd[si.patch].comp[c] : p.comp[c];
-    const int tid = threadIdx.x, lane = lane_id();
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (p.zmode) {  // the planes the item reads: a0 + LO .. a1 - 1 + HI
-        const bool inner = cg.org[2] + a0 + LO >= p.zlo && cg.org[2] + a1 - 1 + HI <= p.zhi;
-        if (inner != (p.zmode == 1)) return;
-    }
-    {
-        bool any = false;  // the same answer in every wave
-        for (int a = a0 + lane; a < a1; a += SW) any = any || bs[bucket(cg, a, col, NBAND)] > bs[bucket(cg, a, col, 0)];
-        if (!__any(any)) return;
-    }
-    const int cx = col % cg.ncx, cy = col / cg.ncx;
-    const int gx0 = cg.org[0] + cx * COLX + LO, gy0 = cg.org[1] + cy * COLY + LO;
-    const int zorg = cg.org[2];
-    const int nlast = p.nsorted - 1;
-    // the thread's staged points q = tid + NT k of each component: array
-    // offsets (clamped) and in-array bits
-    int poff[NC][NPC];
-    unsigned okm = 0;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-#pragma unroll
-        for (int k = 0; k < NPC; ++k) {
-            const int q = min(tid + NT * k, S::PV - 1);
-            const int gxu = gx0 + q % RX, gyu = gy0 + q / RX;
-            const int gx = min(max(gxu, cdv[c].lo[0]), cdv[c].hi[0]), gy = min(max(gyu, cdv[c].lo[1]), cdv[c].hi[1]);
-            poff[c][k] = (gx - cdv[c].lo[0]) + (gy - cdv[c].lo[1]) * (int)cdv[c].s1;
-            if (gx == gxu && gy == gyu) okm |= 1u << (c * NPC + k);
-        }
-    }
-    const int P0 = a0 + LO, plast = a1 - 1 + HI;
-    const int T = plast - P0 + 1;  // steps: one per plane the item reads
-    // relative plane zr -> registers: unconditional loads at clamped addresses
-    // (points outside the array are zeroed when the plane is put)
-    auto plane_load = [&](int zr, double (&v)[NC][NPC]) {
-        const int z = zorg + min(zr, plast);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            const int zc = min(max(z, cdv[c].lo[2]), cdv[c].hi[2]);
-            const double* pb = cdv[c].u + (int64_t)(zc - cdv[c].lo[2]) * cdv[c].s2;
-#pragma unroll
-            for (int k = 0; k < NPC; ++k) v[c][k] = pb[poff[c][k]];
-        }
-    };
-    auto plane_put = [&](int zr, const double (&v)[NC][NPC]) {  // into slot zr mod 2
-        const int z = zorg + min(zr, plast);
-        double* sl = ring + (zr & 1) * (NC * PVP);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            const bool zin = z >= cdv[c].lo[2] && z <= cdv[c].hi[2];
-#pragma unroll
-            for (int k = 0; k < NPC; ++k)
-                if (S::PV % NT == 0 || k < NPC - 1 || tid + NT * k < S::PV)
-                    sl[c * PVP + tid + NT * k] = (zin && ((okm >> (c * NPC + k)) & 1u)) ? v[c][k] : 0.0;
-        }
-    };
-    auto lds_barrier = [&]() {  // LDS barrier; global loads in flight stay in flight
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    };
-    // anchor plane a's sorted entries: lane 0 its first, lane 1 its end (readlane)
-    auto span_load = [&](int a) {
-        const int ac = max(min(min(a, a1 - 1), cg.nz - 1), 0);
-        return bs[bucket(cg, ac, col, lane == 1 ? NBAND : 0)];
-    };
-    auto mk_load = [&](int e, double* X, int& q, bool act) {
-        e = min(e, nlast);
-        const double* xs = p.sorted_X + (int64_t)3 * e;
-        X[0] = xs[0];
-        X[1] = xs[1];
-        X[2] = xs[2];
-        const int qq = p.qdst ? p.qdst[e] : p.sorted_s[e];
-        q = act ? qq : -1;
-    };
-    auto qaddr = [&](int q, int c) { return p.Qout + ((int64_t)p.Q_depth * q + cdv[c].qcomp); };
-
-    double pv[NC][NPC];
-    plane_load(P0, pv);
-    plane_put(P0, pv);
-    plane_load(P0 + 1, pv);
-    // this wave's first anchor plane: its span and its first 64 markers
-    int beg, nA, nq;
-    double nX[3];
-    {
-        const int a = a0 + w;
-        const int v = span_load(a);
-        beg = __builtin_amdgcn_readlane(v, 0);
-        nA = a < a1 ? __builtin_amdgcn_readlane(v, 1) - beg : 0;
-        mk_load(beg + lane, nX, nq, lane < nA);
-    }
-    lds_barrier();
-    auto step_begin = [&](int tt) {  // plane P0+tt+1 into its slot, plane P0+tt+2 into registers
-        plane_put(P0 + tt + 1, pv);
-        plane_load(P0 + tt + 2, pv);
-    };
-    int t = 0;
-    for (; t < w && t < T; ++t) {  // wave w starts its first anchor plane at step w
-        step_begin(t);
-        lds_barrier();
-    }
-    IMk<W, NC> m;
-    double acc[NC];
-    int q = -1, nCur = 0, begCur = 0, vsp = 0;
-    for (int a = a0 + w; t < T; a += NS) {
-        static_for<0, NS>([&](auto sc) {
-            constexpr int s = decltype(sc)::value;
-            if (t >= T) return;
-            step_begin(t);
-            if (a < a1) {
-                if constexpr (s == 0) {  // the anchor plane's first 64 markers: weights into registers
-                    nCur = nA;
-                    begCur = beg;
-                    q = nq;
-                    ipl_weights<K, NC>(p, cdv, nX, gx0, gy0, zorg + a + LO, m);
-                    if (lane < nCur && m.okc != (1u << NC) - 1u) atomicOr(p.err, 1);
-#pragma unroll
-                    for (int c = 0; c < NC; ++c) acc[c] = 0.0;
-                    vsp = span_load(a + NS);  // this wave's next anchor plane
-                }
-                if constexpr (s == 2) {
-                    beg = __builtin_amdgcn_readlane(vsp, 0);
-                    nA = a + NS < a1 ? __builtin_amdgcn_readlane(vsp, 1) - beg : 0;
-                    mk_load(beg + lane, nX, nq, lane < nA);
-                }
-                const double* pl[NC];
-#pragma unroll
-                for (int c = 0; c < NC; ++c) pl[c] = ring + ((P0 + t) & 1) * (NC * PVP) + c * PVP;
-                if (lane < nCur) ipl_stage<K, NC, s>(m, pl, acc);
-                // markers past the first 64: staged again at every stage, partial
-                // sums in Q (each entry written by one lane only)
-                for (int k = 1; SW * k < nCur; ++k) {
-                    const int nk = min(SW, nCur - SW * k);
-                    double Xo[3];
-                    int qo;
-                    mk_load(begCur + SW * k + lane, Xo, qo, lane < nk);
-                    if (qo >= 0) {
-                        // one component at a time (one marker state's registers)
-#pragma unroll
-                        for (int c = 0; c < NC; ++c) {
-                            IMk<W, 1> mo;
-                            ipl_weights<K, 1>(p, cdv + c, Xo, gx0, gy0, zorg + a + LO, mo);
-                            if constexpr (s == 0)
-                                if (mo.okc != 1u) atomicOr(p.err, 1);
-                            double ao = s == 0 ? 0.0 : *qaddr(qo, c);
-                            ipl_stage<K, 1, s>(mo, pl + c, &ao);
-                            *qaddr(qo, c) = ao;
-                        }
-                    }
-                }
-                if constexpr (s == NS - 1) {
-                    if (lane < nCur && q >= 0) {
-#pragma unroll
-                        for (int c = 0; c < NC; ++c) *qaddr(q, c) = acc[c];
-                    }
-                }
-            }
-            lds_barrier();
-            ++t;
-        });
-    }
-}
-
-// Two frames per axis: in every axis d the components other than d share one.
-bool interp_plane_frames(const CompDesc* comp, int nc) {
-    if (nc == 1) return true;
-    if (nc != 3) return false;
-    for (int d = 0; d < 3; ++d) {
-        const int a = d == 0 ? 1 : 0, b = d == 2 ? 1 : 2;  // the components other than d
-        const CompDesc &A = comp[a], &B = comp[b];
-        if (A.xlo[d] != B.xlo[d] || A.ilower[d] != B.ilower[d] || A.lo[d] != B.lo[d] || A.hi[d] != B.hi[d] ||
-            (A.axis == d) != (B.axis == d))
-            return false;
-    }
-    return true;
-}
-
-// ---------------------------------------------------------------------------
 // spreading
 // ---------------------------------------------------------------------------
-#ifndef IBTK_LE_SPREAD_DEAL
-#define IBTK_LE_SPREAD_DEAL 1  // 1: rank-dealt lanes by bank class; 0: none; 2: static blocks; 3: static stride 4
-#endif
-#ifndef IBTK_LE_SPREAD_EARLY
-#define IBTK_LE_SPREAD_EARLY 0
-#endif
-// diagnostics (variant builds only): spread without reading u_old / without
-// the LDS adds; interp without the stencil sums
-#ifndef IBTK_LE_DIAG_SPREAD_NOLOAD
-#define IBTK_LE_DIAG_SPREAD_NOLOAD 0
-#endif
-#ifndef IBTK_LE_SPF
-#define IBTK_LE_SPF 1  // spread: plane prefetch depth in anchor steps (1 or 2)
-#endif
-#ifndef IBTK_LE_SPREAD_FDIRECT
-#define IBTK_LE_SPREAD_FDIRECT 0  // 1: candidates read F through sorted_s (no k_gather_F_col pass)
-#endif
-#ifndef IBTK_LE_SPREAD_ZLOW
-#define IBTK_LE_SPREAD_ZLOW 0  // 1: cell-frame-in-z components with a ring one slot shorter (a launch of their own)
-#endif
-#ifndef IBTK_LE_DIAG_SPREAD_LDSPAD
-#define IBTK_LE_DIAG_SPREAD_LDSPAD 0  // diagnostic: extra doubles of LDS per spread wave (occupancy probe)
-#endif
-#ifndef IBTK_LE_DIAG_SPREAD_NOPROC
-#define IBTK_LE_DIAG_SPREAD_NOPROC 0
-#endif
-#ifndef IBTK_LE_DIAG_SPREAD_NOADD
-#define IBTK_LE_DIAG_SPREAD_NOADD 0
-#endif
-#ifndef IBTK_LE_SPREAD_ROT
-#define IBTK_LE_SPREAD_ROT 0  // measured 30 % slower on cfg4 (the spread is issue-bound)
-#endif
-// ZH: the highest stencil plane relative to the anchor plane that the item's
-// component reaches -- KT::HI in general, HI - 1 for a closed-form kernel whose
-// component has the bin keys' own z frame (cell-like in z: its stencil starts at
-// NINT - W/2, e.g. IB_4 a-2 .. a+1), one ring slot less: 5 slots instead of 6
-// for IB_4, 7 spread waves per CU instead of 6 (spread_zhi).
-template <int K, int ZH = KT<K>::HI> struct SSh {
+// The ring holds one plane of the column's 32 x COLY owned points per slot, in
+// 4 x 4 tiles of 16 consecutive doubles: point (x, y) at
+//     16 ((x >> 2) + (COLX / 4) (y >> 2)) + (x & 3) + 4 (y & 3).
+// ds_add_f64 serves a wave as 4 groups of 16 lanes, each conflict-free when its
+// f64 indices differ mod 16 (tools/ubench_lds2.hip; the microarchitecture
+// guide's ds_write_b64 row), and a point's index mod 16 -- its bank class -- is
+// (x & 3) + 4 (y & 3) in every tile of every slot.  The 4 x 4 points (i0, i1) of
+// a 4-wide stencil plane therefore cover the 16 classes once each, whatever the
+// stencil's position, and the lanes can take them in an order in which the 16
+// lanes of a group always hit 16 different classes (spread_tiled).
+template <int K> struct SSh {
     using T = KT<K>;
-    static constexpr int W = T::W, LO = T::LO, HI = ZH, FAM = T::FAM;
-    static constexpr int NS = HI - LO + 1;              // planes an anchor plane reaches
-    static constexpr int NSL = NS + 1;                  // ring slots: the planes two anchors reach
-    static constexpr int PV = COLX * COLY;              // owned points per plane
-    static constexpr int NPL = PV / SW;
-    static constexpr int NR = 11;                       // candidate ranges per anchor plane
-    // Rotated adds (W = 4, spread_rot): ring rows of RS = 36 doubles (RS = 4 mod
-    // 16), so the 16 points (i0, i1) of a stencil plane fall in the 16 bank
-    // classes i0 + 4 i1 (+ the base's class), and a slot stride that is a
-    // multiple of 16 keeps a point's class independent of its plane.  A trash
-    // row of 16 doubles at the end of every slot takes the zero-weight adds of
-    // the clipped or not-owned points of that plane at their own class.
-    static constexpr bool ROT = IBTK_LE_SPREAD_ROT && W == 4 && (FAM == 0 || FAM == 2);
-    static constexpr int RS = ROT ? 36 : COLX;          // ring row stride
-    // ring slot stride: a 16-double gap after each plane takes the spill of the
-    // zero-weight adds of stencil columns that stick out of the column (x in
-    // [-3, 34] of rows 0..COLY-1); a multiple of 16 keeps every point's bank
-    // class = its x mod 16.  GUARD doubles before slot 0 take its low spill.
-    static constexpr int TROW = (RS * COLY + 15) / 16 * 16;  // ROT: trash row of a slot
-    static constexpr int SLOT = ROT ? TROW + 16 : PV + 16;
-    static constexpr int GUARD = ROT ? 0 : 16;
+    static constexpr int W = T::W, LO = T::LO, HI = T::HI, FAM = T::FAM;
+    static constexpr int NS = HI - LO + 1;   // planes an anchor plane reaches
+    static constexpr int NSL = NS + 1;       // ring slots: the planes two anchors reach
+    static constexpr int PV = COLX * COLY;   // owned points per plane = doubles per slot
+    static constexpr int NPL = PV / SW;      // staged points per lane and plane
+    static constexpr int NR = 11;            // candidate ranges per anchor plane
     static_assert(NS <= 16, "plane field");
-    static_assert(COLX == 32 && COLY >= 8, "32-point rows; bands need COLY >= 8");
+    static_assert(COLX == 32 && COLY % 4 == 0 && COLY >= 8, "32-point rows of 4 x 4 tiles; bands need COLY >= 8");
 };
 
-// ring plane layout: row-major 32 x COLY, rows SSh::RS apart; q = the lane's
-// staged point (x = q mod 32, y = q / 32)
-template <int K> __device__ __forceinline__ int ring_index(int q) {
-    return (q >> 5) * SSh<K>::RS + (q & (COLX - 1));
+// (x, y) in the column of the tile-major slot index i
+__device__ __forceinline__ void ring_xy(int i, int& x, int& y) {
+    const int t = i >> 4, j = i & 15;
+    x = 4 * (t % (COLX / 4)) + (j & 3);
+    y = 4 * (t / (COLX / 4)) + (j >> 2);
+}
+// slot index of (x, y), both wrapped into the column (x mod 32, y mod COLY keep
+// the bank class: 32 and COLY are multiples of 4)
+__device__ __forceinline__ int ring_wrapped(int x, int y) {
+    const int xw = x & (COLX - 1);
+    const int yw = ((y % COLY) + COLY) % COLY;
+    return 16 * ((xw >> 2) + (COLX / 4) * (yw >> 2)) + (xw & 3) + 4 * (yw & 3);
 }
 
-template <int K, int ZH = KT<K>::HI> __device__ __forceinline__ int sslot(int prel) {
-    using S = SSh<K, ZH>;
+template <int K> __device__ __forceinline__ int sslot(int prel) {
+    using S = SSh<K>;
     return (int)((unsigned)(prel + 16 * S::NSL) % (unsigned)S::NSL);  // prel >= -HI + LO > -16*NSL
 }
-
-
 
 // The candidate ranges of anchor plane a for column (cx, cy), in sorted (bucket)
 // order, from the bucket-start table row t[r][i] = bs(a, col(cx-1, cy-1+r), 0) + i
@@ -1180,27 +664,40 @@ struct Cand {
     int s;
 };
 
-// The adds of n <= 64 staged candidates of anchor plane a, one lane per
-// candidate: the lane computes its three 1-D stencils, then walks its W^3
-// points (i2, i1, i0) issuing one ds_add_f64 per point.  A stencil row (i1,
-// i2) outside the owned rows, the clipped stencil or the segment is skipped
-// by the lanes it concerns (one exec mask per row; idle lanes skip them all);
-// within a row, a point outside the owned x range is added with weight 0, its
-// x left to spill (the slot gaps take it).  So an add is one multiply and one
-// ds_add_f64 with an immediate offset -- no select and no branch per add (a
-// branch per add makes the compiler wait for every LDS operation in flight
-// before each one).  Adding +-0 changes no value, except that a -0.0 it lands
-// on becomes +0.0.
-// Every lane's address moves by the same amount from one add to the next, so
-// lanes dealt to distinct bank classes stay conflict-free for all W^3 adds.
-// Within one instruction the lanes that hit the same point add in lane order,
-// so every point receives its contributions in a fixed order (bit-stable).
-template <int K, int ZH>
-__device__ __forceinline__ void spread_lanes_rows(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
+// w[s] <- w[(s + r) & 3] for s < 4 (a two-stage barrel of selects)
+__device__ __forceinline__ void rot4(double* w, int r) {
+    const bool b0 = r & 1, b1 = r & 2;
+    const double c0 = b0 ? w[1] : w[0], c1 = b0 ? w[2] : w[1], c2 = b0 ? w[3] : w[2], c3 = b0 ? w[0] : w[3];
+    w[0] = b1 ? c2 : c0;
+    w[1] = b1 ? c3 : c1;
+    w[2] = b1 ? c0 : c2;
+    w[3] = b1 ? c1 : c3;
+}
+
+// The adds of one staged candidate per lane: the lane computes its three 1-D
+// stencils, then issues its W^3 adds as ds_add_f64, plane by plane.
+// Conflict-free order: lane l = 16 g + 4 jy + jx takes, at step (s0, s1) of a
+// stencil plane (s0, s1 < 4), its point whose x = s0 + jx and y = s1 + jy
+// (mod 4) -- a rotation of its stencil's first four columns and rows by
+// (jx - ox) and (jy - oy) mod 4 -- so the 16 lanes of every lane group hit the
+// 16 bank classes once each, in every instruction, wherever the stencils lie
+// (no ranking or dealing of the candidates).  Wider stencils (IB_6, IB_4_W8)
+// take their further columns and rows unrotated; narrower ones unrotated.
+// A stencil point that is clipped (outside the ghost box) or not owned (outside
+// the column, or in a neighbour item's planes) is added with weight 0 at its
+// position wrapped into the column (a +0 on an owned point of the same class),
+// so a plane's adds need no per-point branch; whole planes that are clipped or
+// not owned are skipped with one exec mask each.  Adding +-0 changes no value,
+// except that a -0.0 it lands on becomes +0.0.  Within one instruction the
+// lanes that hit the same point add in lane order, so every point receives its
+// contributions in a fixed order (bit-stable).
+template <int K>
+__device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
                                              bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
                                              int yhi, int plo, int phi, double inv_h3, const double* inv_d, Clk& clk) {
-    using S = SSh<K, ZH>;
-    constexpr int W = S::W, FAM = S::FAM, LO = S::LO, HI = S::HI, NS = S::NS, NSL = S::NSL;
+    using S = SSh<K>;
+    constexpr int W = S::W, FAM = S::FAM, NSL = S::NSL;
+    constexpr bool ROT = W >= 4;
     St<W> st[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
@@ -1209,249 +706,89 @@ __device__ __forceinline__ void spread_lanes_rows(const Params& p, const CompDes
         stencil1d<K, true>(cdat.X[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis,
                            p.K6, st[d], inv_d[d]);
     }
-    int ox = st[0].icl - X0, oy = st[1].icl - Y0, oz = st[2].icl - (zorg + a);
-    bool ok = act;
-    // binning invariant (and the memory bound of the spill: x in [-16, COLX + 15])
-    if (act && (ox < -S::GUARD || ox > COLX + 15 - (W - 1) || oy < -60 || oy > 60 || oz < -60 || oz > 60)) {
-        atomicOr(p.err, 2);
-        ok = false;
-    }
-    if (!ok) {  // idle: weight 0 at a lane-distinct x
-        ox = lane_id() & 15;
-        oy = oz = 0;
-    }
-    // x: weight x value with the mask folded in (f.m4:1512-1513 order, V applied
-    // first: within rounding of the Fortran's (w0 (w1 w2/h)) V)
-    double w0v[W];
-    unsigned ym = 0, zm = 0;  // bit i: stencil row / plane i is clipped in and owned
-#pragma unroll
-    for (int i = 0; i < W; ++i) {
-        const bool vx = ok && i >= st[0].ist && i <= st[0].isp && ox + i >= xlo && ox + i <= xhi;
-        w0v[i] = vx ? st[0].w[i] * cdat.V : 0.0;
-        if (i >= st[1].ist && i <= st[1].isp && oy + i >= ylo && oy + i <= yhi) ym |= 1u << i;
-        const int k = oz - LO + i, pr = a + oz + i;  // plane a + LO + k
-        if (i >= st[2].ist && i <= st[2].isp && k >= 0 && k < NS && pr >= plo && pr <= phi) zm |= 1u << i;
-    }
-    // bit W i2 + i1: row (i1, i2) is added.  A masked row needs no address, so
-    // rows and planes are not clamped: row i1 of plane i2 is at a constant
-    // offset 8 COLX i1 from the plane's row 0 (folded into the ds_add offsets)
-    using RM = std::conditional_t<(W * W > 32), unsigned long long, unsigned>;
-    RM rm = 0;
-#pragma unroll
-    for (int i2 = 0; i2 < W; ++i2) rm |= ((zm >> i2) & 1u) ? (RM)ym << (W * i2) : (RM)0;
-    char* const base = reinterpret_cast<char*>(ring) + 8 * (ox + COLX * oy);
-    clk.lap(2);
-    // idle lanes sit the adds out (exec-masked, one branch around the loop: a
-    // 16-lane group with no busy lane costs the LDS nothing)
-    if (ok) {
-    int sl = (int)((unsigned)(a + oz + 64 * NSL) % (unsigned)NSL);  // ring slot of plane i2 = 0
-#pragma unroll
-    for (int i2 = 0; i2 < W; ++i2) {
-        char* const plane = base + sl * (8 * S::SLOT);
-        sl = sl + 1 == NSL ? 0 : sl + 1;
-        double wz;
-        if constexpr (FAM == 0) wz = st[2].w[i2] * inv_h3;  // f.m4:1486
-        else wz = st[2].w[i2] * inv_h3;
-#pragma unroll
-        for (int i1 = 0; i1 < W; ++i1) {
-            const double t = st[1].w[i1] * wz;  // f.m4:1489-1492
-            double* const row = reinterpret_cast<double*>(plane + 8 * COLX * i1);
-            if ((rm >> (W * i2 + i1)) & (RM)1) {  // lanes whose row is clipped or not owned sit the row out
-#pragma unroll
-                for (int i0 = 0; i0 < W; ++i0)
-                    __hip_atomic_fetch_add(row + i0, w0v[i0] * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        }
-    }
-    }
-    clk.lap(3);
-}
-
-#ifndef IBTK_LE_SPREAD_FLAT
-#define IBTK_LE_SPREAD_FLAT 1
-#endif
-// spread_lanes with fewer instructions per chunk (the sweep is issue-bound):
-// every stencil row is added by every busy lane, a clipped or not-owned row
-// or plane with weight 0 at its row wrapped into the column (a +0 on an owned
-// point; clamping would pile the masked rows of dense chunks onto one row), so
-// there is no exec mask and branch per row -- one address add per row instead; validity masks from clipped ranges; IB_4's square root by rsq
-// and Newton steps (the spread is compared by tolerance).
-template <int K, int ZH>
-__device__ __forceinline__ void spread_lanes_flat(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
-                                                  bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
-                                                  int yhi, int plo, int phi, double inv_h3, const double* inv_d,
-                                                  Clk& clk) {
-    using S = SSh<K, ZH>;
-    constexpr int W = S::W, FAM = S::FAM, NSL = S::NSL;
-    St<W> st[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        const double Xraw = (FAM == 2) ? p.X[(int64_t)3 * cdat.s + d] : cdat.X[d];
-        stencil1d<K, true>(cdat.X[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis,
-                           p.K6, st[d], inv_d[d]);
-    }
     const int ox = st[0].icl - X0, oy = st[1].icl - Y0, oz = st[2].icl - (zorg + a);
-    // binning invariant (and the memory bound of the x spill: ox in [-16, COLX + 15 - (W - 1)])
-    const bool bad = (unsigned)(ox + S::GUARD) > (unsigned)(COLX + 15 - (W - 1) + S::GUARD) ||
-                     (unsigned)(oy + 60) > 120u || (unsigned)(oz + 60) > 120u;
+    // binning invariant: every stencil index lies in [key + LO, key + HI] and the
+    // candidates' key cells lie within HI / -LO of the column (key_band), +-1 for
+    // a NINT tie of the multiply.  The ring addresses are wrapped, so memory
+    // stays safe anyway.
+    constexpr int LO = S::LO, HI = S::HI;
+    const bool bad = ox < LO - HI - 1 || ox + W - 1 > COLX - LO + HI || oy < LO - HI - 1 || oy + W - 1 > COLY - LO + HI;
     if (act && bad) atomicOr(p.err, 2);
     if (!act || bad) return;  // idle lanes sit the adds out
     // owned and clipped-in ranges of the stencil indices
     const int x0 = max(st[0].ist, xlo - ox), x1 = min(st[0].isp, xhi - ox);
     const int y0 = max(st[1].ist, ylo - oy), y1 = min(st[1].isp, yhi - oy);
-    // planes within the ring's reach of the lane's anchor, [LO, ZH] (a stencil moved
-    // by a NINT tie of the multiply -- a weight of an ulp's order -- is cut there)
+    // planes within the ring's reach of the lane's anchor, [LO, HI] (a stencil
+    // moved by a NINT tie of the multiply -- a weight of an ulp's order -- is cut there)
     const int z0 = max(max(st[2].ist, plo - (a + oz)), S::LO - oz);
     const int z1 = min(min(st[2].isp, phi - (a + oz)), S::HI - oz);
-    double w0v[W], w1m[W], w2m[W];
-    int roff[W];  // byte offset of stencil row i1 (wrapped into the column) from row 0 of the plane
+    double wx[W], wy[W], wz[W];
 #pragma unroll
     for (int i = 0; i < W; ++i) {
-        w0v[i] = (i >= x0 && i <= x1) ? st[0].w[i] * cdat.V : 0.0;
-        w1m[i] = (i >= y0 && i <= y1) ? st[1].w[i] : 0.0;
-        w2m[i] = (i >= z0 && i <= z1) ? st[2].w[i] * inv_h3 : 0.0;
-        roff[i] = 8 * COLX * (((oy + i) % COLY + COLY) % COLY);  // masked rows wrap (no pile-up on one row)
+        wx[i] = (i >= x0 && i <= x1) ? st[0].w[i] * cdat.V : 0.0;  // V applied first (f.m4:1512-1513 up to rounding)
+        wy[i] = (i >= y0 && i <= y1) ? st[1].w[i] : 0.0;
+        wz[i] = (i >= z0 && i <= z1) ? st[2].w[i] * inv_h3 : 0.0;
     }
-    char* const base = reinterpret_cast<char*>(ring) + 8 * ox;
+    int rx = 0, ry = 0;
+    if constexpr (ROT) {
+        const int lane = lane_id();
+        rx = ((lane & 3) - ox) & 3;
+        ry = (((lane >> 2) & 3) - oy) & 3;
+        rot4(wx, rx);
+        rot4(wy, ry);
+    }
+    // byte offsets in a slot of the points of step (s0, s1): the x and y parts
+    // of ring_wrapped, summed
+    int off[W * W];
+    {
+        int bx[W], by[W];
+#pragma unroll
+        for (int s = 0; s < W; ++s) {
+            const int xw = (ox + ((ROT && s < 4) ? ((s + rx) & 3) : s)) & (COLX - 1);
+            const int yv = oy + ((ROT && s < 4) ? ((s + ry) & 3) : s);
+            const int yw = ((yv % COLY) + COLY) % COLY;
+            bx[s] = 8 * (16 * (xw >> 2) + (xw & 3));
+            by[s] = 8 * (16 * (COLX / 4) * (yw >> 2) + 4 * (yw & 3));
+        }
+#pragma unroll
+        for (int s1 = 0; s1 < W; ++s1)
+#pragma unroll
+            for (int s0 = 0; s0 < W; ++s0) off[s1 * W + s0] = bx[s0] + by[s1];
+    }
+    double P[W * W];
+#pragma unroll
+    for (int s1 = 0; s1 < W; ++s1)
+#pragma unroll
+        for (int s0 = 0; s0 < W; ++s0) P[s1 * W + s0] = wx[s0] * wy[s1];
+    char* const rb = reinterpret_cast<char*>(ring);
     int sl = (int)((unsigned)(a + oz + 64 * NSL) % (unsigned)NSL);  // ring slot of plane i2 = 0
     clk.lap(2);
-#if IBTK_LE_DIAG_SPREAD_NOADD
-    double diag = 0.0;
-#endif
 #pragma unroll
     for (int i2 = 0; i2 < W; ++i2) {
-        char* const plane = base + sl * (8 * S::SLOT);
+        char* const plane = rb + sl * (8 * S::PV);
         sl = sl + 1 == NSL ? 0 : sl + 1;
         // lanes whose plane is clipped or not owned sit it out (one exec mask per
         // plane: the edge anchors of a short z-piece reach mostly unowned planes)
         if (!(i2 >= z0 && i2 <= z1)) continue;
+        const double w2 = wz[i2];
+        // the plane's values and addresses first, each in a register of its own
+        // (the empty asm holds it there), then the adds back to back: otherwise
+        // the compiler recycles one register pair, so that every ds_add_f64 waits
+        // for its own multiply and the next multiply for the ds_add
+        double v[W * W];
+        char* ad[W * W];
 #pragma unroll
-        for (int i1 = 0; i1 < W; ++i1) {
-            const double t = w1m[i1] * w2m[i2];
-            double* const row = reinterpret_cast<double*>(plane + roff[i1]);
-#pragma unroll
-            for (int i0 = 0; i0 < W; ++i0) {
-#if IBTK_LE_DIAG_SPREAD_NOADD  // diagnostic: the weights and addresses without the LDS adds
-                diag = diag + w0v[i0] * t + (double)(reinterpret_cast<uintptr_t>(row + i0) & 1);
-#else
-                __hip_atomic_fetch_add(row + i0, w0v[i0] * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
-            }
-        }
-    }
-#if IBTK_LE_DIAG_SPREAD_NOADD
-    __hip_atomic_fetch_add(reinterpret_cast<double*>(base), diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
-    clk.lap(3);
-}
-
-template <int K, int ZH>
-__device__ __forceinline__ void spread_lanes(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
-                                             bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
-                                             int yhi, int plo, int phi, double inv_h3, const double* inv_d, Clk& clk) {
-    if constexpr (IBTK_LE_SPREAD_FLAT)
-        spread_lanes_flat<K, ZH>(p, cd, ring, cdat, act, a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi, inv_h3, inv_d, clk);
-    else
-        spread_lanes_rows<K, ZH>(p, cd, ring, cdat, act, a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi, inv_h3, inv_d, clk);
-}
-
-// The adds of one staged candidate per lane for W = 4 kernels, conflict-free by
-// construction (SSh::ROT).  The 16 points (i0, i1) of a stencil plane sit at
-// ring offsets i0 + RS i1 with RS = 4 mod 16, so point k = i0 + 4 i1 has bank
-// class (B + k) mod 16, B the class of the stencil's first point.  At add step t
-// lane l adds point k = (t + rho) mod 16 with rho = (l - B) mod 16, i.e. the
-// point of class (l + t) mod 16: the 16 lanes of every ds_add_f64 lane group hit
-// 16 distinct classes, whatever the positions (no dealing, no conflicts).  Each
-// lane walks its own 16 points in a rotated order, plane by plane; the order
-// in which one grid point receives its contributions is still fixed by the
-// staging order and the lane order within an instruction (bit-stable).
-// Clipped and not-owned points get weight 0 and a trash address of the same
-// class; idle lanes sit the adds out.
-template <int K, int ZH>
-__device__ __forceinline__ void spread_rot(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
-                                           bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
-                                           int yhi, int plo, int phi, double inv_h3, const double* inv_d) {
-    using S = SSh<K, ZH>;
-    constexpr int W = S::W, FAM = S::FAM, LO = S::LO, NS = S::NS, NSL = S::NSL, RS = S::RS;
-    static_assert(W == 4, "rotated adds: 16 points per stencil plane");
-    St<W> st[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        const double Xraw = (FAM == 2) ? p.X[(int64_t)3 * cdat.s + d] : cdat.X[d];
-        stencil1d<K, true>(cdat.X[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis,
-                           p.K6, st[d], inv_d[d]);
-    }
-    int ox = st[0].icl - X0, oy = st[1].icl - Y0, oz = st[2].icl - (zorg + a);
-    bool ok = act;
-    // binning invariant (a net for binning errors: the owned points a lane adds
-    // lie in the column, and every address stays in the ring whatever it is):
-    // the stencil starts near the anchor's plane range and the column's reach
-    // bands (conservative: a stencil starting at -4 or at COLX / COLY reaches no
-    // owned point; the piecewise-cubic start moves up when it is clipped)
-    if (act && (ox < -8 || ox > COLX + 8 || oy < -8 || oy > COLY + 8 || oz < LO - 4 || oz > LO + NS)) {
-        atomicOr(p.err, 2);
-        ok = false;
-    }
-    if (!ok) return;  // idle lanes sit the adds out
-    double w0v[W], w1m[W], w2m[W];
-    unsigned xv = 0, yv = 0;
-#pragma unroll
-    for (int i = 0; i < W; ++i) {
-        const bool vx = i >= st[0].ist && i <= st[0].isp && ox + i >= xlo && ox + i <= xhi;
-        const bool vy = i >= st[1].ist && i <= st[1].isp && oy + i >= ylo && oy + i <= yhi;
-        const int pr = a + oz + i;  // relative plane
-        const bool vz = i >= st[2].ist && i <= st[2].isp && pr >= plo && pr <= phi;
-        xv |= vx ? 1u << i : 0u;
-        yv |= vy ? 1u << i : 0u;
-        w0v[i] = vx ? st[0].w[i] * cdat.V : 0.0;
-        w1m[i] = vy ? st[1].w[i] : 0.0;
-        w2m[i] = vz ? st[2].w[i] * inv_h3 : 0.0;
-    }
-    // byte offsets (in slot 0) of the 16 points of a stencil plane and their
-    // values before the z weight; not-owned points: the slot's trash row, same class
-    const unsigned rbase = (unsigned)(uintptr_t)ring;  // LDS byte address of the ring
-    const int b0 = ox + RS * oy;                          // ring index of point 0 (< 0 or past the column: spill)
-    const int B = (int)(((rbase >> 3) + (unsigned)b0) & 15u);
-    const int rho = (__lane_id() - B) & 15;
-    double P[16];
-    int A[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int i0 = k & 3, i1 = k >> 2;
-        const bool v = ((xv >> i0) & (yv >> i1) & 1u) != 0;
-        P[k] = w0v[i0] * w1m[i1];
-        A[k] = 8 * (v ? b0 + i0 + RS * i1 : S::TROW + ((B + k - (int)(rbase >> 3)) & 15));
-    }
-    // rotate left by rho: P'[t] = P[(t + rho) mod 16] (barrel, 4 stages)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const int sh = 1 << b;
-        const bool on = (rho >> b) & 1;
-        double Pn[16];
-        int An[16];
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            Pn[t] = on ? P[(t + sh) & 15] : P[t];
-            An[t] = on ? A[(t + sh) & 15] : A[t];
+        for (int k = 0; k < W * W; ++k) {
+            v[k] = P[k] * w2;
+            ad[k] = plane + off[k];
+            asm volatile("" ::"v"(v[k]));
         }
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            P[t] = Pn[t];
-            A[t] = An[t];
-        }
-    }
-    char* const rb = reinterpret_cast<char*>(ring);
-    int sl = (int)((unsigned)(a + oz + 64 * NSL) % (unsigned)NSL);  // ring slot of plane i2 = 0
-#pragma unroll
-    for (int i2 = 0; i2 < W; ++i2) {
-        const int poff = sl * (8 * S::SLOT);
-        sl = sl + 1 == NSL ? 0 : sl + 1;
-        const double wz = w2m[i2];
-#pragma unroll
-        for (int t = 0; t < 16; ++t)
-            __hip_atomic_fetch_add(reinterpret_cast<double*>(rb + A[t] + poff), P[t] * wz, __ATOMIC_RELAXED,
+        for (int k = 0; k < W * W; ++k)
+            __hip_atomic_fetch_add(reinterpret_cast<double*>(ad[k]), v[k], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    clk.lap(3);
 }
 
 // Spread work item = (segment, column, component).  Owned points: the column's
@@ -1460,20 +797,16 @@ __device__ __forceinline__ void spread_rot(const Params& p, const CompDesc& cd, 
 // ring holds planes a+LO..a+HI (u_old, then accumulating) plus a+HI+1 in
 // flight; plane a+LO is written back after anchor a and its slot takes plane
 // a+HI+2.  The candidates of anchor a+1 are staged while anchor a is added.
-template <int K, bool LVL, int ZH>
+template <int K, bool LVL>
 __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
-    using S = SSh<K, ZH>;
+    using S = SSh<K>;
     constexpr int LO = S::LO, HI = S::HI, NPL = S::NPL, FAM = S::FAM;
-    __shared__ double ring_mem[S::GUARD + S::NSL * S::SLOT + IBTK_LE_DIAG_SPREAD_LDSPAD];
-    double* const ring = ring_mem + S::GUARD;
-    if constexpr (IBTK_LE_DIAG_SPREAD_LDSPAD > 0)  // diagnostic: occupancy probe (keep the pad allocated)
-        if (p.dbg == 12345) ring_mem[S::GUARD + S::NSL * S::SLOT] = 0.0;
+    __shared__ double ring[S::NSL * S::PV];
     const int it = sweep_item(p, p.ncomp);
     if (it < 0) return;
     int c;
     SweepItem si;
     item_decode(p, it, c, si);
-    c = p.fcomp[c];  // this launch's component c is the call's component fcomp[c]
     const int col = si.col;
     const int lane = lane_id();
     ColGeom cg;
@@ -1504,14 +837,15 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         if (!__any(any)) return;
     }
     const int nlast = p.nsorted - 1;
-    // the lane's points q = lane + 64 k of a plane: array offsets (clamped into
-    // the array) and owned bits
+    // the lane's points of a plane: slot index lane + 64 k (tile-major, so the
+    // staging stores and writeback loads are contiguous in LDS), their array
+    // offsets (clamped into the array) and owned bits
     int loff[NPL];
     unsigned okxy = 0;
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
-        const int q = lane + k * SW;
-        const int xl = q & (COLX - 1), yl = q / COLX;
+        int xl, yl;
+        ring_xy(lane + k * SW, xl, yl);
         if (xl >= xlo && xl <= xhi && yl >= ylo && yl <= yhi) okxy |= 1u << k;
         const int x = min(max(X0 + xl, cd.lo[0]), cd.hi[0]), y = min(max(Y0 + yl, cd.lo[1]), cd.hi[1]);
         loff[k] = (x - cd.lo[0]) + (y - cd.lo[1]) * (int)cd.s1;
@@ -1533,77 +867,36 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         d.X[0] = xs.v[0];
         d.X[1] = xs.v[1];
         d.X[2] = xs.v[2];
-        if constexpr (IBTK_LE_SPREAD_FDIRECT) {  // F(s, c) through the sorted marker index (no gather pass)
-            const int sm = p.sorted_s[e];
-            const double v = p.Qin[(int64_t)p.Q_depth * sm + cd.qcomp];
-            d.V = p.ds ? v * p.ds[sm] : v;
-            d.s = sm;
-        } else {
-            d.V = p.sorted_F[(int64_t)c * p.nsorted + e];
-            d.s = FAM == 2 ? p.sorted_s[e] : 0;
-        }
+        d.V = p.sorted_F[(int64_t)c * p.nsorted + e];
+        d.s = FAM == 2 ? p.sorted_s[e] : 0;
     };
     Clk clk;
-    const double inv_dx = 1.0 / p.bg.dx[0];  // lane dealing only (approximate class)
     const double inv_h3 = 1.0 / p.h3;
     const double inv_d[3] = {1.0 / p.bg.dx[0], 1.0 / p.bg.dx[1], 1.0 / p.bg.dx[2]};
     // adds of the n <= 64 candidates held one per lane (lane j's anchor plane:
-    // a - 1 for j < r, else a): dealt over the lanes by bank class, then spread
+    // a - 1 for j < r, else a)
     auto process = [&](int a, int r, int n, const Cand& mine) {
-        if constexpr (IBTK_LE_DIAG_SPREAD_NOPROC) {  // diagnostic: the plane and candidate streams alone
-            if (mine.V == 12345.0) atomicOr(p.err, 8);
-            return;
-        }
-        if constexpr (S::ROT) {
-            spread_rot<K, ZH>(p, cd, ring, mine, lane < n, lane < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo,
-                          phi, inv_h3, inv_d);
-            return;
-        }
-#if IBTK_LE_SPREAD_DEAL == 1
-        const int cls = lane < n ? ((int)floor((mine.X[0] - cd.xlo[0]) * inv_dx + 0.5) & 15) : 16;
-        const int src = deal_lanes16<4>(cls);
-#elif IBTK_LE_SPREAD_DEAL == 0
-        const int src = lane;
-        if (true) {
-            spread_lanes<K, ZH>(p, cd, ring, mine, src < n, src < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi,
-                            inv_h3, inv_d, clk);
-            return;
-        }
-#elif IBTK_LE_SPREAD_DEAL == 2
-        const int src = (lane & 3) * 16 + (lane >> 2);  // static: blocks of 4 staged candidates per lane group
-#else
-        // static stride 4: lane group g takes the staged candidates k = g mod 4.
-        // With the bin keys' class digit the candidates of a bucket come in bank
-        // class order, so every 4th one of a range steps the class by about one:
-        // the groups get spread classes without ranking them (DEAL 1's ballots)
-        const int src = 4 * (lane & 15) + (lane >> 4);
-#endif
-        Cand d;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) d.X[k] = shfl_f64(mine.X[k], src);
-        d.V = shfl_f64(mine.V, src);
-        d.s = FAM == 2 ? __builtin_amdgcn_ds_bpermute(src << 2, mine.s) : 0;
-        spread_lanes<K, ZH>(p, cd, ring, d, src < n, src < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi,
+        spread_tiled<K>(p, cd, ring, mine, lane < n, lane < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi,
                         inv_h3, inv_d, clk);
     };
     // plane z -> registers (the lane's NPL points); registers -> ring slot
     auto plane_load = [&](int z, double* v) {
         const double* pb = plane_ptr(z);
 #pragma unroll
-        for (int k = 0; k < NPL; ++k) v[k] = IBTK_LE_DIAG_SPREAD_NOLOAD ? 0.0 : pb[loff[k]];
+        for (int k = 0; k < NPL; ++k) v[k] = pb[loff[k]];
     };
     auto plane_put = [&](int z, const double* v) {
-        double* sl = ring + sslot<K, ZH>(z) * S::SLOT;
+        double* sl = ring + sslot<K>(z) * S::PV;
 #pragma unroll
-        for (int k = 0; k < NPL; ++k) sl[ring_index<K>(lane + k * SW)] = v[k];
+        for (int k = 0; k < NPL; ++k) sl[lane + k * SW] = v[k];
     };
     auto plane_writeback = [&](int z) {  // owned points of plane z, ring -> array
         if (z < plo || z > phi) return;
-        const double* sl = ring + sslot<K, ZH>(z) * S::SLOT;
+        const double* sl = ring + sslot<K>(z) * S::PV;
         double* pb = const_cast<double*>(plane_ptr(z));
         double v[NPL];
 #pragma unroll
-        for (int k = 0; k < NPL; ++k) v[k] = sl[ring_index<K>(lane + k * SW)];
+        for (int k = 0; k < NPL; ++k) v[k] = sl[lane + k * SW];
 #pragma unroll
         for (int k = 0; k < NPL; ++k) {  // not-owned points store to the sink: no branch per store
             double* dst = ((okxy >> k) & 1u) ? pb + loff[k] : p.sink + lane;
@@ -1625,8 +918,6 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         plane_put(z, pv);
     }
     plane_load(afirst + HI, pv);
-    double pv2[IBTK_LE_SPF >= 2 ? NPL : 1];  // SPF 2: the plane after it, loaded a step earlier
-    if constexpr (IBTK_LE_SPF >= 2) plane_load(afirst + HI + 1, pv2);
     int rowv[3];
     rows_load(afirst, rowv);
     Ranges rg;  // ranges of the anchor whose chunk 1 is prefetched (wave-uniform)
@@ -1652,11 +943,6 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         const int nmid = (tCur - h) / SW;       // full middle chunks
         const int r_a = (tCur - h) % SW;        // carried into a+1
         clk.lap(1);
-#if IBTK_LE_SPREAD_EARLY
-        // the adds of chunk 1 first: they drain through the LDS while the prefetch
-        // below computes (the next writeback waits for them)
-        if (cur_n > 0) process(a, cur_r, cur_n, cur);
-#endif
         // prefetch for a+1: its ranges, its chunk 1, plane a+HI+1, the rows of a+2
         if (a + 1 <= alast) {
             make_ranges_lanes(rowv, rg);
@@ -1667,18 +953,10 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
             etail = range_pos(rg, max(tA - SW + lane, 0));
             n1 = r_a + min(SW - r_a, tA);
             r_prev = r_a;
-            if constexpr (IBTK_LE_SPF >= 2) {
-#pragma unroll
-                for (int k = 0; k < NPL; ++k) pv[k] = pv2[k];
-                plane_load(a + HI + 2, pv2);
-            } else {
-                plane_load(a + HI + 1, pv);
-            }
+            plane_load(a + HI + 1, pv);
             if (a + 2 <= alast) rows_load(a + 2, rowv);
         }
-#if !IBTK_LE_SPREAD_EARLY
         if (cur_n > 0) process(a, cur_r, cur_n, cur);
-#endif
         if (nmid > 0) {  // dense planes: the full middle chunks (ranges of a rebuilt)
             int rowm[3];
             rows_load(a, rowm);
@@ -1713,18 +991,13 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
 // Segment length: about IBTK_LE_SEG_ITEMS (column, segment) items over the
 // patch, but no segment shorter than 32 planes (the z halo of a segment is HI-LO
 // planes), and the patch's planes cut into segments of equal length (+-1).
-// Equal lengths matter more than the length: sweep_item gives each XCD an equal
-// share of the items, contiguous in (segment, column) order, so a short last
-// segment leaves the last XCD idle while the others carry its planes -- cfg4 at
-// S = 128 (8 x 128 + 11 planes) and S = 141 (7 x 141 + 48) ran the sweeps 9-11 %
-// slower than at S = 149 (6 x 149 + 141), the round-1 "narrow optimum"
-// (profiles/r02seg).  With equal segments the count hardly matters (5-14
-// segments within a few per cent, profiles/r02seg2).
+// Equal lengths matter more than the length: a short last segment leaves the
+// last XCD idle while the others carry its planes -- cfg4 at S = 128 (8 x 128 +
+// 11 planes) and S = 141 (7 x 141 + 48) ran the sweeps 9-11 % slower than at
+// S = 149 (profiles/r02seg); with equal segments 5-14 segments per patch are
+// within a few per cent (profiles/r02seg2).
 #ifndef IBTK_LE_SEG_ITEMS
 #define IBTK_LE_SEG_ITEMS 16384
-#endif
-#ifndef IBTK_LE_SEG_EQUAL
-#define IBTK_LE_SEG_EQUAL 1  // 0: segments of the target length and a shorter last one (round 1)
 #endif
 // Segments shorter than MIN_SEG planes are not cut: a segment re-reads HI - LO
 // planes of z halo (interp) or anchors (spread), so a thin z-slab (8 GPUs: 139
@@ -1746,10 +1019,8 @@ void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items, bool le
     if (s < 32) s = 32;
     if (s > cg.nz) s = cg.nz;
     if (s < 1) s = 1;
-    if (IBTK_LE_SEG_EQUAL) {
-        const long long ns = (cg.nz + s - 1) / s;  // segments of about s planes, equal (+-1)
-        s = (cg.nz + ns - 1) / ns;
-    }
+    const long long ns = (cg.nz + s - 1) / s;  // segments of about s planes, equal (+-1)
+    s = (cg.nz + ns - 1) / ns;
     S = (int)s;
     nseg = (cg.nz + S - 1) / S;
 }
@@ -1760,7 +1031,7 @@ void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items, bool le
 // disjoint planes, so every grid point still gets its contributions from one
 // item.  The interp does not depend on the split (one lane sums a marker); the
 // spread adds a point's contributions anchor by anchor in sorted order, but two
-// candidates of one 64-lane chunk that hit the same point add in their dealt
+// candidates of one 64-lane chunk that hit the same point add in their step and
 // lane order, and where the chunks start depends on the item's first anchor: so
 // a different split can round a spread sum differently (fixed settings are
 // bit-stable run to run; tests/test_gpu_items.py).  The interp
@@ -1911,20 +1182,20 @@ template <int K> hipError_t launch_bin_col_t(const Params& p, int n, unsigned* k
 }
 // bucket starts before the first and after the last sorted key; -1 (k_bucket_fix)
 // in between
-__global__ __launch_bounds__(BLOCK) void k_bucket_ends(const unsigned* skeys, int kb, int n, int nbuckets, int* bs) {
+__global__ __launch_bounds__(BLOCK) void k_bucket_ends(const unsigned* skeys, int n, int nbuckets, int* bs) {
     const int b = blockIdx.x * BLOCK + threadIdx.x;
     if (b > nbuckets) return;
-    const int first = (int)min(skeys[0] >> kb, (unsigned)nbuckets), last = (int)min(skeys[n - 1] >> kb, (unsigned)nbuckets);
+    const int first = (int)min(skeys[0], (unsigned)nbuckets), last = (int)min(skeys[n - 1], (unsigned)nbuckets);
     bs[b] = b <= first ? 0 : (b > last ? n : -1);
 }
 // the buckets k_gather_col left (long empty runs): the first entry whose key >= b
-__global__ __launch_bounds__(BLOCK) void k_bucket_fix(const unsigned* skeys, int kb, int n, int nbuckets, int* bs) {
+__global__ __launch_bounds__(BLOCK) void k_bucket_fix(const unsigned* skeys, int n, int nbuckets, int* bs) {
     const int b = blockIdx.x * BLOCK + threadIdx.x;
     if (b > nbuckets || bs[b] >= 0) return;
     int lo = 0, hi = n;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if ((int)min(skeys[mid] >> kb, (unsigned)nbuckets) < b) lo = mid + 1;
+        if ((int)min(skeys[mid], (unsigned)nbuckets) < b) lo = mid + 1;
         else hi = mid;
     }
     bs[b] = lo;
@@ -1934,64 +1205,21 @@ template <int K>
 hipError_t launch_gather_col_t(const Params& p, int n, int* ss, double* sx, const unsigned* skeys, int nbuckets,
                                int* bs, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_bucket_ends, dim3((nbuckets + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, skeys, p.kbits, n, nbuckets,
-                       bs);
+    const dim3 gb((nbuckets + 1 + BLOCK - 1) / BLOCK);
+    hipLaunchKernelGGL(k_bucket_ends, gb, dim3(BLOCK), 0, s, skeys, n, nbuckets, bs);
     hipLaunchKernelGGL(k_gather_col<K>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, ss, sx, skeys,
                        nbuckets, bs);
-    hipLaunchKernelGGL(k_bucket_fix, dim3((nbuckets + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, skeys, p.kbits, n, nbuckets,
-                       bs);
+    hipLaunchKernelGGL(k_bucket_fix, gb, dim3(BLOCK), 0, s, skeys, n, nbuckets, bs);
     return hipGetLastError();
 }
 template <int K>
 hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     if (ev0) (void)hipEventRecord(ev0, s);
-    constexpr bool fits3 = 3 * ISh<K>::NSL * ISh<K>::PVP * 8 <= 160 * 1024;  // three rings in one CU's LDS
-    bool planes = false;  // the plane sweep (k_interp_planes): closed-form kernels, 1 or 3 components
-    if constexpr (KT<K>::FAM == 0) {
-        const bool frames = p.ipl_frames < 0 ? interp_plane_frames(p.comp, p.ncomp) : p.ipl_frames == 1;
-        planes = p.tune.interp_planes == 1 && frames && (p.ncomp == 3 || p.ncomp == 1);
-    }
-    if constexpr (KT<K>::FAM == 0) {
-        if (planes) {
-            const long items = (long)p.item_bound;
-            const dim3 g(sweep_grid(p, items)), b(IPl<K>::NT);
-            if (items > 0) {
-                if (p.ncomp == 3) {
-                    if (p.pd) hipLaunchKernelGGL((k_interp_planes<K, true, 3>), g, b, 0, s, p);
-                    else hipLaunchKernelGGL((k_interp_planes<K, false, 3>), g, b, 0, s, p);
-                } else {
-                    if (p.pd) hipLaunchKernelGGL((k_interp_planes<K, true, 1>), g, b, 0, s, p);
-                    else hipLaunchKernelGGL((k_interp_planes<K, false, 1>), g, b, 0, s, p);
-                }
-            }
-        }
-    }
-    if (planes) {
-    } else if constexpr (!fits3 || IBTK_LE_ICW != 3) {
-        const long items = (long)p.item_bound * p.ncomp;
-        if (items > 0) {
-            if (p.pd)
-                hipLaunchKernelGGL((k_interp_sweep<K, true, 1>), dim3(sweep_grid(p, items)), dim3(SW * IWAVES), 0, s, p);
-            else
-                hipLaunchKernelGGL((k_interp_sweep<K, false, 1>), dim3(sweep_grid(p, items)), dim3(SW * IWAVES), 0, s, p);
-        }
-    } else if (p.ncomp == 3) {  // the components of an item in one workgroup
-        const long items = (long)p.item_bound;
-        if (items > 0) {
-            if (p.pd)
-                hipLaunchKernelGGL((k_interp_sweep<K, true, 3>), dim3(sweep_grid(p, items)), dim3(SW * IWAVES * 3), 0, s, p);
-            else
-                hipLaunchKernelGGL((k_interp_sweep<K, false, 3>), dim3(sweep_grid(p, items)), dim3(SW * IWAVES * 3), 0, s,
-                                   p);
-        }
-    } else {
-        const long items = (long)p.item_bound * p.ncomp;
-        if (items > 0) {
-            if (p.pd)
-                hipLaunchKernelGGL((k_interp_sweep<K, true, 1>), dim3(sweep_grid(p, items)), dim3(SW * IWAVES), 0, s, p);
-            else
-                hipLaunchKernelGGL((k_interp_sweep<K, false, 1>), dim3(sweep_grid(p, items)), dim3(SW * IWAVES), 0, s, p);
-        }
+    const long items = (long)p.item_bound * p.ncomp;
+    if (items > 0) {
+        const dim3 g(sweep_grid(p, items)), b(SW * IWAVES);
+        if (p.pd) hipLaunchKernelGGL((k_interp_sweep<K, true>), g, b, 0, s, p);
+        else hipLaunchKernelGGL((k_interp_sweep<K, false>), g, b, 0, s, p);
     }
     if (ev1) (void)hipEventRecord(ev1, s);
     hipError_t e = hipGetLastError();
@@ -2002,9 +1230,6 @@ hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent
 // sorted_F[c * n + e] = Q(qcomp_c, s(e)): the spread values in sorted order.
 // REC3: three components that are a whole 24-byte Q record (Q_depth 3, qcomp
 // 0, 1, 2: the side-centred force), read as one record per lane.
-struct Rec3 {
-    double v[3];
-};
 template <bool REC3>
 __global__ __launch_bounds__(BLOCK) void k_gather_F_col(Params p, int n, double* out) {
     const int e = blockIdx.x * BLOCK + threadIdx.x;
@@ -2013,7 +1238,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather_F_col(Params p, int n, double*
     // density-weighted spread: F ds rounded once, as LDataManager.cpp:446-451 forms it
     const double w = p.ds ? p.ds[s] : 1.0;
     if constexpr (REC3) {
-        const Rec3 r = *reinterpret_cast<const Rec3*>(p.Qin + (int64_t)3 * s);
+        const D3 r = ld3(p.Qin + (int64_t)3 * s);
 #pragma unroll
         for (int c = 0; c < 3; ++c) out[(int64_t)c * n + e] = p.ds ? r.v[c] * w : r.v[c];
     } else {
@@ -2025,36 +1250,20 @@ __global__ __launch_bounds__(BLOCK) void k_gather_F_col(Params p, int n, double*
 }
 
 template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-    if (!IBTK_LE_SPREAD_FDIRECT && p.nsorted > 0) {
+    if (p.nsorted > 0) {
         const bool rec3 = p.ncomp == 3 && p.Q_depth == 3 && p.comp[0].qcomp == 0 && p.comp[1].qcomp == 1 &&
                           p.comp[2].qcomp == 2;
         const dim3 g((p.nsorted + BLOCK - 1) / BLOCK), b(BLOCK);
         if (rec3) hipLaunchKernelGGL(k_gather_F_col<true>, g, b, 0, s, p, p.nsorted, const_cast<double*>(p.sorted_F));
         else hipLaunchKernelGGL(k_gather_F_col<false>, g, b, 0, s, p, p.nsorted, const_cast<double*>(p.sorted_F));
     }
-    if (ev0) (void)hipEventRecord(ev0, s);  // the events bracket the sweep kernels alone
-    // IBTK_LE_SPREAD_ZLOW: components whose z frame is the bin keys' cell frame
-    // take a ring one slot shorter (SSh's ZH: 7 waves per CU instead of 6 for
-    // IB_4), as a launch of their own.  Measured (profiles/r02z/zlow): cfg4
-    // spread 17.3 ms against 17.6 with the groups side by side on two streams,
-    // 17.3 one after the other; cfg5 3.7 / 4.1 against 3.4 (two launches, two
-    // tails).  Off: one launch, every component with the full ring.
-    Params q[2] = {p, p};
-    for (int g = 0; g < 2; ++g) q[g].ncomp = 0;
-    for (int c = 0; c < p.ncomp; ++c) {
-        const bool low = KT<K>::FAM == 0 && !SSh<K>::ROT && p.comp[c].zcell && IBTK_LE_SPREAD_ZLOW;
-        Params& g = q[low ? 0 : 1];
-        g.fcomp[g.ncomp++] = c;
+    if (ev0) (void)hipEventRecord(ev0, s);  // the events bracket the sweep kernel alone
+    const long items = (long)p.item_bound * p.ncomp;
+    if (items > 0) {
+        const dim3 g(sweep_grid(p, items)), b(SW);
+        if (p.pd) hipLaunchKernelGGL((k_spread_sweep<K, true>), g, b, 0, s, p);
+        else hipLaunchKernelGGL((k_spread_sweep<K, false>), g, b, 0, s, p);
     }
-    auto launch = [&](const Params& g, auto zh) {
-        constexpr int ZH = decltype(zh)::value;
-        const long items = (long)g.item_bound * g.ncomp;
-        if (items <= 0) return;
-        if (g.pd) hipLaunchKernelGGL((k_spread_sweep<K, true, ZH>), dim3(sweep_grid(g, items)), dim3(SW), 0, s, g);
-        else hipLaunchKernelGGL((k_spread_sweep<K, false, ZH>), dim3(sweep_grid(g, items)), dim3(SW), 0, s, g);
-    };
-    if constexpr (IBTK_LE_SPREAD_ZLOW) launch(q[0], std::integral_constant<int, KT<K>::HI - 1>{});
-    launch(q[1], std::integral_constant<int, KT<K>::HI>{});
     if (ev1) (void)hipEventRecord(ev1, s);
     return hipGetLastError();
 }

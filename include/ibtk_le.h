@@ -338,12 +338,11 @@ int ibtk_le_ctx_enable_timing(ibtk_le_ctx ctx, int enable);
  * items, which sets the segment length), "split_target" (own markers above
  * which a (column, segment) is cut into sub-segments), "strip" (column rows per
  * strip of the item order), "xcd_block" (light items over the XCDs in blocks of
- * this many table entries: 1 round-robin, -1 one range per XCD; default 8)
- * and "interp_planes" (1: the plane-at-a-time interp sweep, bitwise the same,
- * slower).  Interp results do not
- * depend on them; spread results are bit-stable for fixed settings and may differ
- * in the last bits between settings (same-point adds within one 64-candidate
- * chunk follow its lane order, and the chunk boundaries move with the items). */
+ * this many table entries: 1 round-robin, -1 one range per XCD; default 8).
+ * Interp results do not depend on them; spread results are bit-stable for fixed
+ * settings and may differ in the last bits between settings (same-point adds
+ * within one 64-candidate chunk follow its step and lane order, and the chunk
+ * boundaries move with the items). */
 int ibtk_le_ctx_tune(ibtk_le_ctx ctx, const char* key, int value);
 double ibtk_le_ctx_last_kernel_ms(ibtk_le_ctx ctx);
 

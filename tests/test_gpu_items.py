@@ -5,7 +5,7 @@ segment) pairs ("split_target") and the heavy-first schedule ("heavy") only
 regroup the same sweep.  Interp must be bitwise equal across settings and to
 the oracle; spread must match the oracle within 1e-12 under every setting and be
 bit-stable on a repeat.  (Spread sums may differ in the last bits between
-settings: same-point adds inside one 64-candidate chunk follow its dealt lane
+settings: same-point adds inside one 64-candidate chunk follow its step and lane
 order, and the chunk boundaries move with the items -- see le_sweep.hip.)
 Segment lengths from 32 planes to the whole patch, uniform and clustered."""
 import numpy as np
@@ -26,7 +26,6 @@ SETTINGS = [
     {"heavy": -1},                                        # no heavy-first ordering
     {"xcd_block": 1},                                     # light items round-robin over the XCDs
     {"xcd_block": 3},                                     # ... in blocks of 3 table entries
-    {"interp_planes": 1},                                 # the plane-at-a-time interp sweep
 ]
 
 

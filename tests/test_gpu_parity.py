@@ -103,35 +103,6 @@ CASES = [(k, nd, c) for k in ALL for nd in (2, 3) for c in ("side", "cell", "nod
          if not (c == "edge" and nd == 2)]
 
 
-PLANE_CASES = [(k, c) for k in ("IB_4", "IB_6", "BSPLINE_4", "IB_4_W8") for c in ("side", "cell", "node", "edge")]
-
-
-@pytest.mark.parametrize("kernel,centering", PLANE_CASES, ids=lambda v: str(v))
-def test_plane_interp_bitwise(le, oracle, kernel, centering):
-    """The plane-at-a-time interp sweep (ctx_tune interp_planes=1, k_interp_planes: all
-    components of an item in one workgroup, partial sums in registers across the planes)
-    sums in the Fortran order too: bitwise the oracle's, periodic images and a subset list
-    included (cell data of depth 2 is two components: it keeps the ring sweep)."""
-    geom, X, idx, xs, depth = make_case(kernel, 3, centering, seed=zlib.crc32(f"planes{kernel}{centering}".encode()))
-    rng = np.random.default_rng(17)
-    dev = "cuda:0"
-    q = geom.alloc(centering, depth)
-    for a in q:
-        a.copy_(torch.from_numpy(rng.uniform(-1, 1, tuple(a.shape))))
-    Xd = torch.from_numpy(X).to(dev)
-    pctx = le.Context(0)
-    pctx.tune("interp_planes", 1)
-    Qdepth = 3 if centering in ("side", "edge") else depth
-    Q = torch.full((X.shape[0], Qdepth), np.nan, dtype=torch.float64, device=dev)
-    m = le.Markers(pctx).bin(geom, kernel, Xd, torch.from_numpy(idx).to(dev), torch.from_numpy(xs).to(dev))
-    le.interp(pctx, m, kernel, centering, geom, q, Q, Xd, q_depth=depth)
-    pctx.synchronize()
-    Qg = Q.cpu().numpy()
-    Qo = np.full_like(Qg, np.nan)
-    oracle_call(oracle, "interp", kernel, centering, geom, [a.cpu().numpy().copy() for a in q], idx, xs, X, Qo, depth)
-    assert np.array_equal(Qg[idx], Qo[idx]), f"max diff {np.nanmax(np.abs(Qg[idx] - Qo[idx])):.3e}"
-
-
 @pytest.mark.parametrize("kernel,ndim,centering", CASES, ids=lambda v: str(v))
 def test_interp_matches_oracle(le, ctx, oracle, kernel, ndim, centering):
     geom, X, idx, xs, depth = make_case(kernel, ndim, centering, seed=zlib.crc32(f'{kernel}{ndim}{centering}'.encode()))
