@@ -271,7 +271,11 @@ def run_level(args, cfg, kernel, dev):
     E = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
     acc = {"fill": [], "bin": [], "interp": [], "zero": [], "spread": []}
 
+    dt_move = 0.05 * dx  # |U| <= ~1: markers move <= 1/20 cell per step
+
     def step(record):
+        if args.move:
+            return step_move(record)
         if record:
             E[0].record()
         lvl_i.fill_ghosts("side", u)
@@ -282,6 +286,33 @@ def run_level(args, cfg, kernel, dev):
         if record:
             E[2].record()
         lvl_i.interp("side", u, U, X)
+        if record:
+            E[3].record()
+        lvl_s.zero("side", f)
+        if record:
+            E[4].record()
+        lvl_s.spread("side", f, F, X)
+        if record:
+            E[5].record()
+
+    def step_move(record):
+        # a moving step on the level: interp at the current positions (the interior lists
+        # binned there), X += dt U, the per-patch lists rebuilt at the new positions
+        # (LIndexSetData's lists after redistribution), re-bin, spread
+        if record:
+            E[0].record()
+        lvl_i.fill_ghosts("side", u)
+        if record:
+            E[1].record()
+        lvl_i.interp("side", u, U, X)
+        if record:
+            E[2].record()
+        le.position_update(ctx, "euler", dt_move, X, U, out=X)
+        X.remainder_(1.0)
+        X.masked_fill_(X >= 1.0, 0.0)  # remainder can round up to L
+        (ii2, _, oi2), (si2, sx2, os2) = level_lists(X, N, P, g)
+        lvl_i.relist(ii2, None, oi2).bin(X)
+        lvl_s.relist(si2, sx2, os2).bin(X)
         if record:
             E[3].record()
         lvl_s.zero("side", f)
@@ -304,8 +335,12 @@ def run_level(args, cfg, kernel, dev):
         step(True)
         torch.cuda.synchronize()
         acc["fill"].append(E[0].elapsed_time(E[1]))
-        acc["bin"].append(E[1].elapsed_time(E[2]))
-        acc["interp"].append(E[2].elapsed_time(E[3]))
+        if args.move:  # E1-E2 interp, E2-E3 update + lists + bin
+            acc["interp"].append(E[1].elapsed_time(E[2]))
+            acc["bin"].append(E[2].elapsed_time(E[3]))
+        else:
+            acc["bin"].append(E[1].elapsed_time(E[2]))
+            acc["interp"].append(E[2].elapsed_time(E[3]))
         acc["zero"].append(E[3].elapsed_time(E[4]))
         acc["spread"].append(E[4].elapsed_time(E[5]))
     ctx.enable_timing(True)
@@ -332,8 +367,13 @@ def run_level(args, cfg, kernel, dev):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": cfg["desc"], "kernel": kernel, "grid": [N, N, N], "markers": M,
                    "parallelism": "one GPU", "patches": [P, P, P], "patch_cells": [n, n, n], "ghost": g,
-                   "step": "level ghost fill + bin(interior lists) + bin(ghost-box lists) + interp(3 comps) + "
-                           "zero f + spread(3 comps), one launch per sweep over the 512 patches"},
+                   "move": args.move,
+                   "step": ("level ghost fill + interp(3 comps) + position update + per-patch lists rebuilt "
+                            "(bench.level_lists, torch ops) + bin(interior, ghost-box lists) + zero f + "
+                            "spread(3 comps)" if args.move else
+                            "level ghost fill + bin(interior lists) + bin(ghost-box lists) + interp(3 comps) + "
+                            "zero f + spread(3 comps); stationary markers, per-patch lists built once at setup "
+                            "(LIndexSetData between regrids), one launch per sweep over the 512 patches")},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "algorithmic_bytes": {"interp": B_i, "spread": B_s}, "kernel_ms": {"interp": k_i, "spread": k_s}},
@@ -374,7 +414,15 @@ def main():
     ap.add_argument("--move", action="store_true",
                     help="a full explicit coupling step: interp, X += dt U (ibtk_le_position_update), "
                          "migrate the slab leavers (N > 1), re-bin, spread")
+    ap.add_argument("--renumber", action="store_true",
+                    help="with --move: after the migration, redistribute every step -- the level's local "
+                         "numbering, node offsets, nonlocal nodes and the LData reorder (slab.redistribute; "
+                         "the reference does this at regrid, LDataManager.cpp:1504-1959)")
     args = ap.parse_args()
+    if args.renumber and not args.move:
+        raise SystemExit("--renumber needs --move")
+    if args.renumber and CONFIGS[args.config].get("patches") and not args.single_patch:
+        raise SystemExit("--renumber: slab configurations only (cfg5's level: --single-patch)")
 
     import torch
     cfg = CONFIGS[args.config]
@@ -409,7 +457,7 @@ def main():
         return
 
     from ibamr_amd import le
-    from ibamr_amd.slab import GhostMarkers, Slab, SlabExchange, migrate, update_and_migrate
+    from ibamr_amd.slab import GhostMarkers, Slab, SlabExchange, migrate, redistribute, update_and_migrate
 
     N = cfg["N"]
     ghost = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
@@ -441,6 +489,8 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(4321 + rank)
     F = torch.rand((M_local, 3), dtype=torch.float64, device=dev, generator=gen).mul_(2).sub_(1)
     U = torch.zeros((M_local, 3), dtype=torch.float64, device=dev)
+    # Lagrangian indices (globally unique: rank-major generation order) for --renumber
+    lag = (torch.arange(M_local, dtype=torch.int32, device=dev) * world + rank) if args.renumber else None
     u = geom.alloc("side", device=dev)
     for a in u:
         a.uniform_(-1.0, 1.0, generator=gen)
@@ -514,7 +564,7 @@ def main():
     def step_move(record):
         # interp -> X += dt U -> migrate -> bin -> spread: one bin per step, as in
         # IBMethod's explicit loop (interpolateVelocity, eulerStep, spreadForce)
-        nonlocal X, F, U
+        nonlocal X, F, U, lag
         if record:
             E[0].record()
         interp_with_fill()
@@ -523,11 +573,19 @@ def main():
         if world > 1:
             # fused on the device: update, wrap, owner classes, stable partition;
             # the leavers to the z-neighbours (slab.update_and_migrate)
-            X, (F,) = update_and_migrate(slab, ctx, "euler", dt_move, X, U, [F])
+            if lag is None:
+                X, (F,) = update_and_migrate(slab, ctx, "euler", dt_move, X, U, [F])
+            else:
+                X, (F, lagf) = update_and_migrate(slab, ctx, "euler", dt_move, X, U, [F, lag.to(torch.float64)])
+                lag = lagf.to(torch.int32)
             if U.shape != X.shape:
                 U = torch.empty_like(X)
         else:
             le.position_update(ctx, "euler", dt_move, X, U, out=X)
+        if lag is not None:
+            # the level's numbering and the LData reorder (cell order again after the move)
+            d = redistribute(slab, ctx, X, [F], lag)
+            X, F, lag = d.X, d.fields[0], d.lag
         bin_step()
         if record:
             E[2].record()
@@ -609,6 +667,35 @@ def main():
         kt["spread"].append(ctx.last_kernel_ms())
     ctx.enable_timing(False)
 
+    # N > 1 overlap self-check on this backend (RCCL in the product): the overlapped
+    # exchanges (interior sweep items running while the ghost planes are in flight on
+    # the communicator's stream) must give the bits of the sequential form, on every rank
+    overlap_check = None
+    if world > 1 and not args.no_overlap and gm is None:
+        Xb = cur["X"]
+        Uo, Us = torch.empty_like(cur["U"]), torch.empty_like(cur["U"])
+        ex_u.halo_fill(lambda: le.interp(ctx, bins, kernel, "side", geom, u, Uo, Xb))
+        ex_u.halo_fill()
+        le.interp(ctx, bins, kernel, "side", geom, u, Us, Xb)
+        fo = []
+        for overlapped in (True, False):
+            for a in f:
+                a.zero_()
+            if overlapped:
+                ex_f.ghost_sum(lambda: le.spread(ctx, bins, kernel, "side", geom, f, cur["F"], Xb))
+            else:
+                le.spread(ctx, bins, kernel, "side", geom, f, cur["F"], Xb)
+                ex_f.ghost_sum()
+            fo.append([a.clone() for a in f])
+        same = torch.equal(Uo, Us) and all(torch.equal(a, b) for a, b in zip(*fo))
+        t = torch.tensor([0 if same else 1], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        overlap_check = "bitwise equal to the sequential exchange on every rank" if int(t.item()) == 0 else \
+            "DIFFERS from the sequential exchange"
+        del fo, Uo, Us
+        if int(t.item()):
+            log("overlap self-check FAILED: overlapped exchange differs from the sequential one")
+
     ms_per_step = 1e3 * elapsed / args.steps
     value = 2.0 * M_total * args.steps / elapsed
 
@@ -664,8 +751,11 @@ def main():
         "config": {"workload": cfg["desc"], "kernel": kernel, "grid": [N, N, N], "markers": M_total,
                    "parallelism": f"z-slab x{world}", "ghost": ghost, "marker_order": args.marker_order, "layout": args.layout, "spread_mode": args.spread_mode if world > 1 else "one rank",
                    "solo_slab": args.solo_slab or None,
-                   "move": args.move, "overlap": world > 1 and not args.no_overlap,
-                   "step": ("ghost fill + interp(3 comps) + position update + migrate + bin + zero ghosts + "
+                   "move": args.move, "renumber": args.renumber, "overlap": world > 1 and not args.no_overlap,
+                   "overlap_check": overlap_check,
+                   "step": ("ghost fill + interp(3 comps) + position update + migrate + " +
+                            ("redistribute (numbering + nonlocal nodes + reorder) + " if args.renumber else "") +
+                            "bin + zero ghosts + "
                             "spread(3 comps) + ghost sum" if args.move else
                             "bin + ghost fill + interp(3 comps) + zero ghosts + spread(3 comps) + ghost sum")},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -130,6 +130,16 @@ _SIGS = [
     ("ibtk_le_index_set_list", c_int,
      [c_void_p, ctypes.POINTER(PatchGeom), c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
       c_int, ctypes.POINTER(c_int)]),
+    ("ibtk_le_index_set_box_list", c_int,
+     [c_void_p, ctypes.POINTER(PatchGeom), c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+      c_void_p, c_void_p, c_int, ctypes.POINTER(c_int)]),
+    ("ibtk_le_list_in_box", c_int,
+     [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+      ctypes.POINTER(c_int)]),
+    ("ibtk_le_level_node_distribution", c_int,
+     [c_void_p, c_int, ctypes.POINTER(PatchGeom), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+      c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    ("ibtk_le_ldata_reorder", c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     ("ibtk_le_node_distribution", c_int,
      [c_void_p, ctypes.POINTER(PatchGeom), c_void_p, c_void_p, c_int, c_int, c_void_p, ctypes.POINTER(c_int),
       ctypes.POINTER(c_int)]),

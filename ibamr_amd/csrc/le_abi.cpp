@@ -99,6 +99,8 @@ struct ibtk_le_ctx_s {
     hipStream_t stream = nullptr;
     DevBuf keys_in, vals_in, temp, counts, offsets, fbuf;
     DevBuf lst_idx, lst_xs, lst_key, lst_perm;  // index-list / node-distribution scratch
+    DevBuf lst_cell, lst2_idx, lst2_xs, lst2_cell, lst_flag;  // index lists: cells, the sorted list, unique flags
+    DevBuf num_tab, num_lkey, num_ckey;                        // level numbering: tile table, keys
     DevBuf lvl_tab;                             // level ghost fill tables
     std::vector<char> lvl_host;                 // what lvl_tab holds
     DevBuf zero_tab;                            // level zero tables
@@ -177,7 +179,9 @@ extern "C" int ibtk_le_ctx_destroy(ibtk_le_ctx ctx) {
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->keys_in, &ctx->vals_in, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->fbuf, &ctx->err, &ctx->sink,
-                       &ctx->stamps, &ctx->lst_idx, &ctx->lst_xs, &ctx->lst_key, &ctx->lst_perm,
+                       &ctx->stamps, &ctx->lst_idx, &ctx->lst_xs, &ctx->lst_key, &ctx->lst_perm, &ctx->lst_cell,
+                       &ctx->lst2_idx, &ctx->lst2_xs, &ctx->lst2_cell, &ctx->lst_flag, &ctx->num_tab, &ctx->num_lkey,
+                       &ctx->num_ckey,
                        &ctx->lvl_tab, &ctx->zero_tab, &ctx->mig_cls, &ctx->mig_cnt})
         b->release();
     if (ctx->ev0) hipEventDestroy(ctx->ev0);
@@ -1424,29 +1428,80 @@ extern "C" int ibtk_le_zero_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* ge
 
 static int index_list_impl(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev, const int* lag_dev,
                            int n_markers, int ghost, const int* periodic, int which, const int* box_lo,
-                           const int* box_hi, int* indices_dev, double* Xshift_dev, int capacity, int* count);
+                           const int* box_hi, const int* sub_lo, const int* sub_hi, int* indices_dev,
+                           double* Xshift_dev, int* cells_dev, int capacity, int* count);
 
 extern "C" int ibtk_le_periodic_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
                                            int n_markers, int ghost, const int* periodic, int* indices_dev,
                                            double* Xshift_dev, int capacity, int* count) {
-    return index_list_impl(ctx, geom, X_dev, nullptr, n_markers, ghost, periodic, 0, nullptr, nullptr, indices_dev,
-                           Xshift_dev, capacity, count);
+    return index_list_impl(ctx, geom, X_dev, nullptr, n_markers, ghost, periodic, 0, nullptr, nullptr, nullptr, nullptr,
+                           indices_dev, Xshift_dev, nullptr, capacity, count);
 }
 
 extern "C" int ibtk_le_index_set_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
                                       const int* lag_dev, int n_markers, int ghost, const int* periodic, int which,
                                       int* indices_dev, double* Xshift_dev, int capacity, int* count) {
     if (which < 0 || which > 2) return fail(IBTK_LE_ERR_ARG, "which: 0 all, 1 interior, 2 ghost");
-    return index_list_impl(ctx, geom, X_dev, lag_dev, n_markers, ghost, periodic, which, nullptr, nullptr,
-                           indices_dev, Xshift_dev, capacity, count);
+    return index_list_impl(ctx, geom, X_dev, lag_dev, n_markers, ghost, periodic, which, nullptr, nullptr, nullptr,
+                           nullptr, indices_dev, Xshift_dev, nullptr, capacity, count);
+}
+
+extern "C" int ibtk_le_index_set_box_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
+                                          const int* lag_dev, int n_markers, int ghost, const int* periodic,
+                                          const int* box_lo, const int* box_hi, int* indices_dev, double* Xshift_dev,
+                                          int* cells_dev, int capacity, int* count) {
+    if (!box_lo || !box_hi) return fail(IBTK_LE_ERR_ARG, "null box");
+    return index_list_impl(ctx, geom, X_dev, lag_dev, n_markers, ghost, periodic, 0, nullptr, nullptr, box_lo, box_hi,
+                           indices_dev, Xshift_dev, cells_dev, capacity, count);
 }
 
 extern "C" int ibtk_le_box_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
                                       int n_markers, const int* box_lo, const int* box_hi, int* indices_dev,
                                       int capacity, int* count) {
     if (!box_lo || !box_hi) return fail(IBTK_LE_ERR_ARG, "null box");
-    return index_list_impl(ctx, geom, X_dev, nullptr, n_markers, 0, nullptr, 0, box_lo, box_hi, indices_dev, nullptr,
-                           capacity, count);
+    return index_list_impl(ctx, geom, X_dev, nullptr, n_markers, 0, nullptr, 0, box_lo, box_hi, nullptr, nullptr,
+                           indices_dev, nullptr, nullptr, capacity, count);
+}
+
+// Stable compaction of a list by flags (exclusive scan, one host sync for the count).
+static int compact_by_flags(ibtk_le_ctx ctx, int ndim, int n, const int* flag, const int* idx, const double* xs,
+                            const int* cells, int* idx_out, double* xs_out, int* cells_out, int capacity,
+                            int* count) {
+    const hipStream_t s = ctx->stream;
+    int rc;
+    if ((rc = ctx->lst_flag.ensure(sizeof(int) * (size_t)n))) return rc;
+    int* pos = ctx->lst_flag.as<int>();
+    size_t tb = 0;
+    HIP_TRY(launch_scan(nullptr, tb, flag, pos, n, s));
+    if ((rc = ctx->temp.ensure(tb))) return rc;
+    tb = ctx->temp.cap;
+    HIP_TRY(launch_scan(ctx->temp.p, tb, flag, pos, n, s));
+    int last[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&last[0], pos + n - 1, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&last[1], flag + n - 1, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *count = last[0] + last[1];
+    if (*count > capacity || (*count > 0 && !idx_out))
+        return fail(IBTK_LE_ERR_ARG, "index list needs %d entries, capacity %d", *count, capacity);
+    HIP_TRY(launch_compact_list(flag, pos, idx, xs, cells, ndim, n, idx_out, xs_out, cells_out, s));
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_list_in_box(ibtk_le_ctx ctx, int ndim, const int* cells_dev, const int* indices_dev,
+                                   const double* Xshift_dev, int n, const int* box_lo, const int* box_hi,
+                                   int* indices_out, double* Xshift_out, int capacity, int* count) {
+    if (!ctx || !count || !box_lo || !box_hi) return fail(IBTK_LE_ERR_ARG, "null argument");
+    if (ndim != 2 && ndim != 3) return fail(IBTK_LE_ERR_ARG, "ndim must be 2 or 3");
+    if (n < 0) return fail(IBTK_LE_ERR_ARG, "negative size");
+    *count = 0;
+    if (n == 0) return IBTK_LE_OK;
+    if (!cells_dev || !indices_dev) return fail(IBTK_LE_ERR_ARG, "null list");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    int rc;
+    if ((rc = ctx->lst_perm.ensure(sizeof(int) * (size_t)n))) return rc;
+    HIP_TRY(launch_in_box_flags(cells_dev, ndim, n, box_lo, box_hi, ctx->lst_perm.as<int>(), ctx->stream));
+    return compact_by_flags(ctx, ndim, n, ctx->lst_perm.as<int>(), indices_dev, Xshift_dev, nullptr, indices_out,
+                            Xshift_dev ? Xshift_out : nullptr, nullptr, capacity, count);
 }
 
 static ImageDesc image_desc(const ibtk_le_patch_geom* geom, int ghost) {
@@ -1493,9 +1548,18 @@ static int sort_cell_lag(ibtk_le_ctx ctx, const unsigned* cell_keys, const int* 
     return IBTK_LE_OK;
 }
 
+// The index lists of one patch (LIndexSetData::cacheLocalIndices, LIndexSetData.cpp:
+// 83-169, and LEInteractor::buildLocalIndices' box branch, LEInteractor.cpp:3070-3106):
+// every marker of the patch box at its cell and its periodic images at theirs, the
+// entries in the ghost box's cell iteration order, each cell's set sorted by
+// Lagrangian index and, when Lagrangian indices are given, uniqued
+// (LDataManager.cpp:1487-1493: the lowest marker index of equal ones is kept).
+// which selects interior / ghost cells, [sub_lo, sub_hi] any box of cells.  box_lo
+// instead: the X-only box filter (LEInteractor.cpp:3110-3139, marker order).
 static int index_list_impl(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev, const int* lag_dev,
                            int n_markers, int ghost, const int* periodic, int which, const int* box_lo,
-                           const int* box_hi, int* indices_dev, double* Xshift_dev, int capacity, int* count) {
+                           const int* box_hi, const int* sub_lo, const int* sub_hi, int* indices_dev,
+                           double* Xshift_dev, int* cells_dev, int capacity, int* count) {
     if (!ctx || !count) return fail(IBTK_LE_ERR_ARG, "null argument");
     if (int rc = check_geom(geom)) return rc;
     if (n_markers < 0 || ghost < 0) return fail(IBTK_LE_ERR_ARG, "negative size");
@@ -1511,6 +1575,11 @@ static int index_list_impl(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, cons
             d.filter = 1;
             d.flo[k] = box_lo[k];
             d.fhi[k] = box_hi[k];
+        }
+        if (sub_lo) {
+            d.sub = 1;
+            d.slo[k] = sub_lo[k];
+            d.shi[k] = sub_hi[k];
         }
         gcells *= (unsigned long long)(geom->iupper[k] - geom->ilower[k] + 1 + 2 * ghost);
     }
@@ -1531,29 +1600,47 @@ static int index_list_impl(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, cons
     HIP_TRY(hipStreamSynchronize(s));
     const int total = last[0] + last[1];
     *count = total;
-    if (total > capacity || !indices_dev || (!Xshift_dev && !box_lo))
-        return fail(IBTK_LE_ERR_ARG, "index list needs %d entries, capacity %d", total, capacity);
     if (box_lo) {  // LEInteractor.cpp:3110-3139: marker order
+        if (total > capacity || !indices_dev)
+            return fail(IBTK_LE_ERR_ARG, "index list needs %d entries, capacity %d", total, capacity);
         HIP_TRY(launch_image_write(d, X_dev, n_markers, ctx->offsets.as<int>(), indices_dev, Xshift_dev, nullptr,
-                                   capacity, s));
+                                   nullptr, capacity, s));
         return IBTK_LE_OK;
     }
     if (total == 0) return IBTK_LE_OK;
+    if (!lag_dev && (total > capacity || !indices_dev || !Xshift_dev))
+        return fail(IBTK_LE_ERR_ARG, "index list needs %d entries, capacity %d", total, capacity);
     // entries in marker order into scratch, then the reference's order: cells of
     // the ghost box in iteration order (x fastest), Lagrangian index within a cell
     const size_t nd = (size_t)geom->ndim;
     if ((rc = ctx->lst_idx.ensure(sizeof(int) * (size_t)total))) return rc;
     if ((rc = ctx->lst_xs.ensure(sizeof(double) * nd * (size_t)total))) return rc;
     if ((rc = ctx->lst_key.ensure(sizeof(unsigned) * (size_t)total))) return rc;
+    if ((rc = ctx->lst_cell.ensure(sizeof(int) * nd * (size_t)total))) return rc;
     if ((rc = ctx->lst_perm.ensure(sizeof(int) * (size_t)total))) return rc;
     HIP_TRY(launch_image_write(d, X_dev, n_markers, ctx->offsets.as<int>(), ctx->lst_idx.as<int>(),
-                               ctx->lst_xs.as<double>(), ctx->lst_key.as<unsigned>(), total, s));
+                               ctx->lst_xs.as<double>(), ctx->lst_key.as<unsigned>(), ctx->lst_cell.as<int>(), total,
+                               s));
     if ((rc = sort_cell_lag(ctx, ctx->lst_key.as<unsigned>(), ctx->lst_idx.as<int>(), lag_dev, total, gcells,
                             ctx->lst_perm.as<int>(), ctx->keys_in, ctx->vals_in)))
         return rc;
-    HIP_TRY(launch_perm_list(ctx->lst_perm.as<int>(), ctx->lst_idx.as<int>(), ctx->lst_xs.as<double>(), geom->ndim,
-                             total, indices_dev, Xshift_dev, s));
-    return IBTK_LE_OK;
+    if (!lag_dev) {  // markers by index: no two entries of one cell share one
+        HIP_TRY(launch_perm_list(ctx->lst_perm.as<int>(), ctx->lst_idx.as<int>(), ctx->lst_xs.as<double>(),
+                                 ctx->lst_cell.as<int>(), geom->ndim, total, indices_dev, Xshift_dev, cells_dev, s));
+        return IBTK_LE_OK;
+    }
+    // the sorted list into scratch, then the first of every (cell, Lagrangian index)
+    if ((rc = ctx->lst2_idx.ensure(sizeof(int) * (size_t)total))) return rc;
+    if ((rc = ctx->lst2_xs.ensure(sizeof(double) * nd * (size_t)total))) return rc;
+    if ((rc = ctx->lst2_cell.ensure(sizeof(int) * nd * (size_t)total))) return rc;
+    HIP_TRY(launch_perm_list(ctx->lst_perm.as<int>(), ctx->lst_idx.as<int>(), ctx->lst_xs.as<double>(),
+                             ctx->lst_cell.as<int>(), geom->ndim, total, ctx->lst2_idx.as<int>(),
+                             ctx->lst2_xs.as<double>(), ctx->lst2_cell.as<int>(), s));
+    const unsigned* skeys = ctx->keys_in.as<unsigned>() + total;  // sorted keys (sort_cell_lag)
+    int* flag = ctx->lst_perm.as<int>();                           // the permutation is spent
+    HIP_TRY(launch_unique_flags(skeys, ctx->lst2_idx.as<int>(), lag_dev, total, flag, s));
+    return compact_by_flags(ctx, geom->ndim, total, flag, ctx->lst2_idx.as<int>(), ctx->lst2_xs.as<double>(),
+                            ctx->lst2_cell.as<int>(), indices_dev, Xshift_dev, cells_dev, capacity, count);
 }
 
 // LDataManager::computeNodeDistribution (LDataManager.cpp:2839-3027) for one
@@ -1607,6 +1694,147 @@ extern "C" int ibtk_le_node_distribution(ibtk_le_ctx ctx, const ibtk_le_patch_ge
     HIP_TRY(hipStreamSynchronize(s));
     *n_local = cnt[0];
     *n_nonlocal = cnt[1];
+    return IBTK_LE_OK;
+}
+
+// Stable sort of (keys, vals) on the context stream: out_keys/out_vals may be
+// scratch of the caller; uses ctx->temp.
+static int sort_pairs(ibtk_le_ctx ctx, const unsigned* kin, unsigned* kout, const int* vin, int* vout, int n,
+                      int end_bit) {
+    size_t tb = 0;
+    HIP_TRY(launch_sort(nullptr, tb, kin, kout, vin, vout, n, end_bit, ctx->stream));
+    if (int rc = ctx->temp.ensure(tb)) return rc;
+    tb = ctx->temp.cap;
+    HIP_TRY(launch_sort(ctx->temp.p, tb, kin, kout, vin, vout, n, end_bit, ctx->stream));
+    return IBTK_LE_OK;
+}
+
+// LDataManager::computeNodeDistribution (LDataManager.cpp:2874-2947) over the local
+// patches of a level (geoms[q], q in PatchLevel order): the local nodes patch by
+// patch (data_begin(patch_box): box cells, x fastest; each cell's set by Lagrangian
+// index, uniqued, :1487-1493), then the nonlocal ones -- nodes of the patches' ghost
+// cells whose Lagrangian index no local node has -- each at its first sighting
+// (patches in order, a patch's ghost cells in ghost-box order).  The patches are equal
+// boxes aligned to one tiling of the domain [dom_lo, dom_hi] (periodic images across
+// its periodic sides, the index data's periodic ghost fill).
+extern "C" int ibtk_le_level_node_distribution(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms,
+                                               const int* dom_lo, const int* dom_hi, const int* periodic,
+                                               const double* X_dev, const int* lag_dev, int n_markers, int ghost,
+                                               int* order_dev, int* n_local, int* n_nonlocal) {
+    if (!ctx || !n_local || !n_nonlocal || !geoms || !dom_lo || !dom_hi) return fail(IBTK_LE_ERR_ARG, "null argument");
+    if (npatch < 1 || n_markers < 0 || ghost < 0) return fail(IBTK_LE_ERR_ARG, "bad sizes");
+    *n_local = *n_nonlocal = 0;
+    const int nd = geoms[0].ndim;
+    LevelNum L;
+    std::memset(&L, 0, sizeof(L));
+    L.ndim = nd;
+    L.g = ghost;
+    for (int q = 0; q < npatch; ++q) {
+        if (int rc = check_geom(&geoms[q])) return rc;
+        if (geoms[q].ndim != nd) return fail(IBTK_LE_ERR_ARG, "patches of different dimension");
+        for (int k = 0; k < nd; ++k) {
+            const int nk = geoms[q].iupper[k] - geoms[q].ilower[k] + 1;
+            if (q == 0) {
+                L.n[k] = nk;
+                L.org[k] = geoms[0].ilower[k];
+                L.dx[k] = geoms[0].dx[k];
+            }
+            if (nk != L.n[k] || geoms[q].dx[k] != L.dx[k])
+                return fail(IBTK_LE_ERR_ARG, "level numbering needs patches of one size and spacing");
+            L.org[k] = std::min(L.org[k], geoms[q].ilower[k]);
+        }
+    }
+    long long ntab = 1, pcells = 1, gcells = 1;
+    for (int k = 0; k < nd; ++k) {
+        int tmax = 0;
+        for (int q = 0; q < npatch; ++q) {
+            if ((geoms[q].ilower[k] - L.org[k]) % L.n[k])
+                return fail(IBTK_LE_ERR_ARG, "patch %d is not aligned to the level's tiling", q);
+            tmax = std::max(tmax, (geoms[q].ilower[k] - L.org[k]) / L.n[k]);
+        }
+        L.nt[k] = tmax + 1;
+        ntab *= L.nt[k];
+        pcells *= L.n[k];
+        gcells *= L.n[k] + 2 * ghost;
+        L.dom_lo[k] = dom_lo[k];
+        L.dom_hi[k] = dom_hi[k];
+        L.periodic[k] = periodic ? periodic[k] != 0 : 1;
+        L.xlo[k] = geoms[0].x_lower[k] - (double)(geoms[0].ilower[k] - dom_lo[k]) * L.dx[k];
+        L.xup[k] = L.xlo[k] + (double)(dom_hi[k] - dom_lo[k] + 1) * L.dx[k];
+    }
+    if ((long long)npatch * pcells >= 0xffffffffLL || (long long)npatch * gcells >= 0xfffffffeLL)
+        return fail(IBTK_LE_ERR_RANGE, "level too large for 32-bit node keys");
+    std::vector<int> tab((size_t)ntab, -1);
+    for (int q = 0; q < npatch; ++q) {
+        long long lin = 0, str = 1;
+        for (int k = 0; k < nd; ++k) {
+            lin += (long long)((geoms[q].ilower[k] - L.org[k]) / L.n[k]) * str;
+            str *= L.nt[k];
+        }
+        if (tab[(size_t)lin] >= 0) return fail(IBTK_LE_ERR_ARG, "patches %d and %d overlap", tab[(size_t)lin], q);
+        tab[(size_t)lin] = q;
+    }
+    if (n_markers == 0) return IBTK_LE_OK;
+    if (!X_dev || !order_dev) return fail(IBTK_LE_ERR_ARG, "null array");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    const hipStream_t s = ctx->stream;
+    const int n = n_markers;
+    int rc;
+    if ((rc = ctx->num_tab.ensure(sizeof(int) * tab.size()))) return rc;
+    if ((rc = ctx->num_lkey.ensure(sizeof(unsigned) * (size_t)n))) return rc;
+    if ((rc = ctx->num_ckey.ensure(sizeof(unsigned) * (size_t)n))) return rc;
+    if ((rc = ctx->lst_perm.ensure(sizeof(int) * (size_t)n))) return rc;
+    if ((rc = ctx->lst2_idx.ensure(2 * sizeof(int) * (size_t)n))) return rc;
+    if ((rc = ctx->lst_key.ensure(2 * sizeof(unsigned) * (size_t)n))) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->num_tab.p, tab.data(), sizeof(int) * tab.size(), hipMemcpyHostToDevice, s));
+    unsigned* lkey = ctx->num_lkey.as<unsigned>();
+    unsigned* ckey = ctx->num_ckey.as<unsigned>();
+    HIP_TRY(launch_level_node_keys(L, ctx->num_tab.as<int>(), X_dev, n, lkey, ckey, s));
+    // local nodes: by (patch, cell, Lagrangian index), the first of each (cell, index)
+    int* perm = ctx->lst_perm.as<int>();
+    if ((rc = sort_cell_lag(ctx, lkey, nullptr, lag_dev, n, 0xffffffffull, perm, ctx->keys_in, ctx->vals_in)))
+        return rc;
+    int* flag = ctx->lst2_idx.as<int>();
+    int* spare = flag + n;
+    HIP_TRY(launch_unique_flags(ctx->keys_in.as<unsigned>() + n, perm, lag_dev, n, flag, s));
+    int cnt = 0;
+    if ((rc = compact_by_flags(ctx, 1, n, flag, perm, nullptr, nullptr, order_dev, nullptr, nullptr, n, &cnt)))
+        return rc;
+    const int nl = cnt;
+    // nonlocal nodes: the markers by (Lagrangian index, first sighting), the head of
+    // every index run whose run holds no local node, then by first sighting
+    unsigned* k0 = ctx->lst_key.as<unsigned>();
+    unsigned* k1 = k0 + n;
+    int* v0 = ctx->vals_in.as<int>();
+    HIP_TRY(launch_iota(v0, n, s));
+    if ((rc = sort_pairs(ctx, ckey, k1, v0, perm, n, 32))) return rc;
+    HIP_TRY(launch_perm_keys(0, perm, nullptr, lag_dev, nullptr, n, k0, s));
+    if ((rc = sort_pairs(ctx, k0, k1, perm, spare, n, 32))) return rc;  // spare: markers by (lag, ckey)
+    HIP_TRY(launch_take_keys(ckey, spare, n, k0, s));
+    HIP_TRY(launch_nonlocal_flags(k0, spare, lag_dev, n, flag, s));
+    if ((rc = compact_by_flags(ctx, 1, n, flag, spare, nullptr, nullptr, perm, nullptr, nullptr, n, &cnt))) return rc;
+    const int nn = cnt;
+    if (nn > 0) {
+        HIP_TRY(launch_take_keys(ckey, perm, nn, k0, s));
+        if ((rc = sort_pairs(ctx, k0, k1, perm, order_dev + nl, nn, 32))) return rc;
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    *n_local = nl;
+    *n_nonlocal = nn;
+    return IBTK_LE_OK;
+}
+
+// endDataRedistribution's reorder of an LData (LDataManager.cpp:1823-1917): node i of
+// the new numbering takes the old row order_dev[i] (depth doubles per node).
+extern "C" int ibtk_le_ldata_reorder(ibtk_le_ctx ctx, const int* order_dev, int n, const double* in_dev, int depth,
+                                     double* out_dev) {
+    if (!ctx) return fail(IBTK_LE_ERR_ARG, "null context");
+    if (n < 0 || depth < 1) return fail(IBTK_LE_ERR_ARG, "bad sizes");
+    if (n == 0) return IBTK_LE_OK;
+    if (!order_dev || !in_dev || !out_dev) return fail(IBTK_LE_ERR_ARG, "null array");
+    if (in_dev == out_dev) return fail(IBTK_LE_ERR_ARG, "reorder needs distinct input and output");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    HIP_TRY(launch_rows_gather(order_dev, n, in_dev, depth, out_dev, ctx->stream));
     return IBTK_LE_OK;
 }
 

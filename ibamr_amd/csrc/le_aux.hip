@@ -377,7 +377,7 @@ __device__ __forceinline__ void cell_index(const ImageDesc& d, const double* X, 
 }
 
 __device__ __forceinline__ int image_walk(const ImageDesc& d, const double* X, int* idx_out, double* xs_out,
-                                          unsigned* key_out, int base, int capacity, int s) {
+                                          unsigned* key_out, int* cell_out, int base, int capacity, int s) {
     int c[3] = {0, 0, 0};
     cell_index(d, X, c);
     if (d.filter) {  // LEInteractor.cpp:3129-3137: keep markers whose cell is in the box
@@ -407,19 +407,24 @@ __device__ __forceinline__ int image_walk(const ImageDesc& d, const double* X, i
         }
         if (!ok) continue;
         // the image's cell: in the patch box (interior entry) or a ghost cell
-        bool interior = true;
+        bool interior = true, insub = true;
         unsigned key = 0, stride = 1;
         for (int k = 0; k < d.ndim; ++k) {
             const int n = d.ihi[k] - d.ilo[k] + 1;
             const int ci = c[k] + sh[k] * n;
             interior = interior && ci >= d.ilo[k] && ci <= d.ihi[k];
+            insub = insub && ci >= d.slo[k] && ci <= d.shi[k];
             key += (unsigned)(ci - (d.ilo[k] - d.ghost)) * stride;  // ghost-box linear index, x fastest
             stride *= (unsigned)(n + 2 * d.ghost);
         }
         if ((d.which == 1 && !interior) || (d.which == 2 && interior)) continue;
+        if (d.sub && !insub) continue;  // LEInteractor.cpp:3075: if (!box.contains(i)) continue
         if (idx_out && base + cnt < capacity) {
             idx_out[base + cnt] = s;
             if (key_out) key_out[base + cnt] = key;
+            if (cell_out)
+                for (int k = 0; k < d.ndim; ++k)
+                    cell_out[(int64_t)d.ndim * (base + cnt) + k] = c[k] + sh[k] * (d.ihi[k] - d.ilo[k] + 1);
             for (int k = 0; k < d.ndim; ++k) {
                 const int n = d.ihi[k] - d.ilo[k] + 1;
                 // LIndexSetData.cpp:141: static_cast<double>(offset[d]) * dx[d]
@@ -434,13 +439,14 @@ __device__ __forceinline__ int image_walk(const ImageDesc& d, const double* X, i
 __global__ __launch_bounds__(BLOCK) void k_image_count(ImageDesc d, const double* X, int n, int* counts) {
     const int s = blockIdx.x * BLOCK + threadIdx.x;
     if (s >= n) return;
-    counts[s] = image_walk(d, X + (int64_t)d.ndim * s, nullptr, nullptr, nullptr, 0, 0, s);
+    counts[s] = image_walk(d, X + (int64_t)d.ndim * s, nullptr, nullptr, nullptr, nullptr, 0, 0, s);
 }
 __global__ __launch_bounds__(BLOCK) void k_image_write(ImageDesc d, const double* X, int n, const int* offsets,
-                                                        int* idx, double* xs, unsigned* cellkey, int capacity) {
+                                                        int* idx, double* xs, unsigned* cellkey, int* cells,
+                                                        int capacity) {
     const int s = blockIdx.x * BLOCK + threadIdx.x;
     if (s >= n) return;
-    image_walk(d, X + (int64_t)d.ndim * s, idx, xs, cellkey, offsets[s], capacity, s);
+    image_walk(d, X + (int64_t)d.ndim * s, idx, xs, cellkey, cells, offsets[s], capacity, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -465,14 +471,41 @@ __global__ __launch_bounds__(BLOCK) void k_perm_keys(int mode, const int* perm, 
         out[i] = keys[j];
     }
 }
-__global__ __launch_bounds__(BLOCK) void k_perm_list(const int* perm, const int* idx, const double* xs, int ndim,
-                                                     int n, int* idx_out, double* xs_out) {
+__global__ __launch_bounds__(BLOCK) void k_perm_list(const int* perm, const int* idx, const double* xs,
+                                                     const int* cells, int ndim, int n, int* idx_out, double* xs_out,
+                                                     int* cells_out) {
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     const int j = perm[i];
     idx_out[i] = idx[j];
     if (xs_out)
         for (int k = 0; k < ndim; ++k) xs_out[(int64_t)ndim * i + k] = xs[(int64_t)ndim * j + k];
+    if (cells_out)
+        for (int k = 0; k < ndim; ++k) cells_out[(int64_t)ndim * i + k] = cells[(int64_t)ndim * j + k];
+}
+__global__ __launch_bounds__(BLOCK) void k_compact_list(const int* flag, const int* pos, const int* idx,
+                                                        const double* xs, const int* cells, int ndim, int n,
+                                                        int* idx_out, double* xs_out, int* cells_out) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n || !flag[i]) return;
+    const int o = pos[i];
+    idx_out[o] = idx[i];
+    if (xs_out)
+        for (int k = 0; k < ndim; ++k) xs_out[(int64_t)ndim * o + k] = xs[(int64_t)ndim * i + k];
+    if (cells_out)
+        for (int k = 0; k < ndim; ++k) cells_out[(int64_t)ndim * o + k] = cells[(int64_t)ndim * i + k];
+}
+__global__ __launch_bounds__(BLOCK) void k_in_box_flags(const int* cells, int ndim, int n, int lo0, int lo1, int lo2,
+                                                        int hi0, int hi1, int hi2, int* flag) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const int lo[3] = {lo0, lo1, lo2}, hi[3] = {hi0, hi1, hi2};
+    bool in = true;
+    for (int k = 0; k < ndim; ++k) {
+        const int c = cells[(int64_t)ndim * i + k];
+        in = in && c >= lo[k] && c <= hi[k];
+    }
+    flag[i] = in ? 1 : 0;
 }
 // computeNodeDistribution (LDataManager.cpp:2874-2947) for one patch: key =
 // patch-box linear index (local nodes, numbered first), then ncell + ghost-box
@@ -535,11 +568,30 @@ hipError_t launch_perm_keys(int mode, const int* perm, const int* idx, const int
                        out);
     return hipGetLastError();
 }
-hipError_t launch_perm_list(const int* perm, const int* idx, const double* xs, int ndim, int n, int* idx_out,
-                            double* xs_out, hipStream_t s) {
+hipError_t launch_perm_list(const int* perm, const int* idx, const double* xs, const int* cells, int ndim, int n,
+                            int* idx_out, double* xs_out, int* cells_out, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_perm_list, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, perm, idx, xs, ndim, n, idx_out,
-                       xs_out);
+    hipLaunchKernelGGL(k_perm_list, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, perm, idx, xs, cells, ndim, n,
+                       idx_out, xs_out, cells_out);
+    return hipGetLastError();
+}
+hipError_t launch_compact_list(const int* flag, const int* pos, const int* idx, const double* xs, const int* cells,
+                               int ndim, int n, int* idx_out, double* xs_out, int* cells_out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_compact_list, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, flag, pos, idx, xs, cells,
+                       ndim, n, idx_out, xs_out, cells_out);
+    return hipGetLastError();
+}
+hipError_t launch_in_box_flags(const int* cells, int ndim, int n, const int* lo, const int* hi, int* flag,
+                               hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int l[3] = {0, 0, 0}, h[3] = {0, 0, 0};
+    for (int k = 0; k < ndim; ++k) {
+        l[k] = lo[k];
+        h[k] = hi[k];
+    }
+    hipLaunchKernelGGL(k_in_box_flags, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, cells, ndim, n, l[0], l[1],
+                       l[2], h[0], h[1], h[2], flag);
     return hipGetLastError();
 }
 hipError_t launch_node_keys(const ImageDesc& d, const double* X, int n, unsigned* keys, hipStream_t s) {
@@ -547,6 +599,145 @@ hipError_t launch_node_keys(const ImageDesc& d, const double* X, int n, unsigned
     hipLaunchKernelGGL(k_node_keys, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, d, X, n, keys);
     return hipGetLastError();
 }
+// ---------------------------------------------------------------------------
+// level numbering: LDataManager::computeNodeDistribution (LDataManager.cpp:
+// 2874-2947) over the local patches of a level
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+
+__global__ __launch_bounds__(BLOCK) void k_level_node_keys(LevelNum L, const int* tab, const double* X, int n,
+                                                           unsigned* lkey, unsigned* ckey) {
+    const int s = blockIdx.x * BLOCK + threadIdx.x;
+    if (s >= n) return;
+    const int nd = L.ndim;
+    int c[3] = {0, 0, 0};
+    for (int k = 0; k < nd; ++k) {  // IndexUtilities::getCellIndex, IndexUtilities-inl.h:66-89
+        const double x = X[(int64_t)nd * s + k];
+        const double dl = x - L.xlo[k], du = x - L.xup[k];
+        if (fabs(dl) <= fabs(du)) c[k] = L.dom_lo[k] + (int)floor(dl / L.dx[k]);
+        else c[k] = L.dom_hi[k] + (int)floor(du / L.dx[k]) + 1;
+    }
+    const unsigned pcells = (unsigned)L.n[0] * (nd > 1 ? L.n[1] : 1) * (nd > 2 ? L.n[2] : 1);
+    unsigned gcells = 1;
+    for (int k = 0; k < nd; ++k) gcells *= (unsigned)(L.n[k] + 2 * L.g);
+    // the tile (patch) of a cell; -1 outside the table or not local
+    auto patch_of = [&](const int* cc, int* t) {
+        int lin = 0, str = 1;
+        for (int k = 0; k < nd; ++k) {
+            t[k] = floordiv(cc[k] - L.org[k], L.n[k]);
+            if (t[k] < 0 || t[k] >= L.nt[k]) return -1;
+            lin += t[k] * str;
+            str *= L.nt[k];
+        }
+        return tab[lin];
+    };
+    int t[3] = {0, 0, 0};
+    const int q = patch_of(c, t);
+    if (q >= 0) {  // a local node: its patch's box cells in box order, x fastest
+        unsigned k0 = 0, str = 1;
+        for (int k = 0; k < nd; ++k) {
+            k0 += (unsigned)(c[k] - (L.org[k] + t[k] * L.n[k])) * str;
+            str *= (unsigned)L.n[k];
+        }
+        lkey[s] = (unsigned)q * pcells + k0;
+        ckey[s] = 0u;
+        return;
+    }
+    // ghost cells of local patches (periodic images included): the first sighting
+    // in patch order, each patch's ghost box in box order
+    unsigned best = 0xffffffffu;
+    const int nsh = nd == 3 ? 27 : 9;
+    for (int j = 0; j < nsh; ++j) {
+        const int sh[3] = {j % 3 - 1, (j / 3) % 3 - 1, nd == 3 ? j / 9 - 1 : 0};
+        bool ok = true;
+        int ci[3] = {0, 0, 0};
+        for (int k = 0; k < nd; ++k) {
+            if (sh[k] != 0 && !L.periodic[k]) ok = false;
+            ci[k] = c[k] + sh[k] * (L.dom_hi[k] - L.dom_lo[k] + 1);
+        }
+        if (!ok) continue;
+        for (int m = 0; m < nsh; ++m) {  // the patches around the image's tile
+            const int o[3] = {m % 3 - 1, (m / 3) % 3 - 1, nd == 3 ? m / 9 - 1 : 0};
+            int tt[3] = {0, 0, 0}, lin = 0, str = 1;
+            bool in = true;
+            for (int k = 0; k < nd; ++k) {
+                tt[k] = floordiv(ci[k] - L.org[k], L.n[k]) + o[k];
+                in = in && tt[k] >= 0 && tt[k] < L.nt[k];
+                lin += tt[k] * str;
+                str *= L.nt[k];
+            }
+            if (!in) continue;
+            const int qq = tab[lin];
+            if (qq < 0) continue;
+            unsigned gk = 0, gs = 1;
+            for (int k = 0; k < nd; ++k) {
+                const int lo = L.org[k] + tt[k] * L.n[k] - L.g;
+                const int r = ci[k] - lo;
+                in = in && r >= 0 && r < L.n[k] + 2 * L.g;
+                gk += (unsigned)r * gs;
+                gs *= (unsigned)(L.n[k] + 2 * L.g);
+            }
+            if (!in) continue;
+            const unsigned key = (unsigned)qq * gcells + gk;
+            best = key < best ? key : best;
+        }
+    }
+    lkey[s] = 0xffffffffu;
+    ckey[s] = best == 0xffffffffu ? 0xffffffffu : best + 1u;
+}
+hipError_t launch_level_node_keys(const LevelNum& L, const int* tab, const double* X, int n, unsigned* lkey,
+                                  unsigned* ckey, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_level_node_keys, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, L, tab, X, n, lkey, ckey);
+    return hipGetLastError();
+}
+// entry i of the list sorted by (lag, ckey): the first of its lag run, and that run
+// has no local node (ckey 0 sorts first) -- a nonlocal node at its first sighting
+__global__ __launch_bounds__(BLOCK) void k_nonlocal_flags(const unsigned* sckey, const int* sorder, const int* lag,
+                                                          int n, int* flag) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const int a = sorder[i];
+    const bool first = i == 0 || (lag ? lag[sorder[i - 1]] : sorder[i - 1]) != (lag ? lag[a] : a);
+    flag[i] = first && sckey[i] != 0u && sckey[i] != 0xffffffffu ? 1 : 0;
+}
+hipError_t launch_nonlocal_flags(const unsigned* sckey, const int* sorder, const int* lag, int n, int* flag,
+                                 hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_nonlocal_flags, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, sckey, sorder, lag, n, flag);
+    return hipGetLastError();
+}
+__global__ __launch_bounds__(BLOCK) void k_take_keys(const unsigned* keys, const int* idx, int n, unsigned* out) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < n) out[i] = keys[idx[i]];
+}
+hipError_t launch_take_keys(const unsigned* keys, const int* idx, int n, unsigned* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_take_keys, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, keys, idx, n, out);
+    return hipGetLastError();
+}
+// endDataRedistribution's VecScatter of an LData (LDataManager.cpp:1823-1917): the
+// new node i takes the old row order[i]; 3-deep rows as one 24-byte record
+__global__ __launch_bounds__(BLOCK) void k_rows_gather(const int* order, int n, const double* in, int depth,
+                                                       double* out) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const int64_t j = order[i];
+    if (depth == 3) {
+        struct R3 {
+            double v[3];
+        };
+        *reinterpret_cast<R3*>(out + 3 * (int64_t)i) = *reinterpret_cast<const R3*>(in + 3 * j);
+    } else {
+        for (int k = 0; k < depth; ++k) out[(int64_t)depth * i + k] = in[(int64_t)depth * j + k];
+    }
+}
+hipError_t launch_rows_gather(const int* order, int n, const double* in, int depth, double* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rows_gather, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, order, n, in, depth, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_unique_flags(const unsigned* skeys, const int* sorder, const int* lag, int n, int* flag,
                                hipStream_t s) {
     if (n <= 0) return hipSuccess;
@@ -601,10 +792,10 @@ hipError_t launch_image_count(const ImageDesc& d, const double* X, int n, int* c
     return hipGetLastError();
 }
 hipError_t launch_image_write(const ImageDesc& d, const double* X, int n, const int* offsets, int* idx,
-                              double* xshift, unsigned* cellkey, int capacity, hipStream_t s) {
+                              double* xshift, unsigned* cellkey, int* cells, int capacity, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_image_write, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, d, X, n, offsets, idx,
-                       xshift, cellkey, capacity);
+                       xshift, cellkey, cells, capacity);
     return hipGetLastError();
 }
 

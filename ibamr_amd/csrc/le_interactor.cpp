@@ -48,7 +48,7 @@ struct Facade {
     void* stream = nullptr;
     ibtk_le_ctx ctx = nullptr;
     ibtk_le_markers m = nullptr;
-    DevScratch filt, hostQ, hostX;  // box-filtered list; staged std::vector data
+    DevScratch filt, filt_xs, hostQ, hostX;  // box-filtered list (indices, shifts); staged std::vector data
     void ensure() {
         if (ctx) return;
         check(ibtk_le_ctx_create(device, stream, &ctx));
@@ -160,9 +160,21 @@ List make_list(Facade& f, const Source& src, const PatchView& patch, const Box& 
         const LIndexSetBase& idx = *src.idx;
         if (box == patch.box) return {idx.interior_local_indices, idx.interior_periodic_shifts, idx.n_interior};
         if (box == idx.ghost_box) return {idx.local_indices, idx.periodic_shifts, idx.n};
-        throw LEInteractorError(IBTK_LE_ERR_ARG,
-                                "LEInteractor: index-set overloads support box == patch box (interior nodes) or box "
-                                "== the index set's ghost box (all nodes); other boxes need the per-cell node sets");
+        // LEInteractor.cpp:3070-3106: the nodes of the set's cells inside the box, in
+        // the set's order, each with its cell's periodic offset -- the entries of the
+        // all-nodes list whose cell lies in the box
+        if (!idx.cells)
+            throw LEInteractorError(IBTK_LE_ERR_ARG,
+                                    "LEInteractor: an index-set box other than the patch box or the ghost box needs "
+                                    "the index set's cells (LIndexSetBase::cells)");
+        if (idx.n <= 0) return {nullptr, nullptr, 0};
+        const int nd = patch.box.ndim;
+        int* oi = static_cast<int*>(f.filt.get(sizeof(int) * (size_t)idx.n));
+        double* ox = static_cast<double*>(f.filt_xs.get(sizeof(double) * (size_t)nd * idx.n));
+        int count = 0;
+        Facade::check(ibtk_le_list_in_box(f.ctx, nd, idx.cells, idx.local_indices, idx.periodic_shifts, idx.n,
+                                          box.lower, box.upper, oi, ox, idx.n, &count));
+        return {oi, ox, count};
     }
     const int n = src.n_markers;
     if (n <= 0) return {nullptr, nullptr, 0};

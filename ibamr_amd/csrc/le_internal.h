@@ -235,6 +235,8 @@ struct ImageDesc {
     int filter;           // 1: emit (s, 0) iff the cell lies in [flo, fhi] (no images)
     int flo[3], fhi[3];
     int which;            // images: 0 every cell of the ghost box, 1 patch-box cells, 2 the others
+    int sub;              // 1: images only in cells of [slo, shi] (buildLocalIndices' box, LEInteractor.cpp:3070-3106)
+    int slo[3], shi[3];
 };
 hipError_t launch_cell_keys(const ImageDesc& d, const double* X, int n, unsigned ncells, unsigned* keys, int* vals,
                             int* inside, hipStream_t s);
@@ -244,14 +246,20 @@ hipError_t launch_max_index(const int* idx, int n, int* out, hipStream_t s);
 hipError_t launch_dedup(const int* indices, const int* sorted_l, const int* sorted_s, int n, int* last, int* qdst,
                         int* ndup, hipStream_t s);
 hipError_t launch_image_write(const ImageDesc& d, const double* X, int n, const int* offsets, int* idx,
-                              double* xshift, unsigned* cellkey, int capacity, hipStream_t s);
+                              double* xshift, unsigned* cellkey, int* cells, int capacity, hipStream_t s);
 // small helpers of the reference-ordered lists (le_aux.hip)
 hipError_t launch_iota(int* v, int n, hipStream_t s);
 // out[i] = key_of(src[perm[i]]): mode 0 lag[idx[perm[i]]] (lag null: idx[perm[i]]), mode 1 keys[perm[i]]
 hipError_t launch_perm_keys(int mode, const int* perm, const int* idx, const int* lag, const unsigned* keys, int n,
                             unsigned* out, hipStream_t s);
-hipError_t launch_perm_list(const int* perm, const int* idx, const double* xs, int ndim, int n, int* idx_out,
-                            double* xs_out, hipStream_t s);
+hipError_t launch_perm_list(const int* perm, const int* idx, const double* xs, const int* cells, int ndim, int n,
+                            int* idx_out, double* xs_out, int* cells_out, hipStream_t s);
+// list entries kept where flag[i] (pos = exclusive scan of flag): out[pos[i]] = in[i]
+hipError_t launch_compact_list(const int* flag, const int* pos, const int* idx, const double* xs, const int* cells,
+                               int ndim, int n, int* idx_out, double* xs_out, int* cells_out, hipStream_t s);
+// flag[i] = cells[ndim i ..] lies in [lo, hi]
+hipError_t launch_in_box_flags(const int* cells, int ndim, int n, const int* lo, const int* hi, int* flag,
+                               hipStream_t s);
 // node distribution: region/cell keys (local cells, then the ghost box's others, then out)
 hipError_t launch_node_keys(const ImageDesc& d, const double* X, int n, unsigned* keys, hipStream_t s);
 // unique by (key, lag) over the sorted order: flag[i] = 1 for a first occurrence
@@ -259,6 +267,35 @@ hipError_t launch_unique_flags(const unsigned* skeys, const int* sorder, const i
                                hipStream_t s);
 hipError_t launch_compact(const int* sorder, const int* flag, const int* pos, const unsigned* skeys,
                           unsigned local_end, unsigned ghost_end, int n, int* out, int* counts, hipStream_t s);
+
+// Level numbering (ibtk_le_level_node_distribution, le_aux.hip): the local patches
+// of one level, equal boxes of n cells per dim aligned to a tiling from `org`; a
+// table of nt tiles maps a tile to the patch's rank in the level's patch order
+// (-1: not a local patch).  Cells by getCellIndex in the domain frame.
+struct LevelNum {
+    int ndim;
+    double xlo[3], xup[3], dx[3];  // domain frame
+    int dom_lo[3], dom_hi[3];      // domain cells (periodic images shift by its extent)
+    int periodic[3];
+    int n[3];                      // cells per patch
+    int org[3];                    // lower cell of tile (0, 0, 0)
+    int nt[3];                     // tiles per dim of the table
+    int g;                         // ghost width of the patches' index data
+};
+// cls[s]: 0 the marker lies in a local patch (key_local = patch rank * cells per
+// patch + its cell's box index), 1 only in ghost cells (key_ghost = the first
+// occurrence: patch rank * ghost-box cells + ghost-box index of its (image) cell),
+// 2 neither.  lkey = key_local for cls 0, else 0xffffffff; ckey = 0 for cls 0, 1 +
+// key_ghost for cls 1, 0xffffffff for cls 2.
+hipError_t launch_level_node_keys(const LevelNum& L, const int* tab, const double* X, int n, unsigned* lkey,
+                                  unsigned* ckey, hipStream_t s);
+// out[i * depth + k] = in[order[i] * depth + k]
+hipError_t launch_rows_gather(const int* order, int n, const double* in, int depth, double* out, hipStream_t s);
+// flag[i] = entry i of the (lag, ckey)-sorted list is the first of its lag run and not local
+hipError_t launch_nonlocal_flags(const unsigned* sckey, const int* sorder, const int* lag, int n, int* flag,
+                                 hipStream_t s);
+// out[i] = keys[idx[i]]
+hipError_t launch_take_keys(const unsigned* keys, const int* idx, int n, unsigned* out, hipStream_t s);
 
 // Ghost fill of a level of equal patches tiling a box (le_aux.hip): every ghost
 // point of every patch array takes the value of the patch that owns the point

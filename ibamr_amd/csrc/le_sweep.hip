@@ -41,6 +41,15 @@
 namespace ibtk_le {
 
 constexpr int SW = 64;  // one wavefront per work item
+#ifndef IBTK_LE_EXP_IVOL
+#define IBTK_LE_EXP_IVOL 0
+#endif
+#ifndef IBTK_LE_EXP_SNOSTORE
+#define IBTK_LE_EXP_SNOSTORE 0
+#endif
+#ifndef IBTK_LE_EXP_SNOLOAD
+#define IBTK_LE_EXP_SNOLOAD 0
+#endif
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
@@ -344,7 +353,12 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
 #pragma unroll
                 for (int r = 0; r < R; ++r)
 #pragma unroll
-                    for (int i0 = 0; i0 < W; ++i0) v[r * W + i0] = pl[(r0 + r) * RX + i0];
+                    for (int i0 = 0; i0 < W; ++i0)
+#if IBTK_LE_EXP_IVOL
+                        v[r * W + i0] = *(const volatile __attribute__((address_space(3))) double*)&pl[(r0 + r) * RX + i0];
+#else
+                        v[r * W + i0] = pl[(r0 + r) * RX + i0];
+#endif
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const double wyz = st[1].w[r0 + r] * st[2].w[i2];  // f.m4:1349-1353
@@ -883,7 +897,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     auto plane_load = [&](int z, double* v) {
         const double* pb = plane_ptr(z);
 #pragma unroll
-        for (int k = 0; k < NPL; ++k) v[k] = pb[loff[k]];
+        for (int k = 0; k < NPL; ++k) v[k] = IBTK_LE_EXP_SNOLOAD ? 0.0 : pb[loff[k]];
     };
     auto plane_put = [&](int z, const double* v) {
         double* sl = ring + sslot<K>(z) * S::PV;
@@ -899,7 +913,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         for (int k = 0; k < NPL; ++k) v[k] = sl[lane + k * SW];
 #pragma unroll
         for (int k = 0; k < NPL; ++k) {  // not-owned points store to the sink: no branch per store
-            double* dst = ((okxy >> k) & 1u) ? pb + loff[k] : p.sink + lane;
+            double* dst = ((okxy >> k) & 1u) && !IBTK_LE_EXP_SNOSTORE ? pb + loff[k] : p.sink + lane;
             *dst = v[k];
         }
     };

@@ -159,6 +159,7 @@ class Context:
         h = ctypes.c_void_p()
         check(self.lib.ibtk_le_ctx_create(device, ctypes.c_void_p(s.cuda_stream), ctypes.byref(h)))
         self.h = h
+        self.plane_window = (0, 0, -1)
 
     def set_stream(self, stream: torch.cuda.Stream):
         self.stream = stream
@@ -172,8 +173,10 @@ class Context:
 
     def set_plane_window(self, mode: int, zlo: int = 0, zhi: int = -1):
         """Restrict the next 3-D sweeps to the items inside (1) / outside (2) the planes
-        [zlo, zhi]; 0 = every item (ibtk_le_ctx_set_plane_window)."""
+        [zlo, zhi]; 0 = every item (ibtk_le_ctx_set_plane_window).  With mode 0 a
+        window zlo <= zhi still cuts the sweep items of later binnings at its faces."""
         check(self.lib.ibtk_le_ctx_set_plane_window(self.h, int(mode), int(zlo), int(zhi)))
+        self.plane_window = (int(mode), int(zlo), int(zhi))
 
     def tune(self, key: str, value: int):
         """Diagnostic overrides of the 3-D sweeps' work-item order (ibtk_le_ctx_tune)."""
@@ -352,6 +355,15 @@ class Level:
         self.bin(X)
         return self
 
+    def relist(self, indices: torch.Tensor, xshift: Optional[torch.Tensor], offsets: Sequence[int]):
+        """Replace the patches' lists (a regrid / redistribution; bin again after)."""
+        if len(offsets) != len(self.geoms) + 1:
+            raise ValueError("one offset per patch, plus the end")
+        self.indices = indices.to(torch.int32).contiguous()
+        self.xshift = xshift.contiguous() if xshift is not None else None
+        self._O = (ctypes.c_int * len(offsets))(*[int(o) for o in offsets])
+        return self
+
     def bin(self, X: torch.Tensor):
         """(Re-)bin the level's lists at positions X (ibtk_le_level_bin)."""
         check(self.ctx.lib.ibtk_le_level_bin(self.ctx.h, self.markers.h, len(self.geoms), self._G,
@@ -373,13 +385,17 @@ class Level:
     def _arrays(self, arrays):
         # the pointer table of a list of per-patch arrays, cached on the list object
         # (a level reuses its u and f arrays step after step)
+        # (a level reuses its u and f arrays step after step); reused only when every
+        # entry still has the device pointer it had, so an array replaced in place
+        # (arrays[q] = new tensors) rebuilds the table
         key = id(arrays)
-        hit = self.__dict__.setdefault("_ptr_cache", {}).get(key)
-        if hit is not None and hit[0] is arrays and hit[2] == arrays[0][0].data_ptr():
-            return hit[1]
         flat = [t for per in arrays for t in per]
+        ptrs = tuple(t.data_ptr() for t in flat)
+        hit = self.__dict__.setdefault("_ptr_cache", {}).get(key)
+        if hit is not None and hit[0] is arrays and hit[2] == ptrs:
+            return hit[1]
         tab = _ptr_array(flat)
-        self._ptr_cache[key] = (arrays, tab, arrays[0][0].data_ptr())
+        self._ptr_cache[key] = (arrays, tab, ptrs)
         return tab
 
     def interp(self, centering: str, arrays, Q: torch.Tensor, X: torch.Tensor, q_depth: int = 1,
@@ -535,6 +551,92 @@ def index_set_list(ctx: Context, geom: Geometry, X: torch.Tensor, ghost: int, la
                                          pa[0] if pa else None, w, _ptr(idx), _ptr(xs), cap, ctypes.byref(cnt)))
     n = cnt.value
     return idx[:n].contiguous(), xs[:n].contiguous()
+
+
+class _IntArg:
+    """An int[3] argument kept alive with its c_void_p view."""
+
+    def __init__(self, vals):
+        self.a = (ctypes.c_int * 3)(*([int(v) for v in vals] + [0] * (3 - len(vals))))
+        self.p = ctypes.cast(self.a, ctypes.c_void_p)
+
+
+def _box_arg(lo, hi, ndim):
+    if len(lo) != ndim or len(hi) != ndim:
+        raise ValueError("box: ndim lower and upper cell indices")
+    return _IntArg(lo), _IntArg(hi)
+
+
+def index_set_box_list(ctx: Context, geom: Geometry, X: torch.Tensor, ghost: int, box_lo, box_hi,
+                       lag: Optional[torch.Tensor] = None, periodic=None):
+    """LEInteractor::buildLocalIndices for any box of cells (ibtk_le_index_set_box_list,
+    LEInteractor.cpp:3070-3106): (indices int32, Xshift float64 [n, ndim], cells int32
+    [n, ndim]), the entries of the all-nodes list whose cell lies in [box_lo, box_hi],
+    in that list's order."""
+    M = X.shape[0]
+    cnt = ctypes.c_int(0)
+    pa = _periodic_arg(periodic, geom.ndim)
+    lo, hi = _box_arg(box_lo, box_hi, geom.ndim)
+    if lag is not None and (lag.dtype != torch.int32 or lag.numel() != M):
+        raise ValueError("lag: one int32 per marker")
+    cap = M * (3 ** geom.ndim) if ghost > 0 else M
+    idx = torch.empty(max(1, cap), dtype=torch.int32, device=X.device)
+    xs = torch.empty((max(1, cap), geom.ndim), dtype=torch.float64, device=X.device)
+    cells = torch.empty((max(1, cap), geom.ndim), dtype=torch.int32, device=X.device)
+    check(ctx.lib.ibtk_le_index_set_box_list(ctx.h, ctypes.byref(geom.c), _ptr(X), _ptr(lag), M, ghost,
+                                             pa[0] if pa else None, lo.p, hi.p, _ptr(idx), _ptr(xs), _ptr(cells), cap,
+                                             ctypes.byref(cnt)))
+    n = cnt.value
+    return idx[:n].contiguous(), xs[:n].contiguous(), cells[:n].contiguous()
+
+
+def list_in_box(ctx: Context, cells: torch.Tensor, indices: torch.Tensor, Xshift: Optional[torch.Tensor], box_lo,
+                box_hi):
+    """The entries of a cached list whose cell lies in [box_lo, box_hi], order kept
+    (ibtk_le_list_in_box)."""
+    n, nd = cells.shape
+    lo, hi = _box_arg(box_lo, box_hi, nd)
+    oi = torch.empty(max(1, n), dtype=torch.int32, device=cells.device)
+    ox = torch.empty((max(1, n), nd), dtype=torch.float64, device=cells.device)
+    cnt = ctypes.c_int(0)
+    check(ctx.lib.ibtk_le_list_in_box(ctx.h, nd, _ptr(cells), _ptr(indices), _ptr(Xshift), n, lo.p, hi.p, _ptr(oi),
+                                      _ptr(ox) if Xshift is not None else None, n, ctypes.byref(cnt)))
+    k = cnt.value
+    return oi[:k].contiguous(), (ox[:k].contiguous() if Xshift is not None else None)
+
+
+def level_node_distribution(ctx: Context, geoms: Sequence[Geometry], dom_lo, dom_hi, X: torch.Tensor, ghost: int,
+                            lag: Optional[torch.Tensor] = None, periodic=None):
+    """LDataManager::computeNodeDistribution over the local patches of a level
+    (ibtk_le_level_node_distribution): (order int32 device tensor, n_local, n_nonlocal);
+    order[i] = the input index of node i, local nodes first."""
+    M = X.shape[0]
+    if lag is not None and (lag.dtype != torch.int32 or lag.numel() != M):
+        raise ValueError("lag: one int32 per marker")
+    nd = geoms[0].ndim
+    lo, hi = _box_arg(dom_lo, dom_hi, nd)
+    pa = _periodic_arg(periodic, nd)
+    tab = (PatchGeom * len(geoms))(*[g.c for g in geoms])
+    order = torch.empty(max(M, 1), dtype=torch.int32, device=X.device)
+    nl, ng = ctypes.c_int(0), ctypes.c_int(0)
+    check(ctx.lib.ibtk_le_level_node_distribution(ctx.h, len(geoms), tab, lo.p, hi.p, pa[0] if pa else None,
+                                                  _ptr(X) if M else None, _ptr(lag), M, ghost,
+                                                  _ptr(order), ctypes.byref(nl), ctypes.byref(ng)))
+    return order[:nl.value + ng.value].contiguous(), nl.value, ng.value
+
+
+def ldata_reorder(ctx: Context, order: torch.Tensor, *arrays: torch.Tensor):
+    """endDataRedistribution's reorder of LData arrays (ibtk_le_ldata_reorder): for each
+    (M, ...) float64 device array, a new array whose row i is the old row order[i]."""
+    outs = []
+    for a in arrays:
+        if a.dtype != torch.float64 or not a.is_cuda or not a.is_contiguous():
+            raise ValueError("LData arrays: contiguous float64 device tensors")
+        depth = a[0].numel() if a.shape[0] else 1
+        out = torch.empty((order.numel(),) + tuple(a.shape[1:]), dtype=a.dtype, device=a.device)
+        check(ctx.lib.ibtk_le_ldata_reorder(ctx.h, _ptr(order), order.numel(), _ptr(a), depth, _ptr(out)))
+        outs.append(out)
+    return outs
 
 
 def node_distribution(ctx: Context, geom: Geometry, X: torch.Tensor, ghost: int, lag: Optional[torch.Tensor] = None):

@@ -149,13 +149,15 @@ class SlabExchange:
     def _windowed(self, work, mode):
         """work() restricted to the sweep items inside (1) / outside (2) the rank's
         own planes [z0, z1) (ibtk_le_ctx_set_plane_window); the two halves add up to
-        one unrestricted call bit for bit."""
+        one unrestricted call bit for bit.  The context's previous window (and with it
+        the item cutting of later binnings) is restored afterwards."""
         s = self.slab
+        prev = getattr(self.ctx, "plane_window", (0, 0, -1))
         self.ctx.set_plane_window(mode, s.z0, s.z1 - 1)
         try:
             work()
         finally:
-            self.ctx.set_plane_window(0, s.z0, s.z1 - 1)
+            self.ctx.set_plane_window(*prev)
 
     def cut_items(self):
         """Make the markers binned from now on on this context cut their sweep items
@@ -445,3 +447,96 @@ def migrate(slab: Slab, X: torch.Tensor, fields: Sequence[torch.Tensor] = (), gr
     Xn = outs[0].contiguous()
     fn = [o.reshape((o.shape[0],) + tuple(f.shape[1:])).to(f.dtype).contiguous() for o, f in zip(outs[1:], fields)]
     return Xn, fn
+
+
+@dataclass
+class NodeDistribution:
+    """A rank's nodes after ``redistribute`` (LDataManager's per-level state after
+    endDataRedistribution): the owned nodes in local order -- global (PETSc) index
+    ``offset + i`` for row i -- and the nonlocal (ghost) nodes in the reference's
+    nonlocal order with the global index their owner gave them."""
+    X: torch.Tensor
+    fields: List[torch.Tensor]
+    lag: torch.Tensor             # int32 Lagrangian index of each owned node
+    order: torch.Tensor           # owned row i was input row order[i]
+    offset: int                   # computeNodeOffsets: first global index of this rank
+    num_nodes: int                # computeNodeOffsets: nodes of the whole level
+    ghost_X: torch.Tensor
+    ghost_lag: torch.Tensor       # int32
+    ghost_petsc: torch.Tensor     # int64 global index of each nonlocal node
+
+
+def redistribute(slab: Slab, ctx, X: torch.Tensor, fields: Sequence[torch.Tensor], lag: torch.Tensor,
+                 group=None, numbering: Optional[Callable] = None, reorder: Optional[Callable] = None):
+    """Number a rank's markers the way LDataManager does at redistribution, across ranks.
+
+    After ``migrate``/``update_and_migrate`` every marker sits on the rank whose slab
+    (the rank's one patch of the level) holds its cell.  Then, as
+    LDataManager::computeNodeDistribution (LDataManager.cpp:2839-3027):
+
+    * local numbering -- the owned markers in the slab's cell order (x fastest),
+      Lagrangian order within a cell, repeated (cell, Lagrangian index) pairs kept
+      once (ibtk_le_level_node_distribution), and the LData arrays reordered into it
+      (ibtk_le_ldata_reorder; endDataRedistribution's VecScatter,
+      LDataManager.cpp:1823-1917, for the rows that stayed on this rank);
+    * computeNodeOffsets (LDataManager.cpp:3029-3047) -- one all-gather of the local
+      counts; node i of rank r has global index offset_r + i;
+    * nonlocal nodes -- the neighbours' markers within ``ghost`` cells of the slab
+      faces (GhostMarkers' exchange, which carries each one's Lagrangian and global
+      index, so no AO lookup is needed: AOApplicationToPetsc at :2995-3000 maps the
+      Lagrangian index to the global index its owner assigned), numbered after the
+      local nodes in the ghost-box walk order; ``ghost_X`` holds the owners'
+      positions (in [0, L)), as the reference's ghosted LData does.
+
+    ``numbering(X, lag, ghost) -> (order, n_local, n_nonlocal)`` and
+    ``reorder(order, *arrays) -> [arrays]`` are injectable so the rank logic runs on
+    CPU with gloo (tests); the product default is the HIP library."""
+    import torch.distributed as dist
+    from . import le
+    if lag.dtype != torch.int32 or lag.numel() != X.shape[0]:
+        raise ValueError("lag: one int32 Lagrangian index per marker")
+    if numbering is None:
+        geoms = [slab.geometry()]
+        dom_hi = [n - 1 for n in slab.N]
+
+        def numbering(Xa, la, ghost):
+            return le.level_node_distribution(ctx, geoms, [0, 0, 0], dom_hi, Xa, ghost, lag=la)
+    if reorder is None:
+        def reorder(order, *arrays):
+            return le.ldata_reorder(ctx, order, *arrays)
+    order, nl, nn = numbering(X, lag, 0)
+    if nn:
+        raise RuntimeError(f"rank {slab.rank}: {nn} markers outside the slab; migrate before redistribute")
+    M = X.shape[0]
+    flat = [f.reshape(M, -1).to(X.dtype).contiguous() for f in fields]
+    Xn, *fn = reorder(order, X, *flat) if nl else [X[:0]] + [f[:0] for f in flat]
+    fn = [o.reshape((o.shape[0],) + tuple(f.shape[1:])).to(f.dtype).contiguous() for o, f in zip(fn, fields)]
+    lagn = lag[order.long()]
+    # computeNodeOffsets: the local counts of every rank
+    counts = [nl]
+    if slab.P > 1:
+        host = dist.get_backend(group) == "gloo"
+        c = torch.tensor([nl], dtype=torch.int64, device="cpu" if host else X.device)
+        allc = [torch.empty_like(c) for _ in range(slab.P)]
+        dist.all_gather(allc, c, group=group)
+        counts = [int(v) for v in torch.cat(allc).cpu().tolist()]
+    offset = sum(counts[:slab.rank])
+    num_nodes = sum(counts)
+    # nonlocal nodes: the neighbours' markers near the slab faces, with their indices
+    ids = torch.stack([lagn.to(X.dtype), offset + torch.arange(nl, dtype=X.dtype, device=X.device)], dim=1)
+    Xa, Ia, n_own = GhostMarkers(slab, group).exchange(Xn, ids)
+    gX = Xa[:0]
+    gI = Ia[:0]
+    if Xa.shape[0] > n_own:
+        # the owners' positions: undo the exchange's shift across the periodic z wrap
+        # (exact: z - L_z and back), so cells and images are the owner's
+        Lz = slab.L[2]
+        z = Xa[n_own:, 2]
+        Xa[n_own:, 2] = torch.where(z < 0, z + Lz, torch.where(z >= Lz, z - Lz, z))
+        order2, nl2, nn2 = numbering(Xa, Ia[:, 0].to(torch.int32).contiguous(), slab.ghost)
+        if nl2 != nl:
+            raise RuntimeError(f"rank {slab.rank}: {nl2} local nodes with the ghost markers, {nl} without")
+        sel = order2[nl2:].long()
+        gX, gI = Xa[sel].contiguous(), Ia[sel]
+    return NodeDistribution(Xn, fn, lagn, order, offset, num_nodes, gX, gI[:, 0].to(torch.int32),
+                            gI[:, 1].to(torch.int64))

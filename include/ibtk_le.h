@@ -265,7 +265,11 @@ int ibtk_le_periodic_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom,
                                 double* Xshift_dev, int capacity, int* count);
 /* The same lists with the Lagrangian index of every marker (lag_dev[s]; NULL = s):
  * within a cell the entries follow the LNodeSet order, sorted by Lagrangian index
- * (LDataManager.cpp:1487-1493).  which = 0: every entry (d_local_petsc_indices /
+ * and uniqued (LDataManager.cpp:1487-1493: of markers sharing a cell and a Lagrangian
+ * index the lowest marker index is kept; the reference leaves which one unspecified).
+ * With lag_dev the entry count is known only after uniquing: a capacity below it
+ * writes nothing and returns IBTK_LE_ERR_ARG with *count = the required size.
+ * which = 0: every entry (d_local_petsc_indices /
  * d_periodic_shifts), 1: the cells of the patch box (d_interior_*), 2: the other
  * ghost-box cells (d_ghost_*) -- the three lists cacheLocalIndices caches.
  * SAMRAI's IndexData walks its items in insertion order; the lists take the
@@ -274,6 +278,25 @@ int ibtk_le_periodic_index_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom,
 int ibtk_le_index_set_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev, const int* lag_dev,
                            int n_markers, int ghost, const int* periodic, int which, int* indices_dev,
                            double* Xshift_dev, int capacity, int* count);
+/* LEInteractor::buildLocalIndices for a box that is neither the patch box nor the
+ * ghost box (LEInteractor.cpp:3070-3106): the entries of the which = 0 list above
+ * whose cell -- the cell of the index set's item, an image's shifted cell -- lies in
+ * [box_lo, box_hi], in the same order and with the same periodic shifts (the
+ * reference's per-cell offsets, -/+ periodic_shift * dx beyond the patch's periodic
+ * sides, are the images' shifts).  box == the patch box gives the which = 1 list,
+ * box == the ghost box the which = 0 list.  cells_dev (NULL: not written) receives
+ * NDIM ints per entry: its cell.  Count and capacity as above; synchronises. */
+int ibtk_le_index_set_box_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
+                               const int* lag_dev, int n_markers, int ghost, const int* periodic, const int* box_lo,
+                               const int* box_hi, int* indices_dev, double* Xshift_dev, int* cells_dev, int capacity,
+                               int* count);
+/* The entries of a cached list whose cell (cells_dev, NDIM ints per entry, as
+ * ibtk_le_index_set_box_list writes them) lies in [box_lo, box_hi], order kept:
+ * buildLocalIndices' box branch over a cached index set.  Xshift_dev may be NULL
+ * (then Xshift_out is not written).  Synchronises. */
+int ibtk_le_list_in_box(ibtk_le_ctx ctx, int ndim, const int* cells_dev, const int* indices_dev,
+                        const double* Xshift_dev, int n, const int* box_lo, const int* box_hi, int* indices_out,
+                        double* Xshift_out, int capacity, int* count);
 /* LDataManager::computeNodeDistribution (LDataManager.cpp:2839-3027) for one patch
  * whose marker index data has `ghost` ghost cells: order_dev[i] = the input index
  * of the marker numbered i.  The local nodes (getCellIndex cell in the patch box)
@@ -285,6 +308,33 @@ int ibtk_le_index_set_list(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, cons
 int ibtk_le_node_distribution(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, const double* X_dev,
                               const int* lag_dev, int n_markers, int ghost, int* order_dev, int* n_local,
                               int* n_nonlocal);
+
+/* LDataManager::computeNodeDistribution (LDataManager.cpp:2874-2947) over the local
+ * patches of one level, geoms[q] in PatchLevel order: equal patch boxes aligned to one
+ * tiling of the domain [dom_lo, dom_hi] (periodic in the dims periodic[d] != 0; NULL =
+ * all), cells by getCellIndex in the domain frame.  X_dev holds the rank's markers (its
+ * own and the ghost nodes it holds), lag_dev their Lagrangian indices (NULL = the
+ * marker index).  order_dev[i] = the input index of the marker that is node i:
+ *   nodes 0 .. n_local-1: the markers in a local patch's box, patch by patch, the box's
+ *     cells in box order (x fastest), a cell's set by Lagrangian index and uniqued
+ *     (LDataManager.cpp:1487-1493, lowest marker index kept);
+ *   then n_nonlocal nodes: the markers in some patch's ghost cells (periodic images
+ *     included) whose Lagrangian index no local node has, one per index, at its first
+ *     sighting -- patches in order, a patch's ghost box walked in box order, skipping
+ *     its patch box (SAMRAI's BoxList::removeIntersections order is not vendored: that
+ *     order is the box order here, parity unpinned).
+ * Markers in no patch's ghost box are not numbered.  The global PETSc index of local
+ * node i is node_offset + i, node_offset = the local counts of the lower ranks
+ * (computeNodeOffsets, LDataManager.cpp:3029-3047: an all-gather the caller runs).
+ * Synchronises. */
+int ibtk_le_level_node_distribution(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms, const int* dom_lo,
+                                    const int* dom_hi, const int* periodic, const double* X_dev, const int* lag_dev,
+                                    int n_markers, int ghost, int* order_dev, int* n_local, int* n_nonlocal);
+/* endDataRedistribution's reorder of an LData into the new numbering (the VecScatter of
+ * LDataManager.cpp:1823-1917): out[i][k] = in[order_dev[i]][k], depth doubles per
+ * node, device arrays, in and out distinct. */
+int ibtk_le_ldata_reorder(ibtk_le_ctx ctx, const int* order_dev, int n, const double* in_dev, int depth,
+                          double* out_dev);
 
 /* Markers whose cell (IndexUtilities::getCellIndex against the patch box) lies in
  * [box_lo, box_hi], no periodic shifts: the list LEInteractor's X-only overloads

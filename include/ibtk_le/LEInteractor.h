@@ -101,12 +101,17 @@ struct LDataView {
 };
 
 // LIndexSetData<T> cached lists (LIndexSetData.cpp:83-169), device arrays in
-// the reference's order (ibtk_le_index_set_list builds them).  T is the node
-// type of the reference's template (LNode or LNodeIndex); the lists are the same.
+// the reference's order (ibtk_le_index_set_list / ibtk_le_index_set_box_list
+// build them).  T is the node type of the reference's template (LNode or
+// LNodeIndex); the lists are the same.  `cells` (NDIM ints per entry of the
+// all-nodes list: the IndexData cell each node sits in) lets buildLocalIndices
+// serve boxes other than the patch box and the ghost box (LEInteractor.cpp:
+// 3070-3106); without it those boxes throw IBTK_LE_ERR_ARG.
 struct LIndexSetBase {
     Box ghost_box;                       // idx_data->getGhostBox()
     const int* local_indices = nullptr;  // all nodes in the ghost box
     const double* periodic_shifts = nullptr;
+    const int* cells = nullptr;          // the cell of each of those nodes (optional)
     int n = 0;
     const int* interior_local_indices = nullptr;  // nodes in the patch interior
     const double* interior_periodic_shifts = nullptr;

@@ -19,6 +19,10 @@ adds ctypes bindings and restates the C++ wrappers around it:
 * ``periodic_index_list`` -- ``LIndexSetData::cacheLocalIndices``
   (``LIndexSetData.cpp:83-169``) for one patch covering a periodic domain,
   with ``IndexUtilities::getCellIndex`` (``IndexUtilities-inl.h:66-89``).
+* ``lnode_set_data`` / ``build_local_indices`` -- the patch's per-cell node sets
+  and ``LEInteractor::buildLocalIndices`` over them for any box
+  (``LEInteractor.cpp:3031-3108``), offsets from the cells (an independent
+  restatement of the lists ``periodic_index_list`` builds from the images).
 """
 from __future__ import annotations
 
@@ -296,9 +300,87 @@ def periodic_index_list(X, x_lower, x_upper, dx, box_lo, box_hi, ghost, periodic
     sel = {"all": np.ones(s.size, dtype=bool), "interior": interior, "ghost": ~interior}[which]
     s, off, cell, key = s[sel], off[sel], cell[sel], key[sel]
     lagv = s if lag is None else np.asarray(lag)[s]
-    order = np.lexsort((lagv, key))
+    order = np.lexsort((s, lagv, key))
+    # each cell's LNodeSet is uniqued by Lagrangian index (LDataManager.cpp:1487-1493;
+    # of equal ones the lowest marker index is kept -- the reference's std::sort leaves
+    # it unspecified)
+    ks, ls = key[order], lagv[order]
+    keep = np.ones(order.size, dtype=bool)
+    keep[1:] = (ks[1:] != ks[:-1]) | (ls[1:] != ls[:-1])
+    order = order[keep]
     Xshift = off[order].astype(np.float64) * np.asarray(dx)[None, :]
     return s[order].astype(np.int32), Xshift, cell[order]
+
+
+def lnode_set_data(X, x_lower, x_upper, dx, box_lo, box_hi, ghost, periodic=None, lag=None):
+    """The patch's LNodeSetData over its ghost box for one patch covering a periodic
+    domain: {cell: [marker, ...]}.  A marker sits in the set of its getCellIndex cell
+    (beginDataRedistribution keeps the patch box's markers, LDataManager.cpp:1446-1482),
+    the ghost cells hold the periodic images of the patch's own cells (the index data's
+    periodic ghost fill); each set sorted by Lagrangian index and uniqued
+    (LDataManager.cpp:1487-1493, lowest marker index kept among equal ones)."""
+    import itertools
+    X = np.asarray(X, dtype=np.float64)
+    M, ndim = X.shape
+    periodic = [True] * ndim if periodic is None else periodic
+    lagv = np.arange(M) if lag is None else np.asarray(lag, dtype=np.int64)
+    N = [box_hi[d] - box_lo[d] + 1 for d in range(ndim)]
+    c = get_cell_index(X, x_lower, x_upper, dx, box_lo, box_hi)
+    sets = {}
+    for m in range(M):
+        if not all(box_lo[d] <= c[m, d] <= box_hi[d] for d in range(ndim)):
+            continue
+        for sh in itertools.product(*[(-1, 0, 1) if periodic[d] else (0,) for d in range(ndim)]):
+            ci = tuple(int(c[m, d] + sh[d] * N[d]) for d in range(ndim))
+            if all(box_lo[d] - ghost <= ci[d] <= box_hi[d] + ghost for d in range(ndim)):
+                sets.setdefault(ci, []).append(m)
+    for ci, lst in sets.items():
+        lst.sort(key=lambda m: (lagv[m], m))
+        out = []
+        for m in lst:
+            if not out or lagv[out[-1]] != lagv[m]:
+                out.append(m)
+        sets[ci] = out
+    return sets
+
+
+def build_local_indices(sets, dx, box_lo, box_hi, ghost, box, periodic=None):
+    """LEInteractor::buildLocalIndices (LEInteractor.cpp:3031-3108) over an index set
+    ``sets`` (lnode_set_data) of the patch [box_lo, box_hi] with `ghost` ghost cells, for
+    any ``box`` = (lower, upper): the set's cells are walked in IndexData order (the
+    ghost box's cells, x fastest), cells outside ``box`` skipped (:3075), and every node
+    of a cell gets offset[d] = -periodic_shift(d) where the patch touches its lower
+    periodic boundary in d and i(d) < ilower(d), +periodic_shift(d) where it touches
+    the upper one and i(d) > iupper(d), else 0 (:3077-3093); Xshift = offset * dx (:3100).
+    One patch covering the domain: it touches both periodic boundaries of every periodic
+    dim and periodic_shift(d) = its cell count.  (box == the patch box / ghost box: the
+    cached interior / all lists of cacheLocalIndices, LIndexSetData.cpp:111-166, which
+    apply the same per-cell offsets -- :3061-3069.)  Returns (indices, Xshift, cells)."""
+    import itertools
+    ndim = len(box_lo)
+    periodic = [True] * ndim if periodic is None else periodic
+    N = [box_hi[d] - box_lo[d] + 1 for d in range(ndim)]
+    blo, bhi = box
+    idx, xs, cells = [], [], []
+    ranges = [range(box_lo[d] - ghost, box_hi[d] + ghost + 1) for d in range(ndim)]
+    for ci_rev in itertools.product(*reversed(ranges)):  # x fastest
+        ci = tuple(reversed(ci_rev))
+        if ci not in sets:
+            continue
+        if not all(blo[d] <= ci[d] <= bhi[d] for d in range(ndim)):
+            continue
+        off = [0] * ndim
+        for d in range(ndim):
+            if periodic[d] and ci[d] < box_lo[d]:
+                off[d] = -N[d]
+            elif periodic[d] and ci[d] > box_hi[d]:
+                off[d] = +N[d]
+        for m in sets[ci]:
+            idx.append(m)
+            xs.append([off[d] * dx[d] for d in range(ndim)])
+            cells.append(list(ci))
+    return (np.array(idx, dtype=np.int32), np.array(xs, dtype=np.float64).reshape(-1, ndim),
+            np.array(cells, dtype=np.int64).reshape(-1, ndim))
 
 
 def node_distribution(X, x_lower, x_upper, dx, box_lo, box_hi, ghost, lag=None):
@@ -334,6 +416,73 @@ def node_distribution(X, x_lower, x_upper, dx, box_lo, box_hi, ghost, lag=None):
     order = order[keep]
     n_local = int((key[order] < si).sum())
     return order.astype(np.int32), n_local, int(order.size - n_local)
+
+
+def level_node_distribution(X, lag, patches, dom_lo, dom_hi, x_lower, dx, ghost, periodic=None):
+    """LDataManager::computeNodeDistribution (LDataManager.cpp:2874-2947) over the local
+    patches of a level, written as the reference's loops (small cases only).
+
+    patches: [(lo, hi)] cell boxes in PatchLevel order; the domain [dom_lo, dom_hi] with
+    lower corner x_lower and spacing dx (cells by getCellIndex in that frame), periodic
+    in the dims ``periodic[d]``.  Each patch's LNodeSetData holds, for every cell of its
+    ghost box, the markers whose cell is that cell or -- across a periodic side -- whose
+    image is, each set sorted by Lagrangian index and uniqued (LDataManager.cpp:
+    1487-1493; lowest marker index kept).  Local loop (:2876-2892): patches in order,
+    data_begin(patch_box) -- box cells, x fastest -- every node a new local index.
+    Nonlocal loop (:2914-2944): patches in order, the ghost box minus the patch box
+    walked in box order (SAMRAI's removeIntersections box-list order is not vendored:
+    parity unpinned for that order), a node whose Lagrangian index has no index yet gets
+    the next one.  Returns (order, n_local, n_nonlocal): order[i] = marker of node i."""
+    import itertools
+    X = np.asarray(X, dtype=np.float64)
+    M, ndim = X.shape
+    lagv = np.arange(M) if lag is None else np.asarray(lag, dtype=np.int64)
+    periodic = [True] * ndim if periodic is None else periodic
+    D = [dom_hi[d] - dom_lo[d] + 1 for d in range(ndim)]
+    x_upper = [x_lower[d] + D[d] * dx[d] for d in range(ndim)]
+    c = get_cell_index(X, x_lower, x_upper, dx, dom_lo, dom_hi)
+
+    def cells_of(lo, hi):  # box order, x fastest
+        for ci_rev in itertools.product(*[range(lo[d], hi[d] + 1) for d in reversed(range(ndim))]):
+            yield tuple(reversed(ci_rev))
+
+    def set_data(lo, hi):
+        glo = [lo[d] - ghost for d in range(ndim)]
+        ghi = [hi[d] + ghost for d in range(ndim)]
+        sets = {}
+        for m in range(M):
+            for sh in itertools.product(*[(-1, 0, 1) if periodic[d] else (0,) for d in range(ndim)]):
+                ci = tuple(int(c[m, d] + sh[d] * D[d]) for d in range(ndim))
+                if all(glo[d] <= ci[d] <= ghi[d] for d in range(ndim)):
+                    sets.setdefault(ci, []).append(m)
+        for ci, lst in sets.items():
+            lst.sort(key=lambda m: (lagv[m], m))
+            out = []
+            for m in lst:
+                if not out or lagv[out[-1]] != lagv[m]:
+                    out.append(m)
+            sets[ci] = out
+        return sets
+
+    data = [set_data(lo, hi) for lo, hi in patches]
+    order, seen = [], {}
+    for (lo, hi), sets in zip(patches, data):
+        for ci in cells_of(lo, hi):
+            for m in sets.get(ci, []):
+                seen[lagv[m]] = len(order)
+                order.append(m)
+    n_local = len(order)
+    for (lo, hi), sets in zip(patches, data):
+        glo = [lo[d] - ghost for d in range(ndim)]
+        ghi = [hi[d] + ghost for d in range(ndim)]
+        for ci in cells_of(glo, ghi):
+            if all(lo[d] <= ci[d] <= hi[d] for d in range(ndim)):
+                continue
+            for m in sets.get(ci, []):
+                if lagv[m] not in seen:
+                    seen[lagv[m]] = len(order)
+                    order.append(m)
+    return np.array(order, dtype=np.int32), n_local, len(order) - n_local
 
 
 # --------------------------------------------------------------------------

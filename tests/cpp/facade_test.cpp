@@ -7,8 +7,14 @@
 // with the oracle.  Forms (LEInteractor.h:146-993):
 //   a  LData views + index set      (interior list for interp, ghost list for spread)
 //   b  raw device arrays + index set (same lists: must equal a bit for bit)
-//   c  host std::vector, box filter  (markers whose cell is in the patch box, no shifts)
+//   c  host std::vector, box filter  (markers whose cell is in a sub-box, no shifts)
 //   d  raw device arrays with sizes, box filter (must equal c bit for bit)
+//   e  LData views + index set over a sub-box reaching into the ghost cells
+//      (buildLocalIndices' box branch, LEInteractor.cpp:3070-3106, through the
+//      index set's cells)
+// Then a patch with physical faces: the spread ghost-width check
+// (LEInteractor.cpp:2729-2745) and the spread + physical-boundary fold of
+// LDataManager::spread (LDataManager.cpp:625-659) on side data.
 // Prints "FACADE OK" after the error-convention checks.
 #include <hip/hip_runtime.h>
 
@@ -69,6 +75,7 @@ static std::vector<double> download(const double* d, size_t n) {
 }
 
 int N, g, M, n_int, n_all, depth_c;
+Box sub;  // the sub-box of forms c, d, e
 PatchView patch;
 LIndexSetView idx;
 double *Xd, *Fd;
@@ -133,24 +140,34 @@ static void run(const char* cname, V& u, V& f, int ncomp, int depth, int Qdepth)
     LEInteractor::spread(f, Sd, Qdepth, Xd, 3, idx, patch, ghost_box, pshift, "IB_4");
     LEInteractor::synchronize();
     save_f("b");
-    // c: host vectors, the markers whose cell is in the patch box
+    // c: host vectors, the markers whose cell is in the sub-box
     std::vector<double> Qh(init);
-    LEInteractor::interpolate(Qh, Qdepth, hX, 3, u, patch, patch.box, "IB_4");
+    LEInteractor::interpolate(Qh, Qdepth, hX, 3, u, patch, sub, "IB_4");
     save(std::string("Q_") + cname + "_c.bin", Qh.data(), nQ);
     zero_f();
-    LEInteractor::spread(f, hQ2, Qdepth, hX, 3, patch, patch.box, "IB_4");
+    LEInteractor::spread(f, hQ2, Qdepth, hX, 3, patch, sub, "IB_4");
     LEInteractor::synchronize();
     save_f("c");
     // d: raw arrays with sizes
     HC(hipMemcpy(Qd, init.data(), sizeof(double) * nQ, hipMemcpyHostToDevice));
-    LEInteractor::interpolate(Qd, (int)nQ, Qdepth, Xd, 3 * M, 3, u, patch, patch.box, "IB_4");
+    LEInteractor::interpolate(Qd, (int)nQ, Qdepth, Xd, 3 * M, 3, u, patch, sub, "IB_4");
     LEInteractor::synchronize();
     h = download(Qd, nQ);
     save(std::string("Q_") + cname + "_d.bin", h.data(), nQ);
     zero_f();
-    LEInteractor::spread(f, Sd, (int)nQ, Qdepth, Xd, 3 * M, 3, patch, patch.box, "IB_4");
+    LEInteractor::spread(f, Sd, (int)nQ, Qdepth, Xd, 3 * M, 3, patch, sub, "IB_4");
     LEInteractor::synchronize();
     save_f("d");
+    // e: LData + index set over the sub-box
+    HC(hipMemcpy(Qd, init.data(), sizeof(double) * nQ, hipMemcpyHostToDevice));
+    LEInteractor::interpolate(Qv, Xv, idx, u, patch, sub, pshift, "IB_4");
+    LEInteractor::synchronize();
+    h = download(Qd, nQ);
+    save(std::string("Q_") + cname + "_e.bin", h.data(), nQ);
+    zero_f();
+    LEInteractor::spread(f, Sv, Xv, idx, patch, sub, pshift, "IB_4");
+    LEInteractor::synchronize();
+    save_f("e");
     HC(hipFree(Qd));
     HC(hipFree(Sd));
 }
@@ -160,6 +177,9 @@ int main(int argc, char** argv) {
     D = argv[1];
     FILE* mf = std::fopen((D + "/meta.txt").c_str(), "r");
     EXPECT(mf && std::fscanf(mf, "%d %d %d %d %d %d", &N, &g, &M, &n_int, &n_all, &depth_c) == 6, "meta");
+    sub.ndim = 3;
+    EXPECT(std::fscanf(mf, "%d %d %d %d %d %d", &sub.lower[0], &sub.lower[1], &sub.lower[2], &sub.upper[0],
+                       &sub.upper[1], &sub.upper[2]) == 6, "meta sub-box");
     std::fclose(mf);
     patch.box.ndim = 3;
     for (int d = 0; d < 3; ++d) {
@@ -179,6 +199,7 @@ int main(int argc, char** argv) {
     idx.n_interior = n_int;
     idx.local_indices = upload(load<int>("idx_all.bin", n_all));
     idx.periodic_shifts = upload(load<double>("xs_all.bin", 3 * (size_t)n_all));
+    idx.cells = upload(load<int>("cells_all.bin", 3 * (size_t)n_all));
     idx.n = n_all;
 
     EXPECT(LEInteractor::getStencilSize("IB_4") == 4 && LEInteractor::getMinimumGhostWidth("IB_6") == 4, "stencil");
@@ -245,12 +266,73 @@ int main(int argc, char** argv) {
     EXPECT(thrown, "edge depth mismatch throws");
     thrown = false;
     try {
-        Box other = patch.box.grow(1);
-        LEInteractor::interpolate(Qv, Xv, idx, us, patch, other, pshift, "IB_4");
+        LIndexSetView nocells = idx;
+        nocells.cells = nullptr;
+        LEInteractor::interpolate(Qv, Xv, nocells, us, patch, sub, pshift, "IB_4");
     } catch (const LEInteractorError& e) {
         thrown = e.code == IBTK_LE_ERR_ARG;
     }
-    EXPECT(thrown, "index-set box other than the patch / ghost box throws");
+    EXPECT(thrown, "a sub-box without the index set's cells throws");
+
+    // a patch with physical faces in x and z, periodic in y (LEInteractor.cpp:2729-2745:
+    // spreading near a physical boundary needs the ghost width; the fold follows, as
+    // LDataManager::spread calls accumulateFromPhysicalBoundaryData), with its own
+    // index set (no images across the physical faces)
+    PatchView phys = patch;
+    phys.touches_physical_bdry[0][0] = phys.touches_physical_bdry[0][1] = true;
+    phys.touches_physical_bdry[2][0] = phys.touches_physical_bdry[2][1] = true;
+    int n_phys = 0;
+    {
+        FILE* pf = std::fopen((D + "/meta_phys.txt").c_str(), "r");
+        EXPECT(pf && std::fscanf(pf, "%d", &n_phys) == 1, "meta_phys");
+        std::fclose(pf);
+    }
+    LIndexSetView idxp;
+    idxp.ghost_box = patch.box.grow(g);
+    idxp.local_indices = upload(load<int>("idx_phys.bin", n_phys));
+    idxp.periodic_shifts = upload(load<double>("xs_phys.bin", 3 * (size_t)n_phys));
+    idxp.n = n_phys;
+    SideDataView fs1 = fs;
+    for (int d = 0; d < 3; ++d) fs1.ghost[d] = 1;  // below IB_4's 3
+    thrown = false;
+    try {
+        LEInteractor::spread(fs1, Qv, Xv, idxp, phys, idxp.ghost_box, pshift, "IB_4");
+    } catch (const LEInteractorError& e) {
+        thrown = e.code == IBTK_LE_ERR_GHOST_WIDTH;
+    }
+    EXPECT(thrown, "spread next to a physical boundary with too few ghosts throws");
+    {
+        std::vector<double> hS(3 * (size_t)M);
+        for (size_t i = 0; i < hS.size(); ++i) hS[i] = hF[i];
+        double* Sd = upload(hS);
+        LDataView Sv{Sd, 3, M};
+        for (int a = 0; a < 3; ++a) HC(hipMemset(fs.ptr[a], 0, sizeof(double) * asize("side", a, 1)));
+        LEInteractor::spread(fs, Sv, Xv, idxp, phys, idxp.ghost_box, pshift, "IB_4");  // enough ghosts: no throw
+        ibtk_le_patch_geom pg{};
+        pg.ndim = 3;
+        for (int d = 0; d < 3; ++d) {
+            pg.ilower[d] = 0;
+            pg.iupper[d] = N - 1;
+            pg.gcw[d] = g;
+            pg.dx[d] = 1.0 / N;
+            pg.x_lower[d] = 0.0;
+            pg.x_upper[d] = 1.0;
+        }
+        const int physf[6] = {1, 1, 0, 0, 1, 1};
+        std::vector<double> ac = load<double>("bc_a.bin", 18), bc = load<double>("bc_b.bin", 18),
+                            gc = load<double>("bc_g.bin", 18);
+        ibtk_le_ctx c2 = nullptr;
+        EXPECT(ibtk_le_ctx_create(0, nullptr, &c2) == IBTK_LE_OK, "ctx");
+        double* arr[3] = {fs.ptr[0], fs.ptr[1], fs.ptr[2]};
+        EXPECT(ibtk_le_phys_bdry_side(c2, &pg, arr, physf, ac.data(), bc.data(), gc.data(), 1) == IBTK_LE_OK, "fold");
+        EXPECT(ibtk_le_ctx_synchronize(c2) == IBTK_LE_OK, "fold sync");
+        ibtk_le_ctx_destroy(c2);
+        for (int a = 0; a < 3; ++a) {
+            auto hf = download(fs.ptr[a], asize("side", a, 1));
+            save("f_phys_" + std::to_string(a) + ".bin", hf.data(), hf.size());
+        }
+        HC(hipFree(Sd));
+    }
     std::printf("FACADE OK\n");
     return 0;
 }

@@ -103,10 +103,14 @@ def test_cpp_facade(tmp_path):
     """Every overload form of the C++ facade (include/ibtk_le/LEInteractor.h: LData +
     index set, raw arrays + index set, std::vector and raw arrays with sizes, each on
     Cell / Node / Side / Edge data) against the oracle on one periodic 16^3 patch:
-    interp of the index set's interior list and of the box-filtered markers within
-    1e-13 (the two index-set forms and the two box forms bit for bit alike), spread
-    of the ghost-box list (with periodic images) and of the box-filtered markers
-    within 1e-12 (LEInteractor.cpp:690-2397)."""
+    interp of the index set's interior list, of its sub-box list (buildLocalIndices'
+    box branch, LEInteractor.cpp:3070-3106, cells reaching into the ghost region) and
+    of the markers whose cell is in a sub-box (some outside it) within 1e-13 (the two
+    index-set forms and the two box forms bit for bit alike); spread of the ghost-box
+    list (with periodic images), of the sub-box list and of the sub-box markers within
+    1e-12 (LEInteractor.cpp:690-2397).  Then a patch with physical faces in x and z:
+    too few ghosts throw (LEInteractor.cpp:2729-2745); with enough, spread + the
+    adjoint physical fold (LDataManager.cpp:655-659) within 1e-12 of the oracle."""
     from oracle import oracle as ora
     from test_gpu_parity import oracle_call
 
@@ -119,18 +123,34 @@ def test_cpp_facade(tmp_path):
     F = rng.uniform(-1, 1, (M, 3))
     ii, xi, _ = ora.periodic_index_list(X, geom.x_lower, geom.x_upper, geom.dx, geom.ilower, geom.iupper, g,
                                         which="interior")
-    ia, xa, _ = ora.periodic_index_list(X, geom.x_lower, geom.x_upper, geom.dx, geom.ilower, geom.iupper, g,
-                                        which="all")
-    # the box forms: the markers whose cell is in the patch box, no shifts
-    ib = np.arange(M, dtype=np.int32)
-    xb = np.zeros((M, 3))
+    ia, xa, ca = ora.periodic_index_list(X, geom.x_lower, geom.x_upper, geom.dx, geom.ilower, geom.iupper, g,
+                                         which="all")
+    sub = ([-2, 3, 1], [9, 17, 12])  # reaches below x and above y into the ghost cells
+    sets = ora.lnode_set_data(X, geom.x_lower, geom.x_upper, geom.dx, geom.ilower, geom.iupper, g)
+    ie, xe, _ = ora.build_local_indices(sets, geom.dx, geom.ilower, geom.iupper, g, sub)
+    # the box forms: the markers whose cell is in the sub-box, no shifts (LEInteractor.cpp:3110-3139)
+    cm = ora.get_cell_index(X, geom.x_lower, geom.x_upper, geom.dx, geom.ilower, geom.iupper)
+    inb = np.all((cm >= np.array(sub[0])) & (cm <= np.array(sub[1])), axis=1)
+    assert 0 < inb.sum() < M
+    ib = np.nonzero(inb)[0].astype(np.int32)
+    xb = np.zeros((ib.size, 3))
+    # the physical-face patch: no images across x and z
+    ip, xp, _ = ora.periodic_index_list(X, geom.x_lower, geom.x_upper, geom.dx, geom.ilower, geom.iupper, g,
+                                        periodic=[False, True, False], which="all")
     u = {"cell": [rng.uniform(-1, 1, geom.array_shape("cell", 0, depth_c))],
          "node": [rng.uniform(-1, 1, geom.array_shape("node", 0, 1))],
          "side": [rng.uniform(-1, 1, geom.array_shape("side", a)) for a in range(3)],
          "edge": [rng.uniform(-1, 1, geom.array_shape("edge", a)) for a in range(3)]}
-    (tmp_path / "meta.txt").write_text(f"{N} {g} {M} {ii.size} {ia.size} {depth_c}\n")
+    (tmp_path / "meta.txt").write_text(f"{N} {g} {M} {ii.size} {ia.size} {depth_c}\n"
+                                       f"{' '.join(map(str, sub[0]))} {' '.join(map(str, sub[1]))}\n")
+    (tmp_path / "meta_phys.txt").write_text(f"{ip.size}\n")
+    A = rng.uniform(0.2, 1.0, (3, 6))
+    B = rng.uniform(0.2, 1.0, (3, 6))
+    G = rng.uniform(-1, 1, (3, 6))
     for name, arr in [("X", X), ("F", F), ("idx_int", ii.astype(np.int32)), ("xs_int", xi),
-                      ("idx_all", ia.astype(np.int32)), ("xs_all", xa), ("u_cell", u["cell"][0]),
+                      ("idx_all", ia.astype(np.int32)), ("xs_all", xa), ("cells_all", ca.astype(np.int32)),
+                      ("idx_phys", ip.astype(np.int32)), ("xs_phys", xp), ("bc_a", A), ("bc_b", B), ("bc_g", G),
+                      ("u_cell", u["cell"][0]),
                       ("u_node", u["node"][0])] + [(f"u_side{a}", u["side"][a]) for a in range(3)] + \
             [(f"u_edge{a}", u["edge"][a]) for a in range(3)]:
         np.ascontiguousarray(arr).tofile(tmp_path / f"{name}.bin")
@@ -140,21 +160,29 @@ def test_cpp_facade(tmp_path):
         depth = depth_c if cent == "cell" else 1
         Qd = 3 if cent in ("side", "edge") else depth
         nc = len(u[cent])
-        Q = {f: np.fromfile(tmp_path / f"Q_{cent}_{f}.bin").reshape(M, Qd) for f in "abcd"}
+        Q = {f: np.fromfile(tmp_path / f"Q_{cent}_{f}.bin").reshape(M, Qd) for f in "abcde"}
         fs = {f: [np.fromfile(tmp_path / f"f_{cent}_{f}_{a}.bin").reshape(u[cent][a].shape) for a in range(nc)]
-              for f in "abcd"}
+              for f in "abcde"}
         assert np.array_equal(Q["a"], Q["b"]) and np.array_equal(Q["c"], Q["d"]), cent
         for a in range(nc):
             assert np.array_equal(fs["a"][a], fs["b"][a]) and np.array_equal(fs["c"][a], fs["d"][a]), cent
         Sv = F[:, [k % 3 for k in range(Qd)]].copy()
-        for form, (idx, xs) in (("a", (ii, xi)), ("c", (ib, xb))):
+        for form, (idx, xs) in (("a", (ii, xi)), ("c", (ib, xb)), ("e", (ie, xe))):
             Qo = np.full((M, Qd), -7.0)
             oracle_call(ora, "interp", "IB_4", cent, geom, [x.copy() for x in u[cent]], idx, xs, X, Qo, depth)
             scale = max(np.abs(Qo).max(), 1e-300)
             assert np.abs(Q[form] - Qo).max() <= 1e-13 * scale, f"{cent} {form} interp"
-        for form, (idx, xs) in (("a", (ia, xa)), ("c", (ib, xb))):
+        for form, (idx, xs) in (("a", (ia, xa)), ("c", (ib, xb)), ("e", (ie, xe))):
             fo = [np.zeros_like(x) for x in u[cent]]
             oracle_call(ora, "spread", "IB_4", cent, geom, fo, idx, xs, X, Sv.copy(), depth)
             for a in range(nc):
                 scale = max(np.abs(fo[a]).max(), 1e-300)
                 assert np.abs(fs[form][a] - fo[a]).max() <= 1e-12 * scale, f"{cent} {form} spread comp {a}"
+    # the physical-face patch: spread of its list, then the adjoint fold of x and z
+    fo = [np.zeros(geom.array_shape("side", a)) for a in range(3)]
+    oracle_call(ora, "spread", "IB_4", "side", geom, fo, ip, xp, X, F.copy(), 1)
+    ora.phys_bdry_side(geom.ilower, geom.iupper, g, geom.dx, fo, [1, 1, 0, 0, 1, 1], A, B, G, adjoint=True)
+    for a in range(3):
+        fg = np.fromfile(tmp_path / f"f_phys_{a}.bin").reshape(fo[a].shape)
+        scale = max(np.abs(fo[a]).max(), 1e-300)
+        assert np.abs(fg - fo[a]).max() <= 1e-12 * scale, f"physical faces: spread + fold, comp {a}"

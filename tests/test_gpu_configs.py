@@ -455,19 +455,32 @@ def _mig_worker(rank, world, port, out_q):
         cz = torch.clamp((Xb[:, 2] / slab.dx[2]).floor().long(), 0, N - 1)
         owned = bool(((cz >= slab.z0) & (cz < slab.z1)).all())
         inbox = bool(((Xb >= 0) & (Xb < 1)).all())
-        out_q.put((rank, "ok", ok, same_repeat, owned, inbox, int(Xb.shape[0])))
+        # redistribution after the move (slab.redistribute, HIP numbering + reorder): an
+        # eighth of the markers, so the oracle's loops stay short
+        from ibamr_amd.slab import redistribute
+        sel = (fb[1] % 8 == 0).nonzero().squeeze(1)
+        Xs, Fs, ls = Xb[sel].contiguous(), fb[0][sel].contiguous(), fb[1][sel].to(torch.int32).contiguous()
+        d = redistribute(slab, ctx, Xs, [Fs], ls)
+        o = d.order.long()
+        ok = ok and torch.equal(d.X, Xs[o]) and torch.equal(d.fields[0], Fs[o]) and torch.equal(d.lag, ls[o])
+        dd = dict(lag=d.lag.cpu().numpy(), offset=d.offset, num_nodes=d.num_nodes,
+                  ghost_lag=d.ghost_lag.cpu().numpy(), ghost_petsc=d.ghost_petsc.cpu().numpy())
+        out_q.put((rank, "ok", ok, same_repeat, owned, inbox, int(Xb.shape[0]), dd, Xs.cpu().numpy(),
+                   ls.cpu().numpy()))
         dist.barrier()
         dist.destroy_process_group()
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
-        out_q.put((rank, traceback.format_exc(), False, False, False, False, 0))
+        out_q.put((rank, traceback.format_exc(), False, False, False, False, 0, None, None, None))
 
 
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_device_update_and_migrate(le, world):
     """slab.update_and_migrate (ibtk_le_slab_update_partition + neighbour exchange) moves
     the same markers with the same bits as the position update plus migrate(), leaves
-    every marker on the owner of its wrapped cell, and is deterministic."""
+    every marker on the owner of its wrapped cell, and is deterministic; then
+    slab.redistribute numbers the level across the ranks as the oracle's
+    computeNodeDistribution + computeNodeOffsets do, entry by entry."""
     import torch.multiprocessing as mp
     mpc = mp.get_context("spawn")
     q = mpc.Queue()
@@ -480,7 +493,8 @@ def test_device_update_and_migrate(le, world):
         try:
             res.append(q.get(timeout=240))
         except Exception:
-            res.append((-1, "worker died: " + str([p.exitcode for p in procs]), False, False, False, False, 0))
+            res.append((-1, "worker died: " + str([p.exitcode for p in procs]), False, False, False, False, 0,
+                        None, None, None))
             break
     for p in procs:
         p.join(timeout=60)
@@ -488,6 +502,12 @@ def test_device_update_and_migrate(le, world):
             p.kill()
     bad = [r for r in res if r[1] != "ok"]
     assert not bad, bad[0][1]
-    for rank, _, ok, rep, owned, inbox, n in res:
+    for rank, _, ok, rep, owned, inbox, n, *_ in res:
         assert ok and rep and owned and inbox, (rank, ok, rep, owned, inbox)
     assert sum(r[6] for r in res) == 20000 * world
+    # the level numbering across ranks after the move, entry by entry against the oracle
+    from ldist_check import check_node_distribution
+    res.sort(key=lambda r: r[0])
+    n_ghost = check_node_distribution([r[7] for r in res], np.concatenate([r[8] for r in res]),
+                                      np.concatenate([r[9] for r in res]), [48, 48, 48], world, 3)
+    assert n_ghost > 0

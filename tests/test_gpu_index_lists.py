@@ -67,6 +67,55 @@ def test_index_set_list_matches_oracle(le, ctx, ndim, which, with_lag):
     assert np.array_equal(xs.cpu().numpy(), ex)
 
 
+@pytest.mark.parametrize("ndim", [2, 3])
+def test_index_set_list_uniques_repeated_lagrangian_indices(le, ctx, ndim):
+    """Markers sharing a cell and a Lagrangian index are one LNode of the cell's set
+    (LDataManager.cpp:1487-1493): the device list drops the later ones as the oracle
+    does (lowest marker index kept), in every cell incl. the images'."""
+    geom, X, lag = _case(le, ndim, 3000, 21 + ndim, dup_lag=True)
+    X[1500:1505] = X[:5]  # the repeated Lagrangian indices on the same positions: same cells
+    g = 3
+    Xd = torch.from_numpy(X).cuda()
+    idx, xs = le.index_set_list(ctx, geom, Xd, g, lag=torch.from_numpy(lag).cuda(), which="all")
+    ei, ex, _ = ora.periodic_index_list(X, geom.x_lower, geom.x_upper, geom.dx, geom.ilower, geom.iupper, g,
+                                        lag=lag, which="all")
+    full, _, _ = ora.periodic_index_list(X, geom.x_lower, geom.x_upper, geom.dx, geom.ilower, geom.iupper, g,
+                                         which="all")
+    assert ei.size < full.size  # the duplicates were there to drop
+    assert np.array_equal(idx.cpu().numpy(), ei) and np.array_equal(xs.cpu().numpy(), ex)
+
+
+BOXES3 = [((-3, -3, -3), (26, 22, 18)),   # the ghost box: the all list
+          ((0, 0, 0), (23, 19, 15)),      # the patch box: the interior list
+          ((-2, 4, -3), (5, 19, 2)),      # reaches below the patch in x and z
+          ((20, -3, 10), (26, 3, 18)),    # above in x and z, below in y
+          ((7, 7, 7), (7, 7, 7))]         # one cell
+
+
+@pytest.mark.parametrize("with_lag", [False, True])
+@pytest.mark.parametrize("box", BOXES3, ids=lambda b: f"{b[0]}-{b[1]}")
+def test_index_set_box_list_matches_build_local_indices(le, ctx, box, with_lag):
+    """LEInteractor::buildLocalIndices' box branch (LEInteractor.cpp:3070-3106) on the
+    device (ibtk_le_index_set_box_list, and ibtk_le_list_in_box over the cached
+    all-nodes list with its cells) against the oracle's cell-walk restatement, entry by
+    entry: indices, periodic shifts and cells."""
+    geom, X, lag = _case(le, 3, 4000, 31, dup_lag=with_lag)
+    g = 3
+    Xd = torch.from_numpy(X).cuda()
+    lg = torch.from_numpy(lag).cuda() if with_lag else None
+    idx, xs, cells = le.index_set_box_list(ctx, geom, Xd, g, box[0], box[1], lag=lg)
+    sets = ora.lnode_set_data(X, geom.x_lower, geom.x_upper, geom.dx, geom.ilower, geom.iupper, g,
+                              lag=lag if with_lag else None)
+    ei, ex, ec = ora.build_local_indices(sets, geom.dx, geom.ilower, geom.iupper, g, box)
+    assert np.array_equal(idx.cpu().numpy(), ei)
+    assert np.array_equal(xs.cpu().numpy(), ex)
+    assert np.array_equal(cells.cpu().numpy(), ec)
+    # the facade's path: the all-nodes list with its cells, filtered by the box
+    ai, ax, ac = le.index_set_box_list(ctx, geom, Xd, g, BOXES3[0][0], BOXES3[0][1], lag=lg)
+    fi, fx = le.list_in_box(ctx, ac, ai, ax, box[0], box[1])
+    assert np.array_equal(fi.cpu().numpy(), ei) and np.array_equal(fx.cpu().numpy(), ex)
+
+
 def test_periodic_index_list_is_the_all_list(le, ctx):
     geom, X, lag = _case(le, 3, 2000, 11)
     Xd = torch.from_numpy(X).cuda()

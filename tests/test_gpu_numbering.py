@@ -60,3 +60,60 @@ def test_local_numbering_matches_stable_cell_sort(le, ctx, ndim, M):
     exp, exp_in = _expected(X, geom)
     assert nin == exp_in
     assert np.array_equal(order.cpu().numpy(), exp)
+
+
+def _level(le, P, n, g, order_perm=None, subset=None, dx=None, z_extra=(0, 0)):
+    """Patches of n^3 tiling a periodic P^3 domain (optionally a subset, in a given
+    PatchLevel order); returns (geoms, boxes, dom_lo, dom_hi, dx)."""
+    N = P * n
+    dx = dx or 1.0 / N
+    tiles = [(i, j, k) for k in range(P) for j in range(P) for i in range(P)]
+    if subset is not None:
+        tiles = [t for t in tiles if subset(t)]
+    if order_perm is not None:
+        tiles = [tiles[i] for i in order_perm(len(tiles))]
+    geoms, boxes = [], []
+    for t in tiles:
+        lo = [t[d] * n for d in range(3)]
+        hi = [lo[d] + n - 1 for d in range(3)]
+        geoms.append(le.Geometry(lo, hi, g, [dx] * 3, [lo[d] * dx for d in range(3)]))
+        boxes.append((lo, hi))
+    return geoms, boxes, [0, 0, 0], [N - 1] * 3, dx
+
+
+@pytest.mark.parametrize("case", ["all_local", "half_level", "slab_with_ghosts"])
+def test_level_node_distribution_matches_oracle(le, ctx, case):
+    """LDataManager::computeNodeDistribution over a level's local patches (ibtk_le_level_
+    node_distribution) entry by entry against the oracle's loop restatement
+    (LDataManager.cpp:2874-2947): a clustered level of 4^3 patches of 6^3 cells in a
+    shuffled PatchLevel order, with repeated Lagrangian indices; half the level local
+    (the others' markers near the boundary are nonlocal ghost nodes, periodic images
+    included); a z-slab rank holding its own markers plus the neighbours' ghost markers."""
+    P, n, g = 4, 6, 2
+    rng = np.random.default_rng(7)
+    perm = lambda k: list(rng.permutation(k))
+    if case == "all_local":
+        geoms, boxes, dlo, dhi, dx = _level(le, P, n, g, order_perm=perm)
+    elif case == "half_level":
+        geoms, boxes, dlo, dhi, dx = _level(le, P, n, g, order_perm=perm, subset=lambda t: (t[0] + t[2]) % 2 == 0)
+    else:
+        geoms, boxes, dlo, dhi, dx = _level(le, P, n, g, subset=lambda t: t[2] == 1)
+    M = 3000
+    X = rng.uniform(0, 1, (M, 3))
+    X[:1000, 2] = 0.40 + (X[:1000, 2] - 0.5) / (P * n)           # a sheet one cell thick
+    X[1000:1500, :2] = 0.3 + 0.02 * rng.standard_normal((500, 2))  # a bundle along z
+    X = np.mod(X, 1.0)
+    lag = rng.permutation(M).astype(np.int32)
+    lag[2000:2030] = lag[:30]                                      # repeated Lagrangian indices
+    X[2000:2030] = X[:30]
+    Xd = torch.from_numpy(X).cuda()
+    order, nl, nn = le.level_node_distribution(ctx, geoms, dlo, dhi, Xd, g, lag=torch.from_numpy(lag).cuda())
+    eo, enl, enn = ora.level_node_distribution(X, lag, boxes, dlo, dhi, [0.0] * 3, [dx] * 3, g)
+    assert (nl, nn) == (enl, enn)
+    if case != "all_local":
+        assert nn > 0
+    assert np.array_equal(order.cpu().numpy(), eo)
+    # the LData reorder: row i of the new arrays is the old row order[i]
+    F = torch.from_numpy(rng.standard_normal((M, 3))).cuda()
+    Xn, Fn = le.ldata_reorder(ctx, order, Xd, F)
+    assert torch.equal(Xn, Xd[order.long()]) and torch.equal(Fn, F[order.long()])

@@ -297,3 +297,69 @@ def test_ghost_marker_exchange_gloo(world):
             got.add((i, shift))
         assert got == want, (rank, len(got), len(want))
         assert len(ids) - n_own == len(want)
+
+
+# ---------------------------------------------------------------------------- redistribution
+def _redist_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from oracle import oracle as ora
+        from ibamr_amd.slab import Slab, migrate, redistribute
+        N = [12, 10, 32]
+        slab = Slab(N, world, rank, 2)
+        g = torch.Generator().manual_seed(300 + rank)
+        M = 400 + 23 * rank
+        X = torch.rand((M, 3), dtype=torch.float64, generator=g)
+        X[: M // 4, 2] = (torch.rand(M // 4, dtype=torch.float64, generator=g) * 0.1 - 0.05) % 1.0  # near z = 0
+        lag = (torch.randperm(M, generator=g) * world + rank).to(torch.int32)
+        F = torch.rand((M, 3), dtype=torch.float64, generator=g)
+        Xm, (Fm, lm) = migrate(slab, X, [F, lag.to(torch.float64)], cell_order=False)
+        lm = lm.to(torch.int32)
+        boxes = [([0, 0, slab.z0], [N[0] - 1, N[1] - 1, slab.z1 - 1])]
+        dx = [1.0 / n for n in N]
+
+        def numbering(Xa, la, ghost):  # the oracle stands in for the HIP numbering on CPU
+            o, nl, nn = ora.level_node_distribution(Xa.numpy(), la.numpy(), boxes, [0, 0, 0],
+                                                    [n - 1 for n in N], [0.0] * 3, dx, ghost)
+            return torch.from_numpy(o), nl, nn
+
+        def reorder(order, *arrays):
+            return [a[order.long()] for a in arrays]
+
+        d = redistribute(slab, None, Xm, [Fm], lm, numbering=numbering, reorder=reorder)
+        ok = torch.equal(d.X, Xm[d.order.long()]) and torch.equal(d.fields[0], Fm[d.order.long()])
+        ok = ok and torch.equal(d.lag, lm[d.order.long()])
+        q.put((rank, "ok", ok, dict(lag=d.lag.numpy(), offset=d.offset, num_nodes=d.num_nodes,
+                                    ghost_lag=d.ghost_lag.numpy(), ghost_petsc=d.ghost_petsc.numpy()),
+               Xm.numpy(), lm.numpy()))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc(), False, None, None, None))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_redistribute_numbering_gloo(world):
+    """slab.redistribute after migration: local numbering, computeNodeOffsets and the
+    nonlocal nodes with their owners' global indices, against the oracle's
+    LDataManager::computeNodeDistribution over the whole level (tests/ldist_check.py)."""
+    from ldist_check import check_node_distribution
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_redist_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    bad = [r for r in res if r[1] != "ok"]
+    assert not bad, bad[0][1]
+    res.sort(key=lambda r: r[0])
+    assert all(r[2] for r in res)
+    X_all = np.concatenate([r[4] for r in res])
+    lag_all = np.concatenate([r[5] for r in res])
+    n_ghost = check_node_distribution([r[3] for r in res], X_all, lag_all, [12, 10, 32], world, 2)
+    assert n_ghost > 0
