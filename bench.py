@@ -96,7 +96,8 @@ def make_markers(kind, M, slab, seed, device):
 
 def cpu_baseline(cfg, kernel, seconds_target=15.0):
     """The oracle (the C restatement) timed on a bounded, same-density sample, on 1 thread and
-    on up to 16 host threads (one replica each).
+    on every host thread this process may use, capped by OMP_NUM_THREADS (one replica each;
+    the record states the host's nproc, the affinity set and the cap).
 
     Sample: a periodic N_s^3 grid with the workload's marker density (cell-sorted
     order, as on the GPU), IB_4 side-centred interp + spread (periodic images in the
@@ -151,7 +152,9 @@ def cpu_baseline(cfg, kernel, seconds_target=15.0):
         ncpu = len(os.sched_getaffinity(0))
     except AttributeError:
         ncpu = os.cpu_count() or 1
-    T = max(1, min(ncpu, int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
+    # every core this process may use, up to OMP_NUM_THREADS: the GPU pool sets 16, one GPU's
+    # share of its host (os.cpu_count() there counts the whole machine, shared by 8 GPUs)
+    T = max(1, min(ncpu, int(os.environ.get("OMP_NUM_THREADS", str(ncpu)))))
     reps_t = [0] * T
     t_multi = 0.6 * seconds_target
     start = threading.Barrier(T + 1)
@@ -176,6 +179,8 @@ def cpu_baseline(cfg, kernel, seconds_target=15.0):
     wall = time.perf_counter() - t0
     rateT = 2.0 * Ms * sum(reps_t) / wall
     return {"value": rateT, "unit": "marker-ops/s", "cores": T, "kind": "port", "value_1thread": rate1,
+            "host_nproc": os.cpu_count(), "affinity_cpus": ncpu,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
             "sample": f"{Ns}^3 periodic grid, {Ms} uniform markers (same density as the workload), "
                       f"{kernel} side interp+spread, cell-sorted (oracle C); {T} threads, one replica of the "
                       f"sample each: {sum(reps_t)} passes in {wall:.1f} s; 1 thread: {reps} passes in "
@@ -222,11 +227,33 @@ def level_lists(X, N, P, g):
     return (interior, None, off_i), (es[o2].to(torch.int32).contiguous(), ex[o2].contiguous(), off_s)
 
 
+# ds_add_f64 cost, conflict-free (tools/ubench_lds2.hip): 10 cycles
+# per wave-instruction per CU at 2.4 GHz (MI355X_MICROARCH.md), 256 CUs
+LDS_ADD_CYCLES, CLOCK_GHZ, NCU = 10.0, 2.4, 256
+
+
+def lds_atomic(ctx, spread_call, k_ms):
+    """The spread sweep's LDS-atomic bound: its ds_add_f64 counted on one extra call
+    (ibtk_le_ctx_count_adds), priced at the measured conflict-free rate."""
+    ctx.count_adds(True)
+    spread_call()
+    ctx.synchronize()
+    ctx.count_adds(False)
+    ins, lanes = ctx.last_adds()
+    floor_ms = ins * LDS_ADD_CYCLES / (NCU * CLOCK_GHZ * 1e9) * 1e3
+    return {"bound": "lds_atomic", "ds_add_wave_instr": ins, "lane_adds": lanes,
+            "lane_fill": lanes / max(64 * ins, 1), "cycles_per_instr": LDS_ADD_CYCLES, "cus": NCU,
+            "clock_ghz": CLOCK_GHZ, "floor_ms": floor_ms, "kernel_ms": k_ms, "frac": floor_ms / k_ms if k_ms else None,
+            "note": "floor = wave-instructions x 10 cycles / (256 CUs x 2.4 GHz): the adds alone at the "
+                    "conflict-free ds_add_f64 rate of tools/ubench_lds2.hip"}
+
+
 def run_level(args, cfg, kernel, dev):
     """--config cfg5 (default): the clustered markers on a multi-patch finest level,
     8^3 patches of 64^3, one launch per sweep over every patch.
-    One step = level ghost fill of u, bin of the interior lists, interp, bin of the
-    ghost-box lists, spread (the patches' interiors are complete: no reduction)."""
+    One step = level ghost fill of u, one bin of the ghost-box lists (the interior
+    lists select their entries for interp), interp, zero f, spread (the patches'
+    interiors are complete: no reduction)."""
     import torch
     from ibamr_amd import le
     N, P = cfg["N"], cfg.get("patches", 8)
@@ -251,8 +278,10 @@ def run_level(args, cfg, kernel, dev):
     F = torch.rand((M, 3), dtype=torch.float64, device=dev, generator=gen).mul_(2).sub_(1)
     U = torch.zeros((M, 3), dtype=torch.float64, device=dev)
     (ii, _, oi), (si, sx, os_) = level_lists(X, N, P, g)
-    lvl_i = le.Level.from_flat(ctx, geoms, kernel, X, ii, None, oi)
+    # one binning serves both sweeps: the ghost-box lists (spread), told which of their
+    # entries the interior lists (interp) name (ibtk_le_level_select_interior)
     lvl_s = le.Level.from_flat(ctx, geoms, kernel, X, si, sx, os_)
+    lists = {"ii": ii, "oi": oi}
     u = [[a.uniform_(-1.0, 1.0, generator=gen) for a in geom.alloc("side", device=dev)] for geom in geoms]
     f = [geom.alloc("side", device=dev) for geom in geoms]
     # algorithmic bytes: the distinct points each patch's ghost-box stencils touch
@@ -278,14 +307,14 @@ def run_level(args, cfg, kernel, dev):
             return step_move(record)
         if record:
             E[0].record()
-        lvl_i.fill_ghosts("side", u)
+        lvl_s.fill_ghosts("side", u)
         if record:
             E[1].record()
-        lvl_i.bin(X)
         lvl_s.bin(X)
+        lvl_s.select_interior(M, lists["ii"], lists["oi"])
         if record:
             E[2].record()
-        lvl_i.interp("side", u, U, X)
+        lvl_s.interp("side", u, U, X)
         if record:
             E[3].record()
         lvl_s.zero("side", f)
@@ -301,18 +330,19 @@ def run_level(args, cfg, kernel, dev):
         # (LIndexSetData's lists after redistribution), re-bin, spread
         if record:
             E[0].record()
-        lvl_i.fill_ghosts("side", u)
+        lvl_s.fill_ghosts("side", u)
         if record:
             E[1].record()
-        lvl_i.interp("side", u, U, X)
+        lvl_s.interp("side", u, U, X)
         if record:
             E[2].record()
         le.position_update(ctx, "euler", dt_move, X, U, out=X)
         X.remainder_(1.0)
         X.masked_fill_(X >= 1.0, 0.0)  # remainder can round up to L
         (ii2, _, oi2), (si2, sx2, os2) = level_lists(X, N, P, g)
-        lvl_i.relist(ii2, None, oi2).bin(X)
+        lists.update(ii=ii2, oi=oi2)
         lvl_s.relist(si2, sx2, os2).bin(X)
+        lvl_s.select_interior(M, ii2, oi2)
         if record:
             E[3].record()
         lvl_s.zero("side", f)
@@ -346,7 +376,7 @@ def run_level(args, cfg, kernel, dev):
     ctx.enable_timing(True)
     kt = {"interp": [], "spread": []}
     for _ in range(3):
-        lvl_i.interp("side", u, U, X)
+        lvl_s.interp("side", u, U, X)
         ctx.synchronize()
         kt["interp"].append(ctx.last_kernel_ms())
         lvl_s.spread("side", f, F, X)
@@ -355,6 +385,7 @@ def run_level(args, cfg, kernel, dev):
     ctx.enable_timing(False)
     mean = lambda v: sum(v) / len(v)
     k_i, k_s = mean(kt["interp"]), mean(kt["spread"])
+    lds = lds_atomic(ctx, lambda: lvl_s.spread("side", f, F, X), k_s)
     # per entry X and Q/F (24 + 24 B), per touched point 8 B (interp) or 16 B (spread);
     # the touched points are those of the ghost-box lists (an upper bound for interp's)
     B_i = M * 48 + 8 * sum(S_touched)
@@ -369,14 +400,15 @@ def run_level(args, cfg, kernel, dev):
                    "parallelism": "one GPU", "patches": [P, P, P], "patch_cells": [n, n, n], "ghost": g,
                    "move": args.move,
                    "step": ("level ghost fill + interp(3 comps) + position update + per-patch lists rebuilt "
-                            "(bench.level_lists, torch ops) + bin(interior, ghost-box lists) + zero f + "
+                            "(bench.level_lists, torch ops) + bin(ghost-box lists, interior selected) + zero f + "
                             "spread(3 comps)" if args.move else
-                            "level ghost fill + bin(interior lists) + bin(ghost-box lists) + interp(3 comps) + "
-                            "zero f + spread(3 comps); stationary markers, per-patch lists built once at setup "
+                            "level ghost fill + bin(ghost-box lists; the interior lists select interp's entries) + "
+                            "interp(3 comps) + zero f + spread(3 comps); stationary markers, per-patch lists built once at setup "
                             "(LIndexSetData between regrids), one launch per sweep over the 512 patches")},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "algorithmic_bytes": {"interp": B_i, "spread": B_s}, "kernel_ms": {"interp": k_i, "spread": k_s}},
+                     "algorithmic_bytes": {"interp": B_i, "spread": B_s}, "kernel_ms": {"interp": k_i, "spread": k_s},
+                     "lds_atomic": lds},
         "cpu_baseline": None,
         "breakdown_ms": {k: mean(v) for k, v in acc.items()},
         "touched_points": S_touched,
@@ -457,7 +489,8 @@ def main():
         return
 
     from ibamr_amd import le
-    from ibamr_amd.slab import GhostMarkers, Slab, SlabExchange, migrate, redistribute, update_and_migrate
+    from ibamr_amd.slab import (GhostMarkers, Slab, SlabExchange, migrate, redistribute, update_and_migrate,
+                                update_and_migrate_fixed)
 
     N = cfg["N"]
     ghost = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
@@ -489,6 +522,16 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(4321 + rank)
     F = torch.rand((M_local, 3), dtype=torch.float64, device=dev, generator=gen).mul_(2).sub_(1)
     U = torch.zeros((M_local, 3), dtype=torch.float64, device=dev)
+    # N > 1 moving steps: fixed-capacity marker arrays whose length stays on the device
+    # (slab.update_and_migrate_fixed; no host sync in the step)
+    fixed = world > 1 and args.move and not args.renumber and args.spread_mode == "sum"
+    n_dev, send_cap = None, 0
+    if fixed:
+        cap = M_local + max(M_local // 8, 65536)
+        send_cap = max(M_local // 32, 16384)
+        pad = lambda t: torch.cat([t, torch.zeros((cap - M_local, 3), dtype=t.dtype, device=dev)]).contiguous()
+        X, F, U = pad(X), pad(F), pad(U)
+        n_dev = torch.tensor([M_local], dtype=torch.int32, device=dev)
     # Lagrangian indices (globally unique: rank-major generation order) for --renumber
     lag = (torch.arange(M_local, dtype=torch.int32, device=dev) * world + rank) if args.renumber else None
     u = geom.alloc("side", device=dev)
@@ -506,6 +549,10 @@ def main():
     cur = {"X": X, "F": F, "U": U}
 
     def bin_step():
+        if fixed:
+            bins.bin_count(geom, kernel, X, n_dev)
+            cur.update(X=X, F=F, U=U)
+            return
         if gm is None:
             bins.bin(geom, kernel, X)
             cur.update(X=X, F=F, U=U)
@@ -564,13 +611,15 @@ def main():
     def step_move(record):
         # interp -> X += dt U -> migrate -> bin -> spread: one bin per step, as in
         # IBMethod's explicit loop (interpolateVelocity, eulerStep, spreadForce)
-        nonlocal X, F, U, lag
+        nonlocal X, F, U, lag, n_dev
         if record:
             E[0].record()
         interp_with_fill()
         if record:
             E[1].record()
-        if world > 1:
+        if fixed:
+            X, (F,), n_dev = update_and_migrate_fixed(slab, ctx, "euler", dt_move, X, U, [F], n_dev, send_cap)
+        elif world > 1:
             # fused on the device: update, wrap, owner classes, stable partition;
             # the leavers to the z-neighbours (slab.update_and_migrate)
             if lag is None:
@@ -698,6 +747,8 @@ def main():
 
     ms_per_step = 1e3 * elapsed / args.steps
     value = 2.0 * M_total * args.steps / elapsed
+    lds = lds_atomic(ctx, lambda: le.spread(ctx, bins, kernel, "side", geom, f, cur["F"], cur["X"]),
+                     sum(kt["spread"]) / len(kt["spread"]))
 
     def mean(v):
         return sum(v) / len(v)
@@ -751,7 +802,9 @@ def main():
         "config": {"workload": cfg["desc"], "kernel": kernel, "grid": [N, N, N], "markers": M_total,
                    "parallelism": f"z-slab x{world}", "ghost": ghost, "marker_order": args.marker_order, "layout": args.layout, "spread_mode": args.spread_mode if world > 1 else "one rank",
                    "solo_slab": args.solo_slab or None,
-                   "move": args.move, "renumber": args.renumber, "overlap": world > 1 and not args.no_overlap,
+                   "move": args.move, "renumber": args.renumber,
+                   "migration": ("fixed-capacity, device counts, no host sync" if fixed else
+                                 "counts read by the host" if world > 1 and args.move else None), "overlap": world > 1 and not args.no_overlap,
                    "overlap_check": overlap_check,
                    "step": ("ghost fill + interp(3 comps) + position update + migrate + " +
                             ("redistribute (numbering + nonlocal nodes + reorder) + " if args.renumber else "") +
@@ -762,7 +815,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per launch (PMC)", "traffic_note": traffic_note,
                      "algorithmic_bytes": {"interp": B_i, "spread": B_s},
                      "kernel_ms": {"interp": k_i, "spread": k_s},
-                     "pair_achieved": pair, "pair_frac": pair / HBM_PEAK_GBS},
+                     "pair_achieved": pair, "pair_frac": pair / HBM_PEAK_GBS, "lds_atomic": lds},
         "cpu_baseline": cpu,
         "breakdown_ms": {k: mean(v) for k, v in acc.items()},
         "touched_points": S_touched,

@@ -83,10 +83,14 @@ _SIGS = [
     ("ibtk_le_ctx_tune", c_int, [c_void_p, ctypes.c_char_p, c_int]),
     ("ibtk_le_ctx_set_plane_window", c_int, [c_void_p, c_int, c_int, c_int]),
     ("ibtk_le_ctx_last_kernel_ms", c_double, [c_void_p]),
+    ("ibtk_le_ctx_count_adds", c_int, [c_void_p, c_int]),
+    ("ibtk_le_ctx_last_adds", c_int, [c_void_p, ctypes.POINTER(ctypes.c_ulonglong)]),
     ("ibtk_le_markers_create", c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
     ("ibtk_le_markers_destroy", c_int, [c_void_p]),
     ("ibtk_le_markers_bin", c_int,
      [c_void_p, c_void_p, ctypes.POINTER(PatchGeom), c_int, c_void_p, c_void_p, c_void_p, c_int]),
+    ("ibtk_le_markers_bin_count", c_int,
+     [c_void_p, c_void_p, ctypes.POINTER(PatchGeom), c_int, c_void_p, c_int, c_void_p]),
     ("ibtk_le_markers_count", c_int, [c_void_p]),
     ("ibtk_le_markers_order", c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
     ("ibtk_le_interp", c_int,
@@ -112,6 +116,12 @@ _SIGS = [
     ("ibtk_le_slab_update_partition", c_int,
      [c_void_p, c_int, ctypes.c_longlong, c_double, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
       c_int, c_void_p, c_void_p]),
+    ("ibtk_le_slab_update_partition_count", c_int,
+     [c_void_p, c_int, ctypes.c_longlong, c_double, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+      c_int, c_void_p, c_void_p, c_void_p]),
+    ("ibtk_le_slab_migrate_pack", c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    ("ibtk_le_slab_migrate_unpack", c_int,
+     [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     ("ibtk_le_zero_ghosts", c_int, [c_void_p, ctypes.POINTER(PatchGeom), c_int, ctypes.POINTER(c_void_p), c_int]),
     ("ibtk_le_mark_stencils", c_int,
      [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_int,
@@ -123,6 +133,7 @@ _SIGS = [
      [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(c_void_p), c_int, c_void_p, c_int, c_void_p]),
     ("ibtk_le_level_spread", c_int,
      [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(c_void_p), c_int, c_void_p, c_int, c_void_p]),
+    ("ibtk_le_level_select_interior", c_int, [c_void_p, c_void_p, c_int, ctypes.POINTER(c_int), c_void_p]),
     ("ibtk_le_level_fill_ghosts", c_int,
      [c_void_p, c_int, ctypes.POINTER(PatchGeom), c_int, ctypes.POINTER(c_void_p), c_int, c_void_p]),
     ("ibtk_le_level_zero", c_int,

@@ -110,7 +110,9 @@ struct ibtk_le_ctx_s {
     DevBuf stamps;  // diagnostic phase clocks (IBTK_LE_STAMPS=1)
     DevBuf mig_cls, mig_cnt;  // ibtk_le_slab_update_partition scratch
     bool stamps_on = false;  // IBTK_LE_STAMPS=1, read once at ctx_create
-    int dbg = 0;             // IBTK_LE_DBG, read once at ctx_create
+    bool count_adds = false; // ibtk_le_ctx_count_adds: the spread sweeps count their ds_add_f64
+    DevBuf adds;             // the device counters
+    unsigned long long last_adds[2] = {0, 0};
     SweepTune tune;          // ibtk_le_ctx_tune (diagnostics)
     int zmode = 0, zlo = 0, zhi = -1;  // ibtk_le_ctx_set_plane_window
     bool timing = false;
@@ -143,6 +145,8 @@ struct ibtk_le_markers_s {
     bool has_indices = false, has_xshift = false;
     bool cand_valid = false;
     bool dedup_done = false, has_dups = false;
+    DevBuf qin, owner, int_off;           // ibtk_le_level_select_interior: per sorted entry, its Q target or -1
+    bool qin_valid = false;               // cleared by every bin
 };
 
 static int set_device(ibtk_le_ctx ctx) {
@@ -159,7 +163,6 @@ extern "C" int ibtk_le_ctx_create(int device, void* stream, ibtk_le_ctx* out) {
     c->device = device;
     c->stream = static_cast<hipStream_t>(stream);
     if (const char* e = getenv("IBTK_LE_STAMPS")) c->stamps_on = e[0] == '1';
-    if (const char* e = getenv("IBTK_LE_DBG")) c->dbg = atoi(e);
     HIP_TRY(hipSetDevice(device));
     int rc = c->err.ensure(sizeof(int));
     if (!rc) rc = c->sink.ensure(64 * sizeof(double));
@@ -182,7 +185,7 @@ extern "C" int ibtk_le_ctx_destroy(ibtk_le_ctx ctx) {
                        &ctx->stamps, &ctx->lst_idx, &ctx->lst_xs, &ctx->lst_key, &ctx->lst_perm, &ctx->lst_cell,
                        &ctx->lst2_idx, &ctx->lst2_xs, &ctx->lst2_cell, &ctx->lst_flag, &ctx->num_tab, &ctx->num_lkey,
                        &ctx->num_ckey,
-                       &ctx->lvl_tab, &ctx->zero_tab, &ctx->mig_cls, &ctx->mig_cnt})
+                       &ctx->lvl_tab, &ctx->zero_tab, &ctx->mig_cls, &ctx->mig_cnt, &ctx->adds})
         b->release();
     if (ctx->ev0) hipEventDestroy(ctx->ev0);
     if (ctx->ev1) hipEventDestroy(ctx->ev1);
@@ -205,7 +208,9 @@ extern "C" int ibtk_le_ctx_synchronize(ibtk_le_ctx ctx) {
     if (flag) {
         HIP_TRY(hipMemset(ctx->err.p, 0, sizeof(int)));
         return fail(IBTK_LE_ERR_INVARIANT,
-                    "device invariant failed (flag %d): a stencil left its staged region (1) or its bin bounds (2)",
+                    "device invariant failed (flag %d): a stencil left its staged region (1) or its bin bounds (2), "
+                    "an interior list entry is not in the level's binned lists (4), or a fixed-capacity "
+                    "migration overflowed (8)",
                     flag);
     }
     return IBTK_LE_OK;
@@ -471,7 +476,7 @@ extern "C" int ibtk_le_markers_destroy(ibtk_le_markers m) {
     hipStreamSynchronize(m->ctx->stream);
     for (DevBuf* b : {&m->sorted_key, &m->sorted_l, &m->sorted_s, &m->sorted_X, &m->sorted_a, &m->plane_start, &m->indices,
                       &m->xshift, &m->cand_cnt, &m->cand_off, &m->cand_idx, &m->last, &m->qdst, &m->items,
-                      &m->nsub, &m->isub, &m->nitems, &m->pd, &m->entry_off})
+                      &m->nsub, &m->isub, &m->nitems, &m->pd, &m->entry_off, &m->qin, &m->owner, &m->int_off})
         b->release();
     delete m;
     return IBTK_LE_OK;
@@ -545,9 +550,26 @@ static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel) {
     return IBTK_LE_OK;
 }
 
+static int markers_bin_impl(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_patch_geom* geom, int kernel,
+                            const double* X_dev, const int* indices_dev, const double* Xshift_dev, int nindices,
+                            const int* n_dev);
+
 extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_patch_geom* geom, int kernel,
                                    const double* X_dev, const int* indices_dev, const double* Xshift_dev,
                                    int nindices) {
+    return markers_bin_impl(ctx, m, geom, kernel, X_dev, indices_dev, Xshift_dev, nindices, nullptr);
+}
+
+extern "C" int ibtk_le_markers_bin_count(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_patch_geom* geom,
+                                         int kernel, const double* X_dev, int capacity, const int* n_dev) {
+    if (!n_dev) return fail(IBTK_LE_ERR_ARG, "markers_bin_count: null device count");
+    if (geom && geom->ndim != 3) return fail(IBTK_LE_ERR_ARG, "markers_bin_count: 3-D patches only");
+    return markers_bin_impl(ctx, m, geom, kernel, X_dev, nullptr, nullptr, capacity, n_dev);
+}
+
+static int markers_bin_impl(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_patch_geom* geom, int kernel,
+                            const double* X_dev, const int* indices_dev, const double* Xshift_dev, int nindices,
+                            const int* n_dev) {
     if (!ctx || !m) return fail(IBTK_LE_ERR_ARG, "markers_bin: null ctx/markers");
     if (int rc = check_geom(geom)) return rc;
     if (kernel < 0 || kernel >= K_COUNT) return fail(IBTK_LE_ERR_UNKNOWN_KERNEL, "Unknown kernel function %d", kernel);
@@ -577,6 +599,7 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     m->has_xshift = Xshift_dev != nullptr;
     m->cand_valid = false;
     m->dedup_done = false;
+    m->qin_valid = false;
     m->has_dups = false;
     int rc = 0;
     const int B = geom->ndim == 3 ? BRICK3 : BRICK2;
@@ -610,6 +633,7 @@ extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibt
     p.X = X_dev;
     p.indices = m->has_indices ? m->indices.as<int>() : nullptr;
     p.Xshift = m->has_xshift ? m->xshift.as<double>() : nullptr;
+    p.n_dev = n_dev;
     if (cols) HIP_TRY(launch_bin_col(kernel, p, n, ctx->keys_in.as<unsigned>(), ctx->vals_in.as<int>(), s));
     else HIP_TRY(launch_bin(geom->ndim, kernel, p, n, ctx->keys_in.as<unsigned>(), ctx->vals_in.as<int>(), s));
     int end_bit = 1;
@@ -720,6 +744,42 @@ static int build_dedup(ibtk_le_ctx ctx, ibtk_le_markers m) {
     HIP_TRY(hipMemcpyAsync(&ndup, dv + 1, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     m->has_dups = ndup > 0;
+    return IBTK_LE_OK;
+}
+
+// Counted spread sweeps (ibtk_le_ctx_count_adds): the ds_add_f64 the sweep issues,
+// for the LDS-atomic bound (bench.py's roofline.lds_atomic).  One host sync per
+// launch, so only outside timed regions.
+static int adds_begin(ibtk_le_ctx ctx, Params& p, bool reset) {
+    p.nadd = nullptr;
+    if (!ctx->count_adds) return IBTK_LE_OK;
+    if (int rc = ctx->adds.ensure(2 * sizeof(unsigned long long))) return rc;
+    HIP_TRY(hipMemsetAsync(ctx->adds.p, 0, 2 * sizeof(unsigned long long), ctx->stream));
+    if (reset) ctx->last_adds[0] = ctx->last_adds[1] = 0;
+    p.nadd = ctx->adds.as<unsigned long long>();
+    return IBTK_LE_OK;
+}
+static int adds_end(ibtk_le_ctx ctx, Params& p) {
+    if (!p.nadd) return IBTK_LE_OK;
+    unsigned long long h[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(h, p.nadd, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->last_adds[0] += h[0];
+    ctx->last_adds[1] += h[1];
+    p.nadd = nullptr;
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_ctx_count_adds(ibtk_le_ctx ctx, int enable) {
+    if (!ctx) return fail(IBTK_LE_ERR_ARG, "null ctx");
+    ctx->count_adds = enable != 0;
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_ctx_last_adds(ibtk_le_ctx ctx, unsigned long long* out) {
+    if (!ctx || !out) return fail(IBTK_LE_ERR_ARG, "null argument");
+    out[0] = ctx->last_adds[0];
+    out[1] = ctx->last_adds[1];
     return IBTK_LE_OK;
 }
 
@@ -872,14 +932,16 @@ static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cente
         const int cnt = std::min(MAXC, nc - first);
         if (int rc = make_comps(geom, centering, axis, q_dev, q_depth, Q_depth, first, cnt, p)) return rc;
         const bool t = ctx->timing && first == 0;
-        p.dbg = ctx->dbg;  // diagnostics: variants of the add loop
         const size_t nst = (size_t)m->item_bound * cnt * 8;
         if (geom->ndim == 3)
             if (int rc = stamps_begin(ctx, nst, p)) return rc;
-        if (geom->ndim == 3)
+        if (geom->ndim == 3) {
+            if (int rc = adds_begin(ctx, p, first == 0)) return rc;
             HIP_TRY(launch_spread_sweep(kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
-        else
+            if (int rc = adds_end(ctx, p)) return rc;
+        } else {
             HIP_TRY(launch_spread(geom->ndim, kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
+        }
         if (int rc = stamps_report(ctx, nst, p)) return rc;
         if (t) ctx->ev_valid = true;
     }
@@ -963,6 +1025,7 @@ extern "C" int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch,
     m->has_xshift = Xshift_dev != nullptr;
     m->cand_valid = false;
     m->dedup_done = false;
+    m->qin_valid = false;
     m->has_dups = false;
     int rc;
     if ((rc = upload_patches(ctx, m))) return rc;
@@ -1092,13 +1155,56 @@ extern "C" int ibtk_le_level_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kern
         return rc;
     if (m->n == 0) return IBTK_LE_OK;
     if (!Q_dev) return fail(IBTK_LE_ERR_ARG, "null Q");
-    if (int rc = build_dedup(ctx, m)) return rc;
-    p.qdst = m->has_dups ? m->qdst.as<int>() : nullptr;
+    if (m->qin_valid) {  // the interior entries only (each names its marker once)
+        p.qdst = m->qin.as<int>();
+    } else {
+        if (int rc = build_dedup(ctx, m)) return rc;
+        p.qdst = m->has_dups ? m->qdst.as<int>() : nullptr;
+    }
     p.Qout = Q_dev;
     const bool t = ctx->timing;
     ctx->ev_valid = false;
     HIP_TRY(launch_interp_sweep(kernel, p, m->n, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
     if (t) ctx->ev_valid = true;
+    return IBTK_LE_OK;
+}
+
+// LDataManager::interp's patch loop takes each patch's interior list
+// (LDataManager.cpp:763-807 with LIndexSetData's interior indices), the spread its
+// ghost-box list; the interior list is a sub-list of the ghost-box one (the markers
+// whose cell is in the patch box, unshifted).  Rather than binning both, a level
+// binned on the ghost-box lists is told which of its entries the interior lists name:
+// later level interps write Q from those entries only, and the next bin clears it.
+// An interior entry with no match in its patch's binned list raises device flag 4
+// (reported by ibtk_le_ctx_synchronize; no host sync here).
+extern "C" int ibtk_le_level_select_interior(ibtk_le_ctx ctx, ibtk_le_markers m, int n_markers,
+                                             const int* interior_offsets, const int* interior_indices_dev) {
+    if (!ctx || !m || !interior_offsets) return fail(IBTK_LE_ERR_ARG, "select_interior: null argument");
+    if (m->npatch <= 0) return fail(IBTK_LE_ERR_ARG, "select_interior: not a level binning (ibtk_le_level_bin)");
+    const int np = m->npatch;
+    if (interior_offsets[0] != 0) return fail(IBTK_LE_ERR_ARG, "select_interior: offsets[0] must be 0");
+    for (int q = 0; q < np; ++q)
+        if (interior_offsets[q + 1] < interior_offsets[q]) return fail(IBTK_LE_ERR_ARG, "select_interior: decreasing offsets");
+    const int n_int = interior_offsets[np];
+    if (n_int > 0 && (!interior_indices_dev || n_markers <= 0))
+        return fail(IBTK_LE_ERR_ARG, "select_interior: null indices or no markers");
+    if (!m->has_indices) return fail(IBTK_LE_ERR_ARG, "select_interior: the binned lists must be index lists");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    const hipStream_t s = ctx->stream;
+    int rc;
+    if ((rc = m->qin.ensure(sizeof(int) * (size_t)std::max(m->n, 1)))) return rc;
+    if ((rc = m->owner.ensure(sizeof(int) * (size_t)std::max(n_markers, 1)))) return rc;
+    if ((rc = m->int_off.ensure(sizeof(int) * (size_t)(np + 1)))) return rc;
+    if ((rc = ctx->counts.ensure(sizeof(int)))) return rc;
+    HIP_TRY(hipMemcpyAsync(m->int_off.p, interior_offsets, sizeof(int) * (size_t)(np + 1), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(m->owner.p, 0xff, sizeof(int) * (size_t)std::max(n_markers, 1), s));
+    HIP_TRY(hipMemsetAsync(ctx->counts.p, 0, sizeof(int), s));
+    HIP_TRY(launch_interior_owner(m->int_off.as<int>(), np, interior_indices_dev, n_int, m->owner.as<int>(), s));
+    HIP_TRY(launch_interior_targets(m->sorted_l.as<int>(), m->sorted_s.as<int>(), m->entry_off.as<int>(), np,
+                                    m->has_xshift ? m->xshift.as<double>() : nullptr, m->owner.as<int>(), m->n,
+                                    m->qin.as<int>(), ctx->counts.as<int>(), s));
+    HIP_TRY(launch_check_count(ctx->counts.as<int>(), n_int, ctx->err.as<int>(), 4, s));
+    m->qin_valid = true;
     return IBTK_LE_OK;
 }
 
@@ -1119,7 +1225,9 @@ extern "C" int ibtk_le_level_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kern
     ctx->ev_valid = false;
     const size_t nst = (size_t)m->item_bound * nc * 8;
     if (int rc = stamps_begin(ctx, nst, p)) return rc;
+    if (int rc = adds_begin(ctx, p, true)) return rc;
     HIP_TRY(launch_spread_sweep(kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
+    if (int rc = adds_end(ctx, p)) return rc;
     if (int rc = stamps_report(ctx, nst, p)) return rc;
     if (t) ctx->ev_valid = true;
     return IBTK_LE_OK;
@@ -1377,10 +1485,58 @@ extern "C" int ibtk_le_position_update(ibtk_le_ctx ctx, int scheme, long long n,
     return IBTK_LE_OK;
 }
 
+static int slab_update_partition_impl(ibtk_le_ctx ctx, int scheme, long long M, double dt, const double* X_cur_dev,
+                                      const double* U0_dev, const double* U1_dev, double* X_new_dev, const double* L,
+                                      int Nz, int nranks, int rank, const int* n_dev, int* order_dev, int* counts_dev);
+
 extern "C" int ibtk_le_slab_update_partition(ibtk_le_ctx ctx, int scheme, long long M, double dt,
                                              const double* X_cur_dev, const double* U0_dev, const double* U1_dev,
                                              double* X_new_dev, const double* L, int Nz, int nranks, int rank,
                                              int* order_dev, int* counts_dev) {
+    return slab_update_partition_impl(ctx, scheme, M, dt, X_cur_dev, U0_dev, U1_dev, X_new_dev, L, Nz, nranks, rank,
+                                      nullptr, order_dev, counts_dev);
+}
+
+extern "C" int ibtk_le_slab_update_partition_count(ibtk_le_ctx ctx, int scheme, long long capacity, double dt,
+                                                   const double* X_cur_dev, const double* U0_dev,
+                                                   const double* U1_dev, double* X_new_dev, const double* L, int Nz,
+                                                   int nranks, int rank, const int* n_dev, int* order_dev,
+                                                   int* counts_dev) {
+    if (!n_dev) return fail(IBTK_LE_ERR_ARG, "null device count");
+    return slab_update_partition_impl(ctx, scheme, capacity, dt, X_cur_dev, U0_dev, U1_dev, X_new_dev, L, Nz, nranks,
+                                      rank, n_dev, order_dev, counts_dev);
+}
+
+extern "C" int ibtk_le_slab_migrate_pack(ibtk_le_ctx ctx, const double* rows_dev, int depth, const int* order_dev,
+                                         const int* counts_dev, int send_cap, double* send_down_dev,
+                                         double* send_up_dev) {
+    if (!ctx || !rows_dev || !order_dev || !counts_dev || !send_down_dev || !send_up_dev)
+        return fail(IBTK_LE_ERR_ARG, "migrate_pack: null argument");
+    if (depth < 1 || send_cap < 0) return fail(IBTK_LE_ERR_ARG, "migrate_pack: depth >= 1, send_cap >= 0");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    HIP_TRY(launch_mig_pack(rows_dev, depth, order_dev, counts_dev, send_cap, send_down_dev, send_up_dev,
+                            ctx->err.as<int>(), ctx->stream));
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_slab_migrate_unpack(ibtk_le_ctx ctx, const double* rows_dev, int depth, const int* order_dev,
+                                           const int* counts_dev, const int* recv_counts_dev,
+                                           const double* from_down_dev, const double* from_up_dev, int send_cap,
+                                           double* out_dev, int out_cap, int* n_out_dev) {
+    if (!ctx || !rows_dev || !order_dev || !counts_dev || !recv_counts_dev || !from_down_dev || !from_up_dev ||
+        !out_dev || !n_out_dev)
+        return fail(IBTK_LE_ERR_ARG, "migrate_unpack: null argument");
+    if (depth < 1 || send_cap < 0 || out_cap < 0) return fail(IBTK_LE_ERR_ARG, "migrate_unpack: bad sizes");
+    if (out_dev == rows_dev) return fail(IBTK_LE_ERR_ARG, "migrate_unpack: out must not alias rows");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    HIP_TRY(launch_mig_unpack(rows_dev, depth, order_dev, counts_dev, recv_counts_dev, from_down_dev, from_up_dev,
+                              send_cap, out_dev, out_cap, n_out_dev, ctx->err.as<int>(), ctx->stream));
+    return IBTK_LE_OK;
+}
+
+static int slab_update_partition_impl(ibtk_le_ctx ctx, int scheme, long long M, double dt, const double* X_cur_dev,
+                                      const double* U0_dev, const double* U1_dev, double* X_new_dev, const double* L,
+                                      int Nz, int nranks, int rank, const int* n_dev, int* order_dev, int* counts_dev) {
     if (!ctx) return fail(IBTK_LE_ERR_ARG, "null context");
     if (scheme < IBTK_LE_EULER || scheme > IBTK_LE_TRAPEZOIDAL) return fail(IBTK_LE_ERR_ARG, "unknown update scheme");
     if (M < 0 || M >= (1LL << 31)) return fail(IBTK_LE_ERR_ARG, "marker count out of range");
@@ -1403,6 +1559,7 @@ extern "C" int ibtk_le_slab_update_partition(ibtk_le_ctx ctx, int scheme, long l
     g.nz = Nz / nranks;
     g.rank = rank;
     g.dz = L[2] / Nz;
+    g.n_dev = n_dev;
     const long nb = (long)((M + BLOCK - 1) / BLOCK);
     int rc;
     if ((rc = ctx->mig_cls.ensure((size_t)M))) return rc;

@@ -939,8 +939,10 @@ __global__ __launch_bounds__(BLOCK) void k_slab_update(long M, double dt, const 
     if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
     __syncthreads();
     const long i = (long)blockIdx.x * BLOCK + threadIdx.x;
+    const long Mv = g.n_dev ? min((long)*g.n_dev, M) : M;
     int c = -1;
-    if (i < M) {
+    if (i < M && i >= Mv) cls[i] = 255;  // unused row of a fixed-capacity list
+    if (i < Mv) {
         double w[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
@@ -974,7 +976,7 @@ __global__ __launch_bounds__(BLOCK) void k_slab_partition(long M, const unsigned
                                                           const int* boff, int nb, int* order, int* counts) {
     __shared__ int wcnt[BLOCK / 64][4];
     const long i = (long)blockIdx.x * BLOCK + threadIdx.x;
-    const int c = i < M ? (int)cls[i] : -1;
+    const int c = i < M && cls[i] < 4 ? (int)cls[i] : -1;
     const int w = threadIdx.x >> 6;
     int rank = 0;
 #pragma unroll
@@ -1011,4 +1013,109 @@ hipError_t launch_slab_update_partition(int scheme, long M, double dt, const dou
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// a level's interp on its interior lists, from the binned ghost-box lists
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int patch_of_entry(const int* off, int npatch, int l) {
+    int lo = 0, hi = npatch - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= l) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+__global__ __launch_bounds__(BLOCK) void k_interior_owner(const int* int_off, int npatch, const int* int_idx, int n_int,
+                                                          int* owner) {
+    const int j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= n_int) return;
+    atomicMax(owner + int_idx[j], patch_of_entry(int_off, npatch, j));
+}
+hipError_t launch_interior_owner(const int* int_off, int npatch, const int* int_idx, int n_int, int* owner,
+                                 hipStream_t s) {
+    if (n_int <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_interior_owner, dim3((n_int + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, int_off, npatch, int_idx,
+                       n_int, owner);
+    return hipGetLastError();
+}
+__global__ __launch_bounds__(BLOCK) void k_interior_targets(const int* sorted_l, const int* sorted_s,
+                                                            const int* entry_off, int npatch, const double* xshift,
+                                                            const int* owner, int n, int* qin, int* found) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= n) return;
+    const int l = sorted_l[e], s = sorted_s[e];
+    bool keep = owner[s] == patch_of_entry(entry_off, npatch, l);
+    if (xshift) keep = keep && xshift[3 * (int64_t)l] == 0.0 && xshift[3 * (int64_t)l + 1] == 0.0 &&
+                       xshift[3 * (int64_t)l + 2] == 0.0;
+    qin[e] = keep ? s : -1;
+    const unsigned long long b = __ballot(keep);
+    if (b && (int)threadIdx.x % 64 == __ffsll(b) - 1) atomicAdd(found, __popcll(b));
+}
+hipError_t launch_interior_targets(const int* sorted_l, const int* sorted_s, const int* entry_off, int npatch,
+                                   const double* xshift, const int* owner, int n, int* qin, int* found,
+                                   hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_interior_targets, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, sorted_l, sorted_s,
+                       entry_off, npatch, xshift, owner, n, qin, found);
+    return hipGetLastError();
+}
+// fixed-capacity migration: pack the leavers, unpack stayers + arrivals (no host sync)
+__global__ __launch_bounds__(BLOCK) void k_mig_pack(const double* rows, int D, const int* order, const int* counts,
+                                                    int send_cap, double* send_down, double* send_up, int* err) {
+    const int n_stay = counts[0], n_down = counts[1], n_up = counts[2];
+    const long t = (long)blockIdx.x * BLOCK + threadIdx.x;
+    if (t == 0 && (n_down > send_cap || n_up > send_cap || counts[3] > 0)) atomicOr(err, 8);
+    const long tot = (long)send_cap * D;
+    if (t >= 2 * tot) return;
+    const bool up = t >= tot;
+    const long u = up ? t - tot : t;
+    const int j = (int)(u / D), d = (int)(u - (long)j * D);
+    const int n = up ? n_up : n_down;
+    if (j >= n) return;
+    const int src = order[n_stay + (up ? n_down : 0) + j];
+    (up ? send_up : send_down)[u] = rows[(long)src * D + d];
+}
+hipError_t launch_mig_pack(const double* rows, int D, const int* order, const int* counts, int send_cap,
+                           double* send_down, double* send_up, int* err, hipStream_t s) {
+    const long tot = 2L * send_cap * D;
+    hipLaunchKernelGGL(k_mig_pack, dim3((unsigned)((tot + BLOCK - 1) / BLOCK + (tot == 0))), dim3(BLOCK), 0, s, rows,
+                       D, order, counts, send_cap, send_down, send_up, err);
+    return hipGetLastError();
+}
+__global__ __launch_bounds__(BLOCK) void k_mig_unpack(const double* rows, int D, const int* order, const int* counts,
+                                                      const int* rc, const double* from_down, const double* from_up,
+                                                      int send_cap, double* out, int out_cap, int* n_out, int* err) {
+    const int n_stay = counts[0];
+    const int rd = min(rc[0], send_cap), ru = min(rc[1], send_cap);
+    const long total = (long)n_stay + rd + ru;
+    const long t = (long)blockIdx.x * BLOCK + threadIdx.x;
+    if (t == 0) {
+        if (rc[0] > send_cap || rc[1] > send_cap || total > out_cap) atomicOr(err, 8);
+        *n_out = (int)min(total, (long)out_cap);
+    }
+    const long i = t / D;
+    const int d = (int)(t - i * D);
+    if (i >= min(total, (long)out_cap)) return;
+    double v;
+    if (i < n_stay) v = rows[(long)order[i] * D + d];
+    else if (i < n_stay + rd) v = from_down[(i - n_stay) * D + d];
+    else v = from_up[(i - n_stay - rd) * D + d];
+    out[t] = v;
+}
+hipError_t launch_mig_unpack(const double* rows, int D, const int* order, const int* counts, const int* rc,
+                             const double* from_down, const double* from_up, int send_cap, double* out, int out_cap,
+                             int* n_out, int* err, hipStream_t s) {
+    const long tot = (long)out_cap * D;
+    hipLaunchKernelGGL(k_mig_unpack, dim3((unsigned)((tot + BLOCK - 1) / BLOCK + (tot == 0))), dim3(BLOCK), 0, s, rows,
+                       D, order, counts, rc, from_down, from_up, send_cap, out, out_cap, n_out, err);
+    return hipGetLastError();
+}
+
+__global__ void k_check_count(const int* count, int expect, int* err, int bit) {
+    if (threadIdx.x == 0 && *count != expect) atomicOr(err, bit);
+}
+hipError_t launch_check_count(const int* count, int expect, int* err, int bit, hipStream_t s) {
+    hipLaunchKernelGGL(k_check_count, dim3(1), dim3(64), 0, s, count, expect, err, bit);
+    return hipGetLastError();
+}
 }  // namespace ibtk_le

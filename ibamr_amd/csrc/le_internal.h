@@ -170,8 +170,9 @@ struct Params {
                                // overwrites: the last occurrence wins); nullptr = sorted_s (no duplicates)
     int* err;                  // device error word (0 = fine)
     double* sink;              // 64 doubles: the store target of masked-off lanes (branch-free stores)
-    unsigned long long* stamps;  // diagnostic phase clocks (nullptr: off)
-    int dbg;                     // diagnostic switches (0: off)
+    const int* n_dev = nullptr;  // bin: the list's length on the device (entries beyond it binned outside)
+    unsigned long long* stamps = nullptr;  // diagnostic phase clocks (nullptr: off)
+    unsigned long long* nadd = nullptr;    // spread: [ds_add_f64 wave-instructions, lane adds] issued (nullptr: not counted)
 };
 
 // Host-side launchers (le_kernels.hip).
@@ -195,7 +196,18 @@ struct SlabMig {
     double L[3];
     double dz;
     int Nz, nz, P, rank;
+    const int* n_dev;  // nullptr: all M rows; else the rows in use (a fixed-capacity list)
 };
+// Fixed-capacity migration (no host sync).  rows: [M][D] doubles; order/counts from
+// the partition ([stay | down | up | far]).  pack: the down / up leavers into
+// send_down / send_up (send_cap rows each); unpack: out = stayers in order, then
+// from_down[0:rc[0]], then from_up[0:rc[1]]; *n_out = their number.  Overflow
+// (leavers > send_cap, far markers, arrivals past out_cap) sets err bit 8.
+hipError_t launch_mig_pack(const double* rows, int D, const int* order, const int* counts, int send_cap,
+                           double* send_down, double* send_up, int* err, hipStream_t s);
+hipError_t launch_mig_unpack(const double* rows, int D, const int* order, const int* counts, const int* rc,
+                             const double* from_down, const double* from_up, int send_cap, double* out, int out_cap,
+                             int* n_out, int* err, hipStream_t s);
 hipError_t launch_slab_update_partition(int scheme, long M, double dt, const double* X, const double* U0,
                                         const double* U1, double* Xn, const SlabMig& g, unsigned char* cls,
                                         int* bcount, int* boff, void* temp, size_t& temp_bytes, int* order,
@@ -289,6 +301,17 @@ struct LevelNum {
 // key_ghost for cls 1, 0xffffffff for cls 2.
 hipError_t launch_level_node_keys(const LevelNum& L, const int* tab, const double* X, int n, unsigned* lkey,
                                   unsigned* ckey, hipStream_t s);
+// A level's interp restricted to its interior lists (ibtk_le_level_select_interior):
+// owner[s] = max patch whose interior list names marker s (owner pre-filled with -1);
+// then per sorted entry e of the binned lists: qin[e] = s if owner[s] is the entry's
+// patch and the entry is unshifted, else -1; *found counts the kept entries.
+hipError_t launch_interior_owner(const int* int_off, int npatch, const int* int_idx, int n_int, int* owner,
+                                 hipStream_t s);
+hipError_t launch_interior_targets(const int* sorted_l, const int* sorted_s, const int* entry_off, int npatch,
+                                   const double* xshift, const int* owner, int n, int* qin, int* found,
+                                   hipStream_t s);
+// *count != expect: atomicOr(err, bit)
+hipError_t launch_check_count(const int* count, int expect, int* err, int bit, hipStream_t s);
 // out[i * depth + k] = in[order[i] * depth + k]
 hipError_t launch_rows_gather(const int* order, int n, const double* in, int depth, double* out, hipStream_t s);
 // flag[i] = entry i of the (lag, ckey)-sorted list is the first of its lag run and not local

@@ -41,15 +41,31 @@
 namespace ibtk_le {
 
 constexpr int SW = 64;  // one wavefront per work item
-#ifndef IBTK_LE_EXP_IVOL
-#define IBTK_LE_EXP_IVOL 0
+// Diagnostic builds only (results change by design; tools/var_bench.sh): the spread
+// without its writeback stores / without reading u_old / ...
+#ifndef IBTK_LE_DIAG_SNOSTORE
+#define IBTK_LE_DIAG_SNOSTORE 0
 #endif
-#ifndef IBTK_LE_EXP_SNOSTORE
-#define IBTK_LE_EXP_SNOSTORE 0
+#ifndef IBTK_LE_DIAG_SNOLOAD
+#define IBTK_LE_DIAG_SNOLOAD 0
 #endif
-#ifndef IBTK_LE_EXP_SNOLOAD
-#define IBTK_LE_EXP_SNOLOAD 0
+#ifndef IBTK_LE_EXP_NT  // experiment: nontemporal plane streams (1 interp loads, 2 spread loads, 4 spread stores)
+#define IBTK_LE_EXP_NT 0
 #endif
+#ifndef IBTK_LE_SPREAD_PF  // experiment: u_old planes 1 or 2 anchors ahead
+#define IBTK_LE_SPREAD_PF 2
+#endif
+constexpr int SPF = IBTK_LE_SPREAD_PF;
+#ifndef IBTK_LE_DIAG_SNOPROC  // ... without the candidates' weights and adds (the streams alone)
+#define IBTK_LE_DIAG_SNOPROC 0
+#endif
+
+// LDS read of one double that the compiler may not merge with its neighbour into a
+// ds_read2_b64 (half the rate of two ds_read_b64 on gfx950: interp sweep 10.7 ->
+// 9.9 ms on cfg4, profiles/r03f)
+__device__ __forceinline__ double lds_ld(const double* q) {
+    return *(const volatile __attribute__((address_space(3))) double*)q;
+}
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
@@ -109,6 +125,11 @@ template <int K>
 __global__ __launch_bounds__(BLOCK) void k_bin_col(Params p, int n, unsigned* keys, int* vals) {
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
+    if (p.n_dev && i >= *p.n_dev) {  // a fixed-capacity list's unused rows: outside
+        keys[i] = (unsigned)p.nbuckets_total;
+        vals[i] = i;
+        return;
+    }
     const int s = p.indices ? p.indices[i] : i;
     double Xs[3];
 #pragma unroll
@@ -354,11 +375,7 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
                 for (int r = 0; r < R; ++r)
 #pragma unroll
                     for (int i0 = 0; i0 < W; ++i0)
-#if IBTK_LE_EXP_IVOL
-                        v[r * W + i0] = *(const volatile __attribute__((address_space(3))) double*)&pl[(r0 + r) * RX + i0];
-#else
-                        v[r * W + i0] = pl[(r0 + r) * RX + i0];
-#endif
+                        v[r * W + i0] = lds_ld(&pl[(r0 + r) * RX + i0]);
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const double wyz = st[1].w[r0 + r] * st[2].w[i2];  // f.m4:1349-1353
@@ -461,7 +478,7 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
         const int zc = min(max(z, cd.lo[2]), cd.hi[2]);
         const double* pb = cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2;
 #pragma unroll
-        for (int k = 0; k < NPT; ++k) v[k] = pb[poff[k]];
+        for (int k = 0; k < NPT; ++k) v[k] = (IBTK_LE_EXP_NT & 1) ? __builtin_nontemporal_load(pb + poff[k]) : pb[poff[k]];
     };
     auto plane_put = [&](int zr, const double* v) {  // registers -> ring slot, 0 outside the array
         const int z = zorg + min(zr, plast);
@@ -774,6 +791,19 @@ __device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd
     for (int s1 = 0; s1 < W; ++s1)
 #pragma unroll
         for (int s0 = 0; s0 < W; ++s0) P[s1 * W + s0] = wx[s0] * wy[s1];
+    if (p.nadd) {  // counted launch (ibtk_le_ctx_count_adds): the adds issued below
+        unsigned long long ins = 0, lanes = 0;
+#pragma unroll
+        for (int i2 = 0; i2 < W; ++i2) {
+            const unsigned long long bm = __ballot(i2 >= z0 && i2 <= z1);
+            ins += bm ? (unsigned long long)(W * W) : 0ull;
+            lanes += (unsigned long long)__popcll(bm) * (unsigned long long)(W * W);
+        }
+        if (lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) {
+            atomicAdd(p.nadd, ins);
+            atomicAdd(p.nadd + 1, lanes);
+        }
+    }
     char* const rb = reinterpret_cast<char*>(ring);
     int sl = (int)((unsigned)(a + oz + 64 * NSL) % (unsigned)NSL);  // ring slot of plane i2 = 0
     clk.lap(2);
@@ -890,6 +920,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // adds of the n <= 64 candidates held one per lane (lane j's anchor plane:
     // a - 1 for j < r, else a)
     auto process = [&](int a, int r, int n, const Cand& mine) {
+        if (IBTK_LE_DIAG_SNOPROC) return;
         spread_tiled<K>(p, cd, ring, mine, lane < n, lane < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi,
                         inv_h3, inv_d, clk);
     };
@@ -897,7 +928,8 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     auto plane_load = [&](int z, double* v) {
         const double* pb = plane_ptr(z);
 #pragma unroll
-        for (int k = 0; k < NPL; ++k) v[k] = IBTK_LE_EXP_SNOLOAD ? 0.0 : pb[loff[k]];
+        for (int k = 0; k < NPL; ++k)
+            v[k] = IBTK_LE_DIAG_SNOLOAD ? 0.0 : (IBTK_LE_EXP_NT & 2) ? __builtin_nontemporal_load(pb + loff[k]) : pb[loff[k]];
     };
     auto plane_put = [&](int z, const double* v) {
         double* sl = ring + sslot<K>(z) * S::PV;
@@ -913,8 +945,9 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         for (int k = 0; k < NPL; ++k) v[k] = sl[lane + k * SW];
 #pragma unroll
         for (int k = 0; k < NPL; ++k) {  // not-owned points store to the sink: no branch per store
-            double* dst = ((okxy >> k) & 1u) && !IBTK_LE_EXP_SNOSTORE ? pb + loff[k] : p.sink + lane;
-            *dst = v[k];
+            double* dst = ((okxy >> k) & 1u) && !IBTK_LE_DIAG_SNOSTORE ? pb + loff[k] : p.sink + lane;
+            if (IBTK_LE_EXP_NT & 4) __builtin_nontemporal_store(v[k], dst);
+            else *dst = v[k];
         }
     };
 
@@ -924,14 +957,15 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // a's last partial chunk is carried into a+1's chunk 1.  The ring holds the
     // planes of anchors a-1 and a: [a-1+LO, a+HI].
     clk.start(p.stamps != nullptr);
-    // prologue: planes afirst+LO .. afirst+HI-1 into the ring; plane afirst+HI,
-    // the ranges and chunk 1 of afirst into registers
-    double pv[NPL];
+    // prologue: planes afirst+LO .. afirst+HI-1 into the ring; planes afirst+HI and
+    // afirst+HI+1, the ranges and chunk 1 of afirst into registers
+    double pvA[NPL], pvB[NPL];
     for (int z = afirst + LO; z < afirst + HI; ++z) {
-        plane_load(z, pv);
-        plane_put(z, pv);
+        plane_load(z, pvA);
+        plane_put(z, pvA);
     }
-    plane_load(afirst + HI, pv);
+    plane_load(afirst + HI, pvA);
+    if (SPF == 2) plane_load(afirst + HI + 1, pvB);
     int rowv[3];
     rows_load(afirst, rowv);
     Ranges rg;  // ranges of the anchor whose chunk 1 is prefetched (wave-uniform)
@@ -946,7 +980,11 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     int n1 = min(tA, SW);  // lanes of a's chunk 1
     if (afirst + 1 <= alast) rows_load(afirst + 1, rowv);
     clk.lap(0);
-    for (int a = afirst; a <= alast; ++a) {
+    // One anchor step.  The u_old planes stream two anchors ahead through two
+    // register buffers (pv: plane a+HI in, plane a+HI+2 out): the loop is unrolled
+    // by two so each buffer stays in registers of its own, and twice the plane
+    // loads are in flight per wave (the spread's streams were latency-bound at one).
+    auto anchor_step = [&](int a, double* pv) {
         if (a >= afirst + 2) plane_writeback(a - 2 + LO);  // no anchor left reaches it
         plane_put(a + HI, pv);                               // into its slot
         const Cand cur = nxt;
@@ -957,7 +995,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         const int nmid = (tCur - h) / SW;       // full middle chunks
         const int r_a = (tCur - h) % SW;        // carried into a+1
         clk.lap(1);
-        // prefetch for a+1: its ranges, its chunk 1, plane a+HI+1, the rows of a+2
+        // prefetch for a+1: its ranges, its chunk 1, the rows of a+2; plane a+HI+2
         if (a + 1 <= alast) {
             make_ranges_lanes(rowv, rg);
             tA = rg.pre[S::NR];
@@ -967,8 +1005,8 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
             etail = range_pos(rg, max(tA - SW + lane, 0));
             n1 = r_a + min(SW - r_a, tA);
             r_prev = r_a;
-            plane_load(a + HI + 1, pv);
             if (a + 2 <= alast) rows_load(a + 2, rowv);
+            if (a + SPF <= alast) plane_load(a + HI + SPF, pv);
         }
         if (cur_n > 0) process(a, cur_r, cur_n, cur);
         if (nmid > 0) {  // dense planes: the full middle chunks (ranges of a rebuilt)
@@ -992,6 +1030,14 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
             process(a, 0, r_a, last);
         }
         clk.lap(4);
+    };
+    if constexpr (SPF == 1) {
+        for (int a = afirst; a <= alast; ++a) anchor_step(a, pvA);
+    } else {
+        for (int a = afirst; a <= alast; a += 2) {
+            anchor_step(a, pvA);
+            if (a + 1 <= alast) anchor_step(a + 1, pvB);
+        }
     }
     plane_writeback(alast - 1 + LO);
     plane_writeback(alast + LO);

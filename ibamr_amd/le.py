@@ -185,6 +185,16 @@ class Context:
     def last_kernel_ms(self) -> float:
         return float(self.lib.ibtk_le_ctx_last_kernel_ms(self.h))
 
+    def count_adds(self, on=True):
+        """Counted 3-D spread sweeps (ibtk_le_ctx_count_adds; syncs the host per launch)."""
+        check(self.lib.ibtk_le_ctx_count_adds(self.h, int(on)))
+
+    def last_adds(self):
+        """(ds_add_f64 wave-instructions, lane adds) of the last counted spread call."""
+        out = (ctypes.c_ulonglong * 2)()
+        check(self.lib.ibtk_le_ctx_last_adds(self.h, out))
+        return int(out[0]), int(out[1])
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.ibtk_le_ctx_destroy(self.h)
@@ -225,6 +235,18 @@ class Markers:
         check(self.ctx.lib.ibtk_le_markers_bin(self.ctx.h, self.h, ctypes.byref(geom.c), kernel_id(kernel), _ptr(X),
                                                _ptr(indices), _ptr(Xshift), int(n)))
         self.kernel, self.geom, self.n = kernel, geom, n
+        return self
+
+    def bin_count(self, geom: Geometry, kernel: str, X: torch.Tensor, n_dev: torch.Tensor):
+        """Bin the first n_dev[0] (a device int32) of X's rows (ibtk_le_markers_bin_count):
+        a fixed-capacity marker array, no host sync."""
+        if X.dtype != torch.float64 or not X.is_contiguous() or X.dim() != 2 or X.shape[1] != 3:
+            raise ValueError("X: contiguous (capacity, 3) float64")
+        if n_dev.dtype != torch.int32 or n_dev.numel() < 1 or not n_dev.is_cuda:
+            raise ValueError("n_dev: a device int32")
+        check(self.ctx.lib.ibtk_le_markers_bin_count(self.ctx.h, self.h, ctypes.byref(geom.c), kernel_id(kernel),
+                                                     _ptr(X), int(X.shape[0]), _ptr(n_dev)))
+        self.kernel, self.geom, self.n = kernel, geom, X.shape[0]
         return self
 
     def count(self) -> int:
@@ -369,6 +391,18 @@ class Level:
         check(self.ctx.lib.ibtk_le_level_bin(self.ctx.h, self.markers.h, len(self.geoms), self._G,
                                              kernel_id(self.kernel), _ptr(X), self._O, _ptr(self.indices),
                                              _ptr(self.xshift)))
+        return self
+
+    def select_interior(self, n_markers: int, indices: torch.Tensor, offsets: Sequence[int]):
+        """After a bin on the ghost-box lists: later interps write Q only from the entries
+        the interior lists (patch q: indices[offsets[q]:offsets[q+1]]) name
+        (ibtk_le_level_select_interior); one binning serves both sweeps."""
+        if len(offsets) != len(self.geoms) + 1:
+            raise ValueError("one offset per patch, plus the end")
+        idx = indices.to(torch.int32).contiguous()
+        self._sel = idx  # kept alive until the next bin
+        O = (ctypes.c_int * len(offsets))(*[int(o) for o in offsets])
+        check(self.ctx.lib.ibtk_le_level_select_interior(self.ctx.h, self.markers.h, int(n_markers), O, _ptr(idx)))
         return self
 
     def fill_ghosts(self, centering: str, arrays, q_depth: int = 1, periodic=None):
@@ -530,6 +564,52 @@ def slab_update_partition(ctx: Context, scheme: str, dt: float, X: torch.Tensor,
                                                 ctypes.cast(Ld, ctypes.c_void_p), int(Nz), int(nranks), int(rank),
                                                 _ptr(order), _ptr(counts)))
     return Xn, order[:M], counts
+
+
+def slab_update_partition_count(ctx: Context, scheme: str, dt: float, X: torch.Tensor, U0: torch.Tensor, L,
+                                Nz: int, nranks: int, rank: int, n_dev: torch.Tensor,
+                                U1: Optional[torch.Tensor] = None):
+    """slab_update_partition over the first n_dev[0] rows of capacity-sized arrays
+    (ibtk_le_slab_update_partition_count): (X_new, order, counts), all on the device."""
+    if scheme not in UPDATE_SCHEMES:
+        raise ValueError(f"unknown scheme {scheme!r}")
+    for t in [X, U0] + ([U1] if scheme == "trapezoidal" else []):
+        if t is None or t.dtype != torch.float64 or t.shape != X.shape or X.dim() != 2 or X.shape[1] != 3:
+            raise ValueError("X, U0, U1: (capacity, 3) float64 of one shape")
+    C = X.shape[0]
+    Xn = torch.empty_like(X)
+    order = torch.empty(max(C, 1), dtype=torch.int32, device=X.device)
+    counts = torch.zeros(4, dtype=torch.int32, device=X.device)
+    Ld = (ctypes.c_double * 3)(*[float(v) for v in L])
+    check(ctx.lib.ibtk_le_slab_update_partition_count(ctx.h, UPDATE_SCHEMES[scheme], C, float(dt), _ptr(X), _ptr(U0),
+                                                      _ptr(U1) if scheme == "trapezoidal" else None, _ptr(Xn),
+                                                      ctypes.cast(Ld, ctypes.c_void_p), int(Nz), int(nranks),
+                                                      int(rank), _ptr(n_dev), _ptr(order), _ptr(counts)))
+    return Xn, order, counts
+
+
+def slab_migrate_pack(ctx: Context, rows: torch.Tensor, order: torch.Tensor, counts: torch.Tensor,
+                      send_down: torch.Tensor, send_up: torch.Tensor):
+    """The down / up leavers of rows ([capacity, depth] float64) into the send buffers
+    ([send_cap, depth] each), ibtk_le_slab_migrate_pack."""
+    D = rows.shape[1]
+    if send_down.shape != send_up.shape or send_down.shape[1] != D:
+        raise ValueError("send buffers: (send_cap, depth) each")
+    check(ctx.lib.ibtk_le_slab_migrate_pack(ctx.h, _ptr(rows), D, _ptr(order), _ptr(counts), send_down.shape[0],
+                                            _ptr(send_down), _ptr(send_up)))
+
+
+def slab_migrate_unpack(ctx: Context, rows: torch.Tensor, order: torch.Tensor, counts: torch.Tensor,
+                        recv_counts: torch.Tensor, from_down: torch.Tensor, from_up: torch.Tensor,
+                        out: torch.Tensor, n_out: torch.Tensor):
+    """out = stayers, then the arrivals from below, then from above; n_out[0] = their
+    number (ibtk_le_slab_migrate_unpack)."""
+    D = rows.shape[1]
+    if out.shape[1] != D or from_down.shape != from_up.shape:
+        raise ValueError("buffer shapes")
+    check(ctx.lib.ibtk_le_slab_migrate_unpack(ctx.h, _ptr(rows), D, _ptr(order), _ptr(counts), _ptr(recv_counts),
+                                              _ptr(from_down), _ptr(from_up), from_down.shape[0], _ptr(out),
+                                              out.shape[0], _ptr(n_out)))
 
 
 def index_set_list(ctx: Context, geom: Geometry, X: torch.Tensor, ghost: int, lag: Optional[torch.Tensor] = None,

@@ -379,6 +379,60 @@ def update_and_migrate(slab: Slab, ctx, scheme: str, dt: float, X: torch.Tensor,
     return Xo, outs
 
 
+def update_and_migrate_fixed(slab: Slab, ctx, scheme: str, dt: float, X: torch.Tensor, U0: torch.Tensor,
+                             fields: Sequence[torch.Tensor], n_dev: torch.Tensor, send_cap: int,
+                             U1: Optional[torch.Tensor] = None, group=None):
+    """``update_and_migrate`` without a host sync: fixed-capacity arrays whose row count
+    lives on the device.
+
+    X, U0 (U1) and the fields hold ``capacity`` rows of which the first n_dev[0] (a
+    device int32) are markers.  The fused update + partition runs over those rows
+    (ibtk_le_slab_update_partition_count); the leavers are packed into send buffers of
+    ``send_cap`` rows per neighbour (ibtk_le_slab_migrate_pack) and exchanged at that
+    fixed size together with their counts -- nothing the host must read before posting
+    the receives; the stayers (in order), then the arrivals from below, then from above
+    are unpacked into new capacity-sized arrays (ibtk_le_slab_migrate_unpack).  Returns
+    (X, fields, n_dev), ready for ``Markers.bin_count``.  Leavers beyond send_cap, a
+    marker moving further than one slab, or arrivals beyond the capacity raise device
+    flag 8 at the next ``ctx.synchronize()`` (never a silent drop).  Bitwise the same
+    rows, in the same order, as ``update_and_migrate``."""
+    from . import le
+    C = X.shape[0]
+    Xn, order, counts = le.slab_update_partition_count(ctx, scheme, dt, X, U0, slab.L, slab.N[2], slab.P, slab.rank,
+                                                       n_dev, U1=U1)
+    flat = [f.reshape(C, -1) for f in fields]
+    data = torch.cat([Xn] + [f.to(Xn.dtype) for f in flat], dim=1).contiguous()
+    D = data.shape[1]
+    if slab.P == 1:
+        n_out = counts[0:1].clone()
+        outs, k = [], 3
+        for f, fl in zip(fields, flat):
+            w = fl.shape[1]
+            outs.append(data[:, k:k + w].reshape(f.shape).to(f.dtype).contiguous())
+            k += w
+        return Xn, outs, n_out
+    send_down = torch.empty((send_cap, D), dtype=data.dtype, device=data.device)
+    send_up = torch.empty_like(send_down)
+    le.slab_migrate_pack(ctx, data, order, counts, send_down, send_up)
+    gm = GhostMarkers(slab, group)
+    rc = torch.empty(2, dtype=torch.int32, device=X.device)  # [from below, from above]
+    # each peer's receives in the order it sends (P = 2: up == down): counts, then rows
+    gm._p2p([(counts[2:3], slab.up), (counts[1:2], slab.down)], [(rc[0:1], slab.down), (rc[1:2], slab.up)])
+    from_down = torch.empty_like(send_down)
+    from_up = torch.empty_like(send_down)
+    gm._p2p([(send_up, slab.up), (send_down, slab.down)], [(from_down, slab.down), (from_up, slab.up)])
+    out = torch.empty((C, D), dtype=data.dtype, device=data.device)
+    n_out = torch.empty(1, dtype=torch.int32, device=X.device)
+    le.slab_migrate_unpack(ctx, data, order, counts, rc, from_down, from_up, out, n_out)
+    Xo = out[:, :3].contiguous()
+    outs, k = [], 3
+    for f, fl in zip(fields, flat):
+        w = fl.shape[1]
+        outs.append(out[:, k:k + w].reshape((C,) + tuple(f.shape[1:])).to(f.dtype).contiguous())
+        k += w
+    return Xo, outs, n_out
+
+
 def migrate(slab: Slab, X: torch.Tensor, fields: Sequence[torch.Tensor] = (), group=None, cell_order: bool = True):
     """Move every marker to the rank whose slab holds its cell, after a position update.
 
@@ -471,7 +525,8 @@ def redistribute(slab: Slab, ctx, X: torch.Tensor, fields: Sequence[torch.Tensor
     """Number a rank's markers the way LDataManager does at redistribution, across ranks.
 
     After ``migrate``/``update_and_migrate`` every marker sits on the rank whose slab
-    (the rank's one patch of the level) holds its cell.  Then, as
+    (the rank's one patch of the level) holds its cell.  Positions are wrapped into the
+    periodic box first (beginDataRedistribution, LDataManager.cpp:1385-1399).  Then, as
     LDataManager::computeNodeDistribution (LDataManager.cpp:2839-3027):
 
     * local numbering -- the owned markers in the slab's cell order (x fastest),
@@ -504,6 +559,12 @@ def redistribute(slab: Slab, ctx, X: torch.Tensor, fields: Sequence[torch.Tensor
     if reorder is None:
         def reorder(order, *arrays):
             return le.ldata_reorder(ctx, order, *arrays)
+    # beginDataRedistribution's wrap into the periodic domain (LDataManager.cpp:1385-1399):
+    # one period at most per step, then clamped below the upper face
+    L = torch.tensor(list(slab.L), dtype=X.dtype, device=X.device)
+    X = torch.where(X < 0, X + L, X)
+    X = torch.where(X >= L, X - L, X)
+    X = torch.minimum(torch.clamp(X, min=0.0), L - torch.finfo(X.dtype).eps).contiguous()
     order, nl, nn = numbering(X, lag, 0)
     if nn:
         raise RuntimeError(f"rank {slab.rank}: {nn} markers outside the slab; migrate before redistribute")

@@ -132,6 +132,12 @@ int ibtk_le_markers_create(ibtk_le_ctx ctx, ibtk_le_markers* out);
 int ibtk_le_markers_destroy(ibtk_le_markers m);
 int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_patch_geom* geom, int kernel,
                         const double* X_dev, const int* indices_dev, const double* Xshift_dev, int nindices);
+/* The same for a fixed-capacity marker array whose length lives on the device
+ * (*n_dev <= capacity; a migration's output, no host sync): rows [n_dev, capacity)
+ * are binned outside -- interp writes 0 to their Q rows, spread skips them -- so
+ * Q/F arrays must hold capacity rows.  3-D, identity list. */
+int ibtk_le_markers_bin_count(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_patch_geom* geom, int kernel,
+                              const double* X_dev, int capacity, const int* n_dev);
 /* Number of list entries, and device pointers to the sorted list (entry -> marker
  * index, and entry -> Xshift[NDIM]); valid until the next bin call. */
 int ibtk_le_markers_count(ibtk_le_markers m);
@@ -194,6 +200,16 @@ int ibtk_le_level_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cen
                          const double* const* q_dev, int q_depth, double* Q_dev, int Q_depth, const double* X_dev);
 int ibtk_le_level_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                          double* const* q_dev, int q_depth, const double* Q_dev, int Q_depth, const double* X_dev);
+/* One binning for both sweeps: m binned on the ghost-box lists (the spread's), then
+ * told the interior lists (interior_offsets on the host, npatch + 1; indices on the
+ * device; markers 0 .. n_markers-1): later level interps on m write Q only from the
+ * entries the interior lists name (each patch's interior list is the unshifted
+ * sub-list of its ghost-box list whose cells lie in the patch box, LIndexSetData.cpp:
+ * 111-166), so results equal interp over a binning of the interior lists bit for bit.
+ * Cleared by the next bin.  An interior entry missing from its patch's binned list
+ * raises device flag 4 (ibtk_le_ctx_synchronize). */
+int ibtk_le_level_select_interior(ibtk_le_ctx ctx, ibtk_le_markers m, int n_markers, const int* interior_offsets,
+                                  const int* interior_indices_dev);
 /* Zeroes every patch array of a level, ghosts included, in one launch: the
  * f := 0 before LDataManager::spread accumulates into the level (its
  * f_data_ops->setToScalar(f_data_idx, 0.0, interior_only = false),
@@ -369,6 +385,26 @@ int ibtk_le_position_update(ibtk_le_ctx ctx, int scheme, long long n, double dt,
 int ibtk_le_slab_update_partition(ibtk_le_ctx ctx, int scheme, long long M, double dt, const double* X_cur_dev,
                                   const double* U0_dev, const double* U1_dev, double* X_new_dev, const double* L,
                                   int Nz, int nranks, int rank, int* order_dev, int* counts_dev);
+/* Fixed-capacity migration, no host sync (slab.update_and_migrate_fixed):
+ * ibtk_le_slab_update_partition_count is the partition of the first *n_dev of
+ * `capacity` rows; pack copies the down / up leavers of rows_dev ([capacity][depth]
+ * doubles: X then the LData fields) into send buffers of send_cap rows each; after
+ * the fixed-size exchange, unpack writes the stayers in order, then recv_counts[0]
+ * rows of from_down and recv_counts[1] of from_up, into out_dev (out_cap rows) and
+ * their number into *n_out_dev.  Leavers beyond send_cap, markers moving further
+ * than one slab, or arrivals beyond out_cap raise device flag 8 (reported by
+ * ibtk_le_ctx_synchronize): the caller sizes the buffers, the library never drops
+ * a marker silently. */
+int ibtk_le_slab_update_partition_count(ibtk_le_ctx ctx, int scheme, long long capacity, double dt,
+                                        const double* X_cur_dev, const double* U0_dev, const double* U1_dev,
+                                        double* X_new_dev, const double* L, int Nz, int nranks, int rank,
+                                        const int* n_dev, int* order_dev, int* counts_dev);
+int ibtk_le_slab_migrate_pack(ibtk_le_ctx ctx, const double* rows_dev, int depth, const int* order_dev,
+                              const int* counts_dev, int send_cap, double* send_down_dev, double* send_up_dev);
+int ibtk_le_slab_migrate_unpack(ibtk_le_ctx ctx, const double* rows_dev, int depth, const int* order_dev,
+                                const int* counts_dev, const int* recv_counts_dev, const double* from_down_dev,
+                                const double* from_up_dev, int send_cap, double* out_dev, int out_cap,
+                                int* n_out_dev);
 
 /* Diagnostics: masks_dev[c] (one byte per point of component c's ghosted array,
  * same layout) gets 1 at every point some listed stencil touches after clipping.
@@ -395,6 +431,11 @@ int ibtk_le_ctx_enable_timing(ibtk_le_ctx ctx, int enable);
  * boundaries move with the items). */
 int ibtk_le_ctx_tune(ibtk_le_ctx ctx, const char* key, int value);
 double ibtk_le_ctx_last_kernel_ms(ibtk_le_ctx ctx);
+/* Counted 3-D spread sweeps (a diagnostic for the LDS-atomic bound; one host sync
+ * per launch): while enabled, each spread call records the ds_add_f64 it issues,
+ * out[0] = wave-instructions, out[1] = lane adds (summed over its components). */
+int ibtk_le_ctx_count_adds(ibtk_le_ctx ctx, int enable);
+int ibtk_le_ctx_last_adds(ibtk_le_ctx ctx, unsigned long long* out);
 
 #ifdef __cplusplus
 }

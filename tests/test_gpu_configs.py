@@ -448,9 +448,29 @@ def _mig_worker(rank, world, port, out_q):
         Xb, fb = update_and_migrate(slab, ctx, "euler", dt, Xd, Ud, f)
         Xb2, fb2 = update_and_migrate(slab, ctx, "euler", dt, Xd, Ud, f)
         ctx.synchronize()
+        # the fixed-capacity form (no host sync): the same rows in the same order
+        from ibamr_amd.slab import update_and_migrate_fixed
+        C = M + M // 4
+        pad = lambda t: torch.cat([t, torch.full((C - M,) + tuple(t.shape[1:]), 7.0, dtype=t.dtype,
+                                                 device=t.device)]).contiguous()
+        n_dev = torch.tensor([M], dtype=torch.int32, device="cuda")
+        Xc, fc, nc = update_and_migrate_fixed(slab, ctx, "euler", dt, pad(Xd), pad(Ud), [pad(t) for t in f], n_dev,
+                                              send_cap=M // 5)
+        ctx.synchronize()
+        nfix = int(nc.item())
+        fixed_same = (nfix == Xb.shape[0] and torch.equal(Xc[:nfix], Xb) and torch.equal(fc[0][:nfix], fb[0])
+                      and torch.equal(fc[1][:nfix], fb[1]))
+        # a send buffer too small: device flag 8 at the next synchronize, never a silent drop
+        update_and_migrate_fixed(slab, ctx, "euler", dt, pad(Xd), pad(Ud), [pad(t) for t in f], n_dev, send_cap=1)
+        try:
+            ctx.synchronize()
+            overflow_seen = False
+        except RuntimeError as e:
+            overflow_seen = "flag 8" in str(e)
         same_repeat = torch.equal(Xb, Xb2) and all(torch.equal(a, b) for a, b in zip(fb, fb2))
         oa = torch.argsort(fa[1]); ob = torch.argsort(fb[1])
         ok = (torch.equal(fa[1][oa], fb[1][ob]) and torch.equal(Xa[oa], Xb[ob]) and torch.equal(fa[0][oa], fb[0][ob]))
+        ok = ok and fixed_same and overflow_seen
         # every marker is on the owner of its wrapped cell
         cz = torch.clamp((Xb[:, 2] / slab.dx[2]).floor().long(), 0, N - 1)
         owned = bool(((cz >= slab.z0) & (cz < slab.z1)).all())

@@ -114,7 +114,16 @@ def test_level_matches_patch_by_patch(le, ctx, kernel, P, clustered):
         f = [[torch.zeros_like(a) for a in per] for per in u]
         lvl_s.spread("side", f, Fd, Xd)
         outs.append(f)
+    # one binning for both sweeps: the ghost-box binning told the interior lists
+    # (ibtk_le_level_select_interior) interpolates bit for bit as the interior binning
+    offs = [0]
+    for l in lists_i:
+        offs.append(offs[-1] + l[0].numel())
+    lvl_s.select_interior(M, torch.cat([l[0] for l in lists_i]), offs)
+    U2 = torch.full((M, 3), np.nan, dtype=torch.float64, device="cuda")
+    lvl_s.interp("side", u, U2, Xd)
     ctx.synchronize()
+    assert torch.equal(U2, U), "interp on the selected interior entries of the ghost-box binning"
     Ug = U.cpu().numpy()
     assert not np.isnan(Ug).any(), "every marker is interior to exactly one patch"
     for q, geom in enumerate(geoms):
@@ -125,6 +134,12 @@ def test_level_matches_patch_by_patch(le, ctx, kernel, P, clustered):
         le.interp(ctx, m, kernel, "side", geom, u[q], U1, Xd)
         ctx.synchronize()
         assert np.array_equal(Ug[interior], U1.cpu().numpy()[interior]), f"patch {q} interp"
+        # and the level interp directly against the oracle on the patch's interior list:
+        # bit for bit (the Fortran's order and roundings)
+        Qo = np.zeros((M, 3))
+        ora.side_interp(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw,
+                        [a.cpu().numpy() for a in u[q]], interior, np.zeros((interior.size, 3)), X, Qo)
+        assert np.array_equal(Ug[interior], Qo[interior]), f"patch {q} level interp vs oracle"
         # the oracle on the patch's ghost-box list
         uo = [np.zeros(tuple(a.shape)) for a in u[q]]
         ora.side_spread(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, uo, idx, xs, X, F)
@@ -210,3 +225,29 @@ def test_level_zero(le, ctx, centering, depth):
     lvl.zero(centering, f, q_depth=depth)
     ctx.synchronize()
     assert all(not t.cpu().numpy().any() for row in f for t in row)
+
+
+def test_level_select_interior_rejects_foreign_entries(le, ctx):
+    """An interior list naming a marker its patch's binned list does not hold raises
+    device flag 4 at the next synchronize."""
+    g = ora.min_ghost_width("IB_4")
+    N, P = 32, 2
+    n = N // P
+    dx = 1.0 / N
+    geoms = []
+    for k in range(P):
+        for j in range(P):
+            for i in range(P):
+                lo = [i * n, j * n, k * n]
+                geoms.append(le.Geometry(lo, [v + n - 1 for v in lo], g, [dx] * 3, [v * dx for v in lo]))
+    X = torch.full((4, 3), 0.1, dtype=torch.float64, device="cuda")  # all in patch 0
+    lists = [(torch.arange(4, dtype=torch.int32, device="cuda"), None)] + \
+            [(torch.zeros(0, dtype=torch.int32, device="cuda"), None)] * (len(geoms) - 1)
+    lvl = le.Level(ctx, geoms, "IB_4", X, lists)
+    offs = [0] + [4] * len(geoms)           # patch 0's interior list: markers 0..3 -- fine
+    lvl.select_interior(4, torch.arange(4, dtype=torch.int32, device="cuda"), offs)
+    ctx.synchronize()
+    offs = [0, 0, 4] + [4] * (len(geoms) - 2)  # patch 1 claims them: not in its list
+    lvl.select_interior(4, torch.arange(4, dtype=torch.int32, device="cuda"), offs)
+    with pytest.raises(RuntimeError, match="flag 4"):
+        ctx.synchronize()

@@ -153,9 +153,13 @@ def test_spread_matches_oracle_in_canonical_order(le, ctx, oracle, kernel, ndim,
     ug = [a.cpu().numpy() for a in q]
     uo = [a.copy() for a in u0]
     oracle_call(oracle, "spread", kernel, centering, geom, uo, idx[order], xs[order], X, F.copy(), depth)
+    uc = [a.copy() for a in u0]  # the caller's list order (the reference's summation order)
+    oracle_call(oracle, "spread", kernel, centering, geom, uc, idx, xs, X, F.copy(), depth)
     for a in range(len(ug)):
         err = rel_err(ug[a], uo[a])
         assert err <= SPREAD_TOL, f"spread comp {a} rel err {err:.3e}"
+        err = rel_err(ug[a], uc[a])
+        assert err <= SPREAD_TOL, f"spread comp {a} rel err {err:.3e} against the caller's order"
     bitwise = all(np.array_equal(ug[a], uo[a]) for a in range(len(ug)))
     print(f"{kernel} {ndim}d {centering}: spread bitwise={bitwise}")
 
@@ -188,9 +192,13 @@ def test_bitwise_against_oracle_ib_side(le, ctx, oracle, kernel):
     oracle.side_spread(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, uo, idx[order],
                        xs[order], X, F)
     assert np.array_equal(Q.cpu().numpy()[idx], Qo[idx])
+    # and against the reference's own summation order: the caller's list order
+    uc = [a.copy() for a in u0]
+    oracle.side_spread(kernel, geom.dx, geom.x_lower, geom.ilower, geom.iupper, geom.gcw, uc, idx, xs, X, F)
     for a in range(3):
         ga = q[a].cpu().numpy()
         assert np.abs(ga - uo[a]).max() <= SPREAD_TOL * np.abs(uo[a]).max()
+        assert np.abs(ga - uc[a]).max() <= SPREAD_TOL * np.abs(uc[a]).max(), f"comp {a} vs caller order"
 
 
 def test_spread_bit_stable_run_to_run(le, ctx):

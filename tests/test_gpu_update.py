@@ -100,3 +100,50 @@ def test_update_then_rebin_interp(le, ctx, oracle):
                        np.arange(M, dtype=np.int32), np.zeros((M, 3)), Xn, Uo)
     scale = np.abs(Uo).max()
     assert np.abs(U1.cpu().numpy() - Uo).max() / scale <= 1e-13
+
+
+def test_moving_step_has_no_host_sync(le, ctx):
+    """One explicit coupling step on one GPU -- ghost fill, interp, X += dt U, re-bin,
+    zero ghosts, spread, fold (bench.py --move at N = 1) -- issues no host
+    synchronisation: torch's sync debug mode set to "error" stays silent (the library
+    calls themselves only enqueue work on the context stream), and the results match
+    the same step run with the mode off."""
+    from ibamr_amd.le import Geometry
+    N = 48
+    geom = Geometry.periodic_unit([N, N, N], 3)
+    g = torch.Generator(device="cuda:0").manual_seed(11)
+    M = 20000
+    X0 = torch.rand((M, 3), dtype=torch.float64, device="cuda", generator=g)
+    F = torch.rand((M, 3), dtype=torch.float64, device="cuda", generator=g) - 0.5
+    u = geom.alloc("side")
+    for a in u:
+        a.uniform_(-1, 1, generator=g)
+    dt = 0.05 / N
+
+    def step(X, U, f, bins):
+        le.fill_periodic_ghosts(ctx, geom, "side", u)
+        le.interp(ctx, bins, "IB_4", "side", geom, u, U, X)
+        le.position_update(ctx, "euler", dt, X, U, out=X)
+        bins.bin(geom, "IB_4", X)
+        le.zero_ghosts(ctx, geom, "side", f)
+        le.spread(ctx, bins, "IB_4", "side", geom, f, F, X)
+        le.fold_periodic_ghosts(ctx, geom, "side", f)
+
+    outs = []
+    for mode in ("error", None):
+        X = X0.clone()
+        U = torch.zeros_like(X)
+        f = geom.alloc("side")
+        bins = le.Markers(ctx).bin(geom, "IB_4", X)
+        step(X, U, f, bins)  # first call: the library's buffers are allocated here
+        ctx.synchronize()
+        if mode:
+            torch.cuda.set_sync_debug_mode(mode)
+        try:
+            step(X, U, f, bins)
+        finally:
+            torch.cuda.set_sync_debug_mode(0)
+        ctx.synchronize()
+        outs.append((X.clone(), U.clone(), [a.clone() for a in f]))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert all(torch.equal(a, b) for a, b in zip(outs[0][2], outs[1][2]))

@@ -237,3 +237,28 @@ def test_side_wrapper_periodic_images_match_unwrapped(oracle):
         ref[a] = fb[0, off:off + N, off:off + N, off:off + N]
         got = f[a][0, g:g + N, g:g + N, g:g + N]
         np.testing.assert_allclose(got, ref[a], rtol=0, atol=1e-9 * np.abs(ref[a]).max())
+
+
+def test_oracle_side_ib4_known_answer_3d(oracle):
+    """The oracle's 3-D side-centred IB_4 interp and spread against the 50-digit decimal
+    known answers of tests/golden/kat3d_side_ib4.json (tests/golden/make_kat3d.py, from
+    the Fortran text and LEInteractor's side frame shifts; clipped stencils, periodic
+    images, a repeated list entry)."""
+    import json
+    from pathlib import Path
+    k = json.loads((Path(__file__).parent / "golden" / "kat3d_side_ib4.json").read_text())
+    X = np.array(k["X"])
+    idx = np.array(k["indices"], dtype=np.int32)
+    xs = np.array(k["Xshift"])
+    u = [np.array(a) for a in k["u"]]
+    gcw = [k["gcw"]] * 3
+    Q = np.zeros_like(X)
+    oracle.side_interp("IB_4", k["dx"], k["x_lower"], k["ilower"], k["iupper"], gcw, [a.copy() for a in u], idx, xs,
+                       X, Q)
+    Qe = np.array(k["Q"])
+    assert np.abs(Q - Qe).max() <= 1e-14 * np.abs(Qe).max()
+    uo = [a.copy() for a in u]
+    oracle.side_spread("IB_4", k["dx"], k["x_lower"], k["ilower"], k["iupper"], gcw, uo, idx, xs, X, np.array(k["F"]))
+    for a in range(3):
+        fe = np.array(k["f"][a])
+        assert np.abs(uo[a] - fe).max() <= 1e-13 * np.abs(fe).max()
