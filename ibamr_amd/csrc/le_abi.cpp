@@ -1195,15 +1195,16 @@ extern "C" int ibtk_le_level_select_interior(ibtk_le_ctx ctx, ibtk_le_markers m,
     if ((rc = m->qin.ensure(sizeof(int) * (size_t)std::max(m->n, 1)))) return rc;
     if ((rc = m->owner.ensure(sizeof(int) * (size_t)std::max(n_markers, 1)))) return rc;
     if ((rc = m->int_off.ensure(sizeof(int) * (size_t)(np + 1)))) return rc;
-    if ((rc = ctx->counts.ensure(sizeof(int)))) return rc;
+    const int nblk = (std::max(m->n, 1) + BLOCK - 1) / BLOCK;  // per-block counts of the kept entries
+    if ((rc = ctx->counts.ensure(sizeof(int) * (size_t)nblk))) return rc;
     HIP_TRY(hipMemcpyAsync(m->int_off.p, interior_offsets, sizeof(int) * (size_t)(np + 1), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(m->owner.p, 0xff, sizeof(int) * (size_t)std::max(n_markers, 1), s));
-    HIP_TRY(hipMemsetAsync(ctx->counts.p, 0, sizeof(int), s));
+    HIP_TRY(hipMemsetAsync(ctx->counts.p, 0, sizeof(int) * (size_t)nblk, s));
     HIP_TRY(launch_interior_owner(m->int_off.as<int>(), np, interior_indices_dev, n_int, m->owner.as<int>(), s));
     HIP_TRY(launch_interior_targets(m->sorted_l.as<int>(), m->sorted_s.as<int>(), m->entry_off.as<int>(), np,
                                     m->has_xshift ? m->xshift.as<double>() : nullptr, m->owner.as<int>(), m->n,
                                     m->qin.as<int>(), ctx->counts.as<int>(), s));
-    HIP_TRY(launch_check_count(ctx->counts.as<int>(), n_int, ctx->err.as<int>(), 4, s));
+    HIP_TRY(launch_check_count(ctx->counts.as<int>(), m->n > 0 ? nblk : 0, n_int, ctx->err.as<int>(), 4, s));
     m->qin_valid = true;
     return IBTK_LE_OK;
 }

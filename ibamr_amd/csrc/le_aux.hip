@@ -1042,14 +1042,25 @@ __global__ __launch_bounds__(BLOCK) void k_interior_targets(const int* sorted_l,
                                                             const int* entry_off, int npatch, const double* xshift,
                                                             const int* owner, int n, int* qin, int* found) {
     const int e = blockIdx.x * BLOCK + threadIdx.x;
-    if (e >= n) return;
-    const int l = sorted_l[e], s = sorted_s[e];
-    bool keep = owner[s] == patch_of_entry(entry_off, npatch, l);
-    if (xshift) keep = keep && xshift[3 * (int64_t)l] == 0.0 && xshift[3 * (int64_t)l + 1] == 0.0 &&
-                       xshift[3 * (int64_t)l + 2] == 0.0;
-    qin[e] = keep ? s : -1;
+    bool keep = false;
+    int s = -1;
+    if (e < n) {
+        const int l = sorted_l[e];
+        s = sorted_s[e];
+        keep = owner[s] == patch_of_entry(entry_off, npatch, l);
+        if (xshift) keep = keep && xshift[3 * (int64_t)l] == 0.0 && xshift[3 * (int64_t)l + 1] == 0.0 &&
+                           xshift[3 * (int64_t)l + 2] == 0.0;
+        qin[e] = keep ? s : -1;
+    }
+    // the block's count into found[blockIdx.x] (one atomic per wave into LDS, no
+    // global atomics on one address: 2.1 ms of contention on cfg5's 1.3e7 entries)
+    __shared__ int cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
     const unsigned long long b = __ballot(keep);
-    if (b && (int)threadIdx.x % 64 == __ffsll(b) - 1) atomicAdd(found, __popcll(b));
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(&cnt, __popcll(b));
+    __syncthreads();
+    if (threadIdx.x == 0) found[blockIdx.x] = cnt;
 }
 hipError_t launch_interior_targets(const int* sorted_l, const int* sorted_s, const int* entry_off, int npatch,
                                    const double* xshift, const int* owner, int n, int* qin, int* found,
@@ -1111,11 +1122,18 @@ hipError_t launch_mig_unpack(const double* rows, int D, const int* order, const 
     return hipGetLastError();
 }
 
-__global__ void k_check_count(const int* count, int expect, int* err, int bit) {
-    if (threadIdx.x == 0 && *count != expect) atomicOr(err, bit);
+__global__ __launch_bounds__(BLOCK) void k_check_count(const int* count, int ncount, int expect, int* err, int bit) {
+    __shared__ long long tot;
+    if (threadIdx.x == 0) tot = 0;
+    __syncthreads();
+    long long mine = 0;
+    for (int i = threadIdx.x; i < ncount; i += BLOCK) mine += count[i];
+    atomicAdd((unsigned long long*)&tot, (unsigned long long)mine);
+    __syncthreads();
+    if (threadIdx.x == 0 && tot != expect) atomicOr(err, bit);
 }
-hipError_t launch_check_count(const int* count, int expect, int* err, int bit, hipStream_t s) {
-    hipLaunchKernelGGL(k_check_count, dim3(1), dim3(64), 0, s, count, expect, err, bit);
+hipError_t launch_check_count(const int* count, int ncount, int expect, int* err, int bit, hipStream_t s) {
+    hipLaunchKernelGGL(k_check_count, dim3(1), dim3(BLOCK), 0, s, count, ncount, expect, err, bit);
     return hipGetLastError();
 }
 }  // namespace ibtk_le

@@ -304,14 +304,14 @@ hipError_t launch_level_node_keys(const LevelNum& L, const int* tab, const doubl
 // A level's interp restricted to its interior lists (ibtk_le_level_select_interior):
 // owner[s] = max patch whose interior list names marker s (owner pre-filled with -1);
 // then per sorted entry e of the binned lists: qin[e] = s if owner[s] is the entry's
-// patch and the entry is unshifted, else -1; *found counts the kept entries.
+// patch and the entry is unshifted, else -1; found[block] counts the block's kept entries.
 hipError_t launch_interior_owner(const int* int_off, int npatch, const int* int_idx, int n_int, int* owner,
                                  hipStream_t s);
 hipError_t launch_interior_targets(const int* sorted_l, const int* sorted_s, const int* entry_off, int npatch,
                                    const double* xshift, const int* owner, int n, int* qin, int* found,
                                    hipStream_t s);
-// *count != expect: atomicOr(err, bit)
-hipError_t launch_check_count(const int* count, int expect, int* err, int bit, hipStream_t s);
+// sum(count[0:ncount]) != expect: atomicOr(err, bit)
+hipError_t launch_check_count(const int* count, int ncount, int expect, int* err, int bit, hipStream_t s);
 // out[i * depth + k] = in[order[i] * depth + k]
 hipError_t launch_rows_gather(const int* order, int n, const double* in, int depth, double* out, hipStream_t s);
 // flag[i] = entry i of the (lag, ckey)-sorted list is the first of its lag run and not local

@@ -49,13 +49,6 @@ constexpr int SW = 64;  // one wavefront per work item
 #ifndef IBTK_LE_DIAG_SNOLOAD
 #define IBTK_LE_DIAG_SNOLOAD 0
 #endif
-#ifndef IBTK_LE_EXP_NT  // experiment: nontemporal plane streams (1 interp loads, 2 spread loads, 4 spread stores)
-#define IBTK_LE_EXP_NT 0
-#endif
-#ifndef IBTK_LE_SPREAD_PF  // experiment: u_old planes 1 or 2 anchors ahead
-#define IBTK_LE_SPREAD_PF 2
-#endif
-constexpr int SPF = IBTK_LE_SPREAD_PF;
 #ifndef IBTK_LE_DIAG_SNOPROC  // ... without the candidates' weights and adds (the streams alone)
 #define IBTK_LE_DIAG_SNOPROC 0
 #endif
@@ -478,7 +471,7 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
         const int zc = min(max(z, cd.lo[2]), cd.hi[2]);
         const double* pb = cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2;
 #pragma unroll
-        for (int k = 0; k < NPT; ++k) v[k] = (IBTK_LE_EXP_NT & 1) ? __builtin_nontemporal_load(pb + poff[k]) : pb[poff[k]];
+        for (int k = 0; k < NPT; ++k) v[k] = pb[poff[k]];
     };
     auto plane_put = [&](int zr, const double* v) {  // registers -> ring slot, 0 outside the array
         const int z = zorg + min(zr, plast);
@@ -928,8 +921,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     auto plane_load = [&](int z, double* v) {
         const double* pb = plane_ptr(z);
 #pragma unroll
-        for (int k = 0; k < NPL; ++k)
-            v[k] = IBTK_LE_DIAG_SNOLOAD ? 0.0 : (IBTK_LE_EXP_NT & 2) ? __builtin_nontemporal_load(pb + loff[k]) : pb[loff[k]];
+        for (int k = 0; k < NPL; ++k) v[k] = IBTK_LE_DIAG_SNOLOAD ? 0.0 : pb[loff[k]];
     };
     auto plane_put = [&](int z, const double* v) {
         double* sl = ring + sslot<K>(z) * S::PV;
@@ -946,8 +938,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
 #pragma unroll
         for (int k = 0; k < NPL; ++k) {  // not-owned points store to the sink: no branch per store
             double* dst = ((okxy >> k) & 1u) && !IBTK_LE_DIAG_SNOSTORE ? pb + loff[k] : p.sink + lane;
-            if (IBTK_LE_EXP_NT & 4) __builtin_nontemporal_store(v[k], dst);
-            else *dst = v[k];
+            *dst = v[k];
         }
     };
 
@@ -959,13 +950,12 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     clk.start(p.stamps != nullptr);
     // prologue: planes afirst+LO .. afirst+HI-1 into the ring; planes afirst+HI and
     // afirst+HI+1, the ranges and chunk 1 of afirst into registers
-    double pvA[NPL], pvB[NPL];
+    double pv[NPL];
     for (int z = afirst + LO; z < afirst + HI; ++z) {
-        plane_load(z, pvA);
-        plane_put(z, pvA);
+        plane_load(z, pv);
+        plane_put(z, pv);
     }
-    plane_load(afirst + HI, pvA);
-    if (SPF == 2) plane_load(afirst + HI + 1, pvB);
+    plane_load(afirst + HI, pv);
     int rowv[3];
     rows_load(afirst, rowv);
     Ranges rg;  // ranges of the anchor whose chunk 1 is prefetched (wave-uniform)
@@ -980,11 +970,10 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     int n1 = min(tA, SW);  // lanes of a's chunk 1
     if (afirst + 1 <= alast) rows_load(afirst + 1, rowv);
     clk.lap(0);
-    // One anchor step.  The u_old planes stream two anchors ahead through two
-    // register buffers (pv: plane a+HI in, plane a+HI+2 out): the loop is unrolled
-    // by two so each buffer stays in registers of its own, and twice the plane
-    // loads are in flight per wave (the spread's streams were latency-bound at one).
-    auto anchor_step = [&](int a, double* pv) {
+    // One anchor step: plane a+HI from registers into the ring, plane a+HI+1 into
+    // registers.  (Two anchors ahead through two register buffers measured the same,
+    // 16.1 vs 16.3 ms on cfg4, profiles/r03h: the streams are not what waits.)
+    auto anchor_step = [&](int a) {
         if (a >= afirst + 2) plane_writeback(a - 2 + LO);  // no anchor left reaches it
         plane_put(a + HI, pv);                               // into its slot
         const Cand cur = nxt;
@@ -1005,8 +994,8 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
             etail = range_pos(rg, max(tA - SW + lane, 0));
             n1 = r_a + min(SW - r_a, tA);
             r_prev = r_a;
+            plane_load(a + HI + 1, pv);
             if (a + 2 <= alast) rows_load(a + 2, rowv);
-            if (a + SPF <= alast) plane_load(a + HI + SPF, pv);
         }
         if (cur_n > 0) process(a, cur_r, cur_n, cur);
         if (nmid > 0) {  // dense planes: the full middle chunks (ranges of a rebuilt)
@@ -1031,14 +1020,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         }
         clk.lap(4);
     };
-    if constexpr (SPF == 1) {
-        for (int a = afirst; a <= alast; ++a) anchor_step(a, pvA);
-    } else {
-        for (int a = afirst; a <= alast; a += 2) {
-            anchor_step(a, pvA);
-            if (a + 1 <= alast) anchor_step(a + 1, pvB);
-        }
-    }
+    for (int a = afirst; a <= alast; ++a) anchor_step(a);
     plane_writeback(alast - 1 + LO);
     plane_writeback(alast + LO);
     clk.lap(5);
