@@ -84,6 +84,7 @@ _SIGS = [
     ("ibtk_le_ctx_set_plane_window", c_int, [c_void_p, c_int, c_int, c_int]),
     ("ibtk_le_ctx_last_kernel_ms", c_double, [c_void_p]),
     ("ibtk_le_ctx_count_adds", c_int, [c_void_p, c_int]),
+    ("ibtk_le_wrap_positions", c_int, [c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("ibtk_le_ctx_last_adds", c_int, [c_void_p, ctypes.POINTER(ctypes.c_ulonglong)]),
     ("ibtk_le_markers_create", c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
     ("ibtk_le_markers_destroy", c_int, [c_void_p]),

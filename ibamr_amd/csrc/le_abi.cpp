@@ -1959,6 +1959,10 @@ extern "C" int ibtk_le_level_node_distribution(ibtk_le_ctx ctx, int npatch, cons
     if ((rc = compact_by_flags(ctx, 1, n, flag, perm, nullptr, nullptr, order_dev, nullptr, nullptr, n, &cnt)))
         return rc;
     const int nl = cnt;
+    if (ghost == 0) {  // no ghost cells: every marker outside the local patches is nobody's node here
+        *n_local = nl;
+        return IBTK_LE_OK;
+    }
     // nonlocal nodes: the markers by (Lagrangian index, first sighting), the head of
     // every index run whose run holds no local node, then by first sighting
     unsigned* k0 = ctx->lst_key.as<unsigned>();
@@ -1979,6 +1983,28 @@ extern "C" int ibtk_le_level_node_distribution(ibtk_le_ctx ctx, int npatch, cons
     HIP_TRY(hipStreamSynchronize(s));
     *n_local = nl;
     *n_nonlocal = nn;
+    return IBTK_LE_OK;
+}
+
+// beginDataRedistribution's wrap of the positions into the periodic domain
+// (LDataManager.cpp:1385-1399), in place: per periodic dim, += / -= the domain length
+// while outside [x_lower, x_upper), then clamped into [x_lower, x_upper - eps].
+extern "C" int ibtk_le_wrap_positions(ibtk_le_ctx ctx, int ndim, long long n, double* X_dev, const double* x_lower,
+                                      const double* x_upper, const int* periodic) {
+    if (!ctx || !x_lower || !x_upper) return fail(IBTK_LE_ERR_ARG, "null argument");
+    if (ndim < 1 || ndim > 3 || n < 0) return fail(IBTK_LE_ERR_ARG, "bad sizes");
+    if (n == 0) return IBTK_LE_OK;
+    if (!X_dev) return fail(IBTK_LE_ERR_ARG, "null X");
+    WrapBox w;
+    for (int d = 0; d < 3; ++d) {
+        w.lo[d] = d < ndim ? x_lower[d] : 0.0;
+        w.hi[d] = d < ndim ? x_upper[d] : 1.0;
+        w.per[d] = d < ndim ? (periodic ? periodic[d] != 0 : 1) : 0;
+        if (d < ndim && !(w.hi[d] > w.lo[d])) return fail(IBTK_LE_ERR_ARG, "empty domain");
+    }
+    w.ndim = ndim;
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    HIP_TRY(launch_wrap_positions(w, n, X_dev, ctx->stream));
     return IBTK_LE_OK;
 }
 

@@ -1122,6 +1122,26 @@ hipError_t launch_mig_unpack(const double* rows, int D, const int* order, const 
     return hipGetLastError();
 }
 
+__global__ __launch_bounds__(BLOCK) void k_wrap_positions(WrapBox w, long long n, double* X) {
+    const long long t = (long long)blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= n * w.ndim) return;
+    const int d = (int)(t % w.ndim);
+    double x = X[t];
+    if (w.per[d]) {
+        const double L = w.hi[d] - w.lo[d];
+        while (x < w.lo[d]) x += L;
+        while (x >= w.hi[d]) x -= L;
+    }
+    x = fmax(x, w.lo[d]);
+    x = fmin(x, w.hi[d] - 2.220446049250313e-16);  // std::numeric_limits<double>::epsilon()
+    X[t] = x;
+}
+hipError_t launch_wrap_positions(const WrapBox& w, long long n, double* X, hipStream_t s) {
+    const long long tot = n * w.ndim;
+    hipLaunchKernelGGL(k_wrap_positions, dim3((unsigned)((tot + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, w, n, X);
+    return hipGetLastError();
+}
+
 __global__ __launch_bounds__(BLOCK) void k_check_count(const int* count, int ncount, int expect, int* err, int bit) {
     __shared__ long long tot;
     if (threadIdx.x == 0) tot = 0;

@@ -310,6 +310,12 @@ hipError_t launch_interior_owner(const int* int_off, int npatch, const int* int_
 hipError_t launch_interior_targets(const int* sorted_l, const int* sorted_s, const int* entry_off, int npatch,
                                    const double* xshift, const int* owner, int n, int* qin, int* found,
                                    hipStream_t s);
+struct WrapBox {
+    double lo[3], hi[3];
+    int per[3];
+    int ndim;
+};
+hipError_t launch_wrap_positions(const WrapBox& w, long long n, double* X, hipStream_t s);
 // sum(count[0:ncount]) != expect: atomicOr(err, bit)
 hipError_t launch_check_count(const int* count, int ncount, int expect, int* err, int bit, hipStream_t s);
 // out[i * depth + k] = in[order[i] * depth + k]

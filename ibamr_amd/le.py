@@ -705,6 +705,20 @@ def level_node_distribution(ctx: Context, geoms: Sequence[Geometry], dom_lo, dom
     return order[:nl.value + ng.value].contiguous(), nl.value, ng.value
 
 
+def wrap_positions(ctx: Context, X: torch.Tensor, x_lower, x_upper, periodic=None):
+    """beginDataRedistribution's periodic wrap of X (n, ndim) in place
+    (ibtk_le_wrap_positions, LDataManager.cpp:1385-1399)."""
+    if X.dtype != torch.float64 or not X.is_cuda or not X.is_contiguous() or X.dim() != 2:
+        raise ValueError("X: contiguous (n, ndim) float64 device tensor")
+    nd = X.shape[1]
+    lo = (ctypes.c_double * nd)(*[float(v) for v in x_lower])
+    hi = (ctypes.c_double * nd)(*[float(v) for v in x_upper])
+    pa = _periodic_arg(periodic, nd)
+    check(ctx.lib.ibtk_le_wrap_positions(ctx.h, nd, X.shape[0], _ptr(X), ctypes.cast(lo, ctypes.c_void_p),
+                                         ctypes.cast(hi, ctypes.c_void_p), pa[0] if pa else None))
+    return X
+
+
 def ldata_reorder(ctx: Context, order: torch.Tensor, *arrays: torch.Tensor):
     """endDataRedistribution's reorder of LData arrays (ibtk_le_ldata_reorder): for each
     (M, ...) float64 device array, a new array whose row i is the old row order[i]."""

@@ -521,7 +521,8 @@ class NodeDistribution:
 
 
 def redistribute(slab: Slab, ctx, X: torch.Tensor, fields: Sequence[torch.Tensor], lag: torch.Tensor,
-                 group=None, numbering: Optional[Callable] = None, reorder: Optional[Callable] = None):
+                 group=None, numbering: Optional[Callable] = None, reorder: Optional[Callable] = None,
+                 wrap: Optional[Callable] = None):
     """Number a rank's markers the way LDataManager does at redistribution, across ranks.
 
     After ``migrate``/``update_and_migrate`` every marker sits on the rank whose slab
@@ -543,9 +544,10 @@ def redistribute(slab: Slab, ctx, X: torch.Tensor, fields: Sequence[torch.Tensor
       local nodes in the ghost-box walk order; ``ghost_X`` holds the owners'
       positions (in [0, L)), as the reference's ghosted LData does.
 
-    ``numbering(X, lag, ghost) -> (order, n_local, n_nonlocal)`` and
-    ``reorder(order, *arrays) -> [arrays]`` are injectable so the rank logic runs on
-    CPU with gloo (tests); the product default is the HIP library."""
+    ``numbering(X, lag, ghost) -> (order, n_local, n_nonlocal)``,
+    ``reorder(order, *arrays) -> [arrays]`` and ``wrap(X) -> X`` are injectable so the
+    rank logic runs on CPU with gloo (tests); the product default is the HIP library
+    (ibtk_le_level_node_distribution, ibtk_le_ldata_reorder, ibtk_le_wrap_positions)."""
     import torch.distributed as dist
     from . import le
     if lag.dtype != torch.int32 or lag.numel() != X.shape[0]:
@@ -559,12 +561,11 @@ def redistribute(slab: Slab, ctx, X: torch.Tensor, fields: Sequence[torch.Tensor
     if reorder is None:
         def reorder(order, *arrays):
             return le.ldata_reorder(ctx, order, *arrays)
-    # beginDataRedistribution's wrap into the periodic domain (LDataManager.cpp:1385-1399):
-    # one period at most per step, then clamped below the upper face
-    L = torch.tensor(list(slab.L), dtype=X.dtype, device=X.device)
-    X = torch.where(X < 0, X + L, X)
-    X = torch.where(X >= L, X - L, X)
-    X = torch.minimum(torch.clamp(X, min=0.0), L - torch.finfo(X.dtype).eps).contiguous()
+    # beginDataRedistribution's wrap into the periodic domain (LDataManager.cpp:1385-1399)
+    if wrap is None:
+        def wrap(Xw):
+            return le.wrap_positions(ctx, Xw, [0.0, 0.0, 0.0], list(slab.L))
+    X = wrap(X.contiguous().clone())
     order, nl, nn = numbering(X, lag, 0)
     if nn:
         raise RuntimeError(f"rank {slab.rank}: {nn} markers outside the slab; migrate before redistribute")

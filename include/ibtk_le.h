@@ -346,6 +346,12 @@ int ibtk_le_node_distribution(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, c
 int ibtk_le_level_node_distribution(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms, const int* dom_lo,
                                     const int* dom_hi, const int* periodic, const double* X_dev, const int* lag_dev,
                                     int n_markers, int ghost, int* order_dev, int* n_local, int* n_nonlocal);
+/* beginDataRedistribution's wrap of marker positions into the periodic domain
+ * (LDataManager.cpp:1385-1399), in place on n (ndim)-records: per periodic dim
+ * (periodic NULL: all) add / subtract the domain length while outside
+ * [x_lower, x_upper), then clamp every dim into [x_lower, x_upper - DBL_EPSILON]. */
+int ibtk_le_wrap_positions(ibtk_le_ctx ctx, int ndim, long long n, double* X_dev, const double* x_lower,
+                           const double* x_upper, const int* periodic);
 /* endDataRedistribution's reorder of an LData into the new numbering (the VecScatter of
  * LDataManager.cpp:1823-1917): out[i][k] = in[order_dev[i]][k], depth doubles per
  * node, device arrays, in and out distinct. */

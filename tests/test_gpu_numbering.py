@@ -117,3 +117,32 @@ def test_level_node_distribution_matches_oracle(le, ctx, case):
     F = torch.from_numpy(rng.standard_normal((M, 3))).cuda()
     Xn, Fn = le.ldata_reorder(ctx, order, Xd, F)
     assert torch.equal(Xn, Xd[order.long()]) and torch.equal(Fn, F[order.long()])
+
+
+def test_wrap_positions_matches_reference_loops(le, ctx):
+    """beginDataRedistribution's wrap (LDataManager.cpp:1385-1399) on the device, bit for
+    bit against the reference's loops restated in Python: while X < lower add the length,
+    while X >= upper subtract it (periodic dims), then clamp into [lower, upper - eps]."""
+    rng = np.random.default_rng(5)
+    lo, hi = [0.0, -0.5, 0.25], [1.0, 0.75, 2.0]
+    X = rng.uniform(-3.0, 4.0, (5000, 3))
+    X[:10] = [[1.0, 0.75, 2.0]] * 10             # exactly on the upper faces
+    X[10:20] = [[-1e-17, -0.5, 0.25]] * 10        # just below / on the lower faces
+    periodic = [1, 0, 1]
+    exp = X.copy()
+    eps = np.finfo(np.float64).eps
+    for i in range(X.shape[0]):
+        for d in range(3):
+            x = exp[i, d]
+            if periodic[d]:
+                Ld = hi[d] - lo[d]
+                while x < lo[d]:
+                    x += Ld
+                while x >= hi[d]:
+                    x -= Ld
+            x = max(x, lo[d])
+            x = min(x, hi[d] - eps)
+            exp[i, d] = x
+    Xd = torch.from_numpy(X.copy()).cuda()
+    le.wrap_positions(ctx, Xd, lo, hi, periodic=periodic)
+    assert np.array_equal(Xd.cpu().numpy(), exp)

@@ -328,7 +328,13 @@ def _redist_worker(rank, world, port, q):
         def reorder(order, *arrays):
             return [a[order.long()] for a in arrays]
 
-        d = redistribute(slab, None, Xm, [Fm], lm, numbering=numbering, reorder=reorder)
+        def wrap(Xw):  # beginDataRedistribution's wrap (LDataManager.cpp:1385-1399), one period
+            L = torch.ones(3, dtype=Xw.dtype)
+            Xw = torch.where(Xw < 0, Xw + L, Xw)
+            Xw = torch.where(Xw >= L, Xw - L, Xw)
+            return torch.minimum(torch.clamp(Xw, min=0.0), L - torch.finfo(Xw.dtype).eps)
+
+        d = redistribute(slab, None, Xm, [Fm], lm, numbering=numbering, reorder=reorder, wrap=wrap)
         ok = torch.equal(d.X, Xm[d.order.long()]) and torch.equal(d.fields[0], Fm[d.order.long()])
         ok = ok and torch.equal(d.lag, lm[d.order.long()])
         q.put((rank, "ok", ok, dict(lag=d.lag.numpy(), offset=d.offset, num_nodes=d.num_nodes,
