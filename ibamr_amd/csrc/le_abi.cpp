@@ -272,6 +272,15 @@ static int check_geom(const ibtk_le_patch_geom* g) {
             return fail(IBTK_LE_ERR_ARG, "array pitch {%d, %d} below the ghosted extent {%lld, %lld} (+1 face)",
                         g->pitch[0], g->pitch[1], n0, n1);
     }
+    if (g->ndim == 3) {
+        // the 3-D sweeps address one plane of an array with 32-bit byte offsets
+        const long long n0 = (long long)g->iupper[0] - g->ilower[0] + 2 + 2LL * g->gcw[0];
+        const long long n1 = (long long)g->iupper[1] - g->ilower[1] + 2 + 2LL * g->gcw[1];
+        const long long plane = (g->pitch[0] ? g->pitch[0] : n0) * (g->pitch[1] ? g->pitch[1] : n1);
+        if (8 * plane >= (1LL << 31))
+            return fail(IBTK_LE_ERR_ARG, "an array plane of %lld points exceeds 2^28 (the sweeps' 32-bit offsets)",
+                        plane);
+    }
     return IBTK_LE_OK;
 }
 

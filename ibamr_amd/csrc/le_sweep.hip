@@ -68,6 +68,29 @@ struct D3 {
 };
 __device__ __forceinline__ D3 ld3(const double* q) { return *reinterpret_cast<const D3*>(q); }
 
+// One plane of an Eulerian array as a raw buffer resource (base in SGPRs, a
+// 32-bit byte offset per lane): the sweeps' plane loads and stores take one
+// VGPR offset and no 64-bit address arithmetic.  Accesses at offsets >= `bytes`
+// are dropped by the hardware's range check (loads return 0): the interp stages
+// the points outside the array as 0 that way, the spread drops its stores of
+// points it does not own.  `base` must be wave-uniform.
+constexpr unsigned OFF_NONE = 0x80000000u;  // an offset past every plane (bytes < 2^31)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const void* base, unsigned bytes) {
+    const unsigned long long b = reinterpret_cast<unsigned long long>(base);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+    void* bp = reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo);
+    // dword 3 of a gfx9 buffer resource: 32-bit data format, no swizzle
+    return __builtin_amdgcn_make_buffer_rsrc(bp, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, unsigned off, double v) {
+    using V2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, v), r, (int)off, 0, 0);
+}
+
 // ---------------------------------------------------------------------------
 // binning
 // ---------------------------------------------------------------------------
@@ -452,35 +475,34 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     const int nlast = p.nsorted - 1;
     // the lane's staged points q = lane + 64 k: array offsets (clamped) and
     // in-array bits (x, y)
-    int poff[NPT];
-    unsigned okm = 0;
+    // the lane's staged points q = lane + 64 k: byte offsets in a plane through a
+    // buffer resource (plane_rsrc); a point outside the array has OFF_NONE, and a
+    // plane outside it an empty resource, so their loads return the 0 the
+    // clipped stencil points are staged as (no select per point)
+    unsigned poff[NPT];
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
         const int q = min(lane + SW * k, S::PV - 1);
-        const int gxu = gx0 + q % RX, gyu = gy0 + q / RX;
-        const int gx = min(max(gxu, cd.lo[0]), cd.hi[0]), gy = min(max(gyu, cd.lo[1]), cd.hi[1]);
-        poff[k] = (gx - cd.lo[0]) + (gy - cd.lo[1]) * (int)cd.s1;
-        if (gx == gxu && gy == gyu) okm |= 1u << k;
+        const int gx = gx0 + q % RX, gy = gy0 + q / RX;
+        const bool in = gx >= cd.lo[0] && gx <= cd.hi[0] && gy >= cd.lo[1] && gy <= cd.hi[1];
+        poff[k] = in ? 8u * (unsigned)((gx - cd.lo[0]) + (gy - cd.lo[1]) * (int)cd.s1) : OFF_NONE;
     }
     const int plast = a1 - 1 + HI;  // last plane the item reads
-    // relative plane zr -> registers: unconditional loads at clamped addresses
-    // (points outside the array are zeroed when the plane is put; a select
-    // right behind a load would become a branch around it, CodeGenPrepare)
+    const unsigned plane_bytes = (unsigned)(8 * cd.s2);
+    // relative plane zr -> registers
     auto plane_load = [&](int zr, double* v) {
         const int z = zorg + min(zr, plast);
-        const int zc = min(max(z, cd.lo[2]), cd.hi[2]);
-        const double* pb = cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2;
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) v[k] = pb[poff[k]];
-    };
-    auto plane_put = [&](int zr, const double* v) {  // registers -> ring slot, 0 outside the array
-        const int z = zorg + min(zr, plast);
         const bool zin = z >= cd.lo[2] && z <= cd.hi[2];
+        const int zc = min(max(z, cd.lo[2]), cd.hi[2]);
+        const auto pb = plane_rsrc(cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2, zin ? plane_bytes : 0u);
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) v[k] = buf_ld(pb, poff[k]);
+    };
+    auto plane_put = [&](int zr, const double* v) {  // registers -> ring slot
         double* sl = ring + islot<K>(zr) * S::PVP;
 #pragma unroll
         for (int k = 0; k < NPT; ++k)
-            if (S::PV % SW == 0 || k < NPT - 1 || lane + SW * k < S::PV)
-                sl[lane + SW * k] = (zin && ((okm >> k) & 1u)) ? v[k] : 0.0;
+            if (S::PV % SW == 0 || k < NPT - 1 || lane + SW * k < S::PV) sl[lane + SW * k] = v[k];
     };
     struct Mk {
         int s;
@@ -877,19 +899,20 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // the lane's points of a plane: slot index lane + 64 k (tile-major, so the
     // staging stores and writeback loads are contiguous in LDS), their array
     // offsets (clamped into the array) and owned bits
-    int loff[NPL];
-    unsigned okxy = 0;
+    // (byte offsets in a plane through a buffer resource, plane_rsrc; a point the
+    // item does not own has OFF_NONE: its load returns 0 and its store is dropped)
+    unsigned loff[NPL];
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
         int xl, yl;
         ring_xy(lane + k * SW, xl, yl);
-        if (xl >= xlo && xl <= xhi && yl >= ylo && yl <= yhi) okxy |= 1u << k;
-        const int x = min(max(X0 + xl, cd.lo[0]), cd.hi[0]), y = min(max(Y0 + yl, cd.lo[1]), cd.hi[1]);
-        loff[k] = (x - cd.lo[0]) + (y - cd.lo[1]) * (int)cd.s1;
+        const bool own = xl >= xlo && xl <= xhi && yl >= ylo && yl <= yhi;
+        loff[k] = own ? 8u * (unsigned)((X0 + xl - cd.lo[0]) + (Y0 + yl - cd.lo[1]) * (int)cd.s1) : OFF_NONE;
     }
+    const unsigned plane_bytes = (unsigned)(8 * cd.s2);
     auto plane_ptr = [&](int z) {  // relative plane z, clamped into the array
         const int zc = min(max(zorg + z, cd.lo[2]), cd.hi[2]);
-        return cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2;
+        return plane_rsrc(cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2, plane_bytes);
     };
     // bucket starts of anchor plane a: rows cy-1, cy, cy+1 (28 entries: bands of
     // columns cx-1 .. cx+1), one entry per lane
@@ -917,11 +940,14 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         spread_tiled<K>(p, cd, ring, mine, lane < n, lane < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi,
                         inv_h3, inv_d, clk);
     };
-    // plane z -> registers (the lane's NPL points); registers -> ring slot
+    // plane z -> registers (the lane's NPL points); registers -> ring slot.  A
+    // plane the item does not own receives no adds and is not written back: its
+    // slot's contents do not matter, so it is not read.
     auto plane_load = [&](int z, double* v) {
-        const double* pb = plane_ptr(z);
+        if (z < plo || z > phi) return;
+        const auto pb = plane_ptr(z);
 #pragma unroll
-        for (int k = 0; k < NPL; ++k) v[k] = IBTK_LE_DIAG_SNOLOAD ? 0.0 : pb[loff[k]];
+        for (int k = 0; k < NPL; ++k) v[k] = IBTK_LE_DIAG_SNOLOAD ? 0.0 : buf_ld(pb, loff[k]);
     };
     auto plane_put = [&](int z, const double* v) {
         double* sl = ring + sslot<K>(z) * S::PV;
@@ -931,15 +957,13 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     auto plane_writeback = [&](int z) {  // owned points of plane z, ring -> array
         if (z < plo || z > phi) return;
         const double* sl = ring + sslot<K>(z) * S::PV;
-        double* pb = const_cast<double*>(plane_ptr(z));
+        const auto pb = plane_ptr(z);
         double v[NPL];
 #pragma unroll
         for (int k = 0; k < NPL; ++k) v[k] = sl[lane + k * SW];
+        if (IBTK_LE_DIAG_SNOSTORE) return;
 #pragma unroll
-        for (int k = 0; k < NPL; ++k) {  // not-owned points store to the sink: no branch per store
-            double* dst = ((okxy >> k) & 1u) && !IBTK_LE_DIAG_SNOSTORE ? pb + loff[k] : p.sink + lane;
-            *dst = v[k];
-        }
+        for (int k = 0; k < NPL; ++k) buf_st(pb, loff[k], v[k]);  // not-owned points: dropped
     };
 
     // The candidates stream through 64-lane chunks across anchor planes.  Anchor
@@ -950,7 +974,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     clk.start(p.stamps != nullptr);
     // prologue: planes afirst+LO .. afirst+HI-1 into the ring; planes afirst+HI and
     // afirst+HI+1, the ranges and chunk 1 of afirst into registers
-    double pv[NPL];
+    double pv[NPL] = {};
     for (int z = afirst + LO; z < afirst + HI; ++z) {
         plane_load(z, pv);
         plane_put(z, pv);
