@@ -302,6 +302,13 @@ def run_level(args, cfg, kernel, dev):
 
     dt_move = 0.05 * dx  # |U| <= ~1: markers move <= 1/20 cell per step
 
+    def zero_spread(f):
+        if args.unfused_zero:  # the two launches the fused one replaces (A/B)
+            lvl_s.zero("side", f)
+            lvl_s.spread("side", f, F, X)
+        else:
+            lvl_s.zero_spread("side", f, F, X)
+
     def step(record):
         if args.move:
             return step_move(record)
@@ -317,10 +324,8 @@ def run_level(args, cfg, kernel, dev):
         lvl_s.interp("side", u, U, X)
         if record:
             E[3].record()
-        lvl_s.zero("side", f)
-        if record:
-            E[4].record()
-        lvl_s.spread("side", f, F, X)
+            E[4].record()  # zero f: fused into the spread (ibtk_le_level_zero_spread)
+        zero_spread(f)
         if record:
             E[5].record()
 
@@ -345,10 +350,8 @@ def run_level(args, cfg, kernel, dev):
         lvl_s.select_interior(M, ii2, oi2)
         if record:
             E[3].record()
-        lvl_s.zero("side", f)
-        if record:
             E[4].record()
-        lvl_s.spread("side", f, F, X)
+        zero_spread(f)
         if record:
             E[5].record()
 
@@ -379,13 +382,13 @@ def run_level(args, cfg, kernel, dev):
         lvl_s.interp("side", u, U, X)
         ctx.synchronize()
         kt["interp"].append(ctx.last_kernel_ms())
-        lvl_s.spread("side", f, F, X)
+        zero_spread(f)
         ctx.synchronize()
         kt["spread"].append(ctx.last_kernel_ms())
     ctx.enable_timing(False)
     mean = lambda v: sum(v) / len(v)
     k_i, k_s = mean(kt["interp"]), mean(kt["spread"])
-    lds = lds_atomic(ctx, lambda: lvl_s.spread("side", f, F, X), k_s)
+    lds = lds_atomic(ctx, lambda: zero_spread(f), k_s)
     # per entry X and Q/F (24 + 24 B), per touched point 8 B (interp) or 16 B (spread);
     # the touched points are those of the ghost-box lists (an upper bound for interp's)
     B_i = M * 48 + 8 * sum(S_touched)
@@ -400,10 +403,10 @@ def run_level(args, cfg, kernel, dev):
                    "parallelism": "one GPU", "patches": [P, P, P], "patch_cells": [n, n, n], "ghost": g,
                    "move": args.move,
                    "step": ("level ghost fill + interp(3 comps) + position update + per-patch lists rebuilt "
-                            "(bench.level_lists, torch ops) + bin(ghost-box lists, interior selected) + zero f + "
-                            "spread(3 comps)" if args.move else
+                            "(bench.level_lists, torch ops) + bin(ghost-box lists, interior selected) + zero f and "
+                            "spread(3 comps) in one launch" if args.move else
                             "level ghost fill + bin(ghost-box lists; the interior lists select interp's entries) + "
-                            "interp(3 comps) + zero f + spread(3 comps); stationary markers, per-patch lists built once at setup "
+                            "interp(3 comps) + zero f and spread(3 comps) in one launch (ibtk_le_level_zero_spread); stationary markers, per-patch lists built once at setup "
                             "(LIndexSetData between regrids), one launch per sweep over the 512 patches")},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -423,6 +426,8 @@ def main():
     ap.add_argument("--config", default="cfg4", choices=sorted(CONFIGS))
     ap.add_argument("--kernel", default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--unfused-zero", action="store_true",
+                    help="cfg5: zero f and spread as two launches instead of ibtk_le_level_zero_spread (A/B)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-rebin", action="store_true", help="bin once outside the timed loop")
     ap.add_argument("--solo-slab", type=int, default=0, metavar="S",

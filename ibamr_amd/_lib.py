@@ -134,6 +134,8 @@ _SIGS = [
      [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(c_void_p), c_int, c_void_p, c_int, c_void_p]),
     ("ibtk_le_level_spread", c_int,
      [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(c_void_p), c_int, c_void_p, c_int, c_void_p]),
+    ("ibtk_le_level_zero_spread", c_int,
+     [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(c_void_p), c_int, c_void_p, c_int, c_void_p]),
     ("ibtk_le_level_select_interior", c_int, [c_void_p, c_void_p, c_int, ctypes.POINTER(c_int), c_void_p]),
     ("ibtk_le_level_fill_ghosts", c_int,
      [c_void_p, c_int, ctypes.POINTER(PatchGeom), c_int, ctypes.POINTER(c_void_p), c_int, c_void_p]),
@@ -176,7 +178,11 @@ def load():
         raise ImportError(f"libibtk_le.so not found at {LIB_PATH}; run __graft_entry__.build() "
                           f"or python -m ibamr_amd.build")
     lib = ctypes.CDLL(str(LIB_PATH))
+    # an IBTK_LE_LIB override (an older build for an A/B run) may lack newer symbols
+    lenient = "IBTK_LE_LIB" in os.environ
     for name, res, args in _SIGS:
+        if lenient and not hasattr(lib, name):
+            continue
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args

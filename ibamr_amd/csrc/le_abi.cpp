@@ -1218,17 +1218,19 @@ extern "C" int ibtk_le_level_select_interior(ibtk_le_ctx ctx, ibtk_le_markers m,
     return IBTK_LE_OK;
 }
 
-extern "C" int ibtk_le_level_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
-                                    double* const* q_dev, int q_depth, const double* Q_dev, int Q_depth,
-                                    const double* X_dev) {
+static int level_spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                             double* const* q_dev, int q_depth, const double* Q_dev, int Q_depth, const double* X_dev,
+                             bool zero_first) {
     Params p;
     std::memset(&p, 0, sizeof(p));
     int nc = 0;
     if (int rc = level_params(ctx, m, kernel, centering, axis, q_dev, q_depth, Q_depth, X_dev, false, p, nc))
         return rc;
-    if (m->n == 0) return IBTK_LE_OK;
+    if (m->n == 0)  // nothing to spread: LEInteractor.cpp:2747 (zero_first: the zeroing alone)
+        return zero_first ? ibtk_le_level_zero(ctx, m->npatch, m->geoms.data(), centering, q_dev, q_depth) : IBTK_LE_OK;
     if (!Q_dev) return fail(IBTK_LE_ERR_ARG, "null Q");
     p.Qin = Q_dev;
+    p.zero_first = zero_first ? 1 : 0;
     if (int rc = ctx->fbuf.ensure(sizeof(double) * (size_t)m->n * (size_t)nc)) return rc;
     p.sorted_F = ctx->fbuf.as<double>();
     const bool t = ctx->timing;
@@ -1241,6 +1243,22 @@ extern "C" int ibtk_le_level_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kern
     if (int rc = stamps_report(ctx, nst, p)) return rc;
     if (t) ctx->ev_valid = true;
     return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_level_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                                    double* const* q_dev, int q_depth, const double* Q_dev, int Q_depth,
+                                    const double* X_dev) {
+    return level_spread_impl(ctx, m, kernel, centering, axis, q_dev, q_depth, Q_dev, Q_depth, X_dev, false);
+}
+
+// LDataManager::spread's setToScalar(f, 0, interior_only = false) and its patch loop
+// of LEInteractor::spread (LDataManager.cpp:588-654) fused: the sweep's items start
+// their owned points from 0 instead of reading them, and the items no marker reaches
+// store zeros.  Bitwise ibtk_le_level_zero followed by ibtk_le_level_spread.
+extern "C" int ibtk_le_level_zero_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                                         double* const* q_dev, int q_depth, const double* Q_dev, int Q_depth,
+                                         const double* X_dev) {
+    return level_spread_impl(ctx, m, kernel, centering, axis, q_dev, q_depth, Q_dev, Q_depth, X_dev, true);
 }
 
 // Ghost fill of a level of equal patches tiling a box (periodic in the flagged

@@ -173,6 +173,7 @@ struct Params {
     const int* n_dev = nullptr;  // bin: the list's length on the device (entries beyond it binned outside)
     unsigned long long* stamps = nullptr;  // diagnostic phase clocks (nullptr: off)
     unsigned long long* nadd = nullptr;    // spread: [ds_add_f64 wave-instructions, lane adds] issued (nullptr: not counted)
+    int zero_first = 0;  // 3-D spread: the arrays start from 0 (every point, ghosts included), not their values
 };
 
 // Host-side launchers (le_kernels.hip).

@@ -41,17 +41,6 @@
 namespace ibtk_le {
 
 constexpr int SW = 64;  // one wavefront per work item
-// Diagnostic builds only (results change by design; tools/var_bench.sh): the spread
-// without its writeback stores / without reading u_old / ...
-#ifndef IBTK_LE_DIAG_SNOSTORE
-#define IBTK_LE_DIAG_SNOSTORE 0
-#endif
-#ifndef IBTK_LE_DIAG_SNOLOAD
-#define IBTK_LE_DIAG_SNOLOAD 0
-#endif
-#ifndef IBTK_LE_DIAG_SNOPROC  // ... without the candidates' weights and adds (the streams alone)
-#define IBTK_LE_DIAG_SNOPROC 0
-#endif
 
 // LDS read of one double that the compiler may not merge with its neighbour into a
 // ds_read2_b64 (half the rate of two ds_read_b64 on gfx950: interp sweep 10.7 ->
@@ -737,10 +726,14 @@ __device__ __forceinline__ void rot4(double* w, int r) {
 // except that a -0.0 it lands on becomes +0.0.  Within one instruction the
 // lanes that hit the same point add in lane order, so every point receives its
 // contributions in a fixed order (bit-stable).
-template <int K>
+// `before` runs on every lane after the weights are computed and before any add
+// (the anchor step's writeback stores go there: issued after the candidate loads
+// they would otherwise be counted ahead of, and while the previous adds drain).
+template <int K, bool CNT, typename Before>
 __device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
                                              bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
-                                             int yhi, int plo, int phi, double inv_h3, const double* inv_d, Clk& clk) {
+                                             int yhi, int plo, int phi, double inv_h3, const double* inv_d, Clk& clk,
+                                             unsigned long long* cnt, Before&& before) {
     using S = SSh<K>;
     constexpr int W = S::W, FAM = S::FAM, NSL = S::NSL;
     constexpr bool ROT = W >= 4;
@@ -760,6 +753,7 @@ __device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd
     constexpr int LO = S::LO, HI = S::HI;
     const bool bad = ox < LO - HI - 1 || ox + W - 1 > COLX - LO + HI || oy < LO - HI - 1 || oy + W - 1 > COLY - LO + HI;
     if (act && bad) atomicOr(p.err, 2);
+    before();
     if (!act || bad) return;  // idle lanes sit the adds out
     // owned and clipped-in ranges of the stencil indices
     const int x0 = max(st[0].ist, xlo - ox), x1 = min(st[0].isp, xhi - ox);
@@ -773,7 +767,7 @@ __device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd
     for (int i = 0; i < W; ++i) {
         wx[i] = (i >= x0 && i <= x1) ? st[0].w[i] * cdat.V : 0.0;  // V applied first (f.m4:1512-1513 up to rounding)
         wy[i] = (i >= y0 && i <= y1) ? st[1].w[i] : 0.0;
-        wz[i] = (i >= z0 && i <= z1) ? st[2].w[i] * inv_h3 : 0.0;
+        wz[i] = st[2].w[i] * inv_h3;  // planes outside [z0, z1] are skipped below
     }
     int rx = 0, ry = 0;
     if constexpr (ROT) {
@@ -806,17 +800,12 @@ __device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd
     for (int s1 = 0; s1 < W; ++s1)
 #pragma unroll
         for (int s0 = 0; s0 < W; ++s0) P[s1 * W + s0] = wx[s0] * wy[s1];
-    if (p.nadd) {  // counted launch (ibtk_le_ctx_count_adds): the adds issued below
-        unsigned long long ins = 0, lanes = 0;
+    if constexpr (CNT) {  // counted launch (ibtk_le_ctx_count_adds): the adds issued below
 #pragma unroll
         for (int i2 = 0; i2 < W; ++i2) {
             const unsigned long long bm = __ballot(i2 >= z0 && i2 <= z1);
-            ins += bm ? (unsigned long long)(W * W) : 0ull;
-            lanes += (unsigned long long)__popcll(bm) * (unsigned long long)(W * W);
-        }
-        if (lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) {
-            atomicAdd(p.nadd, ins);
-            atomicAdd(p.nadd + 1, lanes);
+            cnt[0] += bm ? (unsigned long long)(W * W) : 0ull;
+            cnt[1] += (unsigned long long)__popcll(bm) * (unsigned long long)(W * W);
         }
     }
     char* const rb = reinterpret_cast<char*>(ring);
@@ -856,7 +845,9 @@ __device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd
 // ring holds planes a+LO..a+HI (u_old, then accumulating) plus a+HI+1 in
 // flight; plane a+LO is written back after anchor a and its slot takes plane
 // a+HI+2.  The candidates of anchor a+1 are staged while anchor a is added.
-template <int K, bool LVL>
+// CNT: the counted launch of ibtk_le_ctx_count_adds (a kernel of its own name, so
+// profiles of the product sweep do not average it in)
+template <int K, bool LVL, bool CNT>
 __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     using S = SSh<K>;
     constexpr int LO = S::LO, HI = S::HI, NPL = S::NPL, FAM = S::FAM;
@@ -888,13 +879,12 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     }
     const int afirst = max(plo - HI, 0), alast = min(phi - LO, cg.nz - 1);
     const int col0 = (cy - 1) * ncx + (cx - 1);  // column (cx-1, cy-1)
-    {
-        bool any = false;  // no candidate reaches the item: u unchanged
-        for (int a = afirst + lane; a <= alast; a += SW)
-            for (int r = 0; r < 3; ++r)
-                any = any || bs[bucket(cg, a, col0 + r * ncx, 3 * NBAND)] > bs[bucket(cg, a, col0 + r * ncx, 0)];
-        if (!__any(any)) return;
-    }
+    bool any = false;  // no candidate reaches the item: u unchanged (zero_first: 0)
+    for (int a = afirst + lane; a <= alast; a += SW)
+        for (int r = 0; r < 3; ++r)
+            any = any || bs[bucket(cg, a, col0 + r * ncx, 3 * NBAND)] > bs[bucket(cg, a, col0 + r * ncx, 0)];
+    any = __any(any);
+    if (!any && !p.zero_first) return;
     const int nlast = p.nsorted - 1;
     // the lane's points of a plane: slot index lane + 64 k (tile-major, so the
     // staging stores and writeback loads are contiguous in LDS), their array
@@ -914,6 +904,14 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         const int zc = min(max(zorg + z, cd.lo[2]), cd.hi[2]);
         return plane_rsrc(cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2, plane_bytes);
     };
+    if (!any) {  // zero_first, no candidate: the owned points are 0
+        for (int z = plo; z <= phi; ++z) {
+            const auto pb = plane_ptr(z);
+#pragma unroll
+            for (int k = 0; k < NPL; ++k) buf_st(pb, loff[k], 0.0);
+        }
+        return;
+    }
     // bucket starts of anchor plane a: rows cy-1, cy, cy+1 (28 entries: bands of
     // columns cx-1 .. cx+1), one entry per lane
     auto rows_load = [&](int a, int* rowv) {
@@ -931,37 +929,51 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         d.s = FAM == 2 ? p.sorted_s[e] : 0;
     };
     Clk clk;
+    unsigned long long cnt[2] = {0ull, 0ull};  // CNT: wave-uniform totals of the item
     const double inv_h3 = 1.0 / p.h3;
     const double inv_d[3] = {1.0 / p.bg.dx[0], 1.0 / p.bg.dx[1], 1.0 / p.bg.dx[2]};
     // adds of the n <= 64 candidates held one per lane (lane j's anchor plane:
-    // a - 1 for j < r, else a)
-    auto process = [&](int a, int r, int n, const Cand& mine) {
-        if (IBTK_LE_DIAG_SNOPROC) return;
-        spread_tiled<K>(p, cd, ring, mine, lane < n, lane < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi,
-                        inv_h3, inv_d, clk);
+    // a - 1 for j < r, else a); `before` as for spread_tiled
+    auto process = [&](int a, int r, int n, const Cand& mine, auto&& before) {
+        spread_tiled<K, CNT>(p, cd, ring, mine, lane < n, lane < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi,
+                             inv_h3, inv_d, clk, cnt, before);
     };
+    auto nothing = [] {};
     // plane z -> registers (the lane's NPL points); registers -> ring slot.  A
     // plane the item does not own receives no adds and is not written back: its
     // slot's contents do not matter, so it is not read.
     auto plane_load = [&](int z, double* v) {
         if (z < plo || z > phi) return;
+        if (p.zero_first) {  // the owned points start from 0: nothing to read
+#pragma unroll
+            for (int k = 0; k < NPL; ++k) v[k] = 0.0;
+            return;
+        }
         const auto pb = plane_ptr(z);
 #pragma unroll
-        for (int k = 0; k < NPL; ++k) v[k] = IBTK_LE_DIAG_SNOLOAD ? 0.0 : buf_ld(pb, loff[k]);
+        for (int k = 0; k < NPL; ++k) v[k] = buf_ld(pb, loff[k]);
     };
     auto plane_put = [&](int z, const double* v) {
         double* sl = ring + sslot<K>(z) * S::PV;
 #pragma unroll
         for (int k = 0; k < NPL; ++k) sl[lane + k * SW] = v[k];
     };
-    auto plane_writeback = [&](int z) {  // owned points of plane z, ring -> array
-        if (z < plo || z > phi) return;
+    // Writeback of plane z (owned points, ring -> array) in two halves: the slot is
+    // read into registers before the slot is reused (a wave's LDS operations run in
+    // order, so the put that follows needs no wait), the stores go out later.  A
+    // plane the item does not own (or no plane, on: false) gets an empty resource
+    // and its stores are dropped: every anchor step issues the same stores, so the
+    // compiler's waits for later loads count them exactly instead of waiting for
+    // the stores of a conditional path to complete.
+    auto wb_read = [&](int z, double* v) {
         const double* sl = ring + sslot<K>(z) * S::PV;
-        const auto pb = plane_ptr(z);
-        double v[NPL];
 #pragma unroll
         for (int k = 0; k < NPL; ++k) v[k] = sl[lane + k * SW];
-        if (IBTK_LE_DIAG_SNOSTORE) return;
+    };
+    auto wb_store = [&](int z, bool on, const double* v) {
+        const int zc = min(max(zorg + z, cd.lo[2]), cd.hi[2]);
+        const bool own = on && z >= plo && z <= phi;
+        const auto pb = plane_rsrc(cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2, own ? plane_bytes : 0u);
 #pragma unroll
         for (int k = 0; k < NPL; ++k) buf_st(pb, loff[k], v[k]);  // not-owned points: dropped
     };
@@ -987,41 +999,41 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     int tA = rg.pre[S::NR];
     Cand nxt;
     cand_at(range_pos(rg, min(lane, max(tA - 1, 0))), nxt);
-    // per lane l: sorted position of that anchor's candidate tA - 64 + l (its
-    // last 64; the carried ones are taken from here, so only one Ranges is live)
-    int etail = range_pos(rg, max(tA - SW + lane, 0));
     int r_prev = 0;        // candidates of anchor a-1 carried into a's chunk 1
     int n1 = min(tA, SW);  // lanes of a's chunk 1
     if (afirst + 1 <= alast) rows_load(afirst + 1, rowv);
     clk.lap(0);
     // One anchor step: plane a+HI from registers into the ring, plane a+HI+1 into
     // registers.  (Two anchors ahead through two register buffers measured the same,
-    // 16.1 vs 16.3 ms on cfg4, profiles/r03h: the streams are not what waits.)
+    // 16.1 vs 16.3 ms on cfg4: the streams are not what waits.)
     auto anchor_step = [&](int a) {
-        if (a >= afirst + 2) plane_writeback(a - 2 + LO);  // no anchor left reaches it
-        plane_put(a + HI, pv);                               // into its slot
+        const int zw = a - 2 + LO;  // no anchor left reaches it: written back this step
+        double wb[NPL];
+        wb_read(zw, wb);       // its slot ...
+        plane_put(a + HI, pv);  // ... takes plane a+HI
         const Cand cur = nxt;
         const int cur_r = r_prev, cur_n = n1;
         const int tCur = tA;
-        const int etCur = etail;
         const int h = min(SW - r_prev, tCur);  // a's candidates in chunk 1
         const int nmid = (tCur - h) / SW;       // full middle chunks
         const int r_a = (tCur - h) % SW;        // carried into a+1
         clk.lap(1);
-        // prefetch for a+1: its ranges, its chunk 1, the rows of a+2; plane a+HI+2
+        // prefetch for a+1: its ranges, its chunk 1 (a's last r_a, then a+1's
+        // first), the rows of a+2; plane a+HI+1
         if (a + 1 <= alast) {
+            const int eA = range_pos(rg, max(tCur - r_a + lane, 0));  // rg: a's ranges
             make_ranges_lanes(rowv, rg);
             tA = rg.pre[S::NR];
-            const int eA = __builtin_amdgcn_ds_bpermute((SW - r_a + lane) << 2, etCur);  // a's last r_a
             const int eB = range_pos(rg, min(max(lane - r_a, 0), max(tA - 1, 0)));
             cand_at(lane < r_a ? eA : eB, nxt);
-            etail = range_pos(rg, max(tA - SW + lane, 0));
             n1 = r_a + min(SW - r_a, tA);
             r_prev = r_a;
             plane_load(a + HI + 1, pv);
             if (a + 2 <= alast) rows_load(a + 2, rowv);
         }
-        if (cur_n > 0) process(a, cur_r, cur_n, cur);
+        const bool wbon = a >= afirst + 2;
+        if (cur_n > 0) process(a, cur_r, cur_n, cur, [&] { wb_store(zw, wbon, wb); });
+        else wb_store(zw, wbon, wb);
         if (nmid > 0) {  // dense planes: the full middle chunks (ranges of a rebuilt)
             int rowm[3];
             rows_load(a, rowm);
@@ -1034,21 +1046,33 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
             for (int k = 0; k < nmid; ++k) {
                 const Cand now = more;
                 if (k + 1 < nmid) cand_at(range_pos(rgm, h + SW * (k + 1) + lane), more);
-                process(a, 0, SW, now);
+                process(a, 0, SW, now, nothing);
             }
         }
-        if (a == alast && r_a > 0) {  // the last anchor's leftovers
+        if (a == alast && r_a > 0) {  // the last anchor's leftovers (rg: a's ranges)
             Cand last;
-            cand_at(__builtin_amdgcn_ds_bpermute((SW - r_a + min(lane, r_a - 1)) << 2, etCur), last);
-            process(a, 0, r_a, last);
+            cand_at(range_pos(rg, tCur - r_a + min(lane, r_a - 1)), last);
+            process(a, 0, r_a, last, nothing);
         }
         clk.lap(4);
     };
     for (int a = afirst; a <= alast; ++a) anchor_step(a);
-    plane_writeback(alast - 1 + LO);
-    plane_writeback(alast + LO);
+    {
+        double wb[NPL];
+        wb_read(alast - 1 + LO, wb);
+        wb_store(alast - 1 + LO, true, wb);
+        wb_read(alast + LO, wb);
+        wb_store(alast + LO, true, wb);
+    }
+
     clk.lap(5);
     clk.flush(p, it);
+    if constexpr (CNT) {
+        if (lane == 0) {
+            atomicAdd(p.nadd, cnt[0]);
+            atomicAdd(p.nadd + 1, cnt[1]);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1327,8 +1351,13 @@ template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s
     const long items = (long)p.item_bound * p.ncomp;
     if (items > 0) {
         const dim3 g(sweep_grid(p, items)), b(SW);
-        if (p.pd) hipLaunchKernelGGL((k_spread_sweep<K, true>), g, b, 0, s, p);
-        else hipLaunchKernelGGL((k_spread_sweep<K, false>), g, b, 0, s, p);
+        if (p.nadd) {
+            if (p.pd) hipLaunchKernelGGL((k_spread_sweep<K, true, true>), g, b, 0, s, p);
+            else hipLaunchKernelGGL((k_spread_sweep<K, false, true>), g, b, 0, s, p);
+        } else {
+            if (p.pd) hipLaunchKernelGGL((k_spread_sweep<K, true, false>), g, b, 0, s, p);
+            else hipLaunchKernelGGL((k_spread_sweep<K, false, false>), g, b, 0, s, p);
+        }
     }
     if (ev1) (void)hipEventRecord(ev1, s);
     return hipGetLastError();

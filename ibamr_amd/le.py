@@ -448,6 +448,16 @@ class Level:
                                                 CENTERING[centering], axis, self._arrays(arrays), q_depth, _ptr(Q),
                                                 Q_depth, _ptr(X)))
 
+    def zero_spread(self, centering: str, arrays, Q: torch.Tensor, X: torch.Tensor, q_depth: int = 1,
+                    Q_depth: Optional[int] = None, axis: int = 0):
+        """`zero` then `spread` in one launch (ibtk_le_level_zero_spread): LDataManager::spread's
+        setToScalar(f, 0, interior_only=false) fused with its patch loop; bitwise the two calls."""
+        if Q_depth is None:
+            Q_depth = 3 if centering in ("side", "edge") else q_depth
+        check(self.ctx.lib.ibtk_le_level_zero_spread(self.ctx.h, self.markers.h, kernel_id(self.kernel),
+                                                     CENTERING[centering], axis, self._arrays(arrays), q_depth,
+                                                     _ptr(Q), Q_depth, _ptr(X)))
+
 
 def _periodic_arg(periodic, ndim):
     if periodic is None:

@@ -200,6 +200,14 @@ int ibtk_le_level_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cen
                          const double* const* q_dev, int q_depth, double* Q_dev, int Q_depth, const double* X_dev);
 int ibtk_le_level_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                          double* const* q_dev, int q_depth, const double* Q_dev, int Q_depth, const double* X_dev);
+/* q := 0 on every patch array (ghosts included), then ibtk_le_level_spread, in one
+ * launch: LDataManager::spread's setToScalar(f, 0, interior_only = false) fused with
+ * its patch loop (LDataManager.cpp:588-654).  The sweep's items start their owned
+ * points from 0 instead of reading them; items no marker reaches store zeros.
+ * Bitwise ibtk_le_level_zero followed by ibtk_le_level_spread. */
+int ibtk_le_level_zero_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                              double* const* q_dev, int q_depth, const double* Q_dev, int Q_depth,
+                              const double* X_dev);
 /* One binning for both sweeps: m binned on the ghost-box lists (the spread's), then
  * told the interior lists (interior_offsets on the host, npatch + 1; indices on the
  * device; markers 0 .. n_markers-1): later level interps on m write Q only from the

@@ -251,3 +251,44 @@ def test_level_select_interior_rejects_foreign_entries(le, ctx):
     lvl.select_interior(4, torch.arange(4, dtype=torch.int32, device="cuda"), offs)
     with pytest.raises(RuntimeError, match="flag 4"):
         ctx.synchronize()
+
+
+@pytest.mark.parametrize("kernel,clustered", [("IB_4", True), ("IB_6", False)])
+def test_level_zero_spread(le, ctx, kernel, clustered):
+    """ibtk_le_level_zero_spread (LDataManager::spread's setToScalar(f, 0, false) and
+    patch loop in one launch) equals ibtk_le_level_zero then ibtk_le_level_spread bit
+    for bit, on arrays that start as NaN -- every point of every array is written,
+    including the patches and columns no marker reaches."""
+    N, P = 48, 2
+    g = ora.min_ghost_width(kernel)
+    geoms = _patches(le, N, P, g)
+    rng = np.random.default_rng(11)
+    M = 20_000
+    X = rng.uniform(0, 1, (M, 3))
+    if clustered:  # a sheet inside the lower patches only: the upper ones get no marker
+        X[:, 2] = 0.2 + (rng.uniform(0, 1, M) - 0.5) / N
+    F = rng.uniform(-1, 1, (M, 3))
+    Xd, Fd = torch.from_numpy(X).cuda(), torch.from_numpy(F).cuda()
+    lists = []
+    for geom in geoms:
+        _, idx, xs = _lists(geom, X, N, g)
+        lists.append((torch.from_numpy(idx).cuda(), torch.from_numpy(xs).cuda()))
+    lvl = le.Level(ctx, geoms, kernel, Xd, lists)
+    want = [geom.alloc("side", fill=float("nan")) for geom in geoms]
+    lvl.zero("side", want)
+    lvl.spread("side", want, Fd, Xd)
+    got = [geom.alloc("side", fill=float("nan")) for geom in geoms]
+    lvl.zero_spread("side", got, Fd, Xd)
+    ctx.synchronize()
+    for q in range(len(geoms)):
+        for a in range(3):
+            w, o = want[q][a].cpu().numpy(), got[q][a].cpu().numpy()
+            assert not np.isnan(o).any(), f"patch {q} comp {a}: points not written"
+            assert np.array_equal(w, o), f"patch {q} comp {a}"
+    # an empty level binning: the zeroing alone
+    empty = le.Level(ctx, geoms, kernel, Xd, [(torch.zeros(0, dtype=torch.int32, device="cuda"),
+                                                torch.zeros((0, 3), dtype=torch.float64, device="cuda"))] * len(geoms))
+    f = [geom.alloc("side", fill=float("nan")) for geom in geoms]
+    empty.zero_spread("side", f, Fd, Xd)
+    ctx.synchronize()
+    assert all(not t.cpu().numpy().any() and not np.isnan(t.cpu().numpy()).any() for row in f for t in row)
