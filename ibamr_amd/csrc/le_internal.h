@@ -174,6 +174,7 @@ struct Params {
     unsigned long long* stamps = nullptr;  // diagnostic phase clocks (nullptr: off)
     unsigned long long* nadd = nullptr;    // spread: [ds_add_f64 wave-instructions, lane adds] issued (nullptr: not counted)
     int zero_first = 0;  // 3-D spread: the arrays start from 0 (every point, ghosts included), not their values
+    int comp0 = 0;       // 3-D spread: a launch's components are comp[comp0 .. comp0 + ncomp)
 };
 
 // Host-side launchers (le_kernels.hip).

@@ -392,6 +392,7 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
                 }
             }
         }
+
     } else {
         // piecewise kernels: weights outside [ist, isp] are 0 and the index is
         // clamped into the stencil's valid range, acc + 0*u == acc.
@@ -625,11 +626,17 @@ __global__ __launch_bounds__(BLOCK) void k_interp_outside_col(Params p, int n) {
 // a 4-wide stencil plane therefore cover the 16 classes once each, whatever the
 // stencil's position, and the lanes can take them in an order in which the 16
 // lanes of a group always hit 16 different classes (spread_tiled).
-template <int K> struct SSh {
+// ZC: the component's z frame is the bin keys' (cell) frame, where the closed-form
+// kernels' (FAM 0) stencil planes of anchor a are exactly a + [LO, HI - 1]
+// (ic_lower = NINT - W/2): the ring is one slot shorter (IB_4: 5 slots, 20 KB,
+// 8 waves per CU instead of 6).
+template <int K, bool ZC = false> struct SSh {
     using T = KT<K>;
     static constexpr int W = T::W, LO = T::LO, HI = T::HI, FAM = T::FAM;
-    static constexpr int NS = HI - LO + 1;   // planes an anchor plane reaches
-    static constexpr int NSL = NS + 1;       // ring slots: the planes two anchors reach
+    static_assert(!ZC || FAM == 0, "the key-frame ring: closed-form kernels");
+    static constexpr int HIE = ZC ? HI - 1 : HI;  // highest plane an anchor reaches (relative)
+    static constexpr int NS = HIE - LO + 1;       // planes an anchor plane reaches
+    static constexpr int NSL = NS + 1;            // ring slots: the planes two anchors reach
     static constexpr int PV = COLX * COLY;   // owned points per plane = doubles per slot
     static constexpr int NPL = PV / SW;      // staged points per lane and plane
     static constexpr int NR = 11;            // candidate ranges per anchor plane
@@ -651,8 +658,7 @@ __device__ __forceinline__ int ring_wrapped(int x, int y) {
     return 16 * ((xw >> 2) + (COLX / 4) * (yw >> 2)) + (xw & 3) + 4 * (yw & 3);
 }
 
-template <int K> __device__ __forceinline__ int sslot(int prel) {
-    using S = SSh<K>;
+template <class S> __device__ __forceinline__ int sslot(int prel) {
     return (int)((unsigned)(prel + 16 * S::NSL) % (unsigned)S::NSL);  // prel >= -HI + LO > -16*NSL
 }
 
@@ -729,12 +735,12 @@ __device__ __forceinline__ void rot4(double* w, int r) {
 // `before` runs on every lane after the weights are computed and before any add
 // (the anchor step's writeback stores go there: issued after the candidate loads
 // they would otherwise be counted ahead of, and while the previous adds drain).
-template <int K, bool CNT, typename Before>
+template <int K, bool CNT, bool ZC, typename Before>
 __device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
                                              bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
                                              int yhi, int plo, int phi, double inv_h3, const double* inv_d, Clk& clk,
                                              unsigned long long* cnt, Before&& before) {
-    using S = SSh<K>;
+    using S = SSh<K, ZC>;
     constexpr int W = S::W, FAM = S::FAM, NSL = S::NSL;
     constexpr bool ROT = W >= 4;
     St<W> st[3];
@@ -758,10 +764,10 @@ __device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd
     // owned and clipped-in ranges of the stencil indices
     const int x0 = max(st[0].ist, xlo - ox), x1 = min(st[0].isp, xhi - ox);
     const int y0 = max(st[1].ist, ylo - oy), y1 = min(st[1].isp, yhi - oy);
-    // planes within the ring's reach of the lane's anchor, [LO, HI] (a stencil
+    // planes within the ring's reach of the lane's anchor, [LO, HIE] (a stencil
     // moved by a NINT tie of the multiply -- a weight of an ulp's order -- is cut there)
     const int z0 = max(max(st[2].ist, plo - (a + oz)), S::LO - oz);
-    const int z1 = min(min(st[2].isp, phi - (a + oz)), S::HI - oz);
+    const int z1 = min(min(st[2].isp, phi - (a + oz)), S::HIE - oz);
     double wx[W], wy[W], wz[W];
 #pragma unroll
     for (int i = 0; i < W; ++i) {
@@ -847,16 +853,17 @@ __device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd
 // a+HI+2.  The candidates of anchor a+1 are staged while anchor a is added.
 // CNT: the counted launch of ibtk_le_ctx_count_adds (a kernel of its own name, so
 // profiles of the product sweep do not average it in)
-template <int K, bool LVL, bool CNT>
+template <int K, bool LVL, bool CNT, bool ZC>
 __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
-    using S = SSh<K>;
-    constexpr int LO = S::LO, HI = S::HI, NPL = S::NPL, FAM = S::FAM;
+    using S = SSh<K, ZC>;
+    constexpr int LO = S::LO, HI = S::HIE, NPL = S::NPL, FAM = S::FAM;  // HI: the ring's reach
     __shared__ double ring[S::NSL * S::PV];
     const int it = sweep_item(p, p.ncomp);
     if (it < 0) return;
     int c;
     SweepItem si;
     item_decode(p, it, c, si);
+    c += p.comp0;  // the launch's components start at comp0 (launch_spread_sweep_t)
     const int col = si.col;
     const int lane = lane_id();
     ColGeom cg;
@@ -935,7 +942,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // adds of the n <= 64 candidates held one per lane (lane j's anchor plane:
     // a - 1 for j < r, else a); `before` as for spread_tiled
     auto process = [&](int a, int r, int n, const Cand& mine, auto&& before) {
-        spread_tiled<K, CNT>(p, cd, ring, mine, lane < n, lane < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi,
+        spread_tiled<K, CNT, ZC>(p, cd, ring, mine, lane < n, lane < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi,
                              inv_h3, inv_d, clk, cnt, before);
     };
     auto nothing = [] {};
@@ -954,7 +961,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         for (int k = 0; k < NPL; ++k) v[k] = buf_ld(pb, loff[k]);
     };
     auto plane_put = [&](int z, const double* v) {
-        double* sl = ring + sslot<K>(z) * S::PV;
+        double* sl = ring + sslot<S>(z) * S::PV;
 #pragma unroll
         for (int k = 0; k < NPL; ++k) sl[lane + k * SW] = v[k];
     };
@@ -966,7 +973,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // compiler's waits for later loads count them exactly instead of waiting for
     // the stores of a conditional path to complete.
     auto wb_read = [&](int z, double* v) {
-        const double* sl = ring + sslot<K>(z) * S::PV;
+        const double* sl = ring + sslot<S>(z) * S::PV;
 #pragma unroll
         for (int k = 0; k < NPL; ++k) v[k] = sl[lane + k * SW];
     };
@@ -1347,17 +1354,45 @@ template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s
         if (rec3) hipLaunchKernelGGL(k_gather_F_col<true>, g, b, 0, s, p, p.nsorted, const_cast<double*>(p.sorted_F));
         else hipLaunchKernelGGL(k_gather_F_col<false>, g, b, 0, s, p, p.nsorted, const_cast<double*>(p.sorted_F));
     }
-    if (ev0) (void)hipEventRecord(ev0, s);  // the events bracket the sweep kernel alone
-    const long items = (long)p.item_bound * p.ncomp;
-    if (items > 0) {
-        const dim3 g(sweep_grid(p, items)), b(SW);
-        if (p.nadd) {
-            if (p.pd) hipLaunchKernelGGL((k_spread_sweep<K, true, true>), g, b, 0, s, p);
-            else hipLaunchKernelGGL((k_spread_sweep<K, false, true>), g, b, 0, s, p);
-        } else {
-            if (p.pd) hipLaunchKernelGGL((k_spread_sweep<K, true, false>), g, b, 0, s, p);
-            else hipLaunchKernelGGL((k_spread_sweep<K, false, false>), g, b, 0, s, p);
+    if (ev0) (void)hipEventRecord(ev0, s);  // the events bracket the sweep kernels alone
+    // One launch per run of components alike in z frame: the components whose z
+    // frame is the keys' take the shorter ring (SSh ZC; side data: components 0 and
+    // 1 in one launch, then 2), every other one the full ring.  cfg4 spread sweep
+    // 15.6 -> 15.0 ms (profiles/r03j; all components on 5 slots in one launch would
+    // be 14.2, but the z-side component needs 6; the two launches side by side on
+    // two streams measured 15.4).
+    for (int c0 = 0; c0 < p.ncomp;) {
+        const bool zc = KT<K>::FAM == 0 && p.comp[c0].zcell;
+        int c1 = c0 + 1;
+        while (c1 < p.ncomp && (KT<K>::FAM == 0 && p.comp[c1].zcell) == zc) ++c1;
+        Params q = p;
+        q.comp0 = c0;
+        q.ncomp = c1 - c0;
+        const long items = (long)q.item_bound * q.ncomp;
+        if (items > 0) {
+            const dim3 g(sweep_grid(q, items)), b(SW);
+            if constexpr (KT<K>::FAM == 0) {
+                if (zc) {
+                    if (q.nadd) {
+                        if (q.pd) hipLaunchKernelGGL((k_spread_sweep<K, true, true, true>), g, b, 0, s, q);
+                        else hipLaunchKernelGGL((k_spread_sweep<K, false, true, true>), g, b, 0, s, q);
+                    } else {
+                        if (q.pd) hipLaunchKernelGGL((k_spread_sweep<K, true, false, true>), g, b, 0, s, q);
+                        else hipLaunchKernelGGL((k_spread_sweep<K, false, false, true>), g, b, 0, s, q);
+                    }
+                    c0 = c1;
+                    continue;
+                }
+            }
+            if (q.nadd) {
+                if (q.pd) hipLaunchKernelGGL((k_spread_sweep<K, true, true, false>), g, b, 0, s, q);
+                else hipLaunchKernelGGL((k_spread_sweep<K, false, true, false>), g, b, 0, s, q);
+            } else {
+                if (q.pd) hipLaunchKernelGGL((k_spread_sweep<K, true, false, false>), g, b, 0, s, q);
+                else hipLaunchKernelGGL((k_spread_sweep<K, false, false, false>), g, b, 0, s, q);
+            }
         }
+        c0 = c1;
     }
     if (ev1) (void)hipEventRecord(ev1, s);
     return hipGetLastError();
