@@ -248,6 +248,12 @@ def lds_atomic(ctx, spread_call, k_ms):
                     "conflict-free ds_add_f64 rate of tools/ubench_lds2.hip"}
 
 
+# what kernel_ms times (HIP events around the sweep launches on the context stream)
+KERNEL_NOTE = ("interp = k_interp_sweep<K, LVL>; spread = its component launches summed: "
+               "k_spread_sweep<K, LVL, false, true> (the components whose z frame is the keys', a 5-slot ring) "
+               "then k_spread_sweep<K, LVL, false, false> (side data's z component); rocprofv3 lists them apart")
+
+
 def run_level(args, cfg, kernel, dev):
     """--config cfg5 (default): the clustered markers on a multi-patch finest level,
     8^3 patches of 64^3, one launch per sweep over every patch.
@@ -411,7 +417,7 @@ def run_level(args, cfg, kernel, dev):
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "algorithmic_bytes": {"interp": B_i, "spread": B_s}, "kernel_ms": {"interp": k_i, "spread": k_s},
-                     "lds_atomic": lds},
+                     "kernel_note": KERNEL_NOTE, "lds_atomic": lds},
         "cpu_baseline": None,
         "breakdown_ms": {k: mean(v) for k, v in acc.items()},
         "touched_points": S_touched,
@@ -820,6 +826,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per launch (PMC)", "traffic_note": traffic_note,
                      "algorithmic_bytes": {"interp": B_i, "spread": B_s},
                      "kernel_ms": {"interp": k_i, "spread": k_s},
+                     "kernel_note": KERNEL_NOTE,
                      "pair_achieved": pair, "pair_frac": pair / HBM_PEAK_GBS, "lds_atomic": lds},
         "cpu_baseline": cpu,
         "breakdown_ms": {k: mean(v) for k, v in acc.items()},

@@ -44,7 +44,7 @@ constexpr int SW = 64;  // one wavefront per work item
 
 // LDS read of one double that the compiler may not merge with its neighbour into a
 // ds_read2_b64 (half the rate of two ds_read_b64 on gfx950: interp sweep 10.7 ->
-// 9.9 ms on cfg4, profiles/r03f)
+// 9.9 ms on cfg4, round 3)
 __device__ __forceinline__ double lds_ld(const double* q) {
     return *(const volatile __attribute__((address_space(3))) double*)q;
 }
@@ -1104,7 +1104,11 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
 // A level's patches (64^3 on cfg5) take segments down to 32 planes: two per patch
 // instead of one gives the clustered level twice the items to balance (cfg5
 // 2.00e9 -> 2.14e9 marker-ops/s, spread sweep 3.41 -> 3.08 ms, profiles/r02z).
-constexpr int MIN_SEG = 64, MIN_SEG_LEVEL = 32;
+// A patch too narrow to give the chip work in long segments (fewer than
+// SMALL_ITEMS (column, segment) pairs: cfg2's 128^3 sphere has 45 columns) takes
+// segments down to 8 planes instead: its sweeps are latency-bound walks of one
+// wave per item, not plane streams.
+constexpr int MIN_SEG = 64, MIN_SEG_LEVEL = 32, SMALL_ITEMS = 1024, MIN_SEG_SMALL = 8;
 void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items, bool level) {
     const int min_seg = level ? MIN_SEG_LEVEL : MIN_SEG;
     long long want = seg_items > 0 ? seg_items : IBTK_LE_SEG_ITEMS;
@@ -1113,7 +1117,14 @@ void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items, bool le
         const long long ns = cg.nz / min_seg > 1 ? cg.nz / min_seg : 1;  // segments of >= min_seg planes
         s = (cg.nz + ns - 1) / ns;
     }
-    if (s < 32) s = 32;
+    const long long ncol_real = (long long)(cg.ncx > 2 ? cg.ncx - 2 : 1) * (cg.ncy > 2 ? cg.ncy - 2 : 1);
+    if (!level && seg_items <= 0 && ncol_real * ((cg.nz + s - 1) / s) < SMALL_ITEMS) {
+        const long long ns = (SMALL_ITEMS + ncol_real - 1) / ncol_real;
+        s = (cg.nz + ns - 1) / ns;
+        if (s < MIN_SEG_SMALL) s = MIN_SEG_SMALL;
+    } else if (s < 32) {
+        s = 32;
+    }
     if (s > cg.nz) s = cg.nz;
     if (s < 1) s = 1;
     const long long ns = (cg.nz + s - 1) / s;  // segments of about s planes, equal (+-1)

@@ -9,16 +9,18 @@
 # Writes <outdir>/pmc.json with the library's source hash; copy it to
 # profiles/pmc_<cfg>_<kernel>_1gpu.json, which bench.py reads when the hash
 # matches the build it runs.
-# Usage: tools/pmc_traffic.sh <outdir> [cfg] [kernel]
+# Usage: [BENCH_ARGS="..."] tools/pmc_traffic.sh <outdir> [cfg] [kernel]
+# Per step: the spread is one launch per run of components alike in z frame
+# (launch_spread_sweep_t: side data = 2 launches); their per-launch means are summed.
 out=$1; cfg=${2:-cfg4}; kern=${3:-IB_4}
 export TMPDIR=/tmp
 mkdir -p "$out"
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$out/$ctr" -o pmc -- \
-    python3 bench.py --config $cfg --kernel $kern --steps 2 --warmup 1 --no-cpu-baseline > "$out/$ctr.log" 2>&1 || { echo "$ctr pass failed"; exit 1; }
+    python3 bench.py --config $cfg --kernel $kern --steps 2 --warmup 1 --no-cpu-baseline $BENCH_ARGS > "$out/$ctr.log" 2>&1 || { echo "$ctr pass failed"; exit 1; }
 done
 python3 - "$out" "$cfg" "$kern" <<'PY'
-import csv, glob, json, sys, collections
+import csv, glob, json, os, sys, collections
 out, cfg, kern = sys.argv[1:4]
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -33,15 +35,23 @@ for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
 sys.path.insert(0, ".")
 from ibamr_amd.build import source_hash
 res = {"build": source_hash(), "counters_kb": {}, "per_launch_bytes": {}, "read_bytes": {}, "write_bytes": {},
-       "note": "(2 x FETCH_SIZE + WRITE_SIZE) KB x 1024 per launch, mean over launches; FETCH_SIZE x 2 per "
+       "bench_args": os.environ.get("BENCH_ARGS", ""),
+       "note": "(2 x FETCH_SIZE + WRITE_SIZE) KB x 1024 per sweep (the spread's component launches summed), mean over steps; FETCH_SIZE x 2 per "
                "profiles/r02b/fetch_calibration.json (8-B and 16-B-per-lane reads both report 0.50 of the bytes)"}
 for k, d in vals.items():
-    name = "spread" if "k_spread_sweep" in k else "interp" if "k_interp_sweep" in k else None
+    # the counted-add launch (..., true, ...>: CNT) is not the product sweep
+    cnt = "k_spread_sweep" in k and k.split("<")[1].split(",")[2].strip() == "true"
+    name = "spread" if "k_spread_sweep" in k and not cnt else "interp" if "k_interp_sweep" in k else None
     if name is None or not d.get("FETCH_SIZE") or not d.get("WRITE_SIZE"):
         continue
     f = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"])
     w = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"])
-    res["counters_kb"][name] = {"FETCH_SIZE": f, "WRITE_SIZE": w}
+    c = res["counters_kb"].setdefault(name, {"FETCH_SIZE": 0.0, "WRITE_SIZE": 0.0, "kernels": []})
+    c["FETCH_SIZE"] += f
+    c["WRITE_SIZE"] += w
+    c["kernels"].append(k)
+for name, c in res["counters_kb"].items():
+    f, w = c["FETCH_SIZE"], c["WRITE_SIZE"]
     res["per_launch_bytes"][name] = (2 * f + w) * 1024
     res["read_bytes"][name] = 2 * f * 1024
     res["write_bytes"][name] = w * 1024
