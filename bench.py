@@ -279,6 +279,14 @@ def run_level(args, cfg, kernel, dev):
     from ibamr_amd.slab import Slab
     X = make_markers(cfg["markers"], cfg["M"], Slab([N, N, N], 1, 0, g), 1234, dev)
     X = torch.remainder(X, 1.0).contiguous()
+    if args.marker_order == "cell":
+        # the level's local numbering (LDataManager::computeNodeDistribution,
+        # LDataManager.cpp:2874-2892): patch by patch, cell by cell in box order
+        c = torch.clamp((X * N).floor().long(), 0, N - 1)
+        t, r = c // n, c % n
+        pid = (t[:, 2] * P + t[:, 1]) * P + t[:, 0]
+        X = X[torch.argsort((pid * n + r[:, 2]) * n * n + r[:, 1] * n + r[:, 0], stable=True)].contiguous()
+        del c, t, r, pid
     M = X.shape[0]
     gen = torch.Generator(device=dev).manual_seed(4321)
     F = torch.rand((M, 3), dtype=torch.float64, device=dev, generator=gen).mul_(2).sub_(1)
@@ -407,7 +415,7 @@ def run_level(args, cfg, kernel, dev):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": cfg["desc"], "kernel": kernel, "grid": [N, N, N], "markers": M,
                    "parallelism": "one GPU", "patches": [P, P, P], "patch_cells": [n, n, n], "ghost": g,
-                   "move": args.move,
+                   "marker_order": args.marker_order, "move": args.move,
                    "step": ("level ghost fill + interp(3 comps) + position update + per-patch lists rebuilt "
                             "(bench.level_lists, torch ops) + bin(ghost-box lists, interior selected) + zero f and "
                             "spread(3 comps) in one launch" if args.move else

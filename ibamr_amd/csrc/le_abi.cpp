@@ -98,6 +98,7 @@ struct ibtk_le_ctx_s {
     int device = 0;
     hipStream_t stream = nullptr;
     DevBuf keys_in, vals_in, temp, counts, offsets, fbuf;
+    DevBuf bfirst;  // first entry of every bucket (k_gather_col), before the suffix-min scan
     DevBuf lst_idx, lst_xs, lst_key, lst_perm;  // index-list / node-distribution scratch
     DevBuf lst_cell, lst2_idx, lst2_xs, lst2_cell, lst_flag;  // index lists: cells, the sorted list, unique flags
     DevBuf num_tab, num_lkey, num_ckey;                        // level numbering: tile table, keys
@@ -181,7 +182,7 @@ extern "C" int ibtk_le_ctx_destroy(ibtk_le_ctx ctx) {
     if (!ctx) return IBTK_LE_OK;
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
-    for (DevBuf* b : {&ctx->keys_in, &ctx->vals_in, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->fbuf, &ctx->err, &ctx->sink,
+    for (DevBuf* b : {&ctx->keys_in, &ctx->vals_in, &ctx->bfirst, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->fbuf, &ctx->err, &ctx->sink,
                        &ctx->stamps, &ctx->lst_idx, &ctx->lst_xs, &ctx->lst_key, &ctx->lst_perm, &ctx->lst_cell,
                        &ctx->lst2_idx, &ctx->lst2_xs, &ctx->lst2_cell, &ctx->lst_flag, &ctx->num_tab, &ctx->num_lkey,
                        &ctx->num_ckey,
@@ -563,6 +564,23 @@ static int markers_bin_impl(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_pa
                             const double* X_dev, const int* indices_dev, const double* Xshift_dev, int nindices,
                             const int* n_dev);
 
+// The sorted entries' marker indices and positions, and the bucket starts: the
+// gather records each non-empty bucket's first entry, a suffix-min scan fills in
+// the empty buckets.
+static int gather_buckets(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const Params& p, int n, int nbuckets) {
+    int rc;
+    if ((rc = ctx->bfirst.ensure(sizeof(int) * (size_t)(nbuckets + 1)))) return rc;
+    HIP_TRY(launch_gather_col(kernel, p, n, m->sorted_s.as<int>(), m->sorted_X.as<double>(), m->sorted_key.as<unsigned>(),
+                              nbuckets, ctx->bfirst.as<int>(), ctx->stream));
+    size_t tb = 0;
+    HIP_TRY(launch_suffix_min(nullptr, tb, ctx->bfirst.as<int>(), m->plane_start.as<int>(), nbuckets + 1, ctx->stream));
+    if ((rc = ctx->temp.ensure(tb))) return rc;
+    tb = ctx->temp.cap;
+    HIP_TRY(launch_suffix_min(ctx->temp.p, tb, ctx->bfirst.as<int>(), m->plane_start.as<int>(), nbuckets + 1,
+                              ctx->stream));
+    return IBTK_LE_OK;
+}
+
 extern "C" int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_patch_geom* geom, int kernel,
                                    const double* X_dev, const int* indices_dev, const double* Xshift_dev,
                                    int nindices) {
@@ -660,8 +678,7 @@ static int markers_bin_impl(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_pa
                         ctx->vals_in.as<int>(), m->sorted_l.as<int>(), n, end_bit, s));
     p.sorted_l = m->sorted_l.as<int>();
     if (cols) {  // gather fused with the bucket starts
-        HIP_TRY(launch_gather_col(kernel, p, n, m->sorted_s.as<int>(), m->sorted_X.as<double>(),
-                                  m->sorted_key.as<unsigned>(), nplanes, m->plane_start.as<int>(), s));
+        if ((rc = gather_buckets(ctx, m, kernel, p, n, nplanes))) return rc;
         if (int rc2 = build_items(ctx, m, kernel)) return rc2;
     } else {
         HIP_TRY(launch_brick_start(m->sorted_key.as<unsigned>(), n, nplanes, bg.shift - (geom->ndim == 3 ? 3 : 4),
@@ -1086,8 +1103,7 @@ extern "C" int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch,
     HIP_TRY(launch_sort(ctx->temp.p, tb, ctx->keys_in.as<unsigned>(), m->sorted_key.as<unsigned>(),
                         ctx->vals_in.as<int>(), m->sorted_l.as<int>(), n, end_bit, s));
     p.sorted_l = m->sorted_l.as<int>();
-    HIP_TRY(launch_gather_col(kernel, p, n, m->sorted_s.as<int>(), m->sorted_X.as<double>(),
-                              m->sorted_key.as<unsigned>(), (int)nb, m->plane_start.as<int>(), s));
+    if ((rc = gather_buckets(ctx, m, kernel, p, n, (int)nb))) return rc;
     return build_items(ctx, m, kernel);
 }
 
@@ -1204,7 +1220,7 @@ extern "C" int ibtk_le_level_select_interior(ibtk_le_ctx ctx, ibtk_le_markers m,
     if ((rc = m->qin.ensure(sizeof(int) * (size_t)std::max(m->n, 1)))) return rc;
     if ((rc = m->owner.ensure(sizeof(int) * (size_t)std::max(n_markers, 1)))) return rc;
     if ((rc = m->int_off.ensure(sizeof(int) * (size_t)(np + 1)))) return rc;
-    const int nblk = (std::max(m->n, 1) + BLOCK - 1) / BLOCK;  // per-block counts of the kept entries
+    const int nblk = CHECK_STRIPES;  // the kept entries' count, striped over CHECK_STRIPES counters
     if ((rc = ctx->counts.ensure(sizeof(int) * (size_t)nblk))) return rc;
     HIP_TRY(hipMemcpyAsync(m->int_off.p, interior_offsets, sizeof(int) * (size_t)(np + 1), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(m->owner.p, 0xff, sizeof(int) * (size_t)std::max(n_markers, 1), s));

@@ -1052,15 +1052,16 @@ __global__ __launch_bounds__(BLOCK) void k_interior_targets(const int* sorted_l,
                            xshift[3 * (int64_t)l + 2] == 0.0;
         qin[e] = keep ? s : -1;
     }
-    // the block's count into found[blockIdx.x] (one atomic per wave into LDS, no
-    // global atomics on one address: 2.1 ms of contention on cfg5's 1.3e7 entries)
+    // the block's count into one of CHECK_STRIPES counters (one atomic per wave
+    // into LDS, one per block into global memory, spread over the stripes: a single
+    // global address took 2.1 ms of contention on cfg5's 1.3e7 entries)
     __shared__ int cnt;
     if (threadIdx.x == 0) cnt = 0;
     __syncthreads();
     const unsigned long long b = __ballot(keep);
     if ((threadIdx.x & 63) == 0 && b) atomicAdd(&cnt, __popcll(b));
     __syncthreads();
-    if (threadIdx.x == 0) found[blockIdx.x] = cnt;
+    if (threadIdx.x == 0 && cnt) atomicAdd(found + (blockIdx.x % CHECK_STRIPES), cnt);
 }
 hipError_t launch_interior_targets(const int* sorted_l, const int* sorted_s, const int* entry_off, int npatch,
                                    const double* xshift, const int* owner, int n, int* qin, int* found,

@@ -190,6 +190,7 @@ hipError_t launch_mark(int ndim, int kernel, const Params& p, int n, unsigned ch
 hipError_t launch_sort(void* temp, size_t& temp_bytes, const unsigned* kin, unsigned* kout, const int* vin,
                        int* vout, int n, int end_bit, hipStream_t s);
 hipError_t launch_scan(void* temp, size_t& temp_bytes, const int* in, int* out, int n, hipStream_t s);
+hipError_t launch_suffix_min(void* temp, size_t& temp_bytes, const int* in, int* out, int n, hipStream_t s);
 
 // 3-D column sweep (le_sweep.hip)
 hipError_t launch_bin_col(int kernel, const Params& p, int n, unsigned* keys, int* vals, hipStream_t s);
@@ -319,6 +320,7 @@ struct WrapBox {
 };
 hipError_t launch_wrap_positions(const WrapBox& w, long long n, double* X, hipStream_t s);
 // sum(count[0:ncount]) != expect: atomicOr(err, bit)
+constexpr int CHECK_STRIPES = 64;  // counters k_interior_targets adds its block counts into
 hipError_t launch_check_count(const int* count, int ncount, int expect, int* err, int bit, hipStream_t s);
 // out[i * depth + k] = in[order[i] * depth + k]
 hipError_t launch_rows_gather(const int* order, int n, const double* in, int depth, double* out, hipStream_t s);

@@ -5,6 +5,7 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/reverse_iterator.hpp>
 
 #include "le_internal.h"
 
@@ -43,6 +44,13 @@ hipError_t launch_sort(void* temp, size_t& temp_bytes, const unsigned* kin, unsi
 
 hipError_t launch_scan(void* temp, size_t& temp_bytes, const int* in, int* out, int n, hipStream_t s) {
     return rocprim::exclusive_scan(temp, temp_bytes, in, out, 0, (size_t)n, rocprim::plus<int>(), s, false);
+}
+
+// out[i] = min(in[i..n-1]): the bucket starts from the first entry of every
+// non-empty bucket (an empty bucket starts where the next non-empty one does)
+hipError_t launch_suffix_min(void* temp, size_t& temp_bytes, const int* in, int* out, int n, hipStream_t s) {
+    return rocprim::inclusive_scan(temp, temp_bytes, rocprim::make_reverse_iterator(in + n),
+                                   rocprim::make_reverse_iterator(out + n), (size_t)n, rocprim::minimum<int>(), s, false);
 }
 
 }  // namespace ibtk_le

@@ -155,31 +155,22 @@ __global__ __launch_bounds__(BLOCK) void k_bin_col(Params p, int n, unsigned* ke
     vals[i] = i;
 }
 
-// Buckets opened by one entry in k_gather_col; a longer run (the empty columns
-// and patches around clustered markers: a serial walk of millions of buckets by
-// one thread) is left to k_bucket_fix's binary searches.
-constexpr int GATHER_GAP = 32;
-
 // Per sorted entry e: the marker index and the shifted position (coalesced for
-// the sweeps), fused with the bucket starts: entry e > 0 opens every bucket in
-// (key[e-1], key[e]] (keys >= nbuckets: binned outside).  The buckets before
-// the first key and after the last one are k_bucket_ends' (one thread each:
-// a single thread walking them would serialise the launch).  n > 0.
+// the sweeps), fused with the bucket starts: the first entry of every non-empty
+// bucket writes its index into first[] (keys >= nbuckets: binned outside, bucket
+// nbuckets), which k_bucket_init set to n; a suffix-min scan over first[] then
+// gives every bucket's start (launch_suffix_min).  n > 0.
 // The block's 3 BLOCK positions leave through LDS as 16-byte stores (a wave's
 // 8-byte stores at a 24-byte stride would write each cache line in thirds).
 template <int K>
 __global__ __launch_bounds__(BLOCK) void k_gather_col(Params p, int n, int* sorted_s, double* sorted_X,
-                                                      const unsigned* skeys, int nbuckets, int* bs) {
+                                                      const unsigned* skeys, int nbuckets, int* first) {
     __shared__ double sx[3 * BLOCK];
     const int e0 = blockIdx.x * BLOCK;
     const int e = e0 + threadIdx.x;
     if (e < n) {
-        if (e > 0) {
-            const int bi = (int)min(skeys[e], (unsigned)nbuckets);
-            const int bp = (int)min(skeys[e - 1], (unsigned)nbuckets);
-            if (bi - bp <= GATHER_GAP)  // longer runs of empty buckets: k_bucket_fix
-                for (int b = bp + 1; b <= bi; ++b) bs[b] = e;
-        }
+        const int bi = (int)min(skeys[e], (unsigned)nbuckets);
+        if (e == 0 || bi != (int)min(skeys[e - 1], (unsigned)nbuckets)) first[bi] = e;
         const int l = p.sorted_l[e];
         const int s = p.indices ? p.indices[l] : l;
         sorted_s[e] = s;
@@ -1288,36 +1279,18 @@ template <int K> hipError_t launch_bin_col_t(const Params& p, int n, unsigned* k
     hipLaunchKernelGGL(k_bin_col<K>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, keys, vals);
     return hipGetLastError();
 }
-// bucket starts before the first and after the last sorted key; -1 (k_bucket_fix)
-// in between
-__global__ __launch_bounds__(BLOCK) void k_bucket_ends(const unsigned* skeys, int n, int nbuckets, int* bs) {
+__global__ __launch_bounds__(BLOCK) void k_bucket_init(int n, int nbuckets, int* first) {
     const int b = blockIdx.x * BLOCK + threadIdx.x;
-    if (b > nbuckets) return;
-    const int first = (int)min(skeys[0], (unsigned)nbuckets), last = (int)min(skeys[n - 1], (unsigned)nbuckets);
-    bs[b] = b <= first ? 0 : (b > last ? n : -1);
-}
-// the buckets k_gather_col left (long empty runs): the first entry whose key >= b
-__global__ __launch_bounds__(BLOCK) void k_bucket_fix(const unsigned* skeys, int n, int nbuckets, int* bs) {
-    const int b = blockIdx.x * BLOCK + threadIdx.x;
-    if (b > nbuckets || bs[b] >= 0) return;
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if ((int)min(skeys[mid], (unsigned)nbuckets) < b) lo = mid + 1;
-        else hi = mid;
-    }
-    bs[b] = lo;
+    if (b <= nbuckets) first[b] = n;
 }
 
 template <int K>
 hipError_t launch_gather_col_t(const Params& p, int n, int* ss, double* sx, const unsigned* skeys, int nbuckets,
-                               int* bs, hipStream_t s) {
+                               int* first, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    const dim3 gb((nbuckets + 1 + BLOCK - 1) / BLOCK);
-    hipLaunchKernelGGL(k_bucket_ends, gb, dim3(BLOCK), 0, s, skeys, n, nbuckets, bs);
+    hipLaunchKernelGGL(k_bucket_init, dim3((nbuckets + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, n, nbuckets, first);
     hipLaunchKernelGGL(k_gather_col<K>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, n, ss, sx, skeys,
-                       nbuckets, bs);
-    hipLaunchKernelGGL(k_bucket_fix, gb, dim3(BLOCK), 0, s, skeys, n, nbuckets, bs);
+                       nbuckets, first);
     return hipGetLastError();
 }
 template <int K>
