@@ -695,6 +695,40 @@ def main():
         acc["zero"].append(E[2].elapsed_time(E[3]))
         acc["spread"].append(E[3].elapsed_time(E[4]))
 
+    # N > 1 overlap self-check on this backend (RCCL in the product), before the timed
+    # steps: the overlapped exchanges (interior sweep items running while the ghost
+    # planes are in flight on the communicator's stream) must give the bits of the
+    # sequential form on every rank; if they do not, the timed steps use the
+    # sequential exchange (and the record says so)
+    overlap_check = None
+    if world > 1 and not args.no_overlap and gm is None:
+        Xb = cur["X"]
+        Uo, Us = torch.empty_like(cur["U"]), torch.empty_like(cur["U"])
+        ex_u.halo_fill(lambda: le.interp(ctx, bins, kernel, "side", geom, u, Uo, Xb))
+        ex_u.halo_fill()
+        le.interp(ctx, bins, kernel, "side", geom, u, Us, Xb)
+        fo = []
+        for overlapped in (True, False):
+            for a in f:
+                a.zero_()
+            if overlapped:
+                ex_f.ghost_sum(lambda: le.spread(ctx, bins, kernel, "side", geom, f, cur["F"], Xb))
+            else:
+                le.spread(ctx, bins, kernel, "side", geom, f, cur["F"], Xb)
+                ex_f.ghost_sum()
+            fo.append([a.clone() for a in f])
+        same = torch.equal(Uo, Us) and all(torch.equal(a, b) for a, b in zip(*fo))
+        t = torch.tensor([0 if same else 1], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        del fo, Uo, Us
+        if int(t.item()) == 0:
+            overlap_check = "bitwise equal to the sequential exchange on every rank"
+        else:
+            overlap_check = "DIFFERS from the sequential exchange: timed with the sequential exchange"
+            args.no_overlap = True
+            log("overlap self-check FAILED: overlapped exchange differs from the sequential one; "
+                "the timed steps use the sequential exchange")
+
     for _ in range(args.warmup):
         step(False)
     ctx.synchronize()
@@ -734,35 +768,6 @@ def main():
         ctx.synchronize()
         kt["spread"].append(ctx.last_kernel_ms())
     ctx.enable_timing(False)
-
-    # N > 1 overlap self-check on this backend (RCCL in the product): the overlapped
-    # exchanges (interior sweep items running while the ghost planes are in flight on
-    # the communicator's stream) must give the bits of the sequential form, on every rank
-    overlap_check = None
-    if world > 1 and not args.no_overlap and gm is None:
-        Xb = cur["X"]
-        Uo, Us = torch.empty_like(cur["U"]), torch.empty_like(cur["U"])
-        ex_u.halo_fill(lambda: le.interp(ctx, bins, kernel, "side", geom, u, Uo, Xb))
-        ex_u.halo_fill()
-        le.interp(ctx, bins, kernel, "side", geom, u, Us, Xb)
-        fo = []
-        for overlapped in (True, False):
-            for a in f:
-                a.zero_()
-            if overlapped:
-                ex_f.ghost_sum(lambda: le.spread(ctx, bins, kernel, "side", geom, f, cur["F"], Xb))
-            else:
-                le.spread(ctx, bins, kernel, "side", geom, f, cur["F"], Xb)
-                ex_f.ghost_sum()
-            fo.append([a.clone() for a in f])
-        same = torch.equal(Uo, Us) and all(torch.equal(a, b) for a, b in zip(*fo))
-        t = torch.tensor([0 if same else 1], dtype=torch.int64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        overlap_check = "bitwise equal to the sequential exchange on every rank" if int(t.item()) == 0 else \
-            "DIFFERS from the sequential exchange"
-        del fo, Uo, Us
-        if int(t.item()):
-            log("overlap self-check FAILED: overlapped exchange differs from the sequential one")
 
     ms_per_step = 1e3 * elapsed / args.steps
     value = 2.0 * M_total * args.steps / elapsed

@@ -418,7 +418,6 @@ class Level:
 
     def _arrays(self, arrays):
         # the pointer table of a list of per-patch arrays, cached on the list object
-        # (a level reuses its u and f arrays step after step)
         # (a level reuses its u and f arrays step after step); reused only when every
         # entry still has the device pointer it had, so an array replaced in place
         # (arrays[q] = new tensors) rebuilds the table
