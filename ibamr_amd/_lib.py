@@ -100,6 +100,14 @@ _SIGS = [
     ("ibtk_le_spread", c_int,
      [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_int,
       c_void_p, c_int, c_void_p]),
+    ("ibtk_le_set_user_kernel", c_int, [c_void_p, c_int]),
+    ("ibtk_le_user_kernel", c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_int)]),
+    ("ibtk_le_user_interp", c_int,
+     [c_void_p, c_int, c_int, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_int, c_void_p, c_int, c_void_p,
+      c_void_p, c_void_p, c_int]),
+    ("ibtk_le_user_spread", c_int,
+     [c_void_p, c_int, c_int, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_int, c_void_p, c_int, c_void_p,
+      c_void_p, c_void_p, c_int]),
     ("ibtk_le_spread_ds", c_int,
      [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_int,
       c_void_p, c_int, c_void_p, c_void_p]),

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/ibtk_le.h"
@@ -49,16 +50,51 @@ static const char* const kNames[K_COUNT] = {"PIECEWISE_CONSTANT", "DISCONTINUOUS
                                             "IB_4_W8",            "IB_6",                 "BSPLINE_4"};
 static const int kStencil[K_COUNT] = {1, 2, 2, 4, 4, 4, 8, 6, 4};
 
+// USER_DEFINED (LEInteractor.cpp:651-652): the user's kernel function and its
+// stencil size, IB_4's by default (ib4_kernel_fcn, LEInteractor.cpp:629-648)
+static double ib4_kernel_fcn(double r) {
+    r = std::abs(r);
+    if (r < 1.0) {
+        const double t2 = r * r;
+        const double t6 = std::sqrt(-0.4e1 * t2 + 0.4e1 * r + 0.1e1);
+        return -r / 0.4e1 + 0.3e1 / 0.8e1 + t6 / 0.8e1;
+    } else if (r < 2.0) {
+        const double t2 = r * r;
+        const double t6 = std::sqrt(0.12e2 * r - 0.7e1 - 0.4e1 * t2);
+        return -r / 0.4e1 + 0.5e1 / 0.8e1 - t6 / 0.8e1;
+    }
+    return 0.0;
+}
+static ibtk_le_user_kernel_fn g_user_fcn = &ib4_kernel_fcn;
+static int g_user_size = 4;
+constexpr int USER_MAX_STENCIL = 16;
+
+extern "C" int ibtk_le_set_user_kernel(ibtk_le_user_kernel_fn fcn, int stencil_size) {
+    if (stencil_size < 1 || stencil_size > USER_MAX_STENCIL)
+        return fail(IBTK_LE_ERR_ARG, "user kernel stencil size %d outside [1, %d]", stencil_size, USER_MAX_STENCIL);
+    g_user_fcn = fcn ? fcn : &ib4_kernel_fcn;
+    g_user_size = stencil_size;
+    return IBTK_LE_OK;
+}
+extern "C" int ibtk_le_user_kernel(ibtk_le_user_kernel_fn* fcn, int* stencil_size) {
+    if (fcn) *fcn = g_user_fcn;
+    if (stencil_size) *stencil_size = g_user_size;
+    return IBTK_LE_OK;
+}
+
 extern "C" int ibtk_le_kernel_from_name(const char* name) {
     if (!name) return -1;
     for (int k = 0; k < K_COUNT; ++k)
         if (std::strcmp(name, kNames[k]) == 0) return k;
+    if (std::strcmp(name, "USER_DEFINED") == 0) return IBTK_LE_KERNEL_USER_DEFINED;
     return -1;
 }
 extern "C" const char* ibtk_le_kernel_name(int kernel) {
+    if (kernel == IBTK_LE_KERNEL_USER_DEFINED) return "USER_DEFINED";
     return (kernel >= 0 && kernel < K_COUNT) ? kNames[kernel] : nullptr;
 }
 extern "C" int ibtk_le_stencil_size(int kernel) {
+    if (kernel == IBTK_LE_KERNEL_USER_DEFINED) return g_user_size;
     return (kernel >= 0 && kernel < K_COUNT) ? kStencil[kernel] : -1;
 }
 extern "C" int ibtk_le_min_ghost_width(int kernel) {
@@ -99,6 +135,7 @@ struct ibtk_le_ctx_s {
     hipStream_t stream = nullptr;
     DevBuf keys_in, vals_in, temp, counts, offsets, fbuf;
     DevBuf bfirst;  // first entry of every bucket (k_gather_col), before the suffix-min scan
+    DevBuf usr_lo, usr_cnt, usr_w, usr_s, usr_last, usr_x0, usr_x1;  // USER_DEFINED tables
     DevBuf lst_idx, lst_xs, lst_key, lst_perm;  // index-list / node-distribution scratch
     DevBuf lst_cell, lst2_idx, lst2_xs, lst2_cell, lst_flag;  // index lists: cells, the sorted list, unique flags
     DevBuf num_tab, num_lkey, num_ckey;                        // level numbering: tile table, keys
@@ -182,7 +219,8 @@ extern "C" int ibtk_le_ctx_destroy(ibtk_le_ctx ctx) {
     if (!ctx) return IBTK_LE_OK;
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
-    for (DevBuf* b : {&ctx->keys_in, &ctx->vals_in, &ctx->bfirst, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->fbuf, &ctx->err, &ctx->sink,
+    for (DevBuf* b : {&ctx->keys_in, &ctx->vals_in, &ctx->bfirst, &ctx->usr_lo, &ctx->usr_cnt, &ctx->usr_w, &ctx->usr_s,
+                      &ctx->usr_last, &ctx->usr_x0, &ctx->usr_x1, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->fbuf, &ctx->err, &ctx->sink,
                        &ctx->stamps, &ctx->lst_idx, &ctx->lst_xs, &ctx->lst_key, &ctx->lst_perm, &ctx->lst_cell,
                        &ctx->lst2_idx, &ctx->lst2_xs, &ctx->lst2_cell, &ctx->lst_flag, &ctx->num_tab, &ctx->num_lkey,
                        &ctx->num_ckey,
@@ -930,6 +968,163 @@ extern "C" int ibtk_le_spread_ds(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel,
                                  const double* Q_dev, int Q_depth, const double* ds_dev, const double* X_dev) {
     if (!ds_dev && m && m->n > 0) return fail(IBTK_LE_ERR_ARG, "null ds");
     return spread_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, ds_dev, X_dev);
+}
+
+// ---------------------------------------------------------------------------
+// USER_DEFINED kernel function: LEInteractor::userDefinedInterpolate / Spread
+// (LEInteractor.cpp:3141-3266, 3268-3393, dispatched at :2688 and :3007).  The
+// kernel function is a host function pointer, so the host evaluates it: the
+// list's positions come back from the device once, the host forms every entry's
+// clipped stencil and weights per component frame, and the device sums (interp:
+// one lane per entry, the reference's loop order; spread: contributions keyed by
+// grid point, stably sorted and summed point by point in list order -- the
+// sequential l-loop's order, so the result is the reference arithmetic's and
+// bit-stable).  One host synchronization per call.
+// ---------------------------------------------------------------------------
+static int user_call(ibtk_le_ctx ctx, bool spread, int centering, int axis, const ibtk_le_patch_geom* geom,
+                     double* const* q_dev, int q_depth, double* Q_dev, int Q_depth, const double* X_dev,
+                     const int* indices_dev, const double* Xshift_dev, int n) {
+    if (!ctx) return fail(IBTK_LE_ERR_ARG, "null ctx");
+    if (int rc = check_geom(geom)) return rc;
+    if (n < 0) return fail(IBTK_LE_ERR_ARG, "negative list length");
+    const int nd = geom->ndim;
+    const int S = g_user_size;
+    int gmin = geom->gcw[0];
+    for (int d = 1; d < nd; ++d) gmin = std::min(gmin, geom->gcw[d]);
+    if (!spread && gmin < S / 2 + 1)  // LEInteractor.cpp:2416-2426
+        return fail(IBTK_LE_ERR_GHOST_WIDTH,
+                    "LEInteractor::interpolate(): insufficient ghost cells: kernel USER_DEFINED needs %d, ghost width %d",
+                    S / 2 + 1, gmin);
+    const int nc = ncomponents(geom, centering, q_depth, Q_depth);
+    if (nc < 0) return -nc;
+    if (n == 0) return IBTK_LE_OK;
+    if (!X_dev || !Q_dev || !q_dev) return fail(IBTK_LE_ERR_ARG, "null X, Q or q");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    const hipStream_t st = ctx->stream;
+    int rc;
+    if ((rc = ctx->usr_x0.ensure(sizeof(double) * (size_t)n * nd)) || (rc = ctx->usr_x1.ensure(sizeof(double) * (size_t)n * nd)) ||
+        (rc = ctx->usr_s.ensure(sizeof(int) * (size_t)n)))
+        return rc;
+    HIP_TRY(launch_user_gather(X_dev, indices_dev, Xshift_dev, n, nd, ctx->usr_x0.as<double>(), ctx->usr_x1.as<double>(),
+                               ctx->usr_s.as<int>(), st));
+    std::vector<double> Xr((size_t)n * nd), Xs((size_t)n * nd);
+    std::vector<int> sidx((size_t)n);
+    HIP_TRY(hipMemcpyAsync(Xr.data(), ctx->usr_x0.p, sizeof(double) * Xr.size(), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(Xs.data(), ctx->usr_x1.p, sizeof(double) * Xs.size(), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(sidx.data(), ctx->usr_s.p, sizeof(int) * sidx.size(), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<int> last;
+    if (!spread) {  // the last entry naming each marker writes its Q
+        last.assign((size_t)n, 0);
+        std::unordered_map<int, int> at;
+        at.reserve((size_t)n * 2);
+        for (int l = 0; l < n; ++l) at[sidx[l]] = l;
+        for (const auto& kv : at) last[kv.second] = 1;
+        if ((rc = ctx->usr_last.ensure(sizeof(int) * (size_t)n))) return rc;
+        HIP_TRY(hipMemcpyAsync(ctx->usr_last.p, last.data(), sizeof(int) * (size_t)n, hipMemcpyHostToDevice, st));
+    }
+    if ((rc = ctx->usr_lo.ensure(sizeof(int) * (size_t)n * 3)) || (rc = ctx->usr_cnt.ensure(sizeof(int) * (size_t)n * 3)) ||
+        (rc = ctx->usr_w.ensure(sizeof(double) * (size_t)n * 3 * S)))
+        return rc;
+    std::vector<int> lo((size_t)n * 3, 0), cnt((size_t)n * 3, 1);
+    std::vector<double> w((size_t)n * 3 * S, 0.0);
+    for (int c = 0; c < nc; ++c) {
+        Params p;
+        std::memset(&p, 0, sizeof(p));
+        if ((rc = make_comps(geom, centering, axis, q_dev, q_depth, Q_depth, c, 1, p))) return rc;
+        const CompDesc& cd = p.comp[0];
+        if (spread) {
+            int64_t vol = 1;
+            for (int d = 0; d < nd; ++d) vol *= (int64_t)(cd.hi[d] - cd.lo[d] + 1);
+            const int64_t span = (int64_t)(cd.hi[0] - cd.lo[0]) + (nd > 1 ? (int64_t)(cd.hi[1] - cd.lo[1]) * cd.s1 : 0) +
+                                 (nd > 2 ? (int64_t)(cd.hi[2] - cd.lo[2]) * cd.s2 : 0);
+            if (span >= 0xffffffffLL || (int64_t)n * S * S * (nd == 3 ? S : 1) >= (1LL << 31))
+                return fail(IBTK_LE_ERR_RANGE, "USER_DEFINED spread: array or list too large for 32-bit keys");
+            (void)vol;
+        }
+        // userDefinedInterpolate/Spread's stencil and weights (LEInteractor.cpp:3169-3239)
+        for (int l = 0; l < n; ++l) {
+            for (int d = 0; d < nd; ++d) {
+                const double x = Xs[(size_t)nd * l + d];         // X + X_shift
+                const double xraw = Xr[(size_t)nd * l + d];      // X alone (the even-stencil test, :3188)
+                const int center = static_cast<int>(std::floor((x - cd.xlo[d]) / geom->dx[d])) + cd.ilower[d];
+                const double xcell = cd.xlo[d] + (static_cast<double>(center - cd.ilower[d]) + 0.5) * geom->dx[d];
+                int sl, su;
+                if (S % 2 == 0) {
+                    if (xraw < xcell) {
+                        sl = center - S / 2;
+                        su = center + S / 2 - 1;
+                    } else {
+                        sl = center - S / 2 + 1;
+                        su = center + S / 2;
+                    }
+                } else {
+                    sl = center - S / 2;
+                    su = center + S / 2;
+                }
+                sl = std::min(std::max(sl, cd.lo[d]), cd.hi[d]);  // :3209-3213
+                su = std::min(std::max(su, cd.lo[d]), cd.hi[d]);
+                lo[3 * (size_t)l + d] = sl;
+                cnt[3 * (size_t)l + d] = su - sl + 1;
+                double* wl = &w[((size_t)3 * l + d) * S];
+                for (int ic = sl; ic <= su; ++ic)
+                    wl[ic - sl] = g_user_fcn((x - (xcell + static_cast<double>(ic - center) * geom->dx[d])) / geom->dx[d]);
+            }
+        }
+        HIP_TRY(hipMemcpyAsync(ctx->usr_lo.p, lo.data(), sizeof(int) * lo.size(), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(ctx->usr_cnt.p, cnt.data(), sizeof(int) * cnt.size(), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(ctx->usr_w.p, w.data(), sizeof(double) * w.size(), hipMemcpyHostToDevice, st));
+        UserDesc u;
+        std::memset(&u, 0, sizeof(u));
+        u.cd = cd;
+        u.ndim = nd;
+        u.S = S;
+        u.n = n;
+        u.lo = ctx->usr_lo.as<int>();
+        u.cnt = ctx->usr_cnt.as<int>();
+        u.w = ctx->usr_w.as<double>();
+        u.sidx = ctx->usr_s.as<int>();
+        u.last = ctx->usr_last.as<int>();
+        u.Q = Q_dev;
+        u.Qout = Q_dev;
+        u.Q_depth = Q_depth;
+        u.dxprod = nd == 3 ? (geom->dx[0] * geom->dx[1]) * geom->dx[2] : geom->dx[0] * geom->dx[1];
+        if (!spread) {
+            HIP_TRY(launch_user_interp(u, st));
+        } else {
+            const int per = nd == 3 ? S * S * S : S * S;
+            const int ncon = n * per;
+            if ((rc = ctx->keys_in.ensure(sizeof(unsigned) * 2 * (size_t)ncon)) ||
+                (rc = ctx->vals_in.ensure(sizeof(int) * 2 * (size_t)ncon)) ||
+                (rc = ctx->fbuf.ensure(sizeof(double) * (size_t)ncon)))
+                return rc;
+            unsigned* k0 = ctx->keys_in.as<unsigned>();
+            int* v0 = ctx->vals_in.as<int>();
+            HIP_TRY(launch_user_contrib(u, k0, v0, ctx->fbuf.as<double>(), st));
+            size_t tb = 0;
+            HIP_TRY(launch_sort(nullptr, tb, k0, k0 + ncon, v0, v0 + ncon, ncon, 32, st));
+            if ((rc = ctx->temp.ensure(tb))) return rc;
+            tb = ctx->temp.cap;
+            HIP_TRY(launch_sort(ctx->temp.p, tb, k0, k0 + ncon, v0, v0 + ncon, ncon, 32, st));
+            HIP_TRY(launch_user_segsum(u, k0 + ncon, v0 + ncon, ctx->fbuf.as<double>(), ncon, st));
+        }
+        // the host tables are reused by the next component: wait for the uploads
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    return IBTK_LE_OK;
+}
+
+extern "C" int ibtk_le_user_interp(ibtk_le_ctx ctx, int centering, int axis, const ibtk_le_patch_geom* geom,
+                                   const double* const* q_dev, int q_depth, double* Q_dev, int Q_depth,
+                                   const double* X_dev, const int* indices_dev, const double* Xshift_dev, int n) {
+    return user_call(ctx, false, centering, axis, geom, const_cast<double* const*>(q_dev), q_depth, Q_dev, Q_depth, X_dev,
+                     indices_dev, Xshift_dev, n);
+}
+extern "C" int ibtk_le_user_spread(ibtk_le_ctx ctx, int centering, int axis, const ibtk_le_patch_geom* geom,
+                                   double* const* q_dev, int q_depth, const double* Q_dev, int Q_depth,
+                                   const double* X_dev, const int* indices_dev, const double* Xshift_dev, int n) {
+    return user_call(ctx, true, centering, axis, geom, q_dev, q_depth, const_cast<double*>(Q_dev), Q_depth, X_dev,
+                     indices_dev, Xshift_dev, n);
 }
 
 static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,

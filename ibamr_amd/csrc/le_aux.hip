@@ -1157,4 +1157,108 @@ hipError_t launch_check_count(const int* count, int ncount, int expect, int* err
     hipLaunchKernelGGL(k_check_count, dim3(1), dim3(BLOCK), 0, s, count, ncount, expect, err, bit);
     return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// USER_DEFINED kernel function (LEInteractor.cpp:3141-3393; host-evaluated weights)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(BLOCK) void k_user_gather(const double* X, const int* indices, const double* Xshift, int n,
+                                                       int ndim, double* Xraw, double* Xsh, int* sidx) {
+    const int l = blockIdx.x * BLOCK + threadIdx.x;
+    if (l >= n) return;
+    const int s = indices ? indices[l] : l;
+    sidx[l] = s;
+    for (int d = 0; d < ndim; ++d) {
+        const double x = X[(int64_t)ndim * s + d];
+        Xraw[(int64_t)ndim * l + d] = x;
+        Xsh[(int64_t)ndim * l + d] = x + (Xshift ? Xshift[(int64_t)ndim * l + d] : 0.0);  // X + X_shift (:3177)
+    }
+}
+hipError_t launch_user_gather(const double* X, const int* indices, const double* Xshift, int n, int ndim, double* Xraw,
+                              double* Xsh, int* sidx, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_user_gather, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, X, indices, Xshift, n, ndim, Xraw,
+                       Xsh, sidx);
+    return hipGetLastError();
+}
+
+__device__ __forceinline__ int64_t user_off(const CompDesc& cd, int i0, int i1, int i2) {
+    return (int64_t)(i0 - cd.lo[0]) + (int64_t)(i1 - cd.lo[1]) * cd.s1 + (int64_t)(i2 - cd.lo[2]) * cd.s2;
+}
+
+// Q(d, s) = sum over ic2, ic1, ic0 of w0 w1 w2 q, from 0 (LEInteractor.cpp:3241-3263); the
+// last entry naming s writes it, as the sequential l-loop leaves it
+__global__ __launch_bounds__(BLOCK) void k_user_interp(UserDesc u) {
+    const int l = blockIdx.x * BLOCK + threadIdx.x;
+    if (l >= u.n || !u.last[l]) return;
+    const int S = u.S;
+    const int* lo = u.lo + 3 * l;
+    const int* cn = u.cnt + 3 * l;
+    const double* w = u.w + (int64_t)3 * S * l;
+    double acc = 0.0;
+    if (u.ndim == 3) {
+        for (int i2 = 0; i2 < cn[2]; ++i2)
+            for (int i1 = 0; i1 < cn[1]; ++i1)
+                for (int i0 = 0; i0 < cn[0]; ++i0)
+                    acc = acc + w[i0] * w[S + i1] * w[2 * S + i2] * u.cd.u[user_off(u.cd, lo[0] + i0, lo[1] + i1, lo[2] + i2)];
+    } else {
+        for (int i1 = 0; i1 < cn[1]; ++i1)
+            for (int i0 = 0; i0 < cn[0]; ++i0)
+                acc = acc + w[i0] * w[S + i1] * u.cd.u[user_off(u.cd, lo[0] + i0, lo[1] + i1, u.cd.lo[2])];
+    }
+    u.Qout[(int64_t)u.Q_depth * u.sidx[l] + u.cd.qcomp] = acc;
+}
+hipError_t launch_user_interp(const UserDesc& u, hipStream_t s) {
+    if (u.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_user_interp, dim3((u.n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, u);
+    return hipGetLastError();
+}
+
+// contribution k of entry l (stencil point k, x fastest): w0 w1 [w2] Q(d, s) / (dx0 dx1 [dx2])
+// (LEInteractor.cpp:3378-3383), keyed by its array offset; points past the clipped
+// stencil are keyed 0xffffffff (sorted last, never summed)
+__global__ __launch_bounds__(BLOCK) void k_user_contrib(UserDesc u, unsigned* keys, int* vals, double* contrib) {
+    const int S = u.S;
+    const int per = u.ndim == 3 ? S * S * S : S * S;
+    const int64_t t = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= (int64_t)u.n * per) return;
+    const int l = (int)(t / per), k = (int)(t - (int64_t)l * per);
+    const int i0 = k % S, i1 = (k / S) % S, i2 = k / (S * S);
+    const int* lo = u.lo + 3 * l;
+    const int* cn = u.cnt + 3 * l;
+    vals[t] = (int)t;
+    if (i0 >= cn[0] || i1 >= cn[1] || (u.ndim == 3 && i2 >= cn[2])) {
+        keys[t] = 0xffffffffu;
+        return;
+    }
+    const double* w = u.w + (int64_t)3 * S * l;
+    const double V = u.Q[(int64_t)u.Q_depth * u.sidx[l] + u.cd.qcomp];
+    const double term = u.ndim == 3 ? w[i0] * w[S + i1] * w[2 * S + i2] * V : w[i0] * w[S + i1] * V;
+    contrib[t] = term / u.dxprod;
+    keys[t] = (unsigned)user_off(u.cd, lo[0] + i0, lo[1] + i1, u.ndim == 3 ? lo[2] + i2 : u.cd.lo[2]);
+}
+hipError_t launch_user_contrib(const UserDesc& u, unsigned* keys, int* vals, double* contrib, hipStream_t s) {
+    const int per = u.ndim == 3 ? u.S * u.S * u.S : u.S * u.S;
+    const int64_t tot = (int64_t)u.n * per;
+    if (tot <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_user_contrib, dim3((unsigned)((tot + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, u, keys, vals,
+                       contrib);
+    return hipGetLastError();
+}
+// one thread per run of equal keys (a grid point): q += c_1, += c_2, ... in list order
+__global__ __launch_bounds__(BLOCK) void k_user_segsum(UserDesc u, const unsigned* skeys, const int* svals,
+                                                       const double* contrib, int nc) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= nc || skeys[e] == 0xffffffffu || (e > 0 && skeys[e - 1] == skeys[e])) return;
+    double* q = u.cd.u + skeys[e];
+    double v = *q;
+    for (int j = e; j < nc && skeys[j] == skeys[e]; ++j) v = v + contrib[svals[j]];
+    *q = v;
+}
+hipError_t launch_user_segsum(const UserDesc& u, const unsigned* skeys, const int* svals, const double* contrib,
+                              int nc, hipStream_t s) {
+    if (nc <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_user_segsum, dim3((nc + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, u, skeys, svals, contrib, nc);
+    return hipGetLastError();
+}
+
 }  // namespace ibtk_le

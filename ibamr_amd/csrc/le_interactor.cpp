@@ -65,6 +65,10 @@ Facade& F() {
 }
 
 int kernel_of(const std::string& name) {
+    // the user-defined kernel function is read at every call, as the reference's
+    // static pointer is (LEInteractor.cpp:651-652)
+    if (name == "USER_DEFINED")
+        Facade::check(ibtk_le_set_user_kernel(LEInteractor::s_kernel_fcn, LEInteractor::s_kernel_fcn_stencil_size));
     const int k = ibtk_le_kernel_from_name(name.c_str());
     if (k < 0)
         throw LEInteractorError(IBTK_LE_ERR_UNKNOWN_KERNEL,
@@ -198,6 +202,10 @@ void interp_locked(Facade& f, const Euler& e, double* Q, int Q_depth, const doub
                                 "LEInteractor::interpolate(): insufficient ghost cells:  kernel function = " + fcn);
     const List l = make_list(f, src, patch, box, X);
     if (l.n == 0) return;  // LEInteractor.cpp:885 (!local_indices.empty())
+    if (k == IBTK_LE_KERNEL_USER_DEFINED) {  // LEInteractor.cpp:2688-2703
+        Facade::check(ibtk_le_user_interp(f.ctx, e.centering, 0, &g, e.arrays, e.q_depth, Q, Q_depth, X, l.idx, l.xs, l.n));
+        return;
+    }
     Facade::check(ibtk_le_markers_bin(f.ctx, f.m, &g, k, X, l.idx, l.xs, l.n));
     Facade::check(ibtk_le_interp(f.ctx, f.m, k, e.centering, 0, &g, e.arrays, e.q_depth, Q, Q_depth, X));
 }
@@ -214,6 +222,10 @@ void spread_locked(Facade& f, const Euler& e, const double* Q, int Q_depth, cons
                                 "function = " + fcn);
     const List l = make_list(f, src, patch, box, X);
     if (l.n == 0) return;
+    if (k == IBTK_LE_KERNEL_USER_DEFINED) {  // LEInteractor.cpp:3007-3022
+        Facade::check(ibtk_le_user_spread(f.ctx, e.centering, 0, &g, e.arrays, e.q_depth, Q, Q_depth, X, l.idx, l.xs, l.n));
+        return;
+    }
     Facade::check(ibtk_le_markers_bin(f.ctx, f.m, &g, k, X, l.idx, l.xs, l.n));
     Facade::check(ibtk_le_spread(f.ctx, f.m, k, e.centering, 0, &g, e.arrays, e.q_depth, Q, Q_depth, X));
 }
@@ -289,6 +301,9 @@ void spread_host(const V& q, const std::vector<double>& Q, int Q_depth, const st
 }
 
 }  // namespace
+
+double (*LEInteractor::s_kernel_fcn)(double r) = nullptr;  // nullptr: ib4_kernel_fcn
+int LEInteractor::s_kernel_fcn_stencil_size = 4;
 
 void LEInteractor::setFromDatabase(const void*) {}
 void LEInteractor::printClassData(std::ostream& os) { os << "LEInteractor::printClassData():\n"; }

@@ -320,6 +320,32 @@ struct WrapBox {
 };
 hipError_t launch_wrap_positions(const WrapBox& w, long long n, double* X, hipStream_t s);
 // sum(count[0:ncount]) != expect: atomicOr(err, bit)
+// USER_DEFINED kernel function (LEInteractor::userDefinedInterpolate / Spread,
+// LEInteractor.cpp:3141-3393): the host evaluates the user's phi(r) for every list
+// entry (phi is a host function pointer); the device sums and spreads.  Per entry
+// l and dim d: the clipped stencil's first index lo[3 l + d], its length cnt[3 l + d]
+// and its weights w[(3 l + d) S + i].
+struct UserDesc {
+    CompDesc cd;
+    int ndim, S, n;
+    const int* lo;
+    const int* cnt;
+    const double* w;
+    const int* sidx;   // entry -> marker
+    const int* last;   // interp: 1 if the entry is the last one naming its marker (it writes Q)
+    const double* Q;   // spread: marker values
+    double* Qout;      // interp: marker values
+    int Q_depth;
+    double dxprod;     // spread: dx0 dx1 [dx2], associated as the reference does
+};
+hipError_t launch_user_gather(const double* X, const int* indices, const double* Xshift, int n, int ndim, double* Xraw,
+                              double* Xsh, int* sidx, hipStream_t s);
+hipError_t launch_user_interp(const UserDesc& u, hipStream_t s);
+// spread, deterministic: per-point contributions keyed by array offset, stably sorted,
+// then summed point by point in list order (the reference's sequential l-loop)
+hipError_t launch_user_contrib(const UserDesc& u, unsigned* keys, int* vals, double* contrib, hipStream_t s);
+hipError_t launch_user_segsum(const UserDesc& u, const unsigned* skeys, const int* svals, const double* contrib,
+                              int ncontrib, hipStream_t s);
 constexpr int CHECK_STRIPES = 64;  // counters k_interior_targets adds its block counts into
 hipError_t launch_check_count(const int* count, int ncount, int expect, int* err, int bit, hipStream_t s);
 // out[i * depth + k] = in[order[i] * depth + k]

@@ -330,6 +330,50 @@ def spread(ctx: Context, markers: Markers, kernel: str, centering: str, geom: Ge
                                         ctypes.byref(geom.c), arr, q_depth, _ptr(Q), Q_depth, _ptr(ds), _ptr(X)))
 
 
+# USER_DEFINED kernel function (LEInteractor::s_kernel_fcn, LEInteractor.h:100-101):
+# a Python callable phi(r) -> float, called by the library on the host
+USER_KERNEL_FN = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.c_double)
+_user_fn_ref = None  # the ctypes callback the library holds (kept alive here)
+
+
+def set_user_kernel(fcn, stencil_size: int):
+    """LEInteractor::s_kernel_fcn = fcn; s_kernel_fcn_stencil_size = stencil_size.
+    fcn None restores the default (ib4_kernel_fcn, stencil 4)."""
+    global _user_fn_ref
+    lib = _lib.load()
+    cb = USER_KERNEL_FN(fcn) if fcn is not None else None
+    check(lib.ibtk_le_set_user_kernel(ctypes.cast(cb, ctypes.c_void_p) if cb is not None else None, int(stencil_size)))
+    _user_fn_ref = cb
+
+
+def _user_call(fn, ctx, centering, geom, q, Q, X, indices, xshift, q_depth, Q_depth, axis):
+    if Q_depth is None:
+        Q_depth = geom.ndim if centering in ("side", "edge") else q_depth
+    n = indices.numel() if indices is not None else X.shape[0]
+    if indices is not None and indices.dtype != torch.int32:
+        raise ValueError("indices: int32")
+    if xshift is not None and (xshift.dtype != torch.float64 or xshift.numel() != n * geom.ndim):
+        raise ValueError("xshift: float64, NDIM per list entry")
+    check(fn(ctx.h, CENTERING[centering], axis, ctypes.byref(geom.c), _ptr_array(q, geom), q_depth, _ptr(Q), Q_depth,
+             _ptr(X), _ptr(indices), _ptr(xshift), n))
+
+
+def user_interp(ctx: Context, centering: str, geom: Geometry, q: Sequence[torch.Tensor], Q: torch.Tensor,
+                X: torch.Tensor, indices: Optional[torch.Tensor] = None, xshift: Optional[torch.Tensor] = None,
+                q_depth: int = 1, Q_depth: Optional[int] = None, axis: int = 0):
+    """Q(d, s) = sum w q with the USER_DEFINED kernel (LEInteractor::userDefinedInterpolate,
+    LEInteractor.cpp:3141-3266) over the list (indices, xshift)."""
+    _user_call(ctx.lib.ibtk_le_user_interp, ctx, centering, geom, q, Q, X, indices, xshift, q_depth, Q_depth, axis)
+
+
+def user_spread(ctx: Context, centering: str, geom: Geometry, q: Sequence[torch.Tensor], Q: torch.Tensor,
+                X: torch.Tensor, indices: Optional[torch.Tensor] = None, xshift: Optional[torch.Tensor] = None,
+                q_depth: int = 1, Q_depth: Optional[int] = None, axis: int = 0):
+    """q += S Q with the USER_DEFINED kernel (LEInteractor::userDefinedSpread,
+    LEInteractor.cpp:3268-3393): every grid point summed in list order."""
+    _user_call(ctx.lib.ibtk_le_user_spread, ctx, centering, geom, q, Q, X, indices, xshift, q_depth, Q_depth, axis)
+
+
 class Level:
     """A level of 3-D patches binned together (ibtk_le_level_bin): LDataManager's
     patch loop (LDataManager.cpp:625-660, 763-807) as one launch per sweep.

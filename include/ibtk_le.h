@@ -50,7 +50,8 @@ typedef enum {
     IBTK_LE_KERNEL_IB_4 = 5,
     IBTK_LE_KERNEL_IB_4_W8 = 6,
     IBTK_LE_KERNEL_IB_6 = 7,
-    IBTK_LE_KERNEL_BSPLINE_4 = 8 /* not in the reference: cubic B-spline */
+    IBTK_LE_KERNEL_BSPLINE_4 = 8, /* not in the reference: cubic B-spline */
+    IBTK_LE_KERNEL_USER_DEFINED = 9 /* LEInteractor::s_kernel_fcn: ibtk_le_user_interp / ibtk_le_user_spread */
 } ibtk_le_kernel;
 
 /* ---- data centerings (SAMRAI pdat::{Cell,Side,Node,Edge}Data) ---------------- */
@@ -91,6 +92,15 @@ typedef struct ibtk_le_markers_s* ibtk_le_markers;
 /* ---- kernel-string helpers ---------------------------------------------------- */
 /* Returns the kernel id for "IB_4", "IB_6", ... or -1 (LEInteractor.cpp:668-682). */
 int ibtk_le_kernel_from_name(const char* name);
+
+/* The USER_DEFINED kernel function: LEInteractor::s_kernel_fcn and
+ * s_kernel_fcn_stencil_size (LEInteractor.h:100-101, LEInteractor.cpp:651-652), a
+ * host function phi(r) of the signed distance in grid spacings, IB_4's
+ * (ib4_kernel_fcn, LEInteractor.cpp:629-648) with stencil size 4 until set.
+ * fcn == NULL restores the default.  stencil_size in [1, 16]. */
+typedef double (*ibtk_le_user_kernel_fn)(double r);
+int ibtk_le_set_user_kernel(ibtk_le_user_kernel_fn fcn, int stencil_size);
+int ibtk_le_user_kernel(ibtk_le_user_kernel_fn* fcn, int* stencil_size);
 const char* ibtk_le_kernel_name(int kernel);
 /* LEInteractor::getStencilSize / getMinimumGhostWidth (LEInteractor.cpp:668-687). */
 int ibtk_le_stencil_size(int kernel);
@@ -170,6 +180,27 @@ int ibtk_le_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering
 int ibtk_le_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                    const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
                    int Q_depth, const double* X_dev);
+
+/* USER_DEFINED interpolation and spreading: LEInteractor::userDefinedInterpolate /
+ * userDefinedSpread (LEInteractor.cpp:3141-3266, 3268-3393), the branches of the
+ * private interpolate()/spread() at :2688 and :3007.  Arguments as ibtk_le_interp /
+ * ibtk_le_spread, with the list given directly (no binning): indices_dev (n list
+ * entries -> marker, NULL: entry l is marker l) and Xshift_dev (n x NDIM, NULL:
+ * zero).  Per entry and dimension: stencil centre floor((X+Xshift-x_lower)/dx) +
+ * ilower; an even stencil starts below or above it as the UNSHIFTED X lies below
+ * or above the cell centre (:3188, as the reference compares); the stencil is
+ * clipped into the ghost box; weights phi((X+Xshift - x_i)/dx).  phi is a host
+ * function: the host evaluates it (one synchronization per call), the device
+ * sums.  interp: Q(d, s) = sum w0 w1 [w2] q in the reference's loop order (the
+ * last entry naming s writes it); spread: q += w0 w1 [w2] Q(d, s) / (dx0 dx1
+ * [dx2]), every grid point summed in list order (bit-stable; the reference's
+ * sequential order). */
+int ibtk_le_user_interp(ibtk_le_ctx ctx, int centering, int axis, const ibtk_le_patch_geom* geom,
+                        const double* const* q_dev, int q_depth, double* Q_dev, int Q_depth, const double* X_dev,
+                        const int* indices_dev, const double* Xshift_dev, int n);
+int ibtk_le_user_spread(ibtk_le_ctx ctx, int centering, int axis, const ibtk_le_patch_geom* geom,
+                        double* const* q_dev, int q_depth, const double* Q_dev, int Q_depth, const double* X_dev,
+                        const int* indices_dev, const double* Xshift_dev, int n);
 
 /* Density-weighted spread, f += S (F ds): LDataManager::spread with ds_data
  * (LDataManager.cpp:398-470), which forms F_ds[k][d] = F[k][d] * ds[k] and then

@@ -125,6 +125,12 @@ using LIndexSetView = LIndexSetDataView<LNode>;
 
 class LEInteractor {
 public:
+    // The USER_DEFINED kernel function and its stencil size (LEInteractor.h:100-101):
+    // read at every USER_DEFINED call.  nullptr = IB_4's kernel function
+    // (ib4_kernel_fcn, LEInteractor.cpp:629-648), the reference's initial value.
+    static double (*s_kernel_fcn)(double r);
+    static int s_kernel_fcn_stencil_size;
+
     static void setFromDatabase(const void* db = nullptr);  // no settable data (LEInteractor.cpp:654-658)
     static void printClassData(std::ostream& os);
     static int getStencilSize(const std::string& kernel_fcn);

@@ -540,3 +540,81 @@ int ora_spread(int kernel, int ndim, const double* dx, const double* x_lower, in
     return ora_dispatch(kernel, 1, ndim, dx, x_lower, depth, axis, ilower, iupper, nugc, u, indices, Xshift, nindices,
                         X, (double*)V);
 }
+
+/* ---------------------------------------------------------------------- */
+/* USER_DEFINED: LEInteractor::userDefinedInterpolate / userDefinedSpread   */
+/* (LEInteractor.cpp:3141-3266, 3268-3393), a host kernel function phi(r)  */
+/* ---------------------------------------------------------------------- */
+static void ora_user(double (*phi)(double), int S, int spread, const ora_box* b, const double* dx,
+                     const double* x_lower, int depth, const int* ilower, const int* iupper, const int* nugc,
+                     double* u, const int* indices, const double* Xshift, int n, const double* X, double* V)
+{
+    const int nd = b->ndim;
+    double w[3][64];
+    for (int l = 0; l < n; ++l) {
+        const int s = indices[l];
+        int center[3] = {0, 0, 0}, lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+        double xcell[3] = {0.0, 0.0, 0.0};
+        for (int d = 0; d < nd; ++d) { /* :3174-3180 */
+            center[d] = (int)floor((X[d + s * nd] + Xshift[d + l * nd] - x_lower[d]) / dx[d]) + ilower[d];
+            xcell[d] = x_lower[d] + ((double)(center[d] - ilower[d]) + 0.5) * dx[d];
+        }
+        for (int d = 0; d < nd; ++d) { /* :3184-3207 (the unshifted X against the cell centre) */
+            if (S % 2 == 0) {
+                if (X[d + s * nd] < xcell[d]) {
+                    lo[d] = center[d] - S / 2;
+                    hi[d] = center[d] + S / 2 - 1;
+                } else {
+                    lo[d] = center[d] - S / 2 + 1;
+                    hi[d] = center[d] + S / 2;
+                }
+            } else {
+                lo[d] = center[d] - S / 2;
+                hi[d] = center[d] + S / 2;
+            }
+        }
+        for (int d = 0; d < nd; ++d) { /* :3209-3213 */
+            lo[d] = imin(imax(lo[d], ilower[d] - nugc[d]), iupper[d] + nugc[d]);
+            hi[d] = imin(imax(hi[d], ilower[d] - nugc[d]), iupper[d] + nugc[d]);
+        }
+        for (int d = 0; d < nd; ++d) /* :3216-3238 */
+            for (int ic = lo[d]; ic <= hi[d]; ++ic)
+                w[d][ic - lo[d]] =
+                    phi((X[d + s * nd] + Xshift[d + l * nd] - (xcell[d] + (double)(ic - center[d]) * dx[d])) / dx[d]);
+        const int lo2 = nd == 3 ? lo[2] : 0, hi2 = nd == 3 ? hi[2] : 0;
+        for (int dd = 0; dd < depth; ++dd) {
+            if (!spread) V[dd + s * depth] = 0.0; /* :3243 */
+            for (int ic2 = lo2; ic2 <= hi2; ++ic2)
+                for (int ic1 = lo[1]; ic1 <= hi[1]; ++ic1)
+                    for (int ic0 = lo[0]; ic0 <= hi[0]; ++ic0) {
+                        const int64_t k = ora_idx(b, ic0, ic1, ic2, dd);
+                        if (nd == 3) {
+                            const double ww = w[0][ic0 - lo[0]] * w[1][ic1 - lo[1]] * w[2][ic2 - lo2];
+                            if (spread) /* :3381-3382 */
+                                u[k] += ww * V[dd + s * depth] / (dx[0] * dx[1] * dx[2]);
+                            else /* :3256 */
+                                V[dd + s * depth] += ww * u[k];
+                        } else {
+                            const double ww = w[0][ic0 - lo[0]] * w[1][ic1 - lo[1]];
+                            if (spread) /* :3378 */
+                                u[k] += ww * V[dd + s * depth] / (dx[0] * dx[1]);
+                            else /* :3253 */
+                                V[dd + s * depth] += ww * u[k];
+                        }
+                    }
+        }
+    }
+}
+
+int ora_user_call(double (*phi)(double), int S, int spread, int ndim, const double* dx, const double* x_lower,
+                  int depth, const int* ilower, const int* iupper, const int* nugc, double* u, const int* indices,
+                  const double* Xshift, int nindices, const double* X, double* V)
+{
+    ora_box b;
+    if (ndim != 2 && ndim != 3) return -1;
+    if (S < 1 || S > 64) return -3;
+    ora_box_init(&b, ndim, ilower, iupper, nugc);
+    if (nindices <= 0) return 0;
+    ora_user(phi, S, spread, &b, dx, x_lower, depth, ilower, iupper, nugc, u, indices, Xshift, nindices, X, V);
+    return 0;
+}

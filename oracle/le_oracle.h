@@ -47,6 +47,11 @@ int ora_phys_bdry_side(int ndim, const int* ilower, const int* iupper, int gcw, 
                        double* u1, double* u2, const int* phys, const double* acoef, const double* bcoef,
                        const double* gcoef, int adjoint);
 
+/* USER_DEFINED (LEInteractor.cpp:3141-3393): phi a host kernel function, S its stencil size */
+int ora_user_call(double (*phi)(double), int S, int spread, int ndim, const double* dx, const double* x_lower,
+                  int depth, const int* ilower, const int* iupper, const int* nugc, double* u, const int* indices,
+                  const double* Xshift, int nindices, const double* X, double* V);
+
 #ifdef __cplusplus
 }
 #endif

@@ -79,6 +79,9 @@ def lib():
         L.ora_ib_3_delta.argtypes = [ctypes.c_double]
         L.ora_piecewise_cubic_delta.restype = ctypes.c_double
         L.ora_piecewise_cubic_delta.argtypes = [ctypes.c_double]
+        L.ora_user_call.restype = c_int
+        L.ora_user_call.argtypes = [ctypes.c_void_p, c_int, c_int, c_int, dp, dp, c_int, ip, ip, ip, dp, ip, dp, c_int,
+                                    dp, dp]
         L.ora_phys_bdry_side.restype = c_int
         L.ora_phys_bdry_side.argtypes = [c_int, ip, ip, c_int, dp, dp, dp, dp, ip, dp, dp, dp, c_int]
         _lib = L
@@ -99,6 +102,45 @@ def _f64(a):
 
 def _i32(a):
     return np.ascontiguousarray(a, dtype=np.int32)
+
+
+# USER_DEFINED: LEInteractor::s_kernel_fcn / s_kernel_fcn_stencil_size (LEInteractor.cpp:651-652),
+# IB_4's ib4_kernel_fcn (:629-648) and 4 by default
+def ib4_kernel_fcn(r):
+    r = abs(r)
+    if r < 1.0:
+        t2 = r * r
+        t6 = np.sqrt(-0.4e1 * t2 + 0.4e1 * r + 0.1e1)
+        return -r / 0.4e1 + 0.3e1 / 0.8e1 + t6 / 0.8e1
+    if r < 2.0:
+        t2 = r * r
+        t6 = np.sqrt(0.12e2 * r - 0.7e1 - 0.4e1 * t2)
+        return -r / 0.4e1 + 0.5e1 / 0.8e1 - t6 / 0.8e1
+    return 0.0
+
+
+_USER_FN = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.c_double)
+_user = {"fn": ib4_kernel_fcn, "S": 4, "cb": _USER_FN(ib4_kernel_fcn)}
+
+
+def set_user_kernel(fn, stencil_size):
+    """LEInteractor::s_kernel_fcn = fn; s_kernel_fcn_stencil_size = stencil_size (None: the default)."""
+    fn = fn if fn is not None else ib4_kernel_fcn
+    _user.update(fn=fn, S=int(stencil_size), cb=_USER_FN(fn))
+    STENCIL["USER_DEFINED"] = int(stencil_size)
+
+
+STENCIL["USER_DEFINED"] = 4
+
+
+def _user_call(spread_, dx, x_lower, ilower, iupper, nugc, u, indices, Xshift, X, V, depth):
+    ndim = len(ilower)
+    idx, xs, X = _i32(indices), _f64(Xshift), _f64(X)
+    rc = lib().ora_user_call(ctypes.cast(_user["cb"], ctypes.c_void_p), _user["S"], int(spread_), ndim, _dp(_f64(dx)),
+                             _dp(_f64(x_lower)), int(depth), _ip(_i32(ilower)), _ip(_i32(iupper)), _ip(_i32(nugc)),
+                             _dp(u), _ip(idx), _dp(xs), int(idx.size), _dp(X), _dp(V))
+    if rc != 0:
+        raise RuntimeError(f"ora_user_call failed ({rc})")
 
 
 def kernel_id(kernel):
@@ -130,10 +172,15 @@ def ghost_shape(ilower, iupper, nugc, depth=1):
 
 
 def interp(kernel, dx, x_lower, ilower, iupper, nugc, u, indices, Xshift, X, V, depth=1, axis=0):
-    """One call of lagrangian_<kernel>_interp{2,3}d_ (writes V in place)."""
+    """One call of lagrangian_<kernel>_interp{2,3}d_ (writes V in place); USER_DEFINED:
+    LEInteractor::userDefinedInterpolate."""
     ndim = len(ilower)
     u = _f64(u)
     assert u.size == int(np.prod(ghost_shape(ilower, iupper, nugc, depth)))
+    if kernel == "USER_DEFINED":
+        assert V.dtype == np.float64 and V.flags.c_contiguous
+        _user_call(False, dx, x_lower, ilower, iupper, nugc, u, indices, Xshift, X, V, depth)
+        return V
     idx, xs, X = _i32(indices), _f64(Xshift), _f64(X)
     assert V.dtype == np.float64 and V.flags.c_contiguous
     rc = lib().ora_interp(kernel_id(kernel), ndim, _dp(_f64(dx)), _dp(_f64(x_lower)), int(depth), int(axis),
@@ -145,10 +192,14 @@ def interp(kernel, dx, x_lower, ilower, iupper, nugc, u, indices, Xshift, X, V, 
 
 
 def spread(kernel, dx, x_lower, ilower, iupper, nugc, u, indices, Xshift, X, V, depth=1, axis=0):
-    """One call of lagrangian_<kernel>_spread{2,3}d_ (accumulates into u)."""
+    """One call of lagrangian_<kernel>_spread{2,3}d_ (accumulates into u); USER_DEFINED:
+    LEInteractor::userDefinedSpread."""
     ndim = len(ilower)
     assert u.dtype == np.float64 and u.flags.c_contiguous
     assert u.size == int(np.prod(ghost_shape(ilower, iupper, nugc, depth)))
+    if kernel == "USER_DEFINED":
+        _user_call(True, dx, x_lower, ilower, iupper, nugc, u, indices, Xshift, X, _f64(V), depth)
+        return u
     idx, xs, X, V = _i32(indices), _f64(Xshift), _f64(X), _f64(V)
     rc = lib().ora_spread(kernel_id(kernel), ndim, _dp(_f64(dx)), _dp(_f64(x_lower)), int(depth), int(axis),
                           _ip(_i32(ilower)), _ip(_i32(iupper)), _ip(_i32(nugc)), _dp(u), _ip(idx), _dp(xs),

@@ -9,6 +9,7 @@
 //   b  raw device arrays + index set (same lists: must equal a bit for bit)
 //   c  host std::vector, box filter  (markers whose cell is in a sub-box, no shifts)
 //   d  raw device arrays with sizes, box filter (must equal c bit for bit)
+//   u  USER_DEFINED (LEInteractor::s_kernel_fcn), form a's lists
 //   e  LData views + index set over a sub-box reaching into the ghost cells
 //      (buildLocalIndices' box branch, LEInteractor.cpp:3070-3106, through the
 //      index set's cells)
@@ -96,6 +97,13 @@ static size_t asize(const char* c, int a, int depth) {
 }
 
 // the four forms of interp and spread on one data view type
+// the USER_DEFINED form's kernel function: (9/4 - r^2)/4 inside |r| < 3/2 (+ and * only,
+// as tests/test_gpu_boundary.py evaluates it for the oracle)
+static double user_phi3(double r) {
+    const double r2 = r * r;
+    return r2 < 2.25 ? (2.25 - r2) * 0.25 : 0.0;
+}
+
 template <class V>
 static void run(const char* cname, V& u, V& f, int ncomp, int depth, int Qdepth) {
     auto fptr = [&](int a) -> double*& {
@@ -168,6 +176,21 @@ static void run(const char* cname, V& u, V& f, int ncomp, int depth, int Qdepth)
     LEInteractor::spread(f, Sv, Xv, idx, patch, sub, pshift, "IB_4");
     LEInteractor::synchronize();
     save_f("e");
+    // u: USER_DEFINED through LEInteractor::s_kernel_fcn (a 3-point kernel function,
+    // LEInteractor.cpp:2688, 3007), on form a's lists
+    LEInteractor::s_kernel_fcn = &user_phi3;
+    LEInteractor::s_kernel_fcn_stencil_size = 3;
+    HC(hipMemcpy(Qd, init.data(), sizeof(double) * nQ, hipMemcpyHostToDevice));
+    LEInteractor::interpolate(Qv, Xv, idx, u, patch, patch.box, pshift, "USER_DEFINED");
+    LEInteractor::synchronize();
+    h = download(Qd, nQ);
+    save(std::string("Q_") + cname + "_u.bin", h.data(), nQ);
+    zero_f();
+    LEInteractor::spread(f, Sv, Xv, idx, patch, ghost_box, pshift, "USER_DEFINED");
+    LEInteractor::synchronize();
+    save_f("u");
+    LEInteractor::s_kernel_fcn = nullptr;  // the reference's default again (ib4_kernel_fcn)
+    LEInteractor::s_kernel_fcn_stencil_size = 4;
     HC(hipFree(Qd));
     HC(hipFree(Sd));
 }

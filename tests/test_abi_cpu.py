@@ -17,6 +17,7 @@ def declared_functions():
         text = h.read_text()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         text = re.sub(r"//[^\n]*", "", text)
+        text = re.sub(r"\btypedef\b[^;]*;", "", text)  # function-pointer types are not functions
         for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(\w+)\s*\(", text, flags=re.M):
             name = m.group(1)
             if name in ("if", "while", "for", "return", "sizeof", "defined"):
@@ -55,7 +56,8 @@ def test_host_only_helpers(lib):
               "IB_3": 3, "IB_4": 3, "IB_4_W8": 5, "IB_6": 4, "BSPLINE_4": 3}
     for k, g in expect.items():
         assert lib.ibtk_le_min_ghost_width(_lib.kernel_id(k)) == g
-    assert lib.ibtk_le_kernel_from_name(b"USER_DEFINED") == -1
+    assert lib.ibtk_le_kernel_from_name(b"USER_DEFINED") == 9  # ibtk_le_user_interp / _spread
+    assert lib.ibtk_le_stencil_size(9) == 4 and lib.ibtk_le_min_ghost_width(9) == 3  # ib4_kernel_fcn, 4
     with pytest.raises(_lib.IBTKLEError):
         _lib.kernel_id("NOPE")
 

@@ -110,7 +110,9 @@ def test_cpp_facade(tmp_path):
     list (with periodic images), of the sub-box list and of the sub-box markers within
     1e-12 (LEInteractor.cpp:690-2397).  Then a patch with physical faces in x and z:
     too few ghosts throw (LEInteractor.cpp:2729-2745); with enough, spread + the
-    adjoint physical fold (LDataManager.cpp:655-659) within 1e-12 of the oracle."""
+    adjoint physical fold (LDataManager.cpp:655-659) within 1e-12 of the oracle.  Form u:
+    USER_DEFINED through LEInteractor::s_kernel_fcn (a 3-point kernel function) on the
+    index set's lists, against the oracle's userDefinedInterpolate / Spread restatement."""
     from oracle import oracle as ora
     from test_gpu_parity import oracle_call
 
@@ -178,6 +180,26 @@ def test_cpp_facade(tmp_path):
             for a in range(nc):
                 scale = max(np.abs(fo[a]).max(), 1e-300)
                 assert np.abs(fs[form][a] - fo[a]).max() <= 1e-12 * scale, f"{cent} {form} spread comp {a}"
+    # form u: USER_DEFINED through LEInteractor::s_kernel_fcn (facade_test.cpp's user_phi3)
+    from test_gpu_user import phi3
+    ora.set_user_kernel(phi3, 3)
+    try:
+        for cent in ("cell", "node", "side", "edge"):
+            depth = depth_c if cent == "cell" else 1
+            Qd = 3 if cent in ("side", "edge") else depth
+            nc = len(u[cent])
+            Qg = np.fromfile(tmp_path / f"Q_{cent}_u.bin").reshape(M, Qd)
+            Qo = np.full((M, Qd), -7.0)
+            oracle_call(ora, "interp", "USER_DEFINED", cent, geom, [x.copy() for x in u[cent]], ii, xi, X, Qo, depth)
+            assert np.abs(Qg - Qo).max() <= 1e-13 * max(np.abs(Qo).max(), 1e-300), f"{cent} user interp"
+            Sv = F[:, [k % 3 for k in range(Qd)]].copy()
+            fo = [np.zeros_like(x) for x in u[cent]]
+            oracle_call(ora, "spread", "USER_DEFINED", cent, geom, fo, ia, xa, X, Sv, depth)
+            for a in range(nc):
+                fg = np.fromfile(tmp_path / f"f_{cent}_u_{a}.bin").reshape(fo[a].shape)
+                assert np.abs(fg - fo[a]).max() <= 1e-12 * max(np.abs(fo[a]).max(), 1e-300), f"{cent} user spread {a}"
+    finally:
+        ora.set_user_kernel(None, 4)
     # the physical-face patch: spread of its list, then the adjoint fold of x and z
     fo = [np.zeros(geom.array_shape("side", a)) for a in range(3)]
     oracle_call(ora, "spread", "IB_4", "side", geom, fo, ip, xp, X, F.copy(), 1)
