@@ -331,7 +331,10 @@ def run_level(args, cfg, kernel, dev):
         lvl_s.fill_ghosts("side", u)
         if record:
             E[1].record()
-        lvl_s.bin(X)
+        if args.full_bin:
+            lvl_s.bin(X)
+        else:
+            lvl_s.rebin(X)  # the same lists (between regrids): from the previous order
         lvl_s.select_interior(M, lists["ii"], lists["oi"])
         if record:
             E[2].record()
@@ -416,6 +419,9 @@ def run_level(args, cfg, kernel, dev):
         "config": {"workload": cfg["desc"], "kernel": kernel, "grid": [N, N, N], "markers": M,
                    "parallelism": "one GPU", "patches": [P, P, P], "patch_cells": [n, n, n], "ghost": g,
                    "marker_order": args.marker_order, "move": args.move,
+                   "bin": "full device radix sort every step" if args.full_bin or args.move else
+                          "re-binned every step from the previous order (ibtk_le_level_bin's result, "
+                          "ibtk_le_markers_rebin)",
                    "step": ("level ghost fill + interp(3 comps) + position update + per-patch lists rebuilt "
                             "(bench.level_lists, torch ops) + bin(ghost-box lists, interior selected) + zero f and "
                             "spread(3 comps) in one launch" if args.move else
@@ -444,6 +450,9 @@ def main():
                     help="cfg5: zero f and spread as two launches instead of ibtk_le_level_zero_spread (A/B)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-rebin", action="store_true", help="bin once outside the timed loop")
+    ap.add_argument("--full-bin", action="store_true",
+                    help="bin every step from scratch (device radix sort of all keys) instead of re-binning "
+                         "from the previous order (ibtk_le_markers_rebin)")
     ap.add_argument("--solo-slab", type=int, default=0, metavar="S",
                     help="projection aid (one GPU, not a scaling measurement): run rank 0's slab of an S-way z "
                          "split alone, its z ghosts wrapped locally instead of exchanged")
@@ -567,13 +576,21 @@ def main():
     # markers near the slab faces, exchanged with their forces every step
     cur = {"X": X, "F": F, "U": U}
 
+    binned = {"rows": None}
+
     def bin_step():
         if fixed:
             bins.bin_count(geom, kernel, X, n_dev)
             cur.update(X=X, F=F, U=U)
             return
         if gm is None:
-            bins.bin(geom, kernel, X)
+            # the same rows as at the last binning (no migration changed the list): re-bin
+            # from the previous order (ibtk_le_markers_rebin, exact); else bin afresh
+            if not args.full_bin and binned["rows"] == X.shape[0] and not (args.move and world > 1):
+                bins.rebin(X)
+            else:
+                bins.bin(geom, kernel, X)
+                binned["rows"] = X.shape[0]
             cur.update(X=X, F=F, U=U)
             return
         Xa, Fa, _ = gm.exchange(X, F)
@@ -826,6 +843,11 @@ def main():
         "config": {"workload": cfg["desc"], "kernel": kernel, "grid": [N, N, N], "markers": M_total,
                    "parallelism": f"z-slab x{world}", "ghost": ghost, "marker_order": args.marker_order, "layout": args.layout, "spread_mode": args.spread_mode if world > 1 else "one rank",
                    "solo_slab": args.solo_slab or None,
+                   "bin": ("full device radix sort every step" if args.full_bin or fixed or gm is not None
+                           or (args.move and world > 1) else
+                           "re-binned every step from the previous order (ibtk_le_markers_rebin: every key "
+                           "recomputed from the current positions, the entries whose bucket changed inserted; "
+                           "equal to a full binning)"),
                    "move": args.move, "renumber": args.renumber,
                    "migration": ("fixed-capacity, device counts, no host sync" if fixed else
                                  "counts read by the host" if world > 1 and args.move else None), "overlap": world > 1 and not args.no_overlap,

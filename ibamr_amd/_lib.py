@@ -92,6 +92,7 @@ _SIGS = [
      [c_void_p, c_void_p, ctypes.POINTER(PatchGeom), c_int, c_void_p, c_void_p, c_void_p, c_int]),
     ("ibtk_le_markers_bin_count", c_int,
      [c_void_p, c_void_p, ctypes.POINTER(PatchGeom), c_int, c_void_p, c_int, c_void_p]),
+    ("ibtk_le_markers_rebin", c_int, [c_void_p, c_void_p, c_void_p]),
     ("ibtk_le_markers_count", c_int, [c_void_p]),
     ("ibtk_le_markers_order", c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
     ("ibtk_le_interp", c_int,

@@ -52,7 +52,7 @@ static const int kStencil[K_COUNT] = {1, 2, 2, 4, 4, 4, 8, 6, 4};
 
 // USER_DEFINED (LEInteractor.cpp:651-652): the user's kernel function and its
 // stencil size, IB_4's by default (ib4_kernel_fcn, LEInteractor.cpp:629-648)
-static double ib4_kernel_fcn(double r) {
+extern "C" double ibtk_le_ib4_kernel_fcn(double r) {
     r = std::abs(r);
     if (r < 1.0) {
         const double t2 = r * r;
@@ -65,14 +65,17 @@ static double ib4_kernel_fcn(double r) {
     }
     return 0.0;
 }
-static ibtk_le_user_kernel_fn g_user_fcn = &ib4_kernel_fcn;
+static ibtk_le_user_kernel_fn g_user_fcn = &ibtk_le_ib4_kernel_fcn;
 static int g_user_size = 4;
-constexpr int USER_MAX_STENCIL = 16;
+// Any stencil size (LEInteractor.cpp:652, 678): the per-entry weight tables are sized
+// from it at the call; only the spread's 32-bit contribution count limits n S^NDIM
+// (checked there).  This bound keeps S^3 itself inside an int.
+constexpr int USER_MAX_STENCIL = 1024;
 
 extern "C" int ibtk_le_set_user_kernel(ibtk_le_user_kernel_fn fcn, int stencil_size) {
     if (stencil_size < 1 || stencil_size > USER_MAX_STENCIL)
         return fail(IBTK_LE_ERR_ARG, "user kernel stencil size %d outside [1, %d]", stencil_size, USER_MAX_STENCIL);
-    g_user_fcn = fcn ? fcn : &ib4_kernel_fcn;
+    g_user_fcn = fcn ? fcn : &ibtk_le_ib4_kernel_fcn;
     g_user_size = stencil_size;
     return IBTK_LE_OK;
 }
@@ -185,6 +188,12 @@ struct ibtk_le_markers_s {
     bool dedup_done = false, has_dups = false;
     DevBuf qin, owner, int_off;           // ibtk_le_level_select_interior: per sorted entry, its Q target or -1
     bool qin_valid = false;               // cleared by every bin
+    // ibtk_le_markers_rebin: the last binning's list (n_dev of a fixed-capacity one) and its scratch
+    const int* n_dev = nullptr;
+    bool binned3 = false;                 // a 3-D column binning (ibtk_le_markers_bin(_count) / level_bin) holds
+    DevBuf rb_cin, rb_cout, rb_d, rb_dpre, rb_mstart, rb_ps2, rb_mbits, rb_wcnt, rb_wpre, rb_mlist, rb_scr, rb_big,
+        rb_nbig;
+    int rb_zeroed_nb = -1;                // rb_cin / rb_cout are zero for this many buckets
 };
 
 static int set_device(ibtk_le_ctx ctx) {
@@ -524,7 +533,9 @@ extern "C" int ibtk_le_markers_destroy(ibtk_le_markers m) {
     hipStreamSynchronize(m->ctx->stream);
     for (DevBuf* b : {&m->sorted_key, &m->sorted_l, &m->sorted_s, &m->sorted_X, &m->sorted_a, &m->plane_start, &m->indices,
                       &m->xshift, &m->cand_cnt, &m->cand_off, &m->cand_idx, &m->last, &m->qdst, &m->items,
-                      &m->nsub, &m->isub, &m->nitems, &m->pd, &m->entry_off, &m->qin, &m->owner, &m->int_off})
+                      &m->nsub, &m->isub, &m->nitems, &m->pd, &m->entry_off, &m->qin, &m->owner, &m->int_off,
+                      &m->rb_cin, &m->rb_cout, &m->rb_d, &m->rb_dpre, &m->rb_mstart, &m->rb_ps2, &m->rb_mbits,
+                      &m->rb_wcnt, &m->rb_wpre, &m->rb_mlist, &m->rb_scr, &m->rb_big, &m->rb_nbig})
         b->release();
     delete m;
     return IBTK_LE_OK;
@@ -632,6 +643,114 @@ extern "C" int ibtk_le_markers_bin_count(ibtk_le_ctx ctx, ibtk_le_markers m, con
     return markers_bin_impl(ctx, m, geom, kernel, X_dev, nullptr, nullptr, capacity, n_dev);
 }
 
+// exclusive prefix sums on the context stream (rocPRIM), temp storage grown as needed
+static int scan_excl(ibtk_le_ctx ctx, const int* in, int* out, int n) {
+    size_t tb = 0;
+    HIP_TRY(launch_scan(nullptr, tb, in, out, n, ctx->stream));
+    if (int rc = ctx->temp.ensure(tb)) return rc;
+    tb = ctx->temp.cap;
+    HIP_TRY(launch_scan(ctx->temp.p, tb, in, out, n, ctx->stream));
+    return IBTK_LE_OK;
+}
+
+// The last binning's list re-binned at new positions X_dev: the result -- sorted
+// order, bucket starts, sorted positions, sweep items -- is the one
+// ibtk_le_markers_bin / ibtk_le_level_bin would give for the same list at X_dev
+// (the sort by (bucket, list entry) is unique), computed from the old order
+// (le_sweep.hip, k_rekey .. k_rebin_scatter).  No host sync.
+extern "C" int ibtk_le_markers_rebin(ibtk_le_ctx ctx, ibtk_le_markers m, const double* X_dev) {
+    if (!ctx || !m) return fail(IBTK_LE_ERR_ARG, "markers_rebin: null ctx/markers");
+    if (m->kernel < 0) return fail(IBTK_LE_ERR_ARG, "markers_rebin: the list was never binned");
+    const int n = m->n;
+    if (n > 0 && !X_dev) return fail(IBTK_LE_ERR_ARG, "null X");
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    if (!m->binned3) {  // 2-D bricks: a fresh binning of the kept list
+        const ibtk_le_patch_geom g = m->geom;
+        return markers_bin_impl(ctx, m, &g, m->kernel, X_dev, m->has_indices ? m->indices.as<int>() : nullptr,
+                                m->has_xshift ? m->xshift.as<double>() : nullptr, n, nullptr);
+    }
+    m->cand_valid = false;
+    m->dedup_done = false;
+    m->qin_valid = false;
+    m->has_dups = false;
+    if (n == 0) return build_items(ctx, m, m->kernel);
+    const hipStream_t s = ctx->stream;
+    const int nb = m->nbuckets_total;
+    const int nw = (n + 31) / 32;
+    int rc;
+    const size_t bb = sizeof(int) * ((size_t)nb + 2), wb = sizeof(int) * ((size_t)nw + 1);
+    const bool fresh = m->rb_zeroed_nb != nb || !m->rb_cin.p || m->rb_cin.cap < bb || m->rb_cout.cap < bb;
+    for (DevBuf* b : {&m->rb_cin, &m->rb_cout, &m->rb_d, &m->rb_dpre, &m->rb_mstart, &m->rb_ps2, &m->rb_big})
+        if ((rc = b->ensure(bb))) return rc;
+    for (DevBuf* b : {&m->rb_mbits, &m->rb_wcnt, &m->rb_wpre})
+        if ((rc = b->ensure(wb))) return rc;
+    for (DevBuf* b : {&m->rb_mlist, &m->rb_scr})
+        if ((rc = b->ensure(sizeof(int) * (size_t)n))) return rc;
+    if ((rc = m->rb_nbig.ensure(sizeof(int)))) return rc;
+    if ((rc = ctx->keys_in.ensure(sizeof(unsigned) * (size_t)n))) return rc;
+    if ((rc = ctx->vals_in.ensure(sizeof(int) * (size_t)n))) return rc;
+    if (fresh) {  // the in/out counts start from zero (k_rebin_append leaves them so)
+        HIP_TRY(hipMemsetAsync(m->rb_cin.p, 0, bb, s));
+        HIP_TRY(hipMemsetAsync(m->rb_cout.p, 0, bb, s));
+        m->rb_zeroed_nb = nb;
+    }
+    // the sentinel word past the last (k_rekey writes words up to nw; word nw only
+    // with zeros) and the movers' long-list queue
+    HIP_TRY(hipMemsetAsync(m->rb_mbits.as<unsigned>() + nw, 0, sizeof(unsigned), s));
+    HIP_TRY(hipMemsetAsync(m->rb_wcnt.as<int>() + nw, 0, sizeof(int), s));
+    HIP_TRY(hipMemsetAsync(m->rb_nbig.p, 0, sizeof(int), s));
+    Params p;
+    std::memset(&p, 0, sizeof(p));
+    p.bg = m->bg;
+    p.cg = m->cg;
+    p.nbuckets_total = nb;
+    p.X = X_dev;
+    p.indices = m->has_indices ? m->indices.as<int>() : nullptr;
+    p.Xshift = m->has_xshift ? m->xshift.as<double>() : nullptr;
+    p.n_dev = m->n_dev;
+    if (m->npatch) {
+        p.pd = m->pd.as<PatchDesc>();
+        p.npatch = m->npatch;
+        p.entry_off = m->entry_off.as<int>();
+    }
+    RebinBufs r{};
+    r.n = n;
+    r.nb = nb;
+    r.nw = nw;
+    r.kold = m->sorted_key.as<unsigned>();
+    r.lsorted = m->sorted_l.as<int>();
+    r.knew = ctx->keys_in.as<unsigned>();
+    r.lold = ctx->vals_in.as<int>();
+    r.mbits = m->rb_mbits.as<unsigned>();
+    r.wcnt = m->rb_wcnt.as<int>();
+    r.wpre = m->rb_wpre.as<int>();
+    r.cin = m->rb_cin.as<int>();
+    r.cout = m->rb_cout.as<int>();
+    r.d = m->rb_d.as<int>();
+    r.dpre = m->rb_dpre.as<int>();
+    r.mstart = m->rb_mstart.as<int>();
+    r.mlist = m->rb_mlist.as<int>();
+    r.scratch = m->rb_scr.as<int>();
+    r.nbig = m->rb_nbig.as<int>();
+    r.big = m->rb_big.as<int>();
+    r.os = m->plane_start.as<int>();
+    r.ns = m->rb_ps2.as<int>();
+    r.sorted_l = m->sorted_l.as<int>();
+    r.sorted_key = m->sorted_key.as<unsigned>();
+    r.sorted_s = m->sorted_s.as<int>();
+    r.sorted_X = m->sorted_X.as<double>();
+    HIP_TRY(launch_rekey(m->kernel, p, r, s));
+    HIP_TRY(launch_rebin_delta(r, s));
+    if ((rc = scan_excl(ctx, r.d, r.dpre, nb + 2))) return rc;
+    if ((rc = scan_excl(ctx, r.cin, r.mstart, nb + 2))) return rc;
+    if ((rc = scan_excl(ctx, r.wcnt, r.wpre, nw + 1))) return rc;
+    HIP_TRY(launch_rebin_starts(r, s));
+    HIP_TRY(launch_rebin_movers(r, s));
+    HIP_TRY(launch_rebin_scatter(p, r, s));
+    std::swap(m->plane_start, m->rb_ps2);  // the new starts (equal to the old when nothing moved)
+    return build_items(ctx, m, m->kernel);
+}
+
 static int markers_bin_impl(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_patch_geom* geom, int kernel,
                             const double* X_dev, const int* indices_dev, const double* Xshift_dev, int nindices,
                             const int* n_dev) {
@@ -666,6 +785,8 @@ static int markers_bin_impl(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_pa
     m->dedup_done = false;
     m->qin_valid = false;
     m->has_dups = false;
+    m->n_dev = n_dev;
+    m->binned3 = cols;
     int rc = 0;
     const int B = geom->ndim == 3 ? BRICK3 : BRICK2;
     const int nplanes = cols ? cg.nbuckets : bg.nbricks * B;  // bucket starts: nplanes + 1
@@ -683,12 +804,13 @@ static int markers_bin_impl(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_pa
     if ((rc = ctx->vals_in.ensure(sizeof(int) * (size_t)n))) return rc;
     if (m->has_indices) {
         if ((rc = m->indices.ensure(sizeof(int) * (size_t)n))) return rc;
-        HIP_TRY(hipMemcpyAsync(m->indices.p, indices_dev, sizeof(int) * (size_t)n, hipMemcpyDeviceToDevice, s));
+        if (indices_dev != m->indices.p)  // (a re-binning passes the kept list)
+            HIP_TRY(hipMemcpyAsync(m->indices.p, indices_dev, sizeof(int) * (size_t)n, hipMemcpyDeviceToDevice, s));
     }
     if (m->has_xshift) {
         const size_t xb = sizeof(double) * (size_t)n * geom->ndim;
         if ((rc = m->xshift.ensure(xb))) return rc;
-        HIP_TRY(hipMemcpyAsync(m->xshift.p, Xshift_dev, xb, hipMemcpyDeviceToDevice, s));
+        if (Xshift_dev != m->xshift.p) HIP_TRY(hipMemcpyAsync(m->xshift.p, Xshift_dev, xb, hipMemcpyDeviceToDevice, s));
     }
     Params p;
     std::memset(&p, 0, sizeof(p));
@@ -1248,6 +1370,8 @@ extern "C" int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch,
     m->dedup_done = false;
     m->qin_valid = false;
     m->has_dups = false;
+    m->n_dev = nullptr;
+    m->binned3 = true;
     int rc;
     if ((rc = upload_patches(ctx, m))) return rc;
     if (m->off_dev.size() != (size_t)(npatch + 1) ||
@@ -1420,10 +1544,11 @@ extern "C" int ibtk_le_level_select_interior(ibtk_le_ctx ctx, ibtk_le_markers m,
     HIP_TRY(hipMemcpyAsync(m->int_off.p, interior_offsets, sizeof(int) * (size_t)(np + 1), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(m->owner.p, 0xff, sizeof(int) * (size_t)std::max(n_markers, 1), s));
     HIP_TRY(hipMemsetAsync(ctx->counts.p, 0, sizeof(int) * (size_t)nblk, s));
-    HIP_TRY(launch_interior_owner(m->int_off.as<int>(), np, interior_indices_dev, n_int, m->owner.as<int>(), s));
+    HIP_TRY(launch_interior_owner(m->int_off.as<int>(), np, interior_indices_dev, n_int, n_markers, m->owner.as<int>(),
+                                  ctx->err.as<int>(), s));
     HIP_TRY(launch_interior_targets(m->sorted_l.as<int>(), m->sorted_s.as<int>(), m->entry_off.as<int>(), np,
-                                    m->has_xshift ? m->xshift.as<double>() : nullptr, m->owner.as<int>(), m->n,
-                                    m->qin.as<int>(), ctx->counts.as<int>(), s));
+                                    m->has_xshift ? m->xshift.as<double>() : nullptr, m->owner.as<int>(), n_markers,
+                                    m->n, m->qin.as<int>(), ctx->counts.as<int>(), ctx->err.as<int>(), s));
     HIP_TRY(launch_check_count(ctx->counts.as<int>(), m->n > 0 ? nblk : 0, n_int, ctx->err.as<int>(), 4, s));
     m->qin_valid = true;
     return IBTK_LE_OK;

@@ -1026,28 +1026,36 @@ __device__ __forceinline__ int patch_of_entry(const int* off, int npatch, int l)
     return lo;
 }
 __global__ __launch_bounds__(BLOCK) void k_interior_owner(const int* int_off, int npatch, const int* int_idx, int n_int,
-                                                          int* owner) {
+                                                          int n_markers, int* owner, int* err) {
     const int j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= n_int) return;
-    atomicMax(owner + int_idx[j], patch_of_entry(int_off, npatch, j));
+    const int s = int_idx[j];
+    if (s < 0 || s >= n_markers) {  // an interior list naming a marker past n_markers
+        atomicOr(err, 4);
+        return;
+    }
+    atomicMax(owner + s, patch_of_entry(int_off, npatch, j));
 }
-hipError_t launch_interior_owner(const int* int_off, int npatch, const int* int_idx, int n_int, int* owner,
-                                 hipStream_t s) {
+hipError_t launch_interior_owner(const int* int_off, int npatch, const int* int_idx, int n_int, int n_markers,
+                                 int* owner, int* err, hipStream_t s) {
     if (n_int <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_interior_owner, dim3((n_int + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, int_off, npatch, int_idx,
-                       n_int, owner);
+                       n_int, n_markers, owner, err);
     return hipGetLastError();
 }
 __global__ __launch_bounds__(BLOCK) void k_interior_targets(const int* sorted_l, const int* sorted_s,
                                                             const int* entry_off, int npatch, const double* xshift,
-                                                            const int* owner, int n, int* qin, int* found) {
+                                                            const int* owner, int n_markers, int n, int* qin,
+                                                            int* found, int* err) {
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     bool keep = false;
     int s = -1;
     if (e < n) {
         const int l = sorted_l[e];
         s = sorted_s[e];
-        keep = owner[s] == patch_of_entry(entry_off, npatch, l);
+        const bool inr = s >= 0 && s < n_markers;  // a binned list naming a marker past n_markers
+        if (!inr) atomicOr(err, 4);
+        keep = inr && owner[s] == patch_of_entry(entry_off, npatch, l);
         if (xshift) keep = keep && xshift[3 * (int64_t)l] == 0.0 && xshift[3 * (int64_t)l + 1] == 0.0 &&
                            xshift[3 * (int64_t)l + 2] == 0.0;
         qin[e] = keep ? s : -1;
@@ -1064,11 +1072,11 @@ __global__ __launch_bounds__(BLOCK) void k_interior_targets(const int* sorted_l,
     if (threadIdx.x == 0 && cnt) atomicAdd(found + (blockIdx.x % CHECK_STRIPES), cnt);
 }
 hipError_t launch_interior_targets(const int* sorted_l, const int* sorted_s, const int* entry_off, int npatch,
-                                   const double* xshift, const int* owner, int n, int* qin, int* found,
-                                   hipStream_t s) {
+                                   const double* xshift, const int* owner, int n_markers, int n, int* qin, int* found,
+                                   int* err, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_interior_targets, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, sorted_l, sorted_s,
-                       entry_off, npatch, xshift, owner, n, qin, found);
+                       entry_off, npatch, xshift, owner, n_markers, n, qin, found, err);
     return hipGetLastError();
 }
 // fixed-capacity migration: pack the leavers, unpack stayers + arrivals (no host sync)
@@ -1133,8 +1141,11 @@ __global__ __launch_bounds__(BLOCK) void k_wrap_positions(WrapBox w, long long n
         while (x < w.lo[d]) x += L;
         while (x >= w.hi[d]) x -= L;
     }
-    x = fmax(x, w.lo[d]);
-    x = fmin(x, w.hi[d] - 2.220446049250313e-16);  // std::numeric_limits<double>::epsilon()
+    // std::max / std::min as LDataManager.cpp:1398-1399 call them ((a < b) ? b : a and
+    // (b < a) ? b : a): a NaN coordinate stays NaN (fmax / fmin would clamp it)
+    const double lo = w.lo[d], hi = w.hi[d] - 2.220446049250313e-16;  // std::numeric_limits<double>::epsilon()
+    x = (x < lo) ? lo : x;
+    x = (hi < x) ? hi : x;
     X[t] = x;
 }
 hipError_t launch_wrap_positions(const WrapBox& w, long long n, double* X, hipStream_t s) {

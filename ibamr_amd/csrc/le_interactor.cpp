@@ -302,7 +302,7 @@ void spread_host(const V& q, const std::vector<double>& Q, int Q_depth, const st
 
 }  // namespace
 
-double (*LEInteractor::s_kernel_fcn)(double r) = nullptr;  // nullptr: ib4_kernel_fcn
+double (*LEInteractor::s_kernel_fcn)(double r) = &ibtk_le_ib4_kernel_fcn;  // LEInteractor.cpp:651
 int LEInteractor::s_kernel_fcn_stencil_size = 4;
 
 void LEInteractor::setFromDatabase(const void*) {}

@@ -194,6 +194,39 @@ hipError_t launch_suffix_min(void* temp, size_t& temp_bytes, const int* in, int*
 
 // 3-D column sweep (le_sweep.hip)
 hipError_t launch_bin_col(int kernel, const Params& p, int n, unsigned* keys, int* vals, hipStream_t s);
+// Incremental re-binning of a binned list at new positions (ibtk_le_markers_rebin,
+// le_sweep.hip k_rekey .. k_rebin_scatter).  nb = buckets (the outside bucket is nb);
+// per-bucket arrays hold nb + 2 ints, per-word arrays nw + 1 (nw = ceil(n / 32)).
+struct RebinBufs {
+    int n, nb, nw;
+    const unsigned* kold;  // the old sorted keys (sorted_key, read before the scatter rewrites it)
+    const int* lsorted;    // the old sorted_l (read by k_rekey)
+    unsigned* knew;        // new key per old sorted position
+    int* lold;             // copy of the old sorted_l
+    unsigned* mbits;       // mover flag per old sorted position, 32 per word (word nw stays 0)
+    int* wcnt;             // movers per word (entry nw stays 0)
+    int* wpre;             // its exclusive prefix (wpre[nw] = movers)
+    int* cin;              // movers into bucket b (0 on entry; consumed back to 0)
+    int* cout;             // movers out of bucket b (0 on entry; reset)
+    int* d;                // cin - cout, then
+    int* dpre;             // its exclusive prefix
+    int* mstart;           // exclusive prefix of cin: bucket b's movers are mlist[mstart[b] .. mstart[b+1])
+    int* mlist;            // the movers' l, per bucket sorted by l
+    int* scratch;          // long lists' sort
+    int* nbig;             // long lists queued (zeroed before)
+    int* big;
+    const int* os;         // old bucket starts (plane_start)
+    int* ns;               // new bucket starts
+    int* sorted_l;
+    unsigned* sorted_key;
+    int* sorted_s;
+    double* sorted_X;
+};
+hipError_t launch_rekey(int kernel, const Params& p, const RebinBufs& r, hipStream_t s);
+hipError_t launch_rebin_delta(const RebinBufs& r, hipStream_t s);
+hipError_t launch_rebin_starts(const RebinBufs& r, hipStream_t s);
+hipError_t launch_rebin_movers(const RebinBufs& r, hipStream_t s);
+hipError_t launch_rebin_scatter(const Params& p, const RebinBufs& r, hipStream_t s);
 // z-slab migration classes (le_aux.hip)
 struct SlabMig {
     double L[3];
@@ -308,11 +341,12 @@ hipError_t launch_level_node_keys(const LevelNum& L, const int* tab, const doubl
 // owner[s] = max patch whose interior list names marker s (owner pre-filled with -1);
 // then per sorted entry e of the binned lists: qin[e] = s if owner[s] is the entry's
 // patch and the entry is unshifted, else -1; found[block] counts the block's kept entries.
-hipError_t launch_interior_owner(const int* int_off, int npatch, const int* int_idx, int n_int, int* owner,
-                                 hipStream_t s);
+// Marker indices outside [0, n_markers) (in either list) are not dereferenced: err bit 4.
+hipError_t launch_interior_owner(const int* int_off, int npatch, const int* int_idx, int n_int, int n_markers,
+                                 int* owner, int* err, hipStream_t s);
 hipError_t launch_interior_targets(const int* sorted_l, const int* sorted_s, const int* entry_off, int npatch,
-                                   const double* xshift, const int* owner, int n, int* qin, int* found,
-                                   hipStream_t s);
+                                   const double* xshift, const int* owner, int n_markers, int n, int* qin, int* found,
+                                   int* err, hipStream_t s);
 struct WrapBox {
     double lo[3], hi[3];
     int per[3];

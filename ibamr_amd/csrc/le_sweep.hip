@@ -126,19 +126,11 @@ template <int K> __device__ __forceinline__ int key_band(int kx, int ky) {
     return 3 * xb + yb;
 }
 
+// Bucket key of list entry i at shifted position Xs: (anchor plane, column, band)
+// in its patch's bucket range, or nbuckets_total (outside).
 template <int K>
-__global__ __launch_bounds__(BLOCK) void k_bin_col(Params p, int n, unsigned* keys, int* vals) {
-    const int i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    if (p.n_dev && i >= *p.n_dev) {  // a fixed-capacity list's unused rows: outside
-        keys[i] = (unsigned)p.nbuckets_total;
-        vals[i] = i;
-        return;
-    }
-    const int s = p.indices ? p.indices[i] : i;
-    double Xs[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) Xs[d] = p.X[(int64_t)3 * s + d] + (p.Xshift ? p.Xshift[(int64_t)3 * i + d] : 0.0);
+__device__ __forceinline__ unsigned entry_key(const Params& p, int i, const double* Xs) {
+    if (p.n_dev && i >= *p.n_dev) return (unsigned)p.nbuckets_total;  // a fixed-capacity list's unused rows
     int ka[3];
     unsigned key = (unsigned)p.nbuckets_total;  // outside
     if (p.pd) {  // a level: the entry's patch, its frame and its range of buckets
@@ -151,8 +143,221 @@ __global__ __launch_bounds__(BLOCK) void k_bin_col(Params p, int n, unsigned* ke
         const int col = (ka[1] / COLY) * p.cg.ncx + ka[0] / COLX;
         key = (unsigned)((ka[2] * p.cg.ncol + col) * NBAND + key_band<K>(ka[0], ka[1]));
     }
-    keys[i] = key;
+    return key;
+}
+
+template <int K>
+__global__ __launch_bounds__(BLOCK) void k_bin_col(Params p, int n, unsigned* keys, int* vals) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    double Xs[3] = {0.0, 0.0, 0.0};
+    if (!(p.n_dev && i >= *p.n_dev)) {
+        const int s = p.indices ? p.indices[i] : i;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) Xs[d] = p.X[(int64_t)3 * s + d] + (p.Xshift ? p.Xshift[(int64_t)3 * i + d] : 0.0);
+    }
+    keys[i] = entry_key<K>(p, i, Xs);
     vals[i] = i;
+}
+
+// ---------------------------------------------------------------------------
+// incremental re-binning (ibtk_le_markers_rebin)
+// ---------------------------------------------------------------------------
+// The list was binned before: sorted_l / sorted_key hold the order by (key, l)
+// of the old positions.  New keys are computed in that order; entries whose key
+// did not change ("stayers") keep their relative order, so the new order by
+// (key, l) is the stayers' with the changed entries ("movers") inserted.  Per
+// bucket b: new count = old + movers in - movers out; a stayer's new position is
+// the bucket's new start + the stayers before it in its old bucket + the movers
+// into b with a smaller l; a mover's is the new start + the stayers of b with a
+// smaller l (a binary search in b's old segment, which is sorted by l) + the
+// movers into b with a smaller l.  The movers of a bucket are listed sorted by l.
+// Exact: the same order, bucket starts and sorted positions as a fresh binning.
+// Nothing is read back to the host; with no movers only k_rekey does work.
+//
+// R1: new keys in the old order; the shifted positions stored at the old sorted
+// positions (final when nothing moved); per-bucket mover counts in/out; the mover
+// flags as a bit per entry with per-word counts; copies of the old l and the new
+// keys for the scatter (which overwrites the sorted arrays).
+template <int K>
+__global__ __launch_bounds__(BLOCK) void k_rekey(Params p, int n, const unsigned* kold, const int* sl, double* sorted_X,
+                                                 unsigned* knew, int* lold, unsigned* mbits, int* wcnt, int* cin,
+                                                 int* cout) {
+    __shared__ double sx[3 * BLOCK];
+    const int e0 = blockIdx.x * BLOCK;
+    const int e = e0 + threadIdx.x;
+    bool mv = false;
+    if (e < n) {
+        const int l = sl[e];
+        const int s = p.indices ? p.indices[l] : l;
+        const D3 x = ld3(p.X + (int64_t)3 * s);  // as k_gather_col (a fixed-capacity list's rows all exist)
+        double Xs[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) Xs[d] = x.v[d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
+        const unsigned k = entry_key<K>(p, l, Xs);
+        const unsigned ko = kold[e];
+        knew[e] = k;
+        lold[e] = l;
+        mv = k != ko;
+        if (mv) {
+            atomicAdd(cin + k, 1);
+            atomicAdd(cout + ko, 1);
+        }
+#pragma unroll
+        for (int d = 0; d < 3; ++d) sx[3 * threadIdx.x + d] = Xs[d];
+    }
+    const unsigned long long bal = __ballot(mv);
+    if ((threadIdx.x & 63) == 0 && e < n) {  // words e/32, e/32 + 1 (the second may be the zero sentinel)
+        const int w = e >> 5;
+        mbits[w] = (unsigned)bal;
+        mbits[w + 1] = (unsigned)(bal >> 32);
+        wcnt[w] = __popc((unsigned)bal);
+        wcnt[w + 1] = __popc((unsigned)(bal >> 32));
+    }
+    __syncthreads();
+    const int cnt = 3 * min(BLOCK, n - e0);
+    double* out = sorted_X + (int64_t)3 * e0;
+    for (int i = threadIdx.x; 2 * i < cnt; i += BLOCK) {
+        if (2 * i + 1 < cnt) {
+            double2 v;
+            v.x = sx[2 * i];
+            v.y = sx[2 * i + 1];
+            *reinterpret_cast<double2*>(out + 2 * i) = v;
+        } else {
+            out[2 * i] = sx[2 * i];
+        }
+    }
+}
+
+// movers before entry x (0 <= x <= n): word prefix + the word's lower bits
+__device__ __forceinline__ int movers_before(const unsigned* mbits, const int* wpre, int x) {
+    const int w = x >> 5, b = x & 31;
+    return wpre[w] + __popc(mbits[w] & ((1u << b) - 1u));
+}
+// first position in [lo, hi) of the l-sorted v whose value is >= l
+__device__ __forceinline__ int lower_bound_l(const int* v, int lo, int hi, int l) {
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (v[mid] < l) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// R2: d[b] = movers in - movers out (b <= nb), d[nb + 1] = 0
+__global__ __launch_bounds__(BLOCK) void k_rebin_delta(int nb, const int* cin, const int* cout, int* d) {
+    const int b = blockIdx.x * BLOCK + threadIdx.x;
+    if (b <= nb) d[b] = cin[b] - cout[b];
+    else if (b == nb + 1) d[b] = 0;
+}
+// new bucket starts: ns[b] = os[b] + (exclusive prefix of d)[b], b <= nb
+__global__ __launch_bounds__(BLOCK) void k_rebin_starts(int nb, const int* os, const int* dpre, int* ns) {
+    const int b = blockIdx.x * BLOCK + threadIdx.x;
+    if (b <= nb) ns[b] = os[b] + dpre[b];
+}
+
+// R3: every mover appends its l to its new bucket's list (mstart: exclusive prefix
+// of the in-counts); the counts are consumed (cin back to 0, cout reset), so the
+// next re-binning starts from zeros without a memset
+__global__ __launch_bounds__(BLOCK) void k_rebin_append(int n, const unsigned* mbits, const unsigned* knew,
+                                                        const unsigned* kold, const int* lold, const int* mstart,
+                                                        int* cin, int* cout, int* mlist) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= n || !((mbits[e >> 5] >> (e & 31)) & 1u)) return;
+    const unsigned b = knew[e];
+    const int j = atomicSub(cin + b, 1) - 1;
+    mlist[mstart[b] + j] = lold[e];
+    cout[kold[e]] = 0;
+}
+// Each bucket's mover list sorted by l: lists of up to 32 by one thread (insertion
+// sort); longer ones are queued for k_rebin_sort_big
+constexpr int REBIN_SMALL = 32;
+__global__ __launch_bounds__(BLOCK) void k_rebin_sort_small(int nb, const int* mstart, int* mlist, int* nbig,
+                                                            int* big) {
+    const int b = blockIdx.x * BLOCK + threadIdx.x;
+    if (b > nb) return;
+    const int lo = mstart[b], k = mstart[b + 1] - lo;
+    if (k < 2) return;
+    if (k > REBIN_SMALL) {
+        big[atomicAdd(nbig, 1)] = b;
+        return;
+    }
+    int* v = mlist + lo;
+    for (int i = 1; i < k; ++i) {
+        const int x = v[i];
+        int j = i - 1;
+        while (j >= 0 && v[j] > x) {
+            v[j + 1] = v[j];
+            --j;
+        }
+        v[j + 1] = x;
+    }
+}
+// Long lists (clustered markers crossing a plane together): the rank of every
+// entry is the count of smaller l in its list (l are distinct), counted through
+// LDS by a workgroup per list; the sorted list goes to scratch, copied back by
+// k_rebin_copy_big.
+__global__ __launch_bounds__(BLOCK) void k_rebin_sort_big(const int* nbig, const int* big, const int* mstart,
+                                                          const int* mlist, int* scratch) {
+    __shared__ int sh[BLOCK];
+    const int nb_ = *nbig;
+    for (int i = blockIdx.x; i < nb_; i += gridDim.x) {
+        const int b = big[i];
+        const int base = mstart[b], k = mstart[b + 1] - base;
+        for (int t = 0; t < k; t += BLOCK) {
+            const bool own = t + (int)threadIdx.x < k;
+            const int x = own ? mlist[base + t + threadIdx.x] : INT_MAX;
+            int rank = 0;
+            for (int c = 0; c < k; c += BLOCK) {
+                __syncthreads();
+                sh[threadIdx.x] = c + (int)threadIdx.x < k ? mlist[base + c + threadIdx.x] : INT_MAX;
+                __syncthreads();
+                const int m = min(BLOCK, k - c);
+                for (int j = 0; j < m; ++j) rank += sh[j] < x;
+            }
+            if (own) scratch[base + rank] = x;
+        }
+    }
+}
+__global__ __launch_bounds__(BLOCK) void k_rebin_copy_big(const int* nbig, const int* big, const int* mstart,
+                                                          const int* scratch, int* mlist) {
+    const int nb_ = *nbig;
+    for (int i = blockIdx.x; i < nb_; i += gridDim.x) {
+        const int b = big[i];
+        const int base = mstart[b], k = mstart[b + 1] - base;
+        for (int t = threadIdx.x; t < k; t += BLOCK) mlist[base + t] = scratch[base + t];
+    }
+}
+
+// R4 (only when something moved: wpre[nw] is the mover count): every entry to its
+// new sorted position; the sorted arrays rewritten there
+__global__ __launch_bounds__(BLOCK) void k_rebin_scatter(Params p, int n, int nb, const unsigned* mbits, const int* wpre,
+                                                         int nw, const unsigned* knew, const int* lold, const int* os,
+                                                         const int* ns, const int* mstart, const int* mlist,
+                                                         int* sorted_l, unsigned* sorted_key, int* sorted_s,
+                                                         double* sorted_X) {
+    if (wpre[nw] == 0) return;
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= n) return;
+    const int l = lold[e];
+    const int b = (int)knew[e];
+    const int ob = os[b], oe = b < nb ? os[b + 1] : n;
+    const int mb0 = movers_before(mbits, wpre, ob);
+    int pos;
+    if ((mbits[e >> 5] >> (e & 31)) & 1u) {
+        const int lb = lower_bound_l(lold, ob, oe, l);  // old entries of b with a smaller l
+        pos = ns[b] + (lb - ob) - (movers_before(mbits, wpre, lb) - mb0);
+    } else {
+        pos = ns[b] + (e - ob) - (movers_before(mbits, wpre, e) - mb0);
+    }
+    pos += lower_bound_l(mlist, mstart[b], mstart[b + 1], l) - mstart[b];
+    sorted_l[pos] = l;
+    sorted_key[pos] = (unsigned)b;
+    const int s = p.indices ? p.indices[l] : l;
+    const D3 x = ld3(p.X + (int64_t)3 * s);
+    sorted_s[pos] = s;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) sorted_X[(int64_t)3 * pos + d] = x.v[d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
 }
 
 // Per sorted entry e: the marker index and the shifted position (coalesced for
@@ -1415,6 +1620,46 @@ static SpreadSwFn pick_spread_sweep(int k) { IBTK_LE_DISPATCH_K(k, launch_spread
 hipError_t launch_bin_col(int kernel, const Params& p, int n, unsigned* keys, int* vals, hipStream_t s) {
     BinColFn f = pick_bin_col(kernel);
     return f ? f(p, n, keys, vals, s) : hipErrorInvalidValue;
+}
+
+// incremental re-binning (k_rekey .. k_rebin_scatter)
+template <int K>
+hipError_t launch_rekey_t(const Params& p, const RebinBufs& r, hipStream_t s) {
+    if (r.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rekey<K>, dim3((r.n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, r.n, r.kold, r.lsorted,
+                       r.sorted_X, r.knew, r.lold, r.mbits, r.wcnt, r.cin, r.cout);
+    return hipGetLastError();
+}
+using RekeyFn = hipError_t (*)(const Params&, const RebinBufs&, hipStream_t);
+static RekeyFn pick_rekey(int k) { IBTK_LE_DISPATCH_K(k, launch_rekey_t) }
+hipError_t launch_rekey(int kernel, const Params& p, const RebinBufs& r, hipStream_t s) {
+    RekeyFn f = pick_rekey(kernel);
+    return f ? f(p, r, s) : hipErrorInvalidValue;
+}
+static dim3 grid_of(long n) { return dim3((unsigned)((n + BLOCK - 1) / BLOCK)); }
+hipError_t launch_rebin_delta(const RebinBufs& r, hipStream_t s) {
+    hipLaunchKernelGGL(k_rebin_delta, grid_of(r.nb + 2), dim3(BLOCK), 0, s, r.nb, r.cin, r.cout, r.d);
+    return hipGetLastError();
+}
+hipError_t launch_rebin_starts(const RebinBufs& r, hipStream_t s) {
+    hipLaunchKernelGGL(k_rebin_starts, grid_of(r.nb + 1), dim3(BLOCK), 0, s, r.nb, r.os, r.dpre, r.ns);
+    return hipGetLastError();
+}
+hipError_t launch_rebin_movers(const RebinBufs& r, hipStream_t s) {
+    if (r.n > 0)
+        hipLaunchKernelGGL(k_rebin_append, grid_of(r.n), dim3(BLOCK), 0, s, r.n, r.mbits, r.knew, r.kold, r.lold,
+                           r.mstart, r.cin, r.cout, r.mlist);
+    hipLaunchKernelGGL(k_rebin_sort_small, grid_of(r.nb + 1), dim3(BLOCK), 0, s, r.nb, r.mstart, r.mlist, r.nbig,
+                       r.big);
+    hipLaunchKernelGGL(k_rebin_sort_big, dim3(1024), dim3(BLOCK), 0, s, r.nbig, r.big, r.mstart, r.mlist, r.scratch);
+    hipLaunchKernelGGL(k_rebin_copy_big, dim3(1024), dim3(BLOCK), 0, s, r.nbig, r.big, r.mstart, r.scratch, r.mlist);
+    return hipGetLastError();
+}
+hipError_t launch_rebin_scatter(const Params& p, const RebinBufs& r, hipStream_t s) {
+    if (r.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rebin_scatter, grid_of(r.n), dim3(BLOCK), 0, s, p, r.n, r.nb, r.mbits, r.wpre, r.nw, r.knew,
+                       r.lold, r.os, r.ns, r.mstart, r.mlist, r.sorted_l, r.sorted_key, r.sorted_s, r.sorted_X);
+    return hipGetLastError();
 }
 hipError_t launch_gather_col(int kernel, const Params& p, int n, int* sorted_s, double* sorted_X,
                              const unsigned* sorted_key, int nbuckets, int* bucket_start, hipStream_t s) {

@@ -249,6 +249,15 @@ class Markers:
         self.kernel, self.geom, self.n = kernel, geom, X.shape[0]
         return self
 
+    def rebin(self, X: torch.Tensor):
+        """Re-bin the last binned list at new positions X (ibtk_le_markers_rebin): the
+        same result as binning it again, computed from the previous order."""
+        if self.kernel is None:
+            raise RuntimeError("rebin: the list was never binned")
+        assert X.dtype == torch.float64
+        check(self.ctx.lib.ibtk_le_markers_rebin(self.ctx.h, self.h, _ptr(X)))
+        return self
+
     def count(self) -> int:
         return int(self.ctx.lib.ibtk_le_markers_count(self.h))
 
@@ -435,6 +444,12 @@ class Level:
         check(self.ctx.lib.ibtk_le_level_bin(self.ctx.h, self.markers.h, len(self.geoms), self._G,
                                              kernel_id(self.kernel), _ptr(X), self._O, _ptr(self.indices),
                                              _ptr(self.xshift)))
+        return self
+
+    def rebin(self, X: torch.Tensor):
+        """Re-bin the same lists at new positions X (ibtk_le_markers_rebin): the result
+        of bin(X), computed from the previous order."""
+        self.markers.rebin(X)
         return self
 
     def select_interior(self, n_markers: int, indices: torch.Tensor, offsets: Sequence[int]):

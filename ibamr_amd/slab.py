@@ -585,20 +585,24 @@ def redistribute(slab: Slab, ctx, X: torch.Tensor, fields: Sequence[torch.Tensor
     offset = sum(counts[:slab.rank])
     num_nodes = sum(counts)
     # nonlocal nodes: the neighbours' markers near the slab faces, with their indices
-    ids = torch.stack([lagn.to(X.dtype), offset + torch.arange(nl, dtype=X.dtype, device=X.device)], dim=1)
+    # and their owners' z (the exchange shifts the markers that cross the periodic z wrap
+    # by -+L_z, and z + L_z - L_z need not give z back: the owner's bits travel along)
+    ids = torch.stack([lagn.to(X.dtype), offset + torch.arange(nl, dtype=X.dtype, device=X.device), Xn[:, 2]],
+                      dim=1)
     Xa, Ia, n_own = GhostMarkers(slab, group).exchange(Xn, ids)
     gX = Xa[:0]
     gI = Ia[:0]
     if Xa.shape[0] > n_own:
-        # the owners' positions: undo the exchange's shift across the periodic z wrap
-        # (exact: z - L_z and back), so cells and images are the owner's
-        Lz = slab.L[2]
-        z = Xa[n_own:, 2]
-        Xa[n_own:, 2] = torch.where(z < 0, z + Lz, torch.where(z >= Lz, z - Lz, z))
-        order2, nl2, nn2 = numbering(Xa, Ia[:, 0].to(torch.int32).contiguous(), slab.ghost)
-        if nl2 != nl:
-            raise RuntimeError(f"rank {slab.rank}: {nl2} local nodes with the ghost markers, {nl} without")
-        sel = order2[nl2:].long()
-        gX, gI = Xa[sel].contiguous(), Ia[sel]
+        Xg = Xa[n_own:].clone()
+        Ig = Ia[n_own:]
+        Xg[:, 2] = Ig[:, 2]  # the owners' positions, bit for bit
+        # the nonlocal order depends only on the nonlocal markers (their cells, images and
+        # Lagrangian indices), so only they are numbered here: every one lies outside the
+        # slab's box, so all of them come out nonlocal
+        order2, nl2, nn2 = numbering(Xg.contiguous(), Ig[:, 0].to(torch.int32).contiguous(), slab.ghost)
+        if nl2 != 0:
+            raise RuntimeError(f"rank {slab.rank}: {nl2} received ghost markers inside the slab")
+        sel = order2[:nn2].long()
+        gX, gI = Xg[sel].contiguous(), Ig[sel]
     return NodeDistribution(Xn, fn, lagn, order, offset, num_nodes, gX, gI[:, 0].to(torch.int32),
                             gI[:, 1].to(torch.int64))

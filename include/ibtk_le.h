@@ -97,8 +97,12 @@ int ibtk_le_kernel_from_name(const char* name);
  * s_kernel_fcn_stencil_size (LEInteractor.h:100-101, LEInteractor.cpp:651-652), a
  * host function phi(r) of the signed distance in grid spacings, IB_4's
  * (ib4_kernel_fcn, LEInteractor.cpp:629-648) with stencil size 4 until set.
- * fcn == NULL restores the default.  stencil_size in [1, 16]. */
+ * fcn == NULL restores the default.  Any stencil_size >= 1 (the spread's per-call
+ * contribution count n * S^NDIM must stay below 2^31). */
 typedef double (*ibtk_le_user_kernel_fn)(double r);
+/* IB_4's kernel function, the reference's default s_kernel_fcn (ib4_kernel_fcn,
+ * LEInteractor.cpp:629-651). */
+double ibtk_le_ib4_kernel_fcn(double r);
 int ibtk_le_set_user_kernel(ibtk_le_user_kernel_fn fcn, int stencil_size);
 int ibtk_le_user_kernel(ibtk_le_user_kernel_fn* fcn, int* stencil_size);
 const char* ibtk_le_kernel_name(int kernel);
@@ -148,6 +152,16 @@ int ibtk_le_markers_bin(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_patch_
  * Q/F arrays must hold capacity rows.  3-D, identity list. */
 int ibtk_le_markers_bin_count(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_patch_geom* geom, int kernel,
                               const double* X_dev, int capacity, const int* n_dev);
+/* Re-bin the list of the last ibtk_le_markers_bin / _bin_count / ibtk_le_level_bin call
+ * on `m` (same entries, shifts, patches and kernel) at new positions X_dev (the
+ * markers moved, as between two steps of IBMethod's explicit loop).  The result --
+ * sorted order, bucket starts, sorted positions, sweep items -- is exactly that of
+ * binning again, but it is computed from the previous order: the entries whose
+ * bucket did not change keep their relative order and the others are inserted
+ * (with nothing moved, one pass over the list).  No host sync.  Replaces the
+ * per-step re-binning of LDataManager's LIndexSetData (LDataManager.cpp:1446-1493,
+ * IndexUtilities-inl.h:66-89) after a position update. */
+int ibtk_le_markers_rebin(ibtk_le_ctx ctx, ibtk_le_markers m, const double* X_dev);
 /* Number of list entries, and device pointers to the sorted list (entry -> marker
  * index, and entry -> Xshift[NDIM]); valid until the next bin call. */
 int ibtk_le_markers_count(ibtk_le_markers m);

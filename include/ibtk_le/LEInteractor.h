@@ -126,8 +126,9 @@ using LIndexSetView = LIndexSetDataView<LNode>;
 class LEInteractor {
 public:
     // The USER_DEFINED kernel function and its stencil size (LEInteractor.h:100-101):
-    // read at every USER_DEFINED call.  nullptr = IB_4's kernel function
-    // (ib4_kernel_fcn, LEInteractor.cpp:629-648), the reference's initial value.
+    // read at every USER_DEFINED call.  Initially IB_4's kernel function
+    // (ibtk_le_ib4_kernel_fcn = ib4_kernel_fcn, LEInteractor.cpp:629-651), as in the
+    // reference; nullptr also means it.
     static double (*s_kernel_fcn)(double r);
     static int s_kernel_fcn_stencil_size;
 

@@ -189,7 +189,7 @@ static void run(const char* cname, V& u, V& f, int ncomp, int depth, int Qdepth)
     LEInteractor::spread(f, Sv, Xv, idx, patch, ghost_box, pshift, "USER_DEFINED");
     LEInteractor::synchronize();
     save_f("u");
-    LEInteractor::s_kernel_fcn = nullptr;  // the reference's default again (ib4_kernel_fcn)
+    LEInteractor::s_kernel_fcn = &ibtk_le_ib4_kernel_fcn;  // the reference's default again
     LEInteractor::s_kernel_fcn_stencil_size = 4;
     HC(hipFree(Qd));
     HC(hipFree(Sd));
@@ -197,6 +197,10 @@ static void run(const char* cname, V& u, V& f, int ncomp, int depth, int Qdepth)
 
 int main(int argc, char** argv) {
     EXPECT(argc == 2, "usage: facade_test <dir>");
+    // the reference's initial s_kernel_fcn is ib4_kernel_fcn (LEInteractor.cpp:651)
+    EXPECT(LEInteractor::s_kernel_fcn == &ibtk_le_ib4_kernel_fcn && LEInteractor::s_kernel_fcn_stencil_size == 4,
+           "initial s_kernel_fcn");
+    EXPECT(LEInteractor::s_kernel_fcn(0.0) == 0.5, "ib4_kernel_fcn(0)");
     D = argv[1];
     FILE* mf = std::fopen((D + "/meta.txt").c_str(), "r");
     EXPECT(mf && std::fscanf(mf, "%d %d %d %d %d %d", &N, &g, &M, &n_int, &n_all, &depth_c) == 6, "meta");

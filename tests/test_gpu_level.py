@@ -251,6 +251,15 @@ def test_level_select_interior_rejects_foreign_entries(le, ctx):
     lvl.select_interior(4, torch.arange(4, dtype=torch.int32, device="cuda"), offs)
     with pytest.raises(RuntimeError, match="flag 4"):
         ctx.synchronize()
+    # an interior list naming a marker past n_markers (and a binned list beyond it):
+    # flagged, never dereferenced
+    offs = [0] + [4] * len(geoms)
+    lvl.select_interior(4, torch.tensor([0, 1, 2, 1 << 20], dtype=torch.int32, device="cuda"), offs)
+    with pytest.raises(RuntimeError, match="flag 4"):
+        ctx.synchronize()
+    lvl.select_interior(2, torch.tensor([0, 1], dtype=torch.int32, device="cuda"), [0] + [2] * len(geoms))
+    with pytest.raises(RuntimeError, match="flag 4"):
+        ctx.synchronize()
 
 
 @pytest.mark.parametrize("kernel,clustered", [("IB_4", True), ("IB_6", False)])

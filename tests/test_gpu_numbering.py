@@ -146,3 +146,9 @@ def test_wrap_positions_matches_reference_loops(le, ctx):
     Xd = torch.from_numpy(X.copy()).cuda()
     le.wrap_positions(ctx, Xd, lo, hi, periodic=periodic)
     assert np.array_equal(Xd.cpu().numpy(), exp)
+    # a NaN coordinate stays NaN in a non-periodic dim (std::max / std::min keep it,
+    # LDataManager.cpp:1398-1399; fmax / fmin would clamp it to the lower face)
+    Xn = torch.tensor([[0.5, float("nan"), 1.0], [0.5, 0.1, 1.0]], dtype=torch.float64, device="cuda")
+    le.wrap_positions(ctx, Xn, lo, hi, periodic=periodic)
+    out = Xn.cpu().numpy()
+    assert np.isnan(out[0, 1]) and out[1, 1] == 0.1 and out[0, 0] == 0.5

@@ -156,10 +156,50 @@ def test_user_default_is_ib4(le, ctx):
         assert rel_err(a.cpu().numpy(), b.cpu().numpy()) <= 1e-12
 
 
+def phi20(r):  # a 20-point kernel: (100 - r^2)^2 / 53333.33.. inside |r| < 10 (past round 3's cap of 16)
+    r2 = r * r
+    t = 100.0 - r2
+    return t * t / 53333.0 if r2 < 100.0 else 0.0
+
+
+@pytest.mark.parametrize("op", ["interp", "spread"])
+def test_user_wide_stencil(le, ctx, oracle, op):
+    """Stencil size 20 (the reference takes any s_kernel_fcn_stencil_size,
+    LEInteractor.cpp:652, 678): bitwise the oracle, 3-D side data."""
+    le.set_user_kernel(phi20, 20)
+    oracle.set_user_kernel(phi20, 20)
+    try:
+        geom, X, idx, xs, depth = make_case("IB_4", 3, "side", seed=77, M=60, extra_ghost=9)
+        rng = np.random.default_rng(8)
+        dev = "cuda:0"
+        q = geom.alloc("side", 1)
+        for a in q:
+            a.copy_(torch.from_numpy(rng.uniform(-1, 1, tuple(a.shape))))
+        u0 = [a.cpu().numpy().copy() for a in q]
+        Xd, idd, xsd = torch.from_numpy(X).to(dev), torch.from_numpy(idx).to(dev), torch.from_numpy(xs).to(dev)
+        if op == "interp":
+            Q = torch.zeros((X.shape[0], 3), dtype=torch.float64, device=dev)
+            le.user_interp(ctx, "side", geom, q, Q, Xd, idd, xsd)
+            ctx.synchronize()
+            Qo = np.zeros((X.shape[0], 3))
+            oracle_call(oracle, "interp", "USER_DEFINED", "side", geom, u0, idx, xs, X, Qo, 1)
+            assert np.array_equal(Q.cpu().numpy()[idx], Qo[idx])
+        else:
+            F = rng.uniform(-1, 1, (X.shape[0], 3))
+            le.user_spread(ctx, "side", geom, q, torch.from_numpy(F).to(dev), Xd, idd, xsd)
+            ctx.synchronize()
+            oracle_call(oracle, "spread", "USER_DEFINED", "side", geom, u0, idx, xs, X, F.copy(), 1)
+            for a, b in zip(q, u0):
+                assert np.array_equal(a.cpu().numpy(), b)
+    finally:
+        le.set_user_kernel(None, 4)
+        oracle.set_user_kernel(None, 4)
+
+
 def test_user_errors(le, ctx):
     from ibamr_amd import _lib
     with pytest.raises(_lib.IBTKLEError):
-        le.set_user_kernel(phi3, 0)  # stencil size outside [1, 16]
+        le.set_user_kernel(phi3, 0)  # stencil size < 1
     le.set_user_kernel(phi6, 6)  # needs 4 ghosts to interpolate (floor(6/2) + 1)
     try:
         from ibamr_amd.le import Geometry

@@ -313,6 +313,8 @@ def _redist_worker(rank, world, port, q):
         M = 400 + 23 * rank
         X = torch.rand((M, 3), dtype=torch.float64, generator=g)
         X[: M // 4, 2] = (torch.rand(M // 4, dtype=torch.float64, generator=g) * 0.1 - 0.05) % 1.0  # near z = 0
+        # just above z = 0: z + L_z - L_z rounds these to 0, the owner's bits must survive
+        X[M // 4: M // 4 + 20, 2] = torch.rand(20, dtype=torch.float64, generator=g) * 1e-12
         lag = (torch.randperm(M, generator=g) * world + rank).to(torch.int32)
         F = torch.rand((M, 3), dtype=torch.float64, generator=g)
         Xm, (Fm, lm) = migrate(slab, X, [F, lag.to(torch.float64)], cell_order=False)
@@ -338,7 +340,8 @@ def _redist_worker(rank, world, port, q):
         ok = torch.equal(d.X, Xm[d.order.long()]) and torch.equal(d.fields[0], Fm[d.order.long()])
         ok = ok and torch.equal(d.lag, lm[d.order.long()])
         q.put((rank, "ok", ok, dict(lag=d.lag.numpy(), offset=d.offset, num_nodes=d.num_nodes,
-                                    ghost_lag=d.ghost_lag.numpy(), ghost_petsc=d.ghost_petsc.numpy()),
+                                    ghost_lag=d.ghost_lag.numpy(), ghost_petsc=d.ghost_petsc.numpy(),
+                                    X=d.X.numpy(), ghost_X=d.ghost_X.numpy()),
                Xm.numpy(), lm.numpy()))
         dist.destroy_process_group()
     except Exception:  # pragma: no cover - reported to the parent
@@ -369,3 +372,14 @@ def test_redistribute_numbering_gloo(world):
     lag_all = np.concatenate([r[5] for r in res])
     n_ghost = check_node_distribution([r[3] for r in res], X_all, lag_all, [12, 10, 32], world, 2)
     assert n_ghost > 0
+    # ghost_X holds the owners' positions bit for bit (markers just above z = 0 included)
+    owner_X = {}
+    for r in res:
+        for lg, x in zip(r[3]["lag"], r[3]["X"]):
+            owner_X[int(lg)] = x
+    tiny = 0
+    for r in res:
+        for lg, x in zip(r[3]["ghost_lag"], r[3]["ghost_X"]):
+            assert np.array_equal(x, owner_X[int(lg)]), (r[0], int(lg), x, owner_X[int(lg)])
+            tiny += 0.0 < x[2] < 1e-12
+    assert tiny > 0
