@@ -474,6 +474,11 @@ def main():
     ap.add_argument("--move", action="store_true",
                     help="a full explicit coupling step: interp, X += dt U (ibtk_le_position_update), "
                          "migrate the slab leavers (N > 1), re-bin, spread")
+    ap.add_argument("--regrid-every", type=int, default=1, metavar="K",
+                    help="with --move: migrate (and with --renumber redistribute) every K-th step only, the "
+                         "reference's lazy cadence (regrid_interval); between regrids the markers keep their rank "
+                         "and rows, drift at most the ghost width's spare cell past their slab (checked on the "
+                         "device) and the binning is a re-binning")
     ap.add_argument("--renumber", action="store_true",
                     help="with --move: after the migration, redistribute every step -- the level's local "
                          "numbering, node offsets, nonlocal nodes and the LData reorder (slab.redistribute; "
@@ -522,7 +527,11 @@ def main():
 
     N = cfg["N"]
     ghost = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
-    slab = Slab([N, N, N], world, rank, ghost, align=16 if args.layout == "aligned" else 0)
+    # ghost planes exchanged per face: the stencils' reach W/2 (= ghost - 1) while every
+    # marker sits in its slab (stationary, or migrated every step); the full ghost width
+    # when they drift up to a cell past it between regrids (--regrid-every k > 1)
+    width = ghost if (args.move and args.regrid_every > 1) else max(1, ghost - 1)
+    slab = Slab([N, N, N], world, rank, ghost, align=16 if args.layout == "aligned" else 0, width=width)
     xslab = slab  # the slab the exchanges see
     if args.solo_slab > 1:
         if world > 1:
@@ -576,7 +585,22 @@ def main():
     # markers near the slab faces, exchanged with their forces every step
     cur = {"X": X, "F": F, "U": U}
 
-    binned = {"rows": None}
+    binned = {"rows": None, "changed": False}
+    # the lazy cadence's bound: between regrids a marker may drift at most `slack` cells
+    # past its slab (the ghost width's spare plane, LDataManager.cpp:167 CFL_WIDTH), checked
+    # on the device after every update and reported after the run (no host sync per step)
+    slack = ghost - max(1, ghost - 1)
+    drift_flag = torch.zeros(1, dtype=torch.bool, device=dev)
+
+    def check_drift(Xc, n_rows=None):
+        cz = torch.floor(Xc[:, 2] / slab.dx[2])
+        bad = (cz < slab.z0 - slack) | (cz >= slab.z1 + slack)
+        for d in range(2):
+            c = torch.floor(Xc[:, d] / slab.dx[d])
+            bad |= (c < -slack) | (c >= N + slack)
+        if n_rows is not None:  # a fixed-capacity array: the rows in use (device count)
+            bad &= torch.arange(Xc.shape[0], device=Xc.device) < n_rows
+        drift_flag.logical_or_(bad.any())
 
     def bin_step():
         if fixed:
@@ -586,11 +610,12 @@ def main():
         if gm is None:
             # the same rows as at the last binning (no migration changed the list): re-bin
             # from the previous order (ibtk_le_markers_rebin, exact); else bin afresh
-            if not args.full_bin and binned["rows"] == X.shape[0] and not (args.move and world > 1):
+            if not args.full_bin and binned["rows"] == X.shape[0] and not binned["changed"]:
                 bins.rebin(X)
             else:
                 bins.bin(geom, kernel, X)
                 binned["rows"] = X.shape[0]
+                binned["changed"] = False
             cur.update(X=X, F=F, U=U)
             return
         Xa, Fa, _ = gm.exchange(X, F)
@@ -644,17 +669,29 @@ def main():
         else:
             ex_f.ghost_sum(lambda: le.spread(ctx, bins, kernel, "side", geom, f, Fb, Xb))
 
+    nstep = {"k": 0}
+
     def step_move(record):
         # interp -> X += dt U -> migrate -> bin -> spread: one bin per step, as in
-        # IBMethod's explicit loop (interpolateVelocity, eulerStep, spreadForce)
+        # IBMethod's explicit loop (interpolateVelocity, eulerStep, spreadForce).  The
+        # markers migrate (and are renumbered) at regrid steps only: every step by
+        # default, every k-th with --regrid-every k (IBHierarchyIntegrator's
+        # regrid_interval, IBHierarchyIntegrator.cpp:495-508); between regrids they keep
+        # their rank and rows, and the binning is a re-binning of the same list
         nonlocal X, F, U, lag, n_dev
+        at_regrid = nstep["k"] % args.regrid_every == 0
+        nstep["k"] += 1
         if record:
             E[0].record()
         interp_with_fill()
         if record:
             E[1].record()
-        if fixed:
+        if not at_regrid:
+            le.position_update(ctx, "euler", dt_move, X, U, out=X)
+            check_drift(X, n_dev if fixed else None)
+        elif fixed:
             X, (F,), n_dev = update_and_migrate_fixed(slab, ctx, "euler", dt_move, X, U, [F], n_dev, send_cap)
+            binned["changed"] = True
         elif world > 1:
             # fused on the device: update, wrap, owner classes, stable partition;
             # the leavers to the z-neighbours (slab.update_and_migrate)
@@ -665,12 +702,14 @@ def main():
                 lag = lagf.to(torch.int32)
             if U.shape != X.shape:
                 U = torch.empty_like(X)
+            binned["changed"] = True
         else:
             le.position_update(ctx, "euler", dt_move, X, U, out=X)
-        if lag is not None:
+        if lag is not None and at_regrid:
             # the level's numbering and the LData reorder (cell order again after the move)
             d = redistribute(slab, ctx, X, [F], lag)
             X, F, lag = d.X, d.fields[0], d.lag
+            binned["changed"] = True
         bin_step()
         if record:
             E[2].record()
@@ -849,10 +888,15 @@ def main():
                            "recomputed from the current positions, the entries whose bucket changed inserted; "
                            "equal to a full binning)"),
                    "move": args.move, "renumber": args.renumber,
+                   "regrid_every": args.regrid_every if args.move else None,
+                   "exchange_width": slab.width if world > 1 else None,
+                   "drift_within_slack": (not bool(drift_flag.item())) if args.move and args.regrid_every > 1 else None,
                    "migration": ("fixed-capacity, device counts, no host sync" if fixed else
                                  "counts read by the host" if world > 1 and args.move else None), "overlap": world > 1 and not args.no_overlap,
                    "overlap_check": overlap_check,
-                   "step": ("ghost fill + interp(3 comps) + position update + migrate + " +
+                   "step": ("ghost fill + interp(3 comps) + position update + " +
+                            (f"at every {args.regrid_every}-th step (regrid) " if args.regrid_every > 1 else "") +
+                            "migrate + " +
                             ("redistribute (numbering + nonlocal nodes + reorder) + " if args.renumber else "") +
                             "bin + zero ghosts + "
                             "spread(3 comps) + ghost sum" if args.move else

@@ -22,6 +22,14 @@ For the side-centred z component the face z1 of rank r is face z0 of rank r+1;
 each rank treats faces [z0, z1) as its unique interior and z1 as a ghost, so the
 upper ghost block of that component is ghost+1 planes thick.
 
+Only ``width`` ghost planes per face are exchanged (Slab.width, default the ghost
+width).  A stencil of a marker inside the slab reaches W/2 planes beyond it (IB_4:
+2 -- the cell frame's NINT anchor gives ic_lower >= z0 - 2 and ic_upper <= z1 + 1,
+the side frame's one plane less below): that many suffice when the markers are
+migrated every step; the reference's ghost width W/2 + 1 (getMinimumGhostWidth)
+holds the slack for markers that drift up to a cell past the slab between regrids
+(CFL_WIDTH, LDataManager.cpp:167), the lazy cadence's case.
+
 The local periodic operations are injectable (``local_fill``/``local_fold``) so
 the exchange logic can be tested with gloo on CPU; the product default is the
 HIP library, and nothing falls back silently.
@@ -34,6 +42,11 @@ from typing import Callable, List, Optional, Sequence
 import torch
 
 
+def _rows(f: torch.Tensor) -> torch.Tensor:
+    """f as (rows, columns): a rank may hold no markers, and reshape(0, -1) is ambiguous."""
+    return f.reshape(f.shape[0], 1) if f.dim() == 1 else f.flatten(1)
+
+
 @dataclass
 class Slab:
     N: Sequence[int]      # global cells per dim
@@ -42,10 +55,15 @@ class Slab:
     ghost: int
     L: Sequence[float] = (1.0, 1.0, 1.0)
     align: int = 0        # > 0: the arrays' rows padded to a multiple of `align` (Geometry.aligned)
+    width: Optional[int] = None  # ghost planes exchanged per face (None: ghost)
 
     def __post_init__(self):
         if self.N[2] % self.P:
             raise ValueError(f"N_z={self.N[2]} not divisible by {self.P} ranks")
+        if self.width is None:
+            self.width = self.ghost
+        if not 0 < self.width <= self.ghost:
+            raise ValueError(f"exchange width {self.width} outside [1, ghost={self.ghost}]")
         self.nz = self.N[2] // self.P
         if self.P > 1 and self.nz < 2 * self.ghost + 2:
             raise ValueError("slab thinner than 2*ghost+2 planes")
@@ -62,14 +80,15 @@ class Slab:
                      [self.L[0], self.L[1], self.z1 * self.dx[2]])
         return g.aligned(self.align) if self.align else g
 
-    # plane blocks of one side component array (leading dim = z planes)
+    # plane blocks of one side component array (leading dim = z planes): the `width`
+    # ghost planes next to each face and the interior planes they mirror
     def blocks(self, comp: int):
-        g, nz = self.ghost, self.nz
-        up = g + (1 if comp == 2 else 0)   # upper ghost thickness (z-faces carry z1)
+        g, nz, w = self.ghost, self.nz, self.width
+        up = w + (1 if comp == 2 else 0)   # upper ghost thickness (z-faces carry z1)
         return {
-            "lo_ghost": (0, g),                   # -> down neighbour's top interior
+            "lo_ghost": (g - w, g),               # -> down neighbour's top interior
             "hi_ghost": (g + nz, g + nz + up),    # -> up neighbour's bottom interior
-            "top_int": (nz, nz + g),              # <- up neighbour's lo_ghost
+            "top_int": (g + nz - w, g + nz),      # <- up neighbour's lo_ghost
             "bot_int": (g, g + up),               # <- down neighbour's hi_ghost
         }
 
@@ -260,9 +279,12 @@ class GhostMarkers:
     rank within the spread tolerance, and are bit-stable run to run.
     """
 
-    def __init__(self, slab: Slab, group=None):
+    def __init__(self, slab: Slab, group=None, width: Optional[int] = None):
         self.slab = slab
         self.group = group
+        # planes of markers sent per face: the stencils' reach (Slab.width) for the
+        # spread; the full ghost width for redistribute's nonlocal nodes (the ghost box)
+        self.width = slab.width if width is None else width
 
     def _p2p(self, sends, recvs):
         import torch.distributed as dist
@@ -282,12 +304,12 @@ class GhostMarkers:
             t.copy_(h)
 
     def select(self, X: torch.Tensor):
-        """(to_up, to_down): indices of the markers within `ghost` cells of the
+        """(to_up, to_down): indices of the markers within `width` cells of the
         upper / lower slab face (a marker can be in both when the slab is thin)."""
         s = self.slab
         cz = torch.clamp((X[:, 2] / s.dx[2]).floor().long(), 0, s.N[2] - 1)
-        up = (cz >= s.z1 - s.ghost).nonzero().squeeze(1)
-        down = (cz < s.z0 + s.ghost).nonzero().squeeze(1)
+        up = (cz >= s.z1 - self.width).nonzero().squeeze(1)
+        down = (cz < s.z0 + self.width).nonzero().squeeze(1)
         return up, down
 
     def exchange(self, X: torch.Tensor, F: torch.Tensor):
@@ -297,7 +319,7 @@ class GhostMarkers:
         if s.P == 1:
             return X, F, X.shape[0]
         up, down = self.select(X)
-        data = torch.cat([X, F.reshape(X.shape[0], -1).to(X.dtype)], dim=1)
+        data = torch.cat([X, _rows(F).to(X.dtype)], dim=1)
         send_up, send_down = data[up].contiguous(), data[down].contiguous()
         # counts, then data; each peer's receives in the order it sends (RCCL
         # matches a pair's messages in issue order; with P = 2 up == down):
@@ -345,7 +367,7 @@ def update_and_migrate(slab: Slab, ctx, scheme: str, dt: float, X: torch.Tensor,
     M = X.shape[0]
     Xn, order, counts = le.slab_update_partition(ctx, scheme, dt, X, U0, slab.L, slab.N[2], slab.P, slab.rank,
                                                  U1=U1)
-    flat = [f.reshape(M, -1) for f in fields]
+    flat = [_rows(f) for f in fields]
     if slab.P == 1:
         return Xn, list(fields)  # everything stays; the order is the input order
     # counts to the neighbours and the global "further" flag
@@ -400,7 +422,7 @@ def update_and_migrate_fixed(slab: Slab, ctx, scheme: str, dt: float, X: torch.T
     C = X.shape[0]
     Xn, order, counts = le.slab_update_partition_count(ctx, scheme, dt, X, U0, slab.L, slab.N[2], slab.P, slab.rank,
                                                        n_dev, U1=U1)
-    flat = [f.reshape(C, -1) for f in fields]
+    flat = [_rows(f) for f in fields]
     data = torch.cat([Xn] + [f.to(Xn.dtype) for f in flat], dim=1).contiguous()
     D = data.shape[1]
     if slab.P == 1:
@@ -459,7 +481,7 @@ def migrate(slab: Slab, X: torch.Tensor, fields: Sequence[torch.Tensor] = (), gr
     Xw = torch.where(Xw >= L, Xw - L, Xw)  # remainder can round up to L
     cell = [torch.clamp((Xw[:, d] / slab.dx[d]).floor().long(), 0, slab.N[d] - 1) for d in range(3)]
     dest = cell[2] // slab.nz
-    cols = [Xw] + [f.reshape(M, -1).to(X.dtype) for f in fields]
+    cols = [Xw] + [_rows(f).to(X.dtype) for f in fields]
     widths = [c.shape[1] for c in cols]
     data = torch.cat(cols, dim=1)
     stay = None
@@ -570,7 +592,7 @@ def redistribute(slab: Slab, ctx, X: torch.Tensor, fields: Sequence[torch.Tensor
     if nn:
         raise RuntimeError(f"rank {slab.rank}: {nn} markers outside the slab; migrate before redistribute")
     M = X.shape[0]
-    flat = [f.reshape(M, -1).to(X.dtype).contiguous() for f in fields]
+    flat = [_rows(f).to(X.dtype).contiguous() for f in fields]
     Xn, *fn = reorder(order, X, *flat) if nl else [X[:0]] + [f[:0] for f in flat]
     fn = [o.reshape((o.shape[0],) + tuple(f.shape[1:])).to(f.dtype).contiguous() for o, f in zip(fn, fields)]
     lagn = lag[order.long()]
@@ -589,7 +611,7 @@ def redistribute(slab: Slab, ctx, X: torch.Tensor, fields: Sequence[torch.Tensor
     # by -+L_z, and z + L_z - L_z need not give z back: the owner's bits travel along)
     ids = torch.stack([lagn.to(X.dtype), offset + torch.arange(nl, dtype=X.dtype, device=X.device), Xn[:, 2]],
                       dim=1)
-    Xa, Ia, n_own = GhostMarkers(slab, group).exchange(Xn, ids)
+    Xa, Ia, n_own = GhostMarkers(slab, group, width=slab.ghost).exchange(Xn, ids)
     gX = Xa[:0]
     gI = Ia[:0]
     if Xa.shape[0] > n_own:

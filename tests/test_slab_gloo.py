@@ -71,13 +71,21 @@ def _np_local(arrays, periodic, slab, mode):
                     a[tuple(s_dst[::-1])] += a[tuple(s_src[::-1])]
 
 
-def _worker(rank, world, port, N, ghost, out_q):
+def _worker(rank, world, port, N, ghost, out_q, width=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from ibamr_amd.slab import Slab, SlabExchange
-        slab = Slab([N, N, N], world, rank, ghost)
+        slab = Slab([N, N, N], world, rank, ghost, width=width)
+        w = slab.width
+        # z planes the exchanges cover (array coordinates): the interior and `width`
+        # ghost planes per face (the z component's upper block one plane thicker);
+        # with one rank every plane (local periodic fill / fold)
+        def zcov(c):
+            if world == 1:
+                return slice(None)
+            return slice(ghost - w, ghost + slab.nz + w + (1 if c == 2 else 0))
         geom_shapes = []
         for c in range(3):
             n = [N + 2 * ghost + (1 if d == c else 0) for d in range(2)] + [slab.nz + 2 * ghost + (1 if c == 2 else 0)]
@@ -104,10 +112,15 @@ def _worker(rank, world, port, N, ghost, out_q):
             yy = np.arange(a.shape[1]) - ghost
             xx = np.arange(a.shape[2]) - ghost
             expect = Gs[c][np.ix_(zz % N, yy % N, xx % N)]
-            assert np.array_equal(a, expect), f"halo_fill rank {rank} comp {c}"
-        # ---- ghost sum: every point (interior and ghost) carries a value; the
-        # result's interior must equal the sum of all values wrapping onto it
-        arrays = [torch.from_numpy(rng.integers(-20, 20, geom_shapes[c]).astype(np.float64)) for c in range(3)]
+            assert np.array_equal(a[zcov(c)], expect[zcov(c)]), f"halo_fill rank {rank} comp {c}"
+        # ---- ghost sum: every point the exchange covers (interior and ghost) carries a
+        # value (the planes beyond `width` hold none, as a stencil never reaches them);
+        # the result's interior must equal the sum of all values wrapping onto it
+        arrays = []
+        for c in range(3):
+            a = np.zeros(geom_shapes[c])
+            a[zcov(c)] = rng.integers(-20, 20, geom_shapes[c]).astype(np.float64)[zcov(c)]
+            arrays.append(torch.from_numpy(a))
         before = [a.numpy().copy() for a in arrays]
         ex = SlabExchange(slab, arrays, local_fill=lambda arr, per: _np_local(arr, per, slab, "fill"),
                           local_fold=lambda arr, per: _np_local(arr, per, slab, "fold"))
@@ -134,15 +147,17 @@ def _worker(rank, world, port, N, ghost, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [1, 2, 4])
-def test_slab_exchange_gloo(world):
+@pytest.mark.parametrize("world,width", [(1, None), (2, None), (4, None), (2, 2), (4, 2)])
+def test_slab_exchange_gloo(world, width):
+    """width None: the ghost width (3) per face; 2: the planes an IB_4 stencil of a marker
+    inside the slab reaches (Slab.width)."""
     N, ghost = 16, 3
     if world > 1 and N // world < 2 * ghost + 2:
         N = world * (2 * ghost + 2)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, N, ghost, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, ghost, q, width)) for r in range(world)]
     for p in procs:
         p.start()
     results = []
@@ -383,3 +398,97 @@ def test_redistribute_numbering_gloo(world):
             assert np.array_equal(x, owner_X[int(lg)]), (r[0], int(lg), x, owner_X[int(lg)])
             tiny += 0.0 < x[2] < 1e-12
     assert tiny > 0
+
+
+# ---------------------------------------------------------------------------- lazy cadence
+def _cadence_worker(rank, world, port, k, nsteps, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from oracle import oracle as ora
+        from ibamr_amd.slab import Slab, migrate, redistribute
+        N = [16, 16, 32]
+        slab = Slab(N, world, rank, 3)
+        slack = slab.ghost - (slab.ghost - 1)  # the ghost width's spare cell (bench.py --regrid-every)
+        g = torch.Generator().manual_seed(77)
+        M = 3000
+        Xg = torch.rand((M, 3), dtype=torch.float64, generator=g) * 0.6 + 0.2  # no periodic wrap in the test
+        Xg[:, 2] = torch.rand(M, dtype=torch.float64, generator=g) * 0.4 + 0.3
+        lag_g = torch.randperm(M, generator=g).to(torch.int32)
+        Fg = torch.rand((M, 3), dtype=torch.float64, generator=g)
+        cz = (Xg[:, 2] / slab.dx[2]).floor().long()
+        mine = (cz >= slab.z0) & (cz < slab.z1)
+        dt = 0.3 * slab.dx[2]
+
+        def vel(X):  # a smooth field moving markers across the interior slab faces
+            return torch.stack([torch.zeros_like(X[:, 0]), torch.zeros_like(X[:, 0]),
+                                torch.sin(2 * np.pi * X[:, 0]) * torch.cos(2 * np.pi * X[:, 1])], dim=1)
+
+        boxes = [([0, 0, slab.z0], [N[0] - 1, N[1] - 1, slab.z1 - 1])]
+        dx = [1.0 / n for n in N]
+
+        def numbering(Xa, la, ghost):
+            o, nl, nn = ora.level_node_distribution(Xa.numpy(), la.numpy(), boxes, [0, 0, 0], [n - 1 for n in N],
+                                                    [0.0] * 3, dx, ghost)
+            return torch.from_numpy(o), nl, nn
+
+        def reorder(order, *arrays):
+            return [a[order.long()] for a in arrays]
+
+        def wrap(Xw):
+            return Xw
+
+        def run(lazy):
+            X, F, lag = Xg[mine].clone(), Fg[mine].clone(), lag_g[mine].clone()
+            out, drift_ok = [], True
+            for t in range(1, nsteps + 1):
+                X = X + dt * vel(X)
+                regrid = t % k == 0
+                if not lazy or regrid:
+                    X, (F, lagf) = migrate(slab, X, [F, lag.to(torch.float64)], cell_order=False)
+                    lag = lagf.to(torch.int32)
+                else:  # between regrids: the markers keep their rank, within the slack
+                    c = (X[:, 2] / slab.dx[2]).floor()
+                    drift_ok = drift_ok and bool(((c >= slab.z0 - slack) & (c < slab.z1 + slack)).all())
+                if regrid:
+                    d = redistribute(slab, None, X, [F], lag, numbering=numbering, reorder=reorder, wrap=wrap)
+                    X, F, lag = d.X, d.fields[0], d.lag
+                    out.append(d)
+            return out, drift_ok
+
+        per_step, _ = run(False)
+        lazy, drift_ok = run(True)
+        same = len(per_step) == len(lazy) and all(
+            torch.equal(a.X, b.X) and torch.equal(a.lag, b.lag) and torch.equal(a.fields[0], b.fields[0])
+            and a.offset == b.offset and a.num_nodes == b.num_nodes and torch.equal(a.ghost_X, b.ghost_X)
+            and torch.equal(a.ghost_lag, b.ghost_lag) and torch.equal(a.ghost_petsc, b.ghost_petsc)
+            for a, b in zip(per_step, lazy))
+        moved = sum(int(d.num_nodes) for d in lazy)
+        q.put((rank, "ok", same, drift_ok, moved))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc(), False, False, 0))
+
+
+@pytest.mark.parametrize("world,k", [(2, 3), (4, 3), (2, 1)])
+def test_lazy_regrid_cadence_gloo(world, k):
+    """The reference's lazy cadence (migrate and renumber every k-th step, markers kept
+    on their rank in between, IBHierarchyIntegrator.cpp:495-508): at every regrid step
+    the node distribution -- owned positions, fields, Lagrangian indices, offsets,
+    nonlocal nodes -- equals, entry by entry, the one of migrating every step; between
+    regrids every marker stays within the ghost width's spare cell of its slab."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cadence_worker, args=(r, world, port, k, 3 * k, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    bad = [r for r in res if r[1] != "ok"]
+    assert not bad, bad[0][1]
+    assert all(r[2] for r in res), "lazy cadence differs from per-step migration at a regrid step"
+    assert all(r[3] for r in res), "a marker drifted past the slack between regrids"
