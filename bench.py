@@ -447,7 +447,11 @@ def main():
     ap.add_argument("--kernel", default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--unfused-zero", action="store_true",
-                    help="cfg5: zero f and spread as two launches instead of ibtk_le_level_zero_spread (A/B)")
+                    help="zero f's ghosts (cfg5: all of f) and spread as two launches instead of one "
+                         "(ibtk_le_zero_ghosts_spread / ibtk_le_level_zero_spread; A/B)")
+    ap.add_argument("--unfused-fill", action="store_true",
+                    help="fill u's periodic ghosts with their own passes, then interp (instead of "
+                         "ibtk_le_fill_interp reading the ghost points at their periodic images; A/B)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-rebin", action="store_true", help="bin once outside the timed loop")
     ap.add_argument("--full-bin", action="store_true",
@@ -642,32 +646,55 @@ def main():
 
     dt_move = 0.05 * slab.dx[0]  # |U| <= ~1: markers move <= 1/20 cell per step
 
+    # the periodic ghost fill of u fused into the interp's sweep (ibtk_le_fill_interp: the
+    # ghost points read at their periodic images, x/y/z on one rank, x/y on a slab whose z
+    # ghost planes come from its neighbours); --unfused-fill: the fill passes, then interp
+    fused_fill = not args.unfused_fill
+
+    def interp_call(Ub, Xb):
+        if fused_fill:
+            le.fill_interp(ctx, bins, kernel, "side", geom, u, Ub, Xb, periodic=[1, 1, 1 if world == 1 else 0])
+        else:
+            le.interp(ctx, bins, kernel, "side", geom, u, Ub, Xb)
+
     def interp_with_fill():
         # N > 1: the interior sweep items run while the z ghost planes are in flight
         Xb, Ub = cur["X"], cur["U"]
         if args.no_overlap:
-            ex_u.halo_fill()
-            le.interp(ctx, bins, kernel, "side", geom, u, Ub, Xb)
+            ex_u.halo_fill(local=not fused_fill)
+            interp_call(Ub, Xb)
         else:
-            ex_u.halo_fill(lambda: le.interp(ctx, bins, kernel, "side", geom, u, Ub, Xb))
+            ex_u.halo_fill(lambda: interp_call(Ub, Xb), local=not fused_fill)
         if Ub is not U:
             U.copy_(Ub[:U.shape[0]])  # the own markers' velocities (ghost markers' discarded)
 
     def spread_with_sum():
+        # the ghosts of f start from 0: ibtk_le_zero_ghosts fused into the spread's sweep
+        # (its items start their owned ghost points from 0; --unfused-zero: two calls)
         Xb, Fb = cur["X"], cur["F"]
+
+        def spread():
+            if args.unfused_zero:
+                le.spread(ctx, bins, kernel, "side", geom, f, Fb, Xb)
+            else:
+                le.zero_ghosts_spread(ctx, bins, kernel, "side", geom, f, Fb, Xb)
         if gm is not None:
             # ghost markers: every rank spreads what reaches its own planes, no z
             # exchange of the grid; x/y periodic ghosts fold locally
-            le.spread(ctx, bins, kernel, "side", geom, f, Fb, Xb)
+            spread()
             ex_f.local_fold([1, 1, 0])
             return
         # N > 1: the boundary items first, then the interior ones while the ghost
         # planes are in flight
         if args.no_overlap:
-            le.spread(ctx, bins, kernel, "side", geom, f, Fb, Xb)
+            spread()
             ex_f.ghost_sum()
         else:
-            ex_f.ghost_sum(lambda: le.spread(ctx, bins, kernel, "side", geom, f, Fb, Xb))
+            ex_f.ghost_sum(spread)
+
+    def zero_step():
+        if args.unfused_zero:
+            le.zero_ghosts(ctx, geom, "side", f)
 
     nstep = {"k": 0}
 
@@ -713,7 +740,7 @@ def main():
         bin_step()
         if record:
             E[2].record()
-        le.zero_ghosts(ctx, geom, "side", f)
+        zero_step()
         if record:
             E[3].record()
         spread_with_sum()
@@ -732,7 +759,7 @@ def main():
         interp_with_fill()
         if record:
             E[2].record()
-        le.zero_ghosts(ctx, geom, "side", f)
+        zero_step()
         if record:
             E[3].record()
         spread_with_sum()
@@ -760,17 +787,18 @@ def main():
     if world > 1 and not args.no_overlap and gm is None:
         Xb = cur["X"]
         Uo, Us = torch.empty_like(cur["U"]), torch.empty_like(cur["U"])
-        ex_u.halo_fill(lambda: le.interp(ctx, bins, kernel, "side", geom, u, Uo, Xb))
-        ex_u.halo_fill()
-        le.interp(ctx, bins, kernel, "side", geom, u, Us, Xb)
+        ex_u.halo_fill(lambda: interp_call(Uo, Xb), local=not fused_fill)
+        ex_u.halo_fill(local=not fused_fill)
+        interp_call(Us, Xb)
         fo = []
         for overlapped in (True, False):
             for a in f:
                 a.zero_()
+            sp = le.spread if args.unfused_zero else le.zero_ghosts_spread  # the timed steps' form
             if overlapped:
-                ex_f.ghost_sum(lambda: le.spread(ctx, bins, kernel, "side", geom, f, cur["F"], Xb))
+                ex_f.ghost_sum(lambda: sp(ctx, bins, kernel, "side", geom, f, cur["F"], Xb))
             else:
-                le.spread(ctx, bins, kernel, "side", geom, f, cur["F"], Xb)
+                sp(ctx, bins, kernel, "side", geom, f, cur["F"], Xb)
                 ex_f.ghost_sum()
             fo.append([a.clone() for a in f])
         same = torch.equal(Uo, Us) and all(torch.equal(a, b) for a, b in zip(*fo))
@@ -815,12 +843,15 @@ def main():
     ctx.enable_timing(True)
     kt = {"interp": [], "spread": []}
     for _ in range(3):
-        ex_u.halo_fill()
-        le.interp(ctx, bins, kernel, "side", geom, u, cur["U"], cur["X"])
+        ex_u.halo_fill(local=not fused_fill)
+        interp_call(cur["U"], cur["X"])
         ctx.synchronize()
         kt["interp"].append(ctx.last_kernel_ms())
-        le.zero_ghosts(ctx, geom, "side", f)
-        le.spread(ctx, bins, kernel, "side", geom, f, cur["F"], cur["X"])
+        if args.unfused_zero:
+            le.zero_ghosts(ctx, geom, "side", f)
+            le.spread(ctx, bins, kernel, "side", geom, f, cur["F"], cur["X"])
+        else:
+            le.zero_ghosts_spread(ctx, bins, kernel, "side", geom, f, cur["F"], cur["X"])
         ctx.synchronize()
         kt["spread"].append(ctx.last_kernel_ms())
     ctx.enable_timing(False)
@@ -900,7 +931,11 @@ def main():
                             ("redistribute (numbering + nonlocal nodes + reorder) + " if args.renumber else "") +
                             "bin + zero ghosts + "
                             "spread(3 comps) + ghost sum" if args.move else
-                            "bin + ghost fill + interp(3 comps) + zero ghosts + spread(3 comps) + ghost sum")},
+                            "bin + ghost fill + interp(3 comps) + zero ghosts + spread(3 comps) + ghost sum") +
+                           ("" if args.unfused_zero else
+                            "; the ghost zeroing fused into the spread sweep (ibtk_le_zero_ghosts_spread)") +
+                           ("" if args.unfused_fill else
+                            "; the periodic ghost fill fused into the interp sweep (ibtk_le_fill_interp)")},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per launch (PMC)", "traffic_note": traffic_note,
                      "algorithmic_bytes": {"interp": B_i, "spread": B_s},

@@ -133,6 +133,12 @@ _SIGS = [
     ("ibtk_le_slab_migrate_unpack", c_int,
      [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     ("ibtk_le_zero_ghosts", c_int, [c_void_p, ctypes.POINTER(PatchGeom), c_int, ctypes.POINTER(c_void_p), c_int]),
+    ("ibtk_le_fill_interp", c_int,
+     [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_int, c_void_p,
+      c_int, c_void_p, c_void_p]),
+    ("ibtk_le_zero_ghosts_spread", c_int,
+     [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_int, c_void_p,
+      c_int, c_void_p]),
     ("ibtk_le_mark_stencils", c_int,
      [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_int,
       c_void_p]),

@@ -477,6 +477,7 @@ static int make_comps(const ibtk_le_patch_geom* g, int centering, int axis, doub
                 cd.lo[d] = g->ilower[d] - g->gcw[d];
                 cd.hi[d] = g->iupper[d] + g->gcw[d] + ((ext_mask >> d) & 1);
                 cd.ilower[d] = g->ilower[d];
+                cd.iupper[d] = g->iupper[d];
                 cd.xlo[d] = g->x_lower[d];
                 if ((shift_mask >> d) & 1) cd.xlo[d] -= 0.5 * g->dx[d];
                 n[d] = cd.hi[d] - cd.lo[d] + 1;
@@ -1010,10 +1011,12 @@ static int stamps_report(ibtk_le_ctx ctx, size_t nst, Params& p) {
 
 int ibtk_le::interp_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis, const void* geomv,
                          const double* const* q_dev, int q_depth, double* Q_dev, int Q_depth, const double* X_dev,
-                         bool check_ghosts) {
+                         bool check_ghosts, const int* iper) {
     const ibtk_le_patch_geom* geom = static_cast<const ibtk_le_patch_geom*>(geomv);
     Params p;
     if (int rc = prepare(ctx, m, kernel, geom, X_dev, p)) return rc;
+    if (iper)
+        for (int d = 0; d < 3; ++d) p.iper[d] = iper[d] ? 1 : 0;
     // LEInteractor.cpp:2416-2426: interp needs min(gcw) >= floor(stencil/2)+1
     int gmin = geom->gcw[0];
     for (int d = 1; d < geom->ndim; ++d) gmin = std::min(gmin, geom->gcw[d]);
@@ -1053,6 +1056,23 @@ extern "C" int ibtk_le_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, in
     return ibtk_le::interp_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, X_dev, true);
 }
 
+// ibtk_le_fill_periodic_ghosts + ibtk_le_interp: the 3-D column sweep reads every ghost
+// point of the ghost box at its periodic image (the value the fill copies there) and
+// writes no ghost; other binnings: the two calls
+extern "C" int ibtk_le_fill_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                                   const ibtk_le_patch_geom* geom, const double* const* q_dev, int q_depth,
+                                   double* Q_dev, int Q_depth, const double* X_dev, const int* periodic) {
+    int per[3] = {1, 1, 1};
+    if (periodic)
+        for (int d = 0; d < 3; ++d) per[d] = (geom && d < geom->ndim) ? (periodic[d] ? 1 : 0) : 0;
+    if (!geom || geom->ndim != 3 || !m || !m->binned3) {
+        if (int rc = ibtk_le_fill_periodic_ghosts(ctx, geom, centering, const_cast<double* const*>(q_dev), q_depth, per))
+            return rc;
+        return ibtk_le::interp_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, X_dev, true);
+    }
+    return ibtk_le::interp_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, X_dev, true, per);
+}
+
 // Super-brick candidate lists (k_cand): count, exclusive scan, write.  Built once
 // per binning, on the first spread after it.
 static int build_candidates(ibtk_le_ctx ctx, ibtk_le_markers m, const Params& p) {
@@ -1077,12 +1097,24 @@ static int build_candidates(ibtk_le_ctx ctx, ibtk_le_markers m, const Params& p)
 
 static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                        const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
-                       int Q_depth, const double* ds_dev, const double* X_dev);
+                       int Q_depth, const double* ds_dev, const double* X_dev, bool zero_ghosts = false);
 
 extern "C" int ibtk_le_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                               const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
                               int Q_depth, const double* X_dev) {
     return spread_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, nullptr, X_dev);
+}
+
+// ibtk_le_zero_ghosts + ibtk_le_spread: the 3-D column sweeps start the owned ghost
+// points from 0 (no separate pass over the ghost layers); 2-D: the two calls
+extern "C" int ibtk_le_zero_ghosts_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                                          const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth,
+                                          const double* Q_dev, int Q_depth, const double* X_dev) {
+    if (!geom || geom->ndim != 3 || !m || m->n == 0 || !m->binned3) {
+        if (int rc = ibtk_le_zero_ghosts(ctx, geom, centering, q_dev, q_depth)) return rc;
+        return spread_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, nullptr, X_dev);
+    }
+    return spread_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, nullptr, X_dev, true);
 }
 
 extern "C" int ibtk_le_spread_ds(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
@@ -1251,9 +1283,10 @@ extern "C" int ibtk_le_user_spread(ibtk_le_ctx ctx, int centering, int axis, con
 
 static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                        const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
-                       int Q_depth, const double* ds_dev, const double* X_dev) {
+                       int Q_depth, const double* ds_dev, const double* X_dev, bool zero_ghosts) {
     Params p;
     if (int rc = prepare(ctx, m, kernel, geom, X_dev, p)) return rc;
+    p.zero_ghosts = zero_ghosts ? 1 : 0;
     const int nc = ncomponents(geom, centering, q_depth, Q_depth);
     if (nc < 0) return -nc;
     if (m->n == 0) return IBTK_LE_OK;  // LEInteractor.cpp:2747

@@ -52,6 +52,8 @@ struct CompDesc {
     int lo[3];       // ghost box lower
     int hi[3];       // ghost box upper (inclusive)
     int ilower[3];   // the "ilower" argument the Fortran receives (data box lower)
+    int iupper[3];   // the patch box upper: points past it (or below ilower) are the ghost
+                     // points of the periodic ghost operations (a side array's face iupper+1 too)
     double xlo[3];   // the "x_lower" argument the Fortran receives (frame shift applied)
     int qcomp;       // which AoS component of Q this array pairs with
     int axis;        // `axis` argument (DISCONTINUOUS_LINEAR)
@@ -174,6 +176,9 @@ struct Params {
     unsigned long long* stamps = nullptr;  // diagnostic phase clocks (nullptr: off)
     unsigned long long* nadd = nullptr;    // spread: [ds_add_f64 wave-instructions, lane adds] issued (nullptr: not counted)
     int zero_first = 0;  // 3-D spread: the arrays start from 0 (every point, ghosts included), not their values
+    int zero_ghosts = 0; // 3-D spread: the ghost points (outside the data box) start from 0, the others from their values
+    int iper[3] = {0, 0, 0};  // 3-D interp: read the ghost points of the ghost box at their periodic image in
+                              // these dims (ibtk_le_fill_interp: the periodic ghost fill fused in)
     int comp0 = 0;       // 3-D spread: a launch's components are comp[comp0 .. comp0 + ncomp)
 };
 
@@ -431,5 +436,5 @@ struct ibtk_le_patch_geom_s;
 namespace ibtk_le {
 int interp_impl(ibtk_le_ctx_s* ctx, ibtk_le_markers_s* m, int kernel, int centering, int axis, const void* geom,
                 const double* const* q_dev, int q_depth, double* Q_dev, int Q_depth, const double* X_dev,
-                bool check_ghosts);
+                bool check_ghosts, const int* iper = nullptr);
 }  // namespace ibtk_le

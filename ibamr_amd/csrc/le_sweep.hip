@@ -665,20 +665,31 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     // buffer resource (plane_rsrc); a point outside the array has OFF_NONE, and a
     // plane outside it an empty resource, so their loads return the 0 the
     // clipped stencil points are staged as (no select per point)
+    // iper (ibtk_le_fill_interp): a ghost point of the ghost box is read at its periodic
+    // image in the periodic dims -- the value the periodic fill would copy there (k_ghost
+    // mode 0: every periodic dim wrapped into the patch box); points outside the ghost
+    // box stay clipped (staged as 0)
+    auto image = [&](int i, int d) {
+        if (!p.iper[d] || (i >= cd.ilower[d] && i <= cd.iupper[d])) return i;
+        const int n = cd.iupper[d] - cd.ilower[d] + 1;
+        int r = (i - cd.ilower[d]) % n;
+        return cd.ilower[d] + (r < 0 ? r + n : r);
+    };
     unsigned poff[NPT];
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
         const int q = min(lane + SW * k, S::PV - 1);
         const int gx = gx0 + q % RX, gy = gy0 + q / RX;
         const bool in = gx >= cd.lo[0] && gx <= cd.hi[0] && gy >= cd.lo[1] && gy <= cd.hi[1];
-        poff[k] = in ? 8u * (unsigned)((gx - cd.lo[0]) + (gy - cd.lo[1]) * (int)cd.s1) : OFF_NONE;
+        poff[k] = in ? 8u * (unsigned)((image(gx, 0) - cd.lo[0]) + (image(gy, 1) - cd.lo[1]) * (int)cd.s1) : OFF_NONE;
     }
     const int plast = a1 - 1 + HI;  // last plane the item reads
     const unsigned plane_bytes = (unsigned)(8 * cd.s2);
     // relative plane zr -> registers
     auto plane_load = [&](int zr, double* v) {
-        const int z = zorg + min(zr, plast);
-        const bool zin = z >= cd.lo[2] && z <= cd.hi[2];
+        const int z0 = zorg + min(zr, plast);
+        const bool zin = z0 >= cd.lo[2] && z0 <= cd.hi[2];
+        const int z = zin ? image(z0, 2) : z0;
         const int zc = min(max(z, cd.lo[2]), cd.hi[2]);
         const auto pb = plane_rsrc(cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2, zin ? plane_bytes : 0u);
 #pragma unroll
@@ -1082,12 +1093,23 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     }
     const int afirst = max(plo - HI, 0), alast = min(phi - LO, cg.nz - 1);
     const int col0 = (cy - 1) * ncx + (cx - 1);  // column (cx-1, cy-1)
-    bool any = false;  // no candidate reaches the item: u unchanged (zero_first: 0)
+    bool any = false;  // no candidate reaches the item: u unchanged (zero_first: 0; zero_ghosts: ghosts 0)
     for (int a = afirst + lane; a <= alast; a += SW)
         for (int r = 0; r < 3; ++r)
             any = any || bs[bucket(cg, a, col0 + r * ncx, 3 * NBAND)] > bs[bucket(cg, a, col0 + r * ncx, 0)];
     any = __any(any);
-    if (!any && !p.zero_first) return;
+    // zero_ghosts (ibtk_le_zero_ghosts_spread): the owned points outside the component's
+    // data box start from 0 instead of their values -- ibtk_le_zero_ghosts fused in
+    const bool zg = p.zero_ghosts && !p.zero_first;
+    int dlo[3], dhi[3];  // the unique points (patch box): ibtk_le_zero_ghosts zeroes the others
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        dlo[d] = cd.ilower[d];
+        dhi[d] = cd.iupper[d];
+    }
+    const bool xy_inner = X0 >= dlo[0] && X0 + COLX - 1 <= dhi[0] && Y0 >= dlo[1] && Y0 + COLY - 1 <= dhi[1];
+    const bool z_inner = zorg + plo >= dlo[2] && zorg + phi <= dhi[2];
+    if (!any && !p.zero_first && !(zg && !(xy_inner && z_inner))) return;
     const int nlast = p.nsorted - 1;
     // the lane's points of a plane: slot index lane + 64 k (tile-major, so the
     // staging stores and writeback loads are contiguous in LDS), their array
@@ -1095,23 +1117,28 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // (byte offsets in a plane through a buffer resource, plane_rsrc; a point the
     // item does not own has OFF_NONE: its load returns 0 and its store is dropped)
     unsigned loff[NPL];
+    unsigned gmask = 0;  // zero_ghosts: bit k = the lane's point k is an x/y ghost point
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
         int xl, yl;
         ring_xy(lane + k * SW, xl, yl);
         const bool own = xl >= xlo && xl <= xhi && yl >= ylo && yl <= yhi;
         loff[k] = own ? 8u * (unsigned)((X0 + xl - cd.lo[0]) + (Y0 + yl - cd.lo[1]) * (int)cd.s1) : OFF_NONE;
+        const int gx = X0 + xl, gy = Y0 + yl;
+        if (zg && (gx < dlo[0] || gx > dhi[0] || gy < dlo[1] || gy > dhi[1])) gmask |= 1u << k;
     }
+    auto zghost = [&](int z) { return zorg + z < dlo[2] || zorg + z > dhi[2]; };
     const unsigned plane_bytes = (unsigned)(8 * cd.s2);
     auto plane_ptr = [&](int z) {  // relative plane z, clamped into the array
         const int zc = min(max(zorg + z, cd.lo[2]), cd.hi[2]);
         return plane_rsrc(cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2, plane_bytes);
     };
-    if (!any) {  // zero_first, no candidate: the owned points are 0
+    if (!any) {  // no candidate: zero_first, the owned points are 0; zero_ghosts, the owned ghosts
         for (int z = plo; z <= phi; ++z) {
             const auto pb = plane_ptr(z);
+            const bool all = p.zero_first || zghost(z);
 #pragma unroll
-            for (int k = 0; k < NPL; ++k) buf_st(pb, loff[k], 0.0);
+            for (int k = 0; k < NPL; ++k) buf_st(pb, (all || ((gmask >> k) & 1u)) ? loff[k] : OFF_NONE, 0.0);
         }
         return;
     }
@@ -1147,14 +1174,14 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // slot's contents do not matter, so it is not read.
     auto plane_load = [&](int z, double* v) {
         if (z < plo || z > phi) return;
-        if (p.zero_first) {  // the owned points start from 0: nothing to read
+        if (p.zero_first || (zg && zghost(z))) {  // the owned points start from 0: nothing to read
 #pragma unroll
             for (int k = 0; k < NPL; ++k) v[k] = 0.0;
             return;
         }
         const auto pb = plane_ptr(z);
 #pragma unroll
-        for (int k = 0; k < NPL; ++k) v[k] = buf_ld(pb, loff[k]);
+        for (int k = 0; k < NPL; ++k) v[k] = buf_ld(pb, ((gmask >> k) & 1u) ? OFF_NONE : loff[k]);  // ghosts read 0
     };
     auto plane_put = [&](int z, const double* v) {
         double* sl = ring + sslot<S>(z) * S::PV;

@@ -339,6 +339,33 @@ def spread(ctx: Context, markers: Markers, kernel: str, centering: str, geom: Ge
                                         ctypes.byref(geom.c), arr, q_depth, _ptr(Q), Q_depth, _ptr(ds), _ptr(X)))
 
 
+def fill_interp(ctx: Context, markers: Markers, kernel: str, centering: str, geom: Geometry,
+                q: Sequence[torch.Tensor], Q: torch.Tensor, X: torch.Tensor, q_depth: int = 1,
+                Q_depth: Optional[int] = None, axis: int = 0, periodic=None):
+    """fill_periodic_ghosts(q, periodic) then interp, Q bit for bit, in one sweep on a 3-D
+    column binning (ibtk_le_fill_interp): the ghost points are read at their periodic
+    images and q is left unmodified."""
+    if Q_depth is None:
+        Q_depth = geom.ndim if centering in ("side", "edge") else q_depth
+    arr = _ptr_array(q, geom)
+    pa = _periodic_arg(periodic, geom.ndim)
+    check(ctx.lib.ibtk_le_fill_interp(ctx.h, markers.h, kernel_id(kernel), CENTERING[centering], axis,
+                                      ctypes.byref(geom.c), arr, q_depth, _ptr(Q), Q_depth, _ptr(X),
+                                      pa[0] if pa else None))
+
+
+def zero_ghosts_spread(ctx: Context, markers: Markers, kernel: str, centering: str, geom: Geometry,
+                       q: Sequence[torch.Tensor], Q: torch.Tensor, X: torch.Tensor, q_depth: int = 1,
+                       Q_depth: Optional[int] = None, axis: int = 0):
+    """zero_ghosts(q) then spread, bit for bit, in one sweep on a 3-D column binning
+    (ibtk_le_zero_ghosts_spread): the owned ghost points start from 0."""
+    if Q_depth is None:
+        Q_depth = geom.ndim if centering in ("side", "edge") else q_depth
+    arr = _ptr_array(q, geom)
+    check(ctx.lib.ibtk_le_zero_ghosts_spread(ctx.h, markers.h, kernel_id(kernel), CENTERING[centering], axis,
+                                             ctypes.byref(geom.c), arr, q_depth, _ptr(Q), Q_depth, _ptr(X)))
+
+
 # USER_DEFINED kernel function (LEInteractor::s_kernel_fcn, LEInteractor.h:100-101):
 # a Python callable phi(r) -> float, called by the library on the host
 USER_KERNEL_FN = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.c_double)

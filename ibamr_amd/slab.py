@@ -185,19 +185,24 @@ class SlabExchange:
         if self.slab.P > 1 and self.ctx is not None:
             self.ctx.set_plane_window(0, self.slab.z0, self.slab.z1 - 1)
 
-    def halo_fill(self, work=None):
+    def halo_fill(self, work=None, local: bool = True):
         """Every ghost point := its periodic interior value (before interpolation).
 
         work: optional callable (the interpolation); it then runs in two halves,
         the sweep items that read only the rank's own planes while the z planes
-        are in flight, and the items next to the slab faces after they land."""
+        are in flight, and the items next to the slab faces after they land.
+        local=False: no local x/y (one rank: x/y/z) periodic fill -- the work reads
+        those ghosts at their periodic images itself (ibtk_le_fill_interp); only the z
+        planes from the neighbours are exchanged."""
         s = self.slab
         if s.P == 1:
-            self.local_fill([1, 1, 1])
+            if local:
+                self.local_fill([1, 1, 1])
             if work is not None:
                 work()
             return
-        self.local_fill([1, 1, 0])   # x/y ghosts of the interior planes
+        if local:
+            self.local_fill([1, 1, 0])   # x/y ghosts of the interior planes
         sends, recvs = [], []
         for c, a in enumerate(self.arrays):
             b = s.blocks(c)

@@ -285,6 +285,14 @@ int ibtk_le_level_fill_ghosts(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_g
  * (the RefineSchedule::fillData the caller runs before interp, LDataManager.cpp:750). */
 int ibtk_le_fill_periodic_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int centering,
                                  double* const* q_dev, int q_depth, const int* periodic);
+/* ibtk_le_fill_periodic_ghosts followed by ibtk_le_interp, with the same Q bit for bit,
+ * in one sweep for a 3-D column binning: the interp reads every ghost point of the
+ * ghost box at its periodic image in the periodic dims (the value the fill copies
+ * there) and writes no ghost value (q is not modified).  periodic NULL: every dim.
+ * Other binnings: the two calls. */
+int ibtk_le_fill_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                        const ibtk_le_patch_geom* geom, const double* const* q_dev, int q_depth, double* Q_dev,
+                        int Q_depth, const double* X_dev, const int* periodic);
 /* Spreading in ghost-region-sum mode: zero the ghost layers before spreading the
  * interior markers, then fold every ghost value back onto its periodic interior
  * image (dims folded slowest first, one source per destination per pass:
@@ -292,6 +300,14 @@ int ibtk_le_fill_periodic_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom
  * exchange along z. */
 int ibtk_le_zero_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int centering, double* const* q_dev,
                         int q_depth);
+/* ibtk_le_zero_ghosts followed by ibtk_le_spread, bit for bit, in one sweep for a 3-D
+ * column binning: the spread's items start their owned ghost points (outside the data
+ * box) from 0 instead of reading them, and items no marker reaches store the zeros
+ * (the ghost zeroing of LDataManager::spread, LDataManager.cpp:587-671, with no
+ * separate pass over the ghost layers).  Other binnings: the two calls. */
+int ibtk_le_zero_ghosts_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                               const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth,
+                               const double* Q_dev, int Q_depth, const double* X_dev);
 int ibtk_le_fold_periodic_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int centering,
                                  double* const* q_dev, int q_depth, const int* periodic);
 /* Physical-boundary ghost operators for side-centred data on one patch
