@@ -194,6 +194,7 @@ struct ibtk_le_markers_s {
     DevBuf rb_cin, rb_cout, rb_d, rb_dpre, rb_mstart, rb_ps2, rb_mbits, rb_wcnt, rb_wpre, rb_mlist, rb_scr, rb_big,
         rb_nbig;
     int rb_zeroed_nb = -1;                // rb_cin / rb_cout are zero for this many buckets
+    int items_sig[8] = {-1, 0, 0, 0, 0, 0, 0, 0};  // what the item table was built with (cuts, strip, target, heavy)
 };
 
 static int set_device(ibtk_le_ctx ctx) {
@@ -282,6 +283,7 @@ extern "C" int ibtk_le_ctx_tune(ibtk_le_ctx ctx, const char* key, int value) {
     else if (k == "heavy") t.heavy = value;
     else if (k == "strip") t.strip = value;
     else if (k == "xcd_block") t.xcd_block = value;
+    else if (k == "fdirect") t.fdirect = value;
     else return fail(IBTK_LE_ERR_ARG, "unknown tuning key %s", key);
     return IBTK_LE_OK;
 }
@@ -560,7 +562,7 @@ extern "C" int ibtk_le_markers_order(ibtk_le_markers m, const int** order_dev) {
 #ifndef IBTK_LE_SPLIT_TARGET
 #define IBTK_LE_SPLIT_TARGET 12288  // own markers per item above which it is cut (cfg4 items hold ~6.8K)
 #endif
-static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel) {
+static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const int* skip_if_zero = nullptr) {
     const int nj = m->npatch ? m->njobs : m->cg.ncol * m->nseg;
     const int target = ctx->tune.split_target > 0 ? ctx->tune.split_target : IBTK_LE_SPLIT_TARGET;
     Params p;
@@ -591,6 +593,7 @@ static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel) {
     p.njobs = nj;
     p.strip = ctx->tune.strip > 0 ? ctx->tune.strip : IBTK_LE_STRIP;
     p.plane_start = m->plane_start.as<int>();
+    p.items_skip = skip_if_zero;  // a re-binning where nothing moved: the table stands
     if (m->npatch) {
         p.pd = m->pd.as<PatchDesc>();
         p.npatch = m->npatch;
@@ -605,6 +608,10 @@ static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel) {
     int heavy = (int)std::min<long long>(std::max<long long>(4 * mean, 2048), INT_MAX / 2);
     if (ctx->tune.heavy > 0) heavy = ctx->tune.heavy;
     else if (ctx->tune.heavy < 0) heavy = INT_MAX / 2;  // off
+    // a re-binning may keep the table only if it would be built the same way
+    const int sig[8] = {p.ncut, p.cut[0], p.cut[1], p.cut[2], p.cut[3], p.strip, target, heavy};
+    if (std::memcmp(sig, m->items_sig, sizeof(sig)) != 0) p.items_skip = nullptr;
+    std::memcpy(m->items_sig, sig, sizeof(sig));
     HIP_TRY(launch_item_table(kernel, p, target, heavy, m->nsub.as<int>(), m->isub.as<int>(),
                               m->items.as<SweepItem>(), m->nitems.as<int>(), ctx->temp.p, ctx->temp.cap, ctx->stream));
     return IBTK_LE_OK;
@@ -741,15 +748,13 @@ extern "C" int ibtk_le_markers_rebin(ibtk_le_ctx ctx, ibtk_le_markers m, const d
     r.sorted_s = m->sorted_s.as<int>();
     r.sorted_X = m->sorted_X.as<double>();
     HIP_TRY(launch_rekey(m->kernel, p, r, s));
-    HIP_TRY(launch_rebin_delta(r, s));
-    if ((rc = scan_excl(ctx, r.d, r.dpre, nb + 2))) return rc;
-    if ((rc = scan_excl(ctx, r.cin, r.mstart, nb + 2))) return rc;
-    if ((rc = scan_excl(ctx, r.wcnt, r.wpre, nw + 1))) return rc;
+    if ((rc = scan_excl(ctx, r.wcnt, r.wpre, nw + 1))) return rc;  // wpre[nw]: the mover count
+    // everything below returns at once on the device when nothing moved
+    HIP_TRY(launch_rebin_copy(m->kernel, p, r, s));
     HIP_TRY(launch_rebin_starts(r, s));
     HIP_TRY(launch_rebin_movers(r, s));
-    HIP_TRY(launch_rebin_scatter(p, r, s));
-    std::swap(m->plane_start, m->rb_ps2);  // the new starts (equal to the old when nothing moved)
-    return build_items(ctx, m, m->kernel);
+    HIP_TRY(launch_rebin_scatter(p, r, s));  // ... and the new starts into plane_start
+    return build_items(ctx, m, m->kernel, r.wpre + nw);
 }
 
 static int markers_bin_impl(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_patch_geom* geom, int kernel,
@@ -1296,8 +1301,10 @@ static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cente
     p.ds = ds_dev;
     p.Q_depth = Q_depth;
     p.nsorted = m->n;
-    if (int rc = ctx->fbuf.ensure(sizeof(double) * (size_t)m->n * (size_t)std::min(nc, MAXC))) return rc;
-    p.sorted_F = ctx->fbuf.as<double>();
+    if (geom->ndim == 2 || !ctx->tune.fdirect) {  // fdirect: the 3-D sweeps read F through the sorted index
+        if (int rc = ctx->fbuf.ensure(sizeof(double) * (size_t)m->n * (size_t)std::min(nc, MAXC))) return rc;
+        p.sorted_F = ctx->fbuf.as<double>();
+    }
     if (geom->ndim == 2) {
         if (int rc = build_candidates(ctx, m, p)) return rc;
         p.cand_off = m->cand_off.as<int>();
@@ -1600,8 +1607,10 @@ static int level_spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int
     if (!Q_dev) return fail(IBTK_LE_ERR_ARG, "null Q");
     p.Qin = Q_dev;
     p.zero_first = zero_first ? 1 : 0;
-    if (int rc = ctx->fbuf.ensure(sizeof(double) * (size_t)m->n * (size_t)nc)) return rc;
-    p.sorted_F = ctx->fbuf.as<double>();
+    if (!ctx->tune.fdirect) {
+        if (int rc = ctx->fbuf.ensure(sizeof(double) * (size_t)m->n * (size_t)nc)) return rc;
+        p.sorted_F = ctx->fbuf.as<double>();
+    }
     const bool t = ctx->timing;
     ctx->ev_valid = false;
     const size_t nst = (size_t)m->item_bound * nc * 8;

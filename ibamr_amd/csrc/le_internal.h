@@ -109,6 +109,8 @@ struct SweepTune {
     int strip = 0;         // column rows per strip of the item order (0: default)
     int xcd_block = 0;     // light sweep items over the XCDs in blocks of this many table entries (1:
                            // round-robin; -1: one contiguous range per XCD; 0: the default, 8)
+    int fdirect = 0;       // 3-D spread: 1 = the candidates read F through the sorted marker index instead
+                           // of the gather pass k_gather_F_col (diagnostic: slower, profiles/r04c)
 };
 // One 3-D sweep item: a patch, a column and its owned planes [p0, p1) (relative
 // to the patch's cg.org[2]).
@@ -142,6 +144,8 @@ struct Params {
     int zmode, zlo, zhi;       // plane window (ibtk_le_ctx_set_plane_window): 0 every item, 1 the items
                                // whose planes lie in [zlo, zhi], 2 the others
     const SweepItem* items;    // 3-D sweep item table (k_item_write)
+    const int* items_skip;     // k_item_counts / k_item_write: nothing to do when *items_skip == 0 (a
+                               // re-binning that moved nothing leaves the bucket starts, so the table, as they were)
     const int* nitems;         // device: its length, then the count of heavy items heading it
     int item_bound;            // host: an upper bound of the length (the launch grid)
     SweepTune tune;
@@ -213,8 +217,8 @@ struct RebinBufs {
     int* wpre;             // its exclusive prefix (wpre[nw] = movers)
     int* cin;              // movers into bucket b (0 on entry; consumed back to 0)
     int* cout;             // movers out of bucket b (0 on entry; reset)
-    int* d;                // cin - cout, then
-    int* dpre;             // its exclusive prefix
+    int* d;                // scratch: per block of buckets, the sums of (cin - cout, cin) as int2
+    int* dpre;             // (unused)
     int* mstart;           // exclusive prefix of cin: bucket b's movers are mlist[mstart[b] .. mstart[b+1])
     int* mlist;            // the movers' l, per bucket sorted by l
     int* scratch;          // long lists' sort
@@ -228,8 +232,8 @@ struct RebinBufs {
     double* sorted_X;
 };
 hipError_t launch_rekey(int kernel, const Params& p, const RebinBufs& r, hipStream_t s);
-hipError_t launch_rebin_delta(const RebinBufs& r, hipStream_t s);
-hipError_t launch_rebin_starts(const RebinBufs& r, hipStream_t s);
+hipError_t launch_rebin_copy(int kernel, const Params& p, const RebinBufs& r, hipStream_t s);
+hipError_t launch_rebin_starts(const RebinBufs& r, hipStream_t s);  // uses r.d as the block sums (int2)
 hipError_t launch_rebin_movers(const RebinBufs& r, hipStream_t s);
 hipError_t launch_rebin_scatter(const Params& p, const RebinBufs& r, hipStream_t s);
 // z-slab migration classes (le_aux.hip)

@@ -177,12 +177,10 @@ __global__ __launch_bounds__(BLOCK) void k_bin_col(Params p, int n, unsigned* ke
 //
 // R1: new keys in the old order; the shifted positions stored at the old sorted
 // positions (final when nothing moved); per-bucket mover counts in/out; the mover
-// flags as a bit per entry with per-word counts; copies of the old l and the new
-// keys for the scatter (which overwrites the sorted arrays).
+// flags as a bit per entry with per-word counts.
 template <int K>
 __global__ __launch_bounds__(BLOCK) void k_rekey(Params p, int n, const unsigned* kold, const int* sl, double* sorted_X,
-                                                 unsigned* knew, int* lold, unsigned* mbits, int* wcnt, int* cin,
-                                                 int* cout) {
+                                                 unsigned* mbits, int* wcnt, int* cin, int* cout) {
     __shared__ double sx[3 * BLOCK];
     const int e0 = blockIdx.x * BLOCK;
     const int e = e0 + threadIdx.x;
@@ -196,8 +194,6 @@ __global__ __launch_bounds__(BLOCK) void k_rekey(Params p, int n, const unsigned
         for (int d = 0; d < 3; ++d) Xs[d] = x.v[d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
         const unsigned k = entry_key<K>(p, l, Xs);
         const unsigned ko = kold[e];
-        knew[e] = k;
-        lold[e] = l;
         mv = k != ko;
         if (mv) {
             atomicAdd(cin + k, 1);
@@ -229,6 +225,30 @@ __global__ __launch_bounds__(BLOCK) void k_rekey(Params p, int n, const unsigned
     }
 }
 
+// R1b (something moved): copies of the old l and the new keys for the scatter,
+// which overwrites the sorted arrays (a stayer's new key is its old one; a mover's
+// is computed again)
+constexpr int RB_GRID = 4096;  // grid-stride kernels of the re-binning's tail
+template <int K>
+__global__ __launch_bounds__(BLOCK) void k_rebin_copy(Params p, int n, const int* T, const unsigned* mbits,
+                                                      const unsigned* kold, const int* sl, unsigned* knew, int* lold) {
+    if (*T == 0) return;
+    for (int e = blockIdx.x * BLOCK + threadIdx.x; e < n; e += gridDim.x * BLOCK) {
+        const int l = sl[e];
+        lold[e] = l;
+        unsigned k = kold[e];
+        if ((mbits[e >> 5] >> (e & 31)) & 1u) {
+            const int s = p.indices ? p.indices[l] : l;
+            const D3 x = ld3(p.X + (int64_t)3 * s);
+            double Xs[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) Xs[d] = x.v[d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
+            k = entry_key<K>(p, l, Xs);
+        }
+        knew[e] = k;
+    }
+}
+
 // movers before entry x (0 <= x <= n): word prefix + the word's lower bits
 __device__ __forceinline__ int movers_before(const unsigned* mbits, const int* wpre, int x) {
     const int w = x >> 5, b = x & 31;
@@ -244,53 +264,152 @@ __device__ __forceinline__ int lower_bound_l(const int* v, int lo, int hi, int l
     return lo;
 }
 
-// R2: d[b] = movers in - movers out (b <= nb), d[nb + 1] = 0
-__global__ __launch_bounds__(BLOCK) void k_rebin_delta(int nb, const int* cin, const int* cout, int* d) {
-    const int b = blockIdx.x * BLOCK + threadIdx.x;
-    if (b <= nb) d[b] = cin[b] - cout[b];
-    else if (b == nb + 1) d[b] = 0;
+// Every kernel after k_rekey returns at once when nothing moved (the mover count,
+// wpre[nw], is read on the device): a stationary list costs k_rekey and a scan of
+// the per-word counts.
+//
+// R2: per bucket b (0 .. nb + 1; cin / cout[nb + 1] stay 0), the exclusive prefixes of
+// d = cin - cout (the shift of b's start) and of cin (b's offset in the movers' list),
+// in three phases over blocks of RB_BLK buckets: block sums, a scan of the block sums
+// by one workgroup, the blocks' own scans.  ns[b] = os[b] + prefix(d)[b].
+constexpr int RB_IPT = 8, RB_BLK = BLOCK * RB_IPT;
+__global__ __launch_bounds__(BLOCK) void k_rebin_bsum(int nb, const int* cin, const int* cout, const int* T,
+                                                      int2* bsum) {
+    if (*T == 0) return;
+    __shared__ int sd[BLOCK], sc[BLOCK];
+    const long b0 = (long)blockIdx.x * RB_BLK + (long)threadIdx.x * RB_IPT;
+    int d = 0, c = 0;
+#pragma unroll
+    for (int i = 0; i < RB_IPT; ++i)
+        if (b0 + i <= nb + 1) {
+            d += cin[b0 + i] - cout[b0 + i];
+            c += cin[b0 + i];
+        }
+    sd[threadIdx.x] = d;
+    sc[threadIdx.x] = c;
+    __syncthreads();
+    for (int w = BLOCK / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            sd[threadIdx.x] += sd[threadIdx.x + w];
+            sc[threadIdx.x] += sc[threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) bsum[blockIdx.x] = make_int2(sd[0], sc[0]);
 }
-// new bucket starts: ns[b] = os[b] + (exclusive prefix of d)[b], b <= nb
-__global__ __launch_bounds__(BLOCK) void k_rebin_starts(int nb, const int* os, const int* dpre, int* ns) {
-    const int b = blockIdx.x * BLOCK + threadIdx.x;
-    if (b <= nb) ns[b] = os[b] + dpre[b];
+// one workgroup: bsum[i] := exclusive prefix over the blocks
+__global__ __launch_bounds__(BLOCK) void k_rebin_btop(int nblk, const int* T, int2* bsum) {
+    if (*T == 0) return;
+    __shared__ int sd[BLOCK], sc[BLOCK];
+    const int per = (nblk + BLOCK - 1) / BLOCK, i0 = (int)threadIdx.x * per;
+    int d = 0, c = 0;
+    for (int i = i0; i < min(i0 + per, nblk); ++i) {
+        d += bsum[i].x;
+        c += bsum[i].y;
+    }
+    sd[threadIdx.x] = d;
+    sc[threadIdx.x] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {  // exclusive prefix of the BLOCK thread sums
+        int ad = 0, ac = 0;
+        for (int t = 0; t < BLOCK; ++t) {
+            const int vd = sd[t], vc = sc[t];
+            sd[t] = ad;
+            sc[t] = ac;
+            ad += vd;
+            ac += vc;
+        }
+    }
+    __syncthreads();
+    d = sd[threadIdx.x];
+    c = sc[threadIdx.x];
+    for (int i = i0; i < min(i0 + per, nblk); ++i) {
+        const int2 v = bsum[i];
+        bsum[i] = make_int2(d, c);
+        d += v.x;
+        c += v.y;
+    }
+}
+__global__ __launch_bounds__(BLOCK) void k_rebin_bapply(int nb, const int* cin, const int* cout, const int* os,
+                                                        const int* T, const int2* bsum, int* ns, int* mstart) {
+    if (*T == 0) return;
+    __shared__ int sd[BLOCK], sc[BLOCK];
+    const long b0 = (long)blockIdx.x * RB_BLK + (long)threadIdx.x * RB_IPT;
+    int vd[RB_IPT], vc[RB_IPT], d = 0, c = 0;
+#pragma unroll
+    for (int i = 0; i < RB_IPT; ++i) {
+        const bool in = b0 + i <= nb + 1;
+        vd[i] = in ? cin[b0 + i] - cout[b0 + i] : 0;
+        vc[i] = in ? cin[b0 + i] : 0;
+        d += vd[i];
+        c += vc[i];
+    }
+    sd[threadIdx.x] = d;
+    sc[threadIdx.x] = c;
+    __syncthreads();
+    for (int w = 1; w < BLOCK; w <<= 1) {  // inclusive scan of the thread sums
+        const int ad = (int)threadIdx.x >= w ? sd[threadIdx.x - w] : 0;
+        const int ac = (int)threadIdx.x >= w ? sc[threadIdx.x - w] : 0;
+        __syncthreads();
+        sd[threadIdx.x] += ad;
+        sc[threadIdx.x] += ac;
+        __syncthreads();
+    }
+    d = bsum[blockIdx.x].x + sd[threadIdx.x] - d;  // exclusive: the block's and this thread's offsets
+    c = bsum[blockIdx.x].y + sc[threadIdx.x] - c;
+#pragma unroll
+    for (int i = 0; i < RB_IPT; ++i) {
+        const long b = b0 + i;
+        if (b <= nb + 1) {
+            if (b <= nb) ns[b] = os[b] + d;
+            mstart[b] = c;
+        }
+        d += vd[i];
+        c += vc[i];
+    }
 }
 
 // R3: every mover appends its l to its new bucket's list (mstart: exclusive prefix
 // of the in-counts); the counts are consumed (cin back to 0, cout reset), so the
-// next re-binning starts from zeros without a memset
-__global__ __launch_bounds__(BLOCK) void k_rebin_append(int n, const unsigned* mbits, const unsigned* knew,
+// next re-binning starts from zeros without a memset.  One thread per word of flags.
+__global__ __launch_bounds__(BLOCK) void k_rebin_append(int n, int nw, const unsigned* mbits, const unsigned* knew,
                                                         const unsigned* kold, const int* lold, const int* mstart,
                                                         int* cin, int* cout, int* mlist) {
-    const int e = blockIdx.x * BLOCK + threadIdx.x;
-    if (e >= n || !((mbits[e >> 5] >> (e & 31)) & 1u)) return;
-    const unsigned b = knew[e];
-    const int j = atomicSub(cin + b, 1) - 1;
-    mlist[mstart[b] + j] = lold[e];
-    cout[kold[e]] = 0;
+    const int w = blockIdx.x * BLOCK + threadIdx.x;
+    if (w >= nw) return;
+    unsigned bits = mbits[w];
+    while (bits) {
+        const int e = 32 * w + __ffs(bits) - 1;
+        bits &= bits - 1;
+        const unsigned b = knew[e];
+        const int j = atomicSub(cin + b, 1) - 1;
+        mlist[mstart[b] + j] = lold[e];
+        cout[kold[e]] = 0;
+    }
 }
 // Each bucket's mover list sorted by l: lists of up to 32 by one thread (insertion
 // sort); longer ones are queued for k_rebin_sort_big
 constexpr int REBIN_SMALL = 32;
-__global__ __launch_bounds__(BLOCK) void k_rebin_sort_small(int nb, const int* mstart, int* mlist, int* nbig,
-                                                            int* big) {
-    const int b = blockIdx.x * BLOCK + threadIdx.x;
-    if (b > nb) return;
-    const int lo = mstart[b], k = mstart[b + 1] - lo;
-    if (k < 2) return;
-    if (k > REBIN_SMALL) {
-        big[atomicAdd(nbig, 1)] = b;
-        return;
-    }
-    int* v = mlist + lo;
-    for (int i = 1; i < k; ++i) {
-        const int x = v[i];
-        int j = i - 1;
-        while (j >= 0 && v[j] > x) {
-            v[j + 1] = v[j];
-            --j;
+__global__ __launch_bounds__(BLOCK) void k_rebin_sort_small(int nb, const int* T, const int* mstart, int* mlist,
+                                                            int* nbig, int* big) {
+    if (*T == 0) return;
+    for (int b = blockIdx.x * BLOCK + threadIdx.x; b <= nb; b += gridDim.x * BLOCK) {
+        const int lo = mstart[b], k = mstart[b + 1] - lo;
+        if (k < 2) continue;
+        if (k > REBIN_SMALL) {
+            big[atomicAdd(nbig, 1)] = b;
+            continue;
         }
-        v[j + 1] = x;
+        int* v = mlist + lo;
+        for (int i = 1; i < k; ++i) {
+            const int x = v[i];
+            int j = i - 1;
+            while (j >= 0 && v[j] > x) {
+                v[j + 1] = v[j];
+                --j;
+            }
+            v[j + 1] = x;
+        }
     }
 }
 // Long lists (clustered markers crossing a plane together): the rank of every
@@ -329,16 +448,10 @@ __global__ __launch_bounds__(BLOCK) void k_rebin_copy_big(const int* nbig, const
     }
 }
 
-// R4 (only when something moved: wpre[nw] is the mover count): every entry to its
-// new sorted position; the sorted arrays rewritten there
-__global__ __launch_bounds__(BLOCK) void k_rebin_scatter(Params p, int n, int nb, const unsigned* mbits, const int* wpre,
-                                                         int nw, const unsigned* knew, const int* lold, const int* os,
-                                                         const int* ns, const int* mstart, const int* mlist,
-                                                         int* sorted_l, unsigned* sorted_key, int* sorted_s,
-                                                         double* sorted_X) {
-    if (wpre[nw] == 0) return;
-    const int e = blockIdx.x * BLOCK + threadIdx.x;
-    if (e >= n) return;
+__device__ __forceinline__ void rebin_place(const Params& p, int e, int n, int nb, const unsigned* mbits,
+                                            const int* wpre, const unsigned* knew, const int* lold, const int* os,
+                                            const int* ns, const int* mstart, const int* mlist, int* sorted_l,
+                                            unsigned* sorted_key, int* sorted_s, double* sorted_X) {
     const int l = lold[e];
     const int b = (int)knew[e];
     const int ob = os[b], oe = b < nb ? os[b + 1] : n;
@@ -358,6 +471,23 @@ __global__ __launch_bounds__(BLOCK) void k_rebin_scatter(Params p, int n, int nb
     sorted_s[pos] = s;
 #pragma unroll
     for (int d = 0; d < 3; ++d) sorted_X[(int64_t)3 * pos + d] = x.v[d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
+}
+// R4 (only when something moved: wpre[nw] is the mover count): every entry to its
+// new sorted position; the sorted arrays rewritten there
+__global__ __launch_bounds__(BLOCK) void k_rebin_scatter(Params p, int n, int nb, const unsigned* mbits, const int* wpre,
+                                                         int nw, const unsigned* knew, const int* lold, const int* os,
+                                                         const int* ns, const int* mstart, const int* mlist,
+                                                         int* sorted_l, unsigned* sorted_key, int* sorted_s,
+                                                         double* sorted_X) {
+    if (wpre[nw] == 0) return;
+    for (int e = blockIdx.x * BLOCK + threadIdx.x; e < n; e += gridDim.x * BLOCK)
+        rebin_place(p, e, n, nb, mbits, wpre, knew, lold, os, ns, mstart, mlist, sorted_l, sorted_key, sorted_s,
+                    sorted_X);
+}
+// the new bucket starts in place (when something moved)
+__global__ __launch_bounds__(BLOCK) void k_rebin_commit(int nb, const int* T, const int* ns, int* plane_start) {
+    if (*T == 0) return;
+    for (int b = blockIdx.x * BLOCK + threadIdx.x; b <= nb; b += gridDim.x * BLOCK) plane_start[b] = ns[b];
 }
 
 // Per sorted entry e: the marker index and the shifted position (coalesced for
@@ -1155,8 +1285,18 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         d.X[0] = xs.v[0];
         d.X[1] = xs.v[1];
         d.X[2] = xs.v[2];
-        d.V = p.sorted_F[(int64_t)c * p.nsorted + e];
-        d.s = FAM == 2 ? p.sorted_s[e] : 0;
+        if (p.tune.fdirect) {
+            // F through the sorted marker index, no gather pass: measured slower again in
+            // round 4 (cfg4: spread sweep +2.2 ms against k_gather_F_col's 1.13 ms; cfg5 +1.0
+            // ms, profiles/r04c), a diagnostic only
+            const int s = p.sorted_s[e];
+            const double v = p.Qin[(int64_t)p.Q_depth * s + cd.qcomp];
+            d.V = p.ds ? v * p.ds[s] : v;  // F ds rounded once, as LDataManager.cpp:446-451 forms it
+            d.s = s;
+        } else {
+            d.V = p.sorted_F[(int64_t)c * p.nsorted + e];
+            d.s = FAM == 2 ? p.sorted_s[e] : 0;
+        }
     };
     Clk clk;
     unsigned long long cnt[2] = {0ull, 0ull};  // CNT: wave-uniform totals of the item
@@ -1430,6 +1570,7 @@ __device__ __forceinline__ int cuts_inside(const Params& p, int b0, int b1) {
 // markers per piece above `heavy`; they head the item table, see sweep_item)
 template <int K>
 __global__ __launch_bounds__(BLOCK) void k_item_counts(Params p, int target, int heavy, int* nsub) {
+    if (p.items_skip && *p.items_skip == 0) return;  // nsub stands
     const int j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= p.njobs) return;
     int q, S, nseg, j0;
@@ -1451,6 +1592,7 @@ __global__ __launch_bounds__(BLOCK) void k_item_counts(Params p, int target, int
 template <int K>
 __global__ __launch_bounds__(BLOCK) void k_item_write(Params p, int target, int heavy, const int* nsub,
                                                       const int* start, SweepItem* tab, int* ntot) {
+    if (p.items_skip && *p.items_skip == 0) return;  // the table stands
     const int j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= p.njobs) return;
     int q, S, nseg, j0;
@@ -1563,7 +1705,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather_F_col(Params p, int n, double*
 }
 
 template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-    if (p.nsorted > 0) {
+    if (p.nsorted > 0 && !p.tune.fdirect) {
         const bool rec3 = p.ncomp == 3 && p.Q_depth == 3 && p.comp[0].qcomp == 0 && p.comp[1].qcomp == 1 &&
                           p.comp[2].qcomp == 2;
         const dim3 g((p.nsorted + BLOCK - 1) / BLOCK), b(BLOCK);
@@ -1654,29 +1796,46 @@ template <int K>
 hipError_t launch_rekey_t(const Params& p, const RebinBufs& r, hipStream_t s) {
     if (r.n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_rekey<K>, dim3((r.n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, r.n, r.kold, r.lsorted,
-                       r.sorted_X, r.knew, r.lold, r.mbits, r.wcnt, r.cin, r.cout);
+                       r.sorted_X, r.mbits, r.wcnt, r.cin, r.cout);
+    return hipGetLastError();
+}
+template <int K>
+hipError_t launch_rebin_copy_t(const Params& p, const RebinBufs& r, hipStream_t s) {
+    if (r.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rebin_copy<K>, dim3(RB_GRID), dim3(BLOCK), 0, s, p, r.n, r.wpre + r.nw, r.mbits, r.kold,
+                       r.lsorted, r.knew, r.lold);
     return hipGetLastError();
 }
 using RekeyFn = hipError_t (*)(const Params&, const RebinBufs&, hipStream_t);
 static RekeyFn pick_rekey(int k) { IBTK_LE_DISPATCH_K(k, launch_rekey_t) }
+static RekeyFn pick_rebin_copy(int k) { IBTK_LE_DISPATCH_K(k, launch_rebin_copy_t) }
 hipError_t launch_rekey(int kernel, const Params& p, const RebinBufs& r, hipStream_t s) {
     RekeyFn f = pick_rekey(kernel);
     return f ? f(p, r, s) : hipErrorInvalidValue;
 }
-static dim3 grid_of(long n) { return dim3((unsigned)((n + BLOCK - 1) / BLOCK)); }
-hipError_t launch_rebin_delta(const RebinBufs& r, hipStream_t s) {
-    hipLaunchKernelGGL(k_rebin_delta, grid_of(r.nb + 2), dim3(BLOCK), 0, s, r.nb, r.cin, r.cout, r.d);
-    return hipGetLastError();
+hipError_t launch_rebin_copy(int kernel, const Params& p, const RebinBufs& r, hipStream_t s) {
+    RekeyFn f = pick_rebin_copy(kernel);
+    return f ? f(p, r, s) : hipErrorInvalidValue;
 }
+static dim3 grid_of(long n) { return dim3((unsigned)((n + BLOCK - 1) / BLOCK)); }
+int rebin_blocks(int nb) { return (int)(((long)nb + 2 + RB_BLK - 1) / RB_BLK); }
 hipError_t launch_rebin_starts(const RebinBufs& r, hipStream_t s) {
-    hipLaunchKernelGGL(k_rebin_starts, grid_of(r.nb + 1), dim3(BLOCK), 0, s, r.nb, r.os, r.dpre, r.ns);
+    const int T_off = r.nw;
+    const int* T = r.wpre + T_off;
+    const int nblk = rebin_blocks(r.nb);
+    int2* bsum = reinterpret_cast<int2*>(r.d);
+    hipLaunchKernelGGL(k_rebin_bsum, dim3(nblk), dim3(BLOCK), 0, s, r.nb, r.cin, r.cout, T, bsum);
+    hipLaunchKernelGGL(k_rebin_btop, dim3(1), dim3(BLOCK), 0, s, nblk, T, bsum);
+    hipLaunchKernelGGL(k_rebin_bapply, dim3(nblk), dim3(BLOCK), 0, s, r.nb, r.cin, r.cout, r.os, T, bsum, r.ns,
+                       r.mstart);
     return hipGetLastError();
 }
 hipError_t launch_rebin_movers(const RebinBufs& r, hipStream_t s) {
+    const int* T = r.wpre + r.nw;
     if (r.n > 0)
-        hipLaunchKernelGGL(k_rebin_append, grid_of(r.n), dim3(BLOCK), 0, s, r.n, r.mbits, r.knew, r.kold, r.lold,
-                           r.mstart, r.cin, r.cout, r.mlist);
-    hipLaunchKernelGGL(k_rebin_sort_small, grid_of(r.nb + 1), dim3(BLOCK), 0, s, r.nb, r.mstart, r.mlist, r.nbig,
+        hipLaunchKernelGGL(k_rebin_append, grid_of(r.nw), dim3(BLOCK), 0, s, r.n, r.nw, r.mbits, r.knew, r.kold,
+                           r.lold, r.mstart, r.cin, r.cout, r.mlist);
+    hipLaunchKernelGGL(k_rebin_sort_small, dim3(RB_GRID), dim3(BLOCK), 0, s, r.nb, T, r.mstart, r.mlist, r.nbig,
                        r.big);
     hipLaunchKernelGGL(k_rebin_sort_big, dim3(1024), dim3(BLOCK), 0, s, r.nbig, r.big, r.mstart, r.mlist, r.scratch);
     hipLaunchKernelGGL(k_rebin_copy_big, dim3(1024), dim3(BLOCK), 0, s, r.nbig, r.big, r.mstart, r.scratch, r.mlist);
@@ -1684,8 +1843,10 @@ hipError_t launch_rebin_movers(const RebinBufs& r, hipStream_t s) {
 }
 hipError_t launch_rebin_scatter(const Params& p, const RebinBufs& r, hipStream_t s) {
     if (r.n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_rebin_scatter, grid_of(r.n), dim3(BLOCK), 0, s, p, r.n, r.nb, r.mbits, r.wpre, r.nw, r.knew,
+    hipLaunchKernelGGL(k_rebin_scatter, dim3(RB_GRID), dim3(BLOCK), 0, s, p, r.n, r.nb, r.mbits, r.wpre, r.nw, r.knew,
                        r.lold, r.os, r.ns, r.mstart, r.mlist, r.sorted_l, r.sorted_key, r.sorted_s, r.sorted_X);
+    hipLaunchKernelGGL(k_rebin_commit, dim3(RB_GRID), dim3(BLOCK), 0, s, r.nb, r.wpre + r.nw, r.ns,
+                       const_cast<int*>(r.os));
     return hipGetLastError();
 }
 hipError_t launch_gather_col(int kernel, const Params& p, int n, int* sorted_s, double* sorted_X,

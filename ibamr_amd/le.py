@@ -476,7 +476,8 @@ class Level:
     def rebin(self, X: torch.Tensor):
         """Re-bin the same lists at new positions X (ibtk_le_markers_rebin): the result
         of bin(X), computed from the previous order."""
-        self.markers.rebin(X)
+        assert X.dtype == torch.float64
+        check(self.ctx.lib.ibtk_le_markers_rebin(self.ctx.h, self.markers.h, _ptr(X)))
         return self
 
     def select_interior(self, n_markers: int, indices: torch.Tensor, offsets: Sequence[int]):
