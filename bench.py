@@ -5,7 +5,9 @@ One step = one IB coupling pass over the resident markers of every rank:
   bin      re-bin the markers by stencil anchor (device radix sort)
   fill     ghost fill of u (x/y periodic locally, z from the slab neighbours)
   interp   U = J u   (LEInteractor::interpolate, side-centred, all 3 components)
-  spread   f += S F  (LEInteractor::spread into the ghosted slab, ghosts zeroed first)
+  spread   f = S F   (LDataManager::spread: f zeroed, ghosts included, then
+           LEInteractor::spread into the ghosted slab -- one sweep that writes f and
+           never reads it; --spread-into existing: f += S F with only the ghosts zeroed)
   sum      ghost-region sum of f (z over RCCL, x/y periodic locally)
 Marker-ops per step = 2 x markers (one interpolate and one spread per marker).
 
@@ -452,6 +454,10 @@ def main():
     ap.add_argument("--unfused-fill", action="store_true",
                     help="fill u's periodic ghosts with their own passes, then interp (instead of "
                          "ibtk_le_fill_interp reading the ghost points at their periodic images; A/B)")
+    ap.add_argument("--spread-into", default="zero", choices=["zero", "existing"],
+                    help="zero: f set to 0 (ghosts included) and spread into, as LDataManager::spread hands "
+                         "f to LEInteractor::spread (LDataManager.cpp:596; ibtk_le_zero_spread, one sweep); "
+                         "existing: f += S F into the current values, ghosts zeroed (ibtk_le_zero_ghosts_spread)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-rebin", action="store_true", help="bin once outside the timed loop")
     ap.add_argument("--full-bin", action="store_true",
@@ -668,16 +674,23 @@ def main():
         if Ub is not U:
             U.copy_(Ub[:U.shape[0]])  # the own markers' velocities (ghost markers' discarded)
 
+    # f's zeroing fused into the spread's sweep: --spread-into zero (default), the whole
+    # of f (ibtk_le_zero_spread: items start every owned point from 0 and read nothing);
+    # existing, the ghosts (ibtk_le_zero_ghosts_spread).  --unfused-zero: the zeroing
+    # (zero_step) and the spread as separate launches
+    def spread_call(Fb, Xb):
+        if args.unfused_zero:
+            le.spread(ctx, bins, kernel, "side", geom, f, Fb, Xb)
+        elif args.spread_into == "zero":
+            le.zero_spread(ctx, bins, kernel, "side", geom, f, Fb, Xb)
+        else:
+            le.zero_ghosts_spread(ctx, bins, kernel, "side", geom, f, Fb, Xb)
+
     def spread_with_sum():
-        # the ghosts of f start from 0: ibtk_le_zero_ghosts fused into the spread's sweep
-        # (its items start their owned ghost points from 0; --unfused-zero: two calls)
         Xb, Fb = cur["X"], cur["F"]
 
         def spread():
-            if args.unfused_zero:
-                le.spread(ctx, bins, kernel, "side", geom, f, Fb, Xb)
-            else:
-                le.zero_ghosts_spread(ctx, bins, kernel, "side", geom, f, Fb, Xb)
+            spread_call(Fb, Xb)
         if gm is not None:
             # ghost markers: every rank spreads what reaches its own planes, no z
             # exchange of the grid; x/y periodic ghosts fold locally
@@ -694,7 +707,11 @@ def main():
 
     def zero_step():
         if args.unfused_zero:
-            le.zero_ghosts(ctx, geom, "side", f)
+            if args.spread_into == "zero":
+                for a in f:
+                    a.zero_()
+            else:
+                le.zero_ghosts(ctx, geom, "side", f)
 
     nstep = {"k": 0}
 
@@ -794,11 +811,10 @@ def main():
         for overlapped in (True, False):
             for a in f:
                 a.zero_()
-            sp = le.spread if args.unfused_zero else le.zero_ghosts_spread  # the timed steps' form
-            if overlapped:
-                ex_f.ghost_sum(lambda: sp(ctx, bins, kernel, "side", geom, f, cur["F"], Xb))
+            if overlapped:  # the timed steps' form
+                ex_f.ghost_sum(lambda: spread_call(cur["F"], Xb))
             else:
-                sp(ctx, bins, kernel, "side", geom, f, cur["F"], Xb)
+                spread_call(cur["F"], Xb)
                 ex_f.ghost_sum()
             fo.append([a.clone() for a in f])
         same = torch.equal(Uo, Us) and all(torch.equal(a, b) for a, b in zip(*fo))
@@ -847,11 +863,8 @@ def main():
         interp_call(cur["U"], cur["X"])
         ctx.synchronize()
         kt["interp"].append(ctx.last_kernel_ms())
-        if args.unfused_zero:
-            le.zero_ghosts(ctx, geom, "side", f)
-            le.spread(ctx, bins, kernel, "side", geom, f, cur["F"], cur["X"])
-        else:
-            le.zero_ghosts_spread(ctx, bins, kernel, "side", geom, f, cur["F"], cur["X"])
+        zero_step()
+        spread_call(cur["F"], cur["X"])
         ctx.synchronize()
         kt["spread"].append(ctx.last_kernel_ms())
     ctx.enable_timing(False)
@@ -867,7 +880,9 @@ def main():
     t_i, t_s = mean(acc["interp"]), mean(acc["spread"])
     k_i, k_s = mean(kt["interp"]), mean(kt["spread"])
     B_i = M_local * 48 + 8 * sum(S_touched)
-    B_s = M_local * 48 + 16 * sum(S_touched)
+    # the spread reads and writes the touched points; into a zeroed f (the default) it
+    # writes every point of f once and reads none
+    B_s = M_local * 48 + (8 * sum(a.numel() for a in f) if args.spread_into == "zero" else 16 * sum(S_touched))
     dominant = "spread" if k_s >= k_i else "interp"
     achieved = (B_s / (k_s * 1e-3) if dominant == "spread" else B_i / (k_i * 1e-3)) / 1e9
     pair = (B_i + B_s) / ((t_i + t_s) * 1e-3) / 1e9
@@ -897,6 +912,7 @@ def main():
         except Exception as e:  # the baseline must never hide the GPU result
             cpu = {"value": None, "error": repr(e)}
 
+    zname = "zero f" if args.spread_into == "zero" else "zero ghosts"
     out = {
         "metric": METRIC,
         "value": value,
@@ -919,6 +935,8 @@ def main():
                            "recomputed from the current positions, the entries whose bucket changed inserted; "
                            "equal to a full binning)"),
                    "move": args.move, "renumber": args.renumber,
+                   "spread_into": ("zeroed f (LDataManager::spread, LDataManager.cpp:596)" if args.spread_into == "zero"
+                                   else "f += S F, ghosts zeroed"),
                    "regrid_every": args.regrid_every if args.move else None,
                    "exchange_width": slab.width if world > 1 else None,
                    "drift_within_slack": (not bool(drift_flag.item())) if args.move and args.regrid_every > 1 else None,
@@ -929,11 +947,13 @@ def main():
                             (f"at every {args.regrid_every}-th step (regrid) " if args.regrid_every > 1 else "") +
                             "migrate + " +
                             ("redistribute (numbering + nonlocal nodes + reorder) + " if args.renumber else "") +
-                            "bin + zero ghosts + "
+                            "bin + " + zname + " + "
                             "spread(3 comps) + ghost sum" if args.move else
-                            "bin + ghost fill + interp(3 comps) + zero ghosts + spread(3 comps) + ghost sum") +
+                            "bin + ghost fill + interp(3 comps) + " + zname + " + spread(3 comps) + ghost sum") +
                            ("" if args.unfused_zero else
-                            "; the ghost zeroing fused into the spread sweep (ibtk_le_zero_ghosts_spread)") +
+                            ("; f's zeroing fused into the spread sweep (ibtk_le_zero_spread: f written once, not read)"
+                             if args.spread_into == "zero" else
+                             "; the ghost zeroing fused into the spread sweep (ibtk_le_zero_ghosts_spread)")) +
                            ("" if args.unfused_fill else
                             "; the periodic ghost fill fused into the interp sweep (ibtk_le_fill_interp)")},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

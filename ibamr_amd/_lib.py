@@ -139,6 +139,9 @@ _SIGS = [
     ("ibtk_le_zero_ghosts_spread", c_int,
      [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_int, c_void_p,
       c_int, c_void_p]),
+    ("ibtk_le_zero_spread", c_int,
+     [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_int, c_void_p,
+      c_int, c_void_p]),
     ("ibtk_le_mark_stencils", c_int,
      [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(PatchGeom), ctypes.POINTER(c_void_p), c_int,
       c_void_p]),

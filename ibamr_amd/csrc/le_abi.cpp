@@ -1102,7 +1102,8 @@ static int build_candidates(ibtk_le_ctx ctx, ibtk_le_markers m, const Params& p)
 
 static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                        const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
-                       int Q_depth, const double* ds_dev, const double* X_dev, bool zero_ghosts = false);
+                       int Q_depth, const double* ds_dev, const double* X_dev, bool zero_ghosts = false,
+                       bool zero_first = false);
 
 extern "C" int ibtk_le_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                               const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
@@ -1120,6 +1121,46 @@ extern "C" int ibtk_le_zero_ghosts_spread(ibtk_le_ctx ctx, ibtk_le_markers m, in
         return spread_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, nullptr, X_dev);
     }
     return spread_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, nullptr, X_dev, true);
+}
+
+// Every point of the component arrays to 0 (a pitched layout: the whole span, row
+// padding included), on the context stream
+static int zero_comps(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int centering, int axis, double* const* q_dev,
+                      int q_depth, int Q_depth) {
+    if (int rc = check_geom(geom)) return rc;
+    if (!q_dev) return fail(IBTK_LE_ERR_ARG, "null q");
+    const int nc = ncomponents(geom, centering, q_depth, Q_depth);
+    if (nc < 0) return -nc;
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    Params p;
+    for (int first = 0; first < nc; first += MAXC) {
+        const int cnt = std::min(MAXC, nc - first);
+        if (int rc = make_comps(geom, centering, axis, q_dev, q_depth, Q_depth, first, cnt, p)) return rc;
+        for (int c = 0; c < cnt; ++c) {
+            const CompDesc& cd = p.comp[c];
+            const size_t pts = (size_t)cd.s2 * (size_t)(cd.hi[2] - cd.lo[2] + 1);
+            HIP_TRY(hipMemsetAsync(cd.u, 0, sizeof(double) * pts, ctx->stream));
+        }
+    }
+    return IBTK_LE_OK;
+}
+
+// LDataManager::spread's target: the whole of f set to 0, ghosts included
+// (LDataManager.cpp:596, setToScalar(f, 0, interior_only = false)), then
+// LEInteractor::spread into it (:625-660).  A 3-D column binning does both in the
+// spread's sweep: its items start every owned point from 0 instead of reading it and
+// items no marker reaches store the zeros, so f is written once and never read.
+// Other binnings: the zeroing, then ibtk_le_spread.
+extern "C" int ibtk_le_zero_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                                   const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth,
+                                   const double* Q_dev, int Q_depth, const double* X_dev) {
+    if (!ctx || !m) return fail(IBTK_LE_ERR_ARG, "zero_spread: null ctx/markers");
+    if (!geom || geom->ndim != 3 || !m || m->n == 0 || !m->binned3) {
+        if (int rc = zero_comps(ctx, geom, centering, axis, q_dev, q_depth, Q_depth)) return rc;
+        return spread_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, nullptr, X_dev);
+    }
+    return spread_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, nullptr, X_dev, false,
+                       true);
 }
 
 extern "C" int ibtk_le_spread_ds(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
@@ -1288,10 +1329,11 @@ extern "C" int ibtk_le_user_spread(ibtk_le_ctx ctx, int centering, int axis, con
 
 static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                        const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
-                       int Q_depth, const double* ds_dev, const double* X_dev, bool zero_ghosts) {
+                       int Q_depth, const double* ds_dev, const double* X_dev, bool zero_ghosts, bool zero_first) {
     Params p;
     if (int rc = prepare(ctx, m, kernel, geom, X_dev, p)) return rc;
     p.zero_ghosts = zero_ghosts ? 1 : 0;
+    p.zero_first = zero_first ? 1 : 0;
     const int nc = ncomponents(geom, centering, q_depth, Q_depth);
     if (nc < 0) return -nc;
     if (m->n == 0) return IBTK_LE_OK;  // LEInteractor.cpp:2747

@@ -448,10 +448,12 @@ __global__ __launch_bounds__(BLOCK) void k_rebin_copy_big(const int* nbig, const
     }
 }
 
-__device__ __forceinline__ void rebin_place(const Params& p, int e, int n, int nb, const unsigned* mbits,
-                                            const int* wpre, const unsigned* knew, const int* lold, const int* os,
-                                            const int* ns, const int* mstart, const int* mlist, int* sorted_l,
-                                            unsigned* sorted_key, int* sorted_s, double* sorted_X) {
+// old entry e's new sorted position, returned; l, key and marker index written
+// there, the shifted position into x
+__device__ __forceinline__ int rebin_place(const Params& p, int e, int n, int nb, const unsigned* mbits,
+                                           const int* wpre, const unsigned* knew, const int* lold, const int* os,
+                                           const int* ns, const int* mstart, const int* mlist, int* sorted_l,
+                                           unsigned* sorted_key, int* sorted_s, double* x) {
     const int l = lold[e];
     const int b = (int)knew[e];
     const int ob = os[b], oe = b < nb ? os[b + 1] : n;
@@ -467,22 +469,42 @@ __device__ __forceinline__ void rebin_place(const Params& p, int e, int n, int n
     sorted_l[pos] = l;
     sorted_key[pos] = (unsigned)b;
     const int s = p.indices ? p.indices[l] : l;
-    const D3 x = ld3(p.X + (int64_t)3 * s);
+    const D3 xs = ld3(p.X + (int64_t)3 * s);
     sorted_s[pos] = s;
 #pragma unroll
-    for (int d = 0; d < 3; ++d) sorted_X[(int64_t)3 * pos + d] = x.v[d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
+    for (int d = 0; d < 3; ++d) x[d] = xs.v[d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
+    return pos;
 }
 // R4 (only when something moved: wpre[nw] is the mover count): every entry to its
-// new sorted position; the sorted arrays rewritten there
+// new sorted position; the sorted arrays rewritten there.  The positions leave
+// through LDS: a block's records go out as consecutive doubles of consecutive
+// records (a stayer run's new positions are consecutive), not as a wave's 8-byte
+// stores at a 24-byte stride, which write every 64-byte piece three times.
 __global__ __launch_bounds__(BLOCK) void k_rebin_scatter(Params p, int n, int nb, const unsigned* mbits, const int* wpre,
                                                          int nw, const unsigned* knew, const int* lold, const int* os,
                                                          const int* ns, const int* mstart, const int* mlist,
                                                          int* sorted_l, unsigned* sorted_key, int* sorted_s,
                                                          double* sorted_X) {
     if (wpre[nw] == 0) return;
-    for (int e = blockIdx.x * BLOCK + threadIdx.x; e < n; e += gridDim.x * BLOCK)
-        rebin_place(p, e, n, nb, mbits, wpre, knew, lold, os, ns, mstart, mlist, sorted_l, sorted_key, sorted_s,
-                    sorted_X);
+    __shared__ double sx[3 * BLOCK];
+    __shared__ int sp[BLOCK];
+    for (int e0 = blockIdx.x * BLOCK; e0 < n; e0 += gridDim.x * BLOCK) {
+        const int e = e0 + threadIdx.x;
+        if (e < n) {
+            double x[3];
+            sp[threadIdx.x] = rebin_place(p, e, n, nb, mbits, wpre, knew, lold, os, ns, mstart, mlist, sorted_l,
+                                          sorted_key, sorted_s, x);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) sx[3 * threadIdx.x + d] = x[d];
+        }
+        __syncthreads();
+        const int cnt = 3 * min(BLOCK, n - e0);
+        for (int i = threadIdx.x; i < cnt; i += BLOCK) {
+            const int r = i / 3;
+            sorted_X[(int64_t)3 * sp[r] + (i - 3 * r)] = sx[i];
+        }
+        __syncthreads();
+    }
 }
 // the new bucket starts in place (when something moved)
 __global__ __launch_bounds__(BLOCK) void k_rebin_commit(int nb, const int* T, const int* ns, int* plane_start) {

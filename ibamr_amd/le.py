@@ -366,6 +366,20 @@ def zero_ghosts_spread(ctx: Context, markers: Markers, kernel: str, centering: s
                                              ctypes.byref(geom.c), arr, q_depth, _ptr(Q), Q_depth, _ptr(X)))
 
 
+def zero_spread(ctx: Context, markers: Markers, kernel: str, centering: str, geom: Geometry,
+                q: Sequence[torch.Tensor], Q: torch.Tensor, X: torch.Tensor, q_depth: int = 1,
+                Q_depth: Optional[int] = None, axis: int = 0):
+    """q := 0 (every point, ghosts included) then spread, bit for bit: the target as
+    LDataManager::spread hands it to LEInteractor::spread (LDataManager.cpp:596-660;
+    ibtk_le_zero_spread).  On a 3-D column binning one sweep that writes q and never
+    reads it."""
+    if Q_depth is None:
+        Q_depth = geom.ndim if centering in ("side", "edge") else q_depth
+    arr = _ptr_array(q, geom)
+    check(ctx.lib.ibtk_le_zero_spread(ctx.h, markers.h, kernel_id(kernel), CENTERING[centering], axis,
+                                      ctypes.byref(geom.c), arr, q_depth, _ptr(Q), Q_depth, _ptr(X)))
+
+
 # USER_DEFINED kernel function (LEInteractor::s_kernel_fcn, LEInteractor.h:100-101):
 # a Python callable phi(r) -> float, called by the library on the host
 USER_KERNEL_FN = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.c_double)

@@ -308,6 +308,16 @@ int ibtk_le_zero_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int cen
 int ibtk_le_zero_ghosts_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                                const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth,
                                const double* Q_dev, int Q_depth, const double* X_dev);
+/* The target as LDataManager::spread hands it to LEInteractor::spread: every point of
+ * q set to 0, ghosts included (LDataManager.cpp:596, setToScalar(f, 0,
+ * interior_only = false)), then ibtk_le_spread into it -- bit for bit those two steps.
+ * A 3-D column binning does both in the spread's sweep (items start every owned point
+ * from 0 and never read q; items no marker reaches store zeros), so q is written once
+ * and not read.  Other binnings (2-D, an empty list): the zeroing (pitched arrays: the
+ * whole span, row padding included), then ibtk_le_spread. */
+int ibtk_le_zero_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                        const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
+                        int Q_depth, const double* X_dev);
 int ibtk_le_fold_periodic_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, int centering,
                                  double* const* q_dev, int q_depth, const int* periodic);
 /* Physical-boundary ghost operators for side-centred data on one patch

@@ -113,3 +113,50 @@ def test_fill_interp_equals_two_calls(le, ctx, kernel, centering, periodic):
     assert np.array_equal(a, b), f"max diff {np.nanmax(np.abs(a - b))}"
     for b0, b1 in zip(q_before, qb):  # nothing written
         assert torch.equal(torch.nan_to_num(b0, nan=7.0), torch.nan_to_num(b1, nan=7.0))
+
+
+@pytest.mark.parametrize("kernel,centering,ndim", [("IB_4", "side", 3), ("IB_6", "side", 3), ("PIECEWISE_LINEAR", "side", 3),
+                                                   ("IB_4", "cell", 3), ("IB_3", "node", 3), ("PIECEWISE_CUBIC", "edge", 3),
+                                                   ("BSPLINE_4", "side", 3), ("IB_4_W8", "cell", 3),
+                                                   ("IB_4", "side", 2), ("IB_6", "cell", 2)])
+@pytest.mark.parametrize("pitched", [False, True])
+@pytest.mark.parametrize("empty", [False, True])
+def test_zero_spread_equals_two_calls(le, ctx, kernel, centering, ndim, pitched, empty):
+    """ibtk_le_zero_spread = every point of q to 0, then ibtk_le_spread (LDataManager::spread's
+    target, LDataManager.cpp:596): q starts NaN everywhere in the fused call (no point may be
+    read, every point must be written); markers cover part of the patch only, so that items
+    without candidates occur; an empty list (the zeroing alone) and 2-D (the two steps)."""
+    if pitched and ndim != 3:
+        pytest.skip("pitched layouts are 3-D")
+    geom, X, idx, xs, depth = make_case(kernel, ndim, centering, seed=zlib.crc32(f"zs{kernel}{centering}{ndim}".encode()),
+                                        M=400)
+    if pitched:
+        geom = geom.aligned()
+    if empty:
+        idx = idx[:0]
+        xs = xs[:0]
+    rng = np.random.default_rng(53)
+    a_ = ndim - 1  # markers in the lower half of the slowest dim
+    L = (geom.iupper[a_] - geom.ilower[a_] + 1) * geom.dx[a_]
+    X[:, a_] = np.minimum(X[:, a_], geom.x_lower[a_] + 0.45 * L)
+    dev = "cuda:0"
+    Xd, idd, xsd = torch.from_numpy(X).to(dev), torch.from_numpy(idx).to(dev), torch.from_numpy(xs).to(dev)
+    Qd = ndim if centering in ("side", "edge") else depth
+    F = torch.from_numpy(rng.uniform(-1, 1, (X.shape[0], Qd))).to(dev)
+    m = le.Markers(ctx).bin(geom, kernel, Xd, idd, xsd)
+    qa = geom.alloc(centering, depth)
+    for a in qa:
+        a.copy_(torch.from_numpy(rng.uniform(-1, 1, tuple(a.shape))))
+    qb = geom.alloc(centering, depth)
+    for a in qb:
+        a.fill_(np.nan)
+    for a in qa:
+        a.zero_()
+    le.spread(ctx, m, kernel, centering, geom, qa, F, Xd, q_depth=depth)
+    le.zero_spread(ctx, m, kernel, centering, geom, qb, F, Xd, q_depth=depth)
+    ctx.synchronize()
+    for a, b in zip(qa, qb):
+        assert not torch.isnan(b).any(), "a point was left unwritten"
+        assert torch.equal(a, b)
+    if empty:
+        assert all(not b.any() for b in qb)
