@@ -171,6 +171,10 @@ struct ibtk_le_markers_s {
     int S = 0, nseg = 0;  // 3-D: sweep segments
     ibtk_le_patch_geom geom{};
     DevBuf sorted_key, sorted_l, sorted_s, sorted_X, sorted_a, plane_start, indices, xshift;
+    // 3-D: the sorted positions are sorted_X or sorted_X2, the one the device cell xcur
+    // names (ibtk_le_markers_rebin swaps them on the device); xcur_set once it is written
+    DevBuf sorted_X2, xcur;
+    bool xcur_set = false;
     DevBuf cand_cnt, cand_off, cand_idx;  // spread candidate lists, built on first use after a bin
     DevBuf last, qdst;                    // interp with duplicate list entries (Params::qdst)
     DevBuf items, nsub, isub, nitems;     // 3-D sweep item table
@@ -534,6 +538,8 @@ extern "C" int ibtk_le_markers_destroy(ibtk_le_markers m) {
     if (!m) return IBTK_LE_OK;
     hipSetDevice(m->ctx->device);
     hipStreamSynchronize(m->ctx->stream);
+    for (DevBuf* b : {&m->sorted_X2, &m->xcur})
+        b->release();
     for (DevBuf* b : {&m->sorted_key, &m->sorted_l, &m->sorted_s, &m->sorted_X, &m->sorted_a, &m->plane_start, &m->indices,
                       &m->xshift, &m->cand_cnt, &m->cand_off, &m->cand_idx, &m->last, &m->qdst, &m->items,
                       &m->nsub, &m->isub, &m->nitems, &m->pd, &m->entry_off, &m->qin, &m->owner, &m->int_off,
@@ -629,6 +635,9 @@ static int gather_buckets(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const 
     if ((rc = ctx->bfirst.ensure(sizeof(int) * (size_t)(nbuckets + 1)))) return rc;
     HIP_TRY(launch_gather_col(kernel, p, n, m->sorted_s.as<int>(), m->sorted_X.as<double>(), m->sorted_key.as<unsigned>(),
                               nbuckets, ctx->bfirst.as<int>(), ctx->stream));
+    if ((rc = m->xcur.ensure(sizeof(double*)))) return rc;
+    HIP_TRY(launch_set_xcur(m->xcur.as<double*>(), m->sorted_X.as<double>(), ctx->stream));
+    m->xcur_set = true;
     size_t tb = 0;
     HIP_TRY(launch_suffix_min(nullptr, tb, ctx->bfirst.as<int>(), m->plane_start.as<int>(), nbuckets + 1, ctx->stream));
     if ((rc = ctx->temp.ensure(tb))) return rc;
@@ -746,7 +755,15 @@ extern "C" int ibtk_le_markers_rebin(ibtk_le_ctx ctx, ibtk_le_markers m, const d
     r.sorted_l = m->sorted_l.as<int>();
     r.sorted_key = m->sorted_key.as<unsigned>();
     r.sorted_s = m->sorted_s.as<int>();
-    r.sorted_X = m->sorted_X.as<double>();
+    if ((rc = m->sorted_X2.ensure(3 * sizeof(double) * (size_t)n))) return rc;
+    if ((rc = m->xcur.ensure(sizeof(double*)))) return rc;
+    if (!m->xcur_set) {
+        HIP_TRY(launch_set_xcur(m->xcur.as<double*>(), m->sorted_X.as<double>(), s));
+        m->xcur_set = true;
+    }
+    r.xcur = m->xcur.as<double*>();
+    r.xa = m->sorted_X.as<double>();
+    r.xb = m->sorted_X2.as<double>();
     HIP_TRY(launch_rekey(m->kernel, p, r, s));
     if ((rc = scan_excl(ctx, r.wcnt, r.wpre, nw + 1))) return rc;  // wpre[nw]: the mover count
     // everything below returns at once on the device when nothing moved
@@ -894,6 +911,7 @@ static int prepare(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const ibtk_le
     p.sorted_l = m->sorted_l.as<int>();
     p.sorted_s = m->sorted_s.as<int>();
     p.sorted_X = m->sorted_X.as<double>();
+    p.sorted_X_ref = m->xcur_set ? m->xcur.as<double*>() : nullptr;
     p.sorted_key = m->sorted_key.as<unsigned>();
     p.plane_start = m->plane_start.as<int>();
     p.err = ctx->err.as<int>();
@@ -1560,6 +1578,7 @@ static int level_params(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cent
     p.sorted_l = m->sorted_l.as<int>();
     p.sorted_s = m->sorted_s.as<int>();
     p.sorted_X = m->sorted_X.as<double>();
+    p.sorted_X_ref = m->xcur_set ? m->xcur.as<double*>() : nullptr;
     p.sorted_key = m->sorted_key.as<unsigned>();
     p.plane_start = m->plane_start.as<int>();
     p.err = ctx->err.as<int>();

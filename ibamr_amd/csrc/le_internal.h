@@ -160,6 +160,7 @@ struct Params {
     const int* sorted_l;       // sorted position -> list entry
     const int* sorted_s;       // sorted position -> marker index
     const double* sorted_X;    // sorted position -> X(s) + Xshift(l) [NDIM]
+    const double* const* sorted_X_ref;  // 3-D: device cell naming the current sorted positions (or null: sorted_X)
     const unsigned* sorted_key;
     const int* plane_start;    // nbricks*B + 1 offsets into the sorted list: bucket = key >> (shift - log2 B)
                                // (brick b's entries are [plane_start[b*B], plane_start[(b+1)*B]))
@@ -229,9 +230,13 @@ struct RebinBufs {
     int* sorted_l;
     unsigned* sorted_key;
     int* sorted_s;
-    double* sorted_X;
+    double** xcur;          // the current sorted-position buffer (xa or xb; le_sweep.hip rebin_other)
+    double* xa;
+    double* xb;
 };
+hipError_t launch_set_xcur(double** xcur, double* x, hipStream_t s);
 hipError_t launch_rekey(int kernel, const Params& p, const RebinBufs& r, hipStream_t s);
+
 hipError_t launch_rebin_copy(int kernel, const Params& p, const RebinBufs& r, hipStream_t s);
 hipError_t launch_rebin_starts(const RebinBufs& r, hipStream_t s);  // uses r.d as the block sums (int2)
 hipError_t launch_rebin_movers(const RebinBufs& r, hipStream_t s);

@@ -175,12 +175,21 @@ __global__ __launch_bounds__(BLOCK) void k_bin_col(Params p, int n, unsigned* ke
 // Exact: the same order, bucket starts and sorted positions as a fresh binning.
 // Nothing is read back to the host; with no movers only k_rekey does work.
 //
+// The sorted positions live in one of two buffers, xa and xb; *xcur names the
+// current one (the sweeps read it through Params::sorted_X_ref).  R1 writes the
+// new positions, in the old order, into the other buffer: with nothing moved that
+// order is the new one and the commit makes it current; else the scatter reads it
+// there (coalesced) and writes the new order into the current buffer.
+__device__ __forceinline__ double* rebin_other(double* const* xcur, double* xa, double* xb) {
+    return *xcur == xa ? xb : xa;
+}
 // R1: new keys in the old order; the shifted positions stored at the old sorted
-// positions (final when nothing moved); per-bucket mover counts in/out; the mover
-// flags as a bit per entry with per-word counts.
+// positions in the other buffer; per-bucket mover counts in/out; the mover flags
+// as a bit per entry with per-word counts.
 template <int K>
-__global__ __launch_bounds__(BLOCK) void k_rekey(Params p, int n, const unsigned* kold, const int* sl, double* sorted_X,
-                                                 unsigned* mbits, int* wcnt, int* cin, int* cout) {
+__global__ __launch_bounds__(BLOCK) void k_rekey(Params p, int n, const unsigned* kold, const int* sl,
+                                                 double* const* xcur, double* xa, double* xb, unsigned* mbits,
+                                                 int* wcnt, int* cin, int* cout) {
     __shared__ double sx[3 * BLOCK];
     const int e0 = blockIdx.x * BLOCK;
     const int e = e0 + threadIdx.x;
@@ -212,7 +221,7 @@ __global__ __launch_bounds__(BLOCK) void k_rekey(Params p, int n, const unsigned
     }
     __syncthreads();
     const int cnt = 3 * min(BLOCK, n - e0);
-    double* out = sorted_X + (int64_t)3 * e0;
+    double* out = rebin_other(xcur, xa, xb) + (int64_t)3 * e0;
     for (int i = threadIdx.x; 2 * i < cnt; i += BLOCK) {
         if (2 * i + 1 < cnt) {
             double2 v;
@@ -227,22 +236,22 @@ __global__ __launch_bounds__(BLOCK) void k_rekey(Params p, int n, const unsigned
 
 // R1b (something moved): copies of the old l and the new keys for the scatter,
 // which overwrites the sorted arrays (a stayer's new key is its old one; a mover's
-// is computed again)
+// is computed again from its new position, which R1 left in the other buffer)
 constexpr int RB_GRID = 4096;  // grid-stride kernels of the re-binning's tail
 template <int K>
 __global__ __launch_bounds__(BLOCK) void k_rebin_copy(Params p, int n, const int* T, const unsigned* mbits,
-                                                      const unsigned* kold, const int* sl, unsigned* knew, int* lold) {
+                                                      const unsigned* kold, const int* sl, double* const* xcur,
+                                                      double* xa, double* xb, unsigned* knew, int* lold) {
     if (*T == 0) return;
+    const double* xo = rebin_other(xcur, xa, xb);
     for (int e = blockIdx.x * BLOCK + threadIdx.x; e < n; e += gridDim.x * BLOCK) {
         const int l = sl[e];
         lold[e] = l;
         unsigned k = kold[e];
         if ((mbits[e >> 5] >> (e & 31)) & 1u) {
-            const int s = p.indices ? p.indices[l] : l;
-            const D3 x = ld3(p.X + (int64_t)3 * s);
             double Xs[3];
 #pragma unroll
-            for (int d = 0; d < 3; ++d) Xs[d] = x.v[d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
+            for (int d = 0; d < 3; ++d) Xs[d] = xo[(int64_t)3 * e + d];
             k = entry_key<K>(p, l, Xs);
         }
         knew[e] = k;
@@ -273,18 +282,42 @@ __device__ __forceinline__ int lower_bound_l(const int* v, int lo, int hi, int l
 // in three phases over blocks of RB_BLK buckets: block sums, a scan of the block sums
 // by one workgroup, the blocks' own scans.  ns[b] = os[b] + prefix(d)[b].
 constexpr int RB_IPT = 8, RB_BLK = BLOCK * RB_IPT;
+// v[i] = a[b0 + i] for b0 + i <= last, else 0 (b0 a multiple of 8: two 16-byte loads)
+__device__ __forceinline__ void rb_load8(const int* a, long b0, long last, int* v) {
+    if (b0 + 7 <= last) {
+        const int4 x = *reinterpret_cast<const int4*>(a + b0), y = *reinterpret_cast<const int4*>(a + b0 + 4);
+        v[0] = x.x, v[1] = x.y, v[2] = x.z, v[3] = x.w, v[4] = y.x, v[5] = y.y, v[6] = y.z, v[7] = y.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = b0 + i <= last ? a[b0 + i] : 0;
+    }
+}
+// a[b0 + i] = v[i] for b0 + i <= last
+__device__ __forceinline__ void rb_store8(int* a, long b0, long last, const int* v) {
+    if (b0 + 7 <= last) {
+        *reinterpret_cast<int4*>(a + b0) = make_int4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<int4*>(a + b0 + 4) = make_int4(v[4], v[5], v[6], v[7]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (b0 + i <= last) a[b0 + i] = v[i];
+    }
+}
+static_assert(RB_IPT == 8, "rb_load8 / rb_store8");
 __global__ __launch_bounds__(BLOCK) void k_rebin_bsum(int nb, const int* cin, const int* cout, const int* T,
                                                       int2* bsum) {
     if (*T == 0) return;
     __shared__ int sd[BLOCK], sc[BLOCK];
     const long b0 = (long)blockIdx.x * RB_BLK + (long)threadIdx.x * RB_IPT;
+    int vi[RB_IPT], vo[RB_IPT];
+    rb_load8(cin, b0, nb + 1, vi);
+    rb_load8(cout, b0, nb + 1, vo);
     int d = 0, c = 0;
 #pragma unroll
-    for (int i = 0; i < RB_IPT; ++i)
-        if (b0 + i <= nb + 1) {
-            d += cin[b0 + i] - cout[b0 + i];
-            c += cin[b0 + i];
-        }
+    for (int i = 0; i < RB_IPT; ++i) {
+        d += vi[i] - vo[i];
+        c += vi[i];
+    }
     sd[threadIdx.x] = d;
     sc[threadIdx.x] = c;
     __syncthreads();
@@ -335,12 +368,12 @@ __global__ __launch_bounds__(BLOCK) void k_rebin_bapply(int nb, const int* cin, 
     if (*T == 0) return;
     __shared__ int sd[BLOCK], sc[BLOCK];
     const long b0 = (long)blockIdx.x * RB_BLK + (long)threadIdx.x * RB_IPT;
-    int vd[RB_IPT], vc[RB_IPT], d = 0, c = 0;
+    int vd[RB_IPT], vc[RB_IPT], vo[RB_IPT], d = 0, c = 0;
+    rb_load8(cin, b0, nb + 1, vc);
+    rb_load8(cout, b0, nb + 1, vo);
 #pragma unroll
     for (int i = 0; i < RB_IPT; ++i) {
-        const bool in = b0 + i <= nb + 1;
-        vd[i] = in ? cin[b0 + i] - cout[b0 + i] : 0;
-        vc[i] = in ? cin[b0 + i] : 0;
+        vd[i] = vc[i] - vo[i];
         d += vd[i];
         c += vc[i];
     }
@@ -357,16 +390,17 @@ __global__ __launch_bounds__(BLOCK) void k_rebin_bapply(int nb, const int* cin, 
     }
     d = bsum[blockIdx.x].x + sd[threadIdx.x] - d;  // exclusive: the block's and this thread's offsets
     c = bsum[blockIdx.x].y + sc[threadIdx.x] - c;
+    int vs[RB_IPT], vn[RB_IPT], vm[RB_IPT];
+    rb_load8(os, b0, nb, vs);
 #pragma unroll
     for (int i = 0; i < RB_IPT; ++i) {
-        const long b = b0 + i;
-        if (b <= nb + 1) {
-            if (b <= nb) ns[b] = os[b] + d;
-            mstart[b] = c;
-        }
+        vn[i] = vs[i] + d;
+        vm[i] = c;
         d += vd[i];
         c += vc[i];
     }
+    rb_store8(ns, b0, nb, vn);
+    rb_store8(mstart, b0, nb + 1, vm);
 }
 
 // R3: every mover appends its l to its new bucket's list (mstart: exclusive prefix
@@ -449,11 +483,11 @@ __global__ __launch_bounds__(BLOCK) void k_rebin_copy_big(const int* nbig, const
 }
 
 // old entry e's new sorted position, returned; l, key and marker index written
-// there, the shifted position into x
+// there, its shifted position (R1's, in the other buffer xo) into x
 __device__ __forceinline__ int rebin_place(const Params& p, int e, int n, int nb, const unsigned* mbits,
                                            const int* wpre, const unsigned* knew, const int* lold, const int* os,
-                                           const int* ns, const int* mstart, const int* mlist, int* sorted_l,
-                                           unsigned* sorted_key, int* sorted_s, double* x) {
+                                           const int* ns, const int* mstart, const int* mlist, const double* xo,
+                                           int* sorted_l, unsigned* sorted_key, int* sorted_s, double* x) {
     const int l = lold[e];
     const int b = (int)knew[e];
     const int ob = os[b], oe = b < nb ? os[b + 1] : n;
@@ -468,37 +502,46 @@ __device__ __forceinline__ int rebin_place(const Params& p, int e, int n, int nb
     pos += lower_bound_l(mlist, mstart[b], mstart[b + 1], l) - mstart[b];
     sorted_l[pos] = l;
     sorted_key[pos] = (unsigned)b;
-    const int s = p.indices ? p.indices[l] : l;
-    const D3 xs = ld3(p.X + (int64_t)3 * s);
-    sorted_s[pos] = s;
+    sorted_s[pos] = p.indices ? p.indices[l] : l;
 #pragma unroll
-    for (int d = 0; d < 3; ++d) x[d] = xs.v[d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
+    for (int d = 0; d < 3; ++d) x[d] = xo[(int64_t)3 * e + d];
     return pos;
 }
 // R4 (only when something moved: wpre[nw] is the mover count): every entry to its
-// new sorted position; the sorted arrays rewritten there.  The positions leave
-// through LDS: a block's records go out as consecutive doubles of consecutive
-// records (a stayer run's new positions are consecutive), not as a wave's 8-byte
-// stores at a 24-byte stride, which write every 64-byte piece three times.
-__global__ __launch_bounds__(BLOCK) void k_rebin_scatter(Params p, int n, int nb, const unsigned* mbits, const int* wpre,
-                                                         int nw, const unsigned* knew, const int* lold, const int* os,
-                                                         const int* ns, const int* mstart, const int* mlist,
-                                                         int* sorted_l, unsigned* sorted_key, int* sorted_s,
-                                                         double* sorted_X) {
+// new sorted position; the sorted arrays rewritten there, the positions read from
+// the other buffer in the old order and written into the current one.  The
+// positions leave through LDS: a block's records go
+// out as consecutive doubles of consecutive records (a stayer run's new positions
+// are consecutive), not as a wave's 8-byte stores at a 24-byte stride, which write
+// every 64-byte piece three times.
+constexpr int RB_U = 1;
+__global__ __launch_bounds__(BLOCK) void k_rebin_scatter(Params p, int n, int nb, const unsigned* __restrict__ mbits,
+                                                         const int* __restrict__ wpre, int nw,
+                                                         const unsigned* __restrict__ knew,
+                                                         const int* __restrict__ lold, const int* __restrict__ os,
+                                                         const int* __restrict__ ns, const int* __restrict__ mstart,
+                                                         const int* __restrict__ mlist, int* __restrict__ sorted_l,
+                                                         unsigned* __restrict__ sorted_key, int* __restrict__ sorted_s,
+                                                         double* const* xcur, double* xa, double* xb) {
     if (wpre[nw] == 0) return;
-    __shared__ double sx[3 * BLOCK];
-    __shared__ int sp[BLOCK];
-    for (int e0 = blockIdx.x * BLOCK; e0 < n; e0 += gridDim.x * BLOCK) {
-        const int e = e0 + threadIdx.x;
-        if (e < n) {
-            double x[3];
-            sp[threadIdx.x] = rebin_place(p, e, n, nb, mbits, wpre, knew, lold, os, ns, mstart, mlist, sorted_l,
-                                          sorted_key, sorted_s, x);
+    double* const sorted_X = *xcur;
+    const double* const xo = rebin_other(xcur, xa, xb);
+    __shared__ double sx[3 * RB_U * BLOCK];
+    __shared__ int sp[RB_U * BLOCK];
+    for (int e0 = blockIdx.x * RB_U * BLOCK; e0 < n; e0 += gridDim.x * RB_U * BLOCK) {
 #pragma unroll
-            for (int d = 0; d < 3; ++d) sx[3 * threadIdx.x + d] = x[d];
+        for (int u = 0; u < RB_U; ++u) {
+            const int i = u * BLOCK + threadIdx.x, e = e0 + i;
+            if (e < n) {
+                double x[3];
+                sp[i] = rebin_place(p, e, n, nb, mbits, wpre, knew, lold, os, ns, mstart, mlist, xo, sorted_l,
+                                    sorted_key, sorted_s, x);
+#pragma unroll
+                for (int d = 0; d < 3; ++d) sx[3 * i + d] = x[d];
+            }
         }
         __syncthreads();
-        const int cnt = 3 * min(BLOCK, n - e0);
+        const int cnt = 3 * min(RB_U * BLOCK, n - e0);
         for (int i = threadIdx.x; i < cnt; i += BLOCK) {
             const int r = i / 3;
             sorted_X[(int64_t)3 * sp[r] + (i - 3 * r)] = sx[i];
@@ -506,10 +549,21 @@ __global__ __launch_bounds__(BLOCK) void k_rebin_scatter(Params p, int n, int nb
         __syncthreads();
     }
 }
-// the new bucket starts in place (when something moved)
-__global__ __launch_bounds__(BLOCK) void k_rebin_commit(int nb, const int* T, const int* ns, int* plane_start) {
-    if (*T == 0) return;
+// the new bucket starts in place when something moved; else the other buffer,
+// which holds the new positions in the unchanged order, becomes current
+__global__ __launch_bounds__(BLOCK) void k_rebin_commit(int nb, const int* T, const int* ns, int* plane_start,
+                                                        double** xcur, double* xa, double* xb) {
+    if (*T == 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) *xcur = rebin_other(xcur, xa, xb);
+        return;
+    }
     for (int b = blockIdx.x * BLOCK + threadIdx.x; b <= nb; b += gridDim.x * BLOCK) plane_start[b] = ns[b];
+}
+// *xcur := x (a fresh binning gathered the positions into x)
+__global__ void k_set_xcur(double** xcur, double* x) { *xcur = x; }
+hipError_t launch_set_xcur(double** xcur, double* x, hipStream_t s) {
+    hipLaunchKernelGGL(k_set_xcur, dim3(1), dim3(1), 0, s, xcur, x);
+    return hipGetLastError();
 }
 
 // Per sorted entry e: the marker index and the shifted position (coalesced for
@@ -548,6 +602,12 @@ __global__ __launch_bounds__(BLOCK) void k_gather_col(Params p, int n, int* sort
             out[2 * i] = sx[2 * i];
         }
     }
+}
+
+// the current sorted positions of a 3-D binning (Params::sorted_X_ref: xa or xb of
+// the re-binning), read once per kernel
+__device__ __forceinline__ const double* cur_sorted_X(const Params& p) {
+    return p.sorted_X_ref ? *p.sorted_X_ref : p.sorted_X;
 }
 
 // ---------------------------------------------------------------------------
@@ -798,6 +858,7 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     CompDesc cd;
     const int* bs;
     item_patch<LVL>(p, si, c, cg, cd, bs);
+    const double* const sorted_X = cur_sorted_X(p);
     if (p.zmode) {  // the planes the item reads: a0 + LO .. a1 - 1 + HI
         const bool inner = cg.org[2] + a0 + LO >= p.zlo && cg.org[2] + a1 - 1 + HI <= p.zhi;
         if (inner != (p.zmode == 1)) return;
@@ -908,7 +969,7 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
         e = min(e, nlast);
         m.s = p.sorted_s[e];
         m.q = p.qdst ? p.qdst[e] : m.s;
-        const D3 xs = ld3(p.sorted_X + (int64_t)3 * e);
+        const D3 xs = ld3(sorted_X + (int64_t)3 * e);
         m.X[0] = xs.v[0];
         m.X[1] = xs.v[1];
         m.X[2] = xs.v[2];
@@ -1229,6 +1290,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     CompDesc cd;
     const int* bs;
     item_patch<LVL>(p, si, c, cg, cd, bs);
+    const double* const sorted_X = cur_sorted_X(p);
     const int ncx = cg.ncx;
     const int cx = col % ncx, cy = col / ncx;
     if (cx == 0 || cx == ncx - 1 || cy == 0 || cy == cg.ncy - 1) return;  // guard columns own no points
@@ -1303,7 +1365,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // candidate data of sorted position e
     auto cand_at = [&](int e, Cand& d) {
         e = min(e, nlast);
-        const D3 xs = ld3(p.sorted_X + (int64_t)3 * e);
+        const D3 xs = ld3(sorted_X + (int64_t)3 * e);
         d.X[0] = xs.v[0];
         d.X[1] = xs.v[1];
         d.X[2] = xs.v[2];
@@ -1818,14 +1880,14 @@ template <int K>
 hipError_t launch_rekey_t(const Params& p, const RebinBufs& r, hipStream_t s) {
     if (r.n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_rekey<K>, dim3((r.n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, r.n, r.kold, r.lsorted,
-                       r.sorted_X, r.mbits, r.wcnt, r.cin, r.cout);
+                       r.xcur, r.xa, r.xb, r.mbits, r.wcnt, r.cin, r.cout);
     return hipGetLastError();
 }
 template <int K>
 hipError_t launch_rebin_copy_t(const Params& p, const RebinBufs& r, hipStream_t s) {
     if (r.n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_rebin_copy<K>, dim3(RB_GRID), dim3(BLOCK), 0, s, p, r.n, r.wpre + r.nw, r.mbits, r.kold,
-                       r.lsorted, r.knew, r.lold);
+                       r.lsorted, r.xcur, r.xa, r.xb, r.knew, r.lold);
     return hipGetLastError();
 }
 using RekeyFn = hipError_t (*)(const Params&, const RebinBufs&, hipStream_t);
@@ -1866,9 +1928,9 @@ hipError_t launch_rebin_movers(const RebinBufs& r, hipStream_t s) {
 hipError_t launch_rebin_scatter(const Params& p, const RebinBufs& r, hipStream_t s) {
     if (r.n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_rebin_scatter, dim3(RB_GRID), dim3(BLOCK), 0, s, p, r.n, r.nb, r.mbits, r.wpre, r.nw, r.knew,
-                       r.lold, r.os, r.ns, r.mstart, r.mlist, r.sorted_l, r.sorted_key, r.sorted_s, r.sorted_X);
+                       r.lold, r.os, r.ns, r.mstart, r.mlist, r.sorted_l, r.sorted_key, r.sorted_s, r.xcur, r.xa, r.xb);
     hipLaunchKernelGGL(k_rebin_commit, dim3(RB_GRID), dim3(BLOCK), 0, s, r.nb, r.wpre + r.nw, r.ns,
-                       const_cast<int*>(r.os));
+                       const_cast<int*>(r.os), r.xcur, r.xa, r.xb);
     return hipGetLastError();
 }
 hipError_t launch_gather_col(int kernel, const Params& p, int n, int* sorted_s, double* sorted_X,
