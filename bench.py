@@ -298,8 +298,13 @@ def run_level(args, cfg, kernel, dev):
     # entries the interior lists (interp) name (ibtk_le_level_select_interior)
     lvl_s = le.Level.from_flat(ctx, geoms, kernel, X, si, sx, os_)
     lists = {"ii": ii, "oi": oi}
-    u = [[a.uniform_(-1.0, 1.0, generator=gen) for a in geom.alloc("side", device=dev)] for geom in geoms]
-    f = [geom.alloc("side", device=dev) for geom in geoms]
+    # each component's patch arrays carved from one allocation (le.alloc_level): the layout the
+    # fused level fill + interp reads across patches (ibtk_le_level_fill_interp)
+    u = le.alloc_level(geoms, "side", device=dev)
+    for per in u:
+        for a in per:
+            a.uniform_(-1.0, 1.0, generator=gen)
+    f = le.alloc_level(geoms, "side", device=dev)
     # algorithmic bytes: the distinct points each patch's ghost-box stencils touch
     S_touched = [0, 0, 0]
     for q, geom in enumerate(geoms):
@@ -325,12 +330,24 @@ def run_level(args, cfg, kernel, dev):
         else:
             lvl_s.zero_spread("side", f, F, X)
 
+    # the level's ghost fill fused into the interp (ibtk_le_level_fill_interp: each ghost point
+    # read in the neighbour patch the fill copies it from); --unfused-fill: the two calls
+    def fill():
+        if args.unfused_fill:
+            lvl_s.fill_ghosts("side", u)
+
+    def interp():
+        if args.unfused_fill:
+            lvl_s.interp("side", u, U, X)
+        else:
+            lvl_s.fill_interp("side", u, U, X)
+
     def step(record):
         if args.move:
             return step_move(record)
         if record:
             E[0].record()
-        lvl_s.fill_ghosts("side", u)
+        fill()
         if record:
             E[1].record()
         if args.full_bin:
@@ -340,7 +357,7 @@ def run_level(args, cfg, kernel, dev):
         lvl_s.select_interior(M, lists["ii"], lists["oi"])
         if record:
             E[2].record()
-        lvl_s.interp("side", u, U, X)
+        interp()
         if record:
             E[3].record()
             E[4].record()  # zero f: fused into the spread (ibtk_le_level_zero_spread)
@@ -354,10 +371,10 @@ def run_level(args, cfg, kernel, dev):
         # (LIndexSetData's lists after redistribution), re-bin, spread
         if record:
             E[0].record()
-        lvl_s.fill_ghosts("side", u)
+        fill()
         if record:
             E[1].record()
-        lvl_s.interp("side", u, U, X)
+        interp()
         if record:
             E[2].record()
         le.position_update(ctx, "euler", dt_move, X, U, out=X)
@@ -398,7 +415,7 @@ def run_level(args, cfg, kernel, dev):
     ctx.enable_timing(True)
     kt = {"interp": [], "spread": []}
     for _ in range(3):
-        lvl_s.interp("side", u, U, X)
+        interp()
         ctx.synchronize()
         kt["interp"].append(ctx.last_kernel_ms())
         zero_spread(f)
@@ -411,7 +428,8 @@ def run_level(args, cfg, kernel, dev):
     # per entry X and Q/F (24 + 24 B), per touched point 8 B (interp) or 16 B (spread);
     # the touched points are those of the ghost-box lists (an upper bound for interp's)
     B_i = M * 48 + 8 * sum(S_touched)
-    B_s = os_[-1] * 48 + 16 * sum(S_touched)
+    # the spread into the zeroed f (one sweep) writes every point of f and reads none
+    B_s = os_[-1] * 48 + 8 * sum(a.numel() for per in f for a in per)
     dominant = "spread" if k_s >= k_i else "interp"
     achieved = (B_s / (k_s * 1e-3) if dominant == "spread" else B_i / (k_i * 1e-3)) / 1e9
     return {
@@ -427,9 +445,13 @@ def run_level(args, cfg, kernel, dev):
                    "step": ("level ghost fill + interp(3 comps) + position update + per-patch lists rebuilt "
                             "(bench.level_lists, torch ops) + bin(ghost-box lists, interior selected) + zero f and "
                             "spread(3 comps) in one launch" if args.move else
-                            "level ghost fill + bin(ghost-box lists; the interior lists select interp's entries) + "
-                            "interp(3 comps) + zero f and spread(3 comps) in one launch (ibtk_le_level_zero_spread); stationary markers, per-patch lists built once at setup "
-                            "(LIndexSetData between regrids), one launch per sweep over the 512 patches")},
+                            "bin(ghost-box lists; the interior lists select interp's entries) + "
+                            + ("level ghost fill + interp(3 comps)" if args.unfused_fill else
+                               "level ghost fill and interp(3 comps) in one launch (ibtk_le_level_fill_interp: ghost points "
+                               "read in the neighbour patches)") +
+                            " + zero f and spread(3 comps) in one launch (ibtk_le_level_zero_spread); stationary markers, "
+                            "per-patch lists built once at setup (LIndexSetData between regrids), one launch per sweep over "
+                            "the 512 patches")},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "algorithmic_bytes": {"interp": B_i, "spread": B_s}, "kernel_ms": {"interp": k_i, "spread": k_s},

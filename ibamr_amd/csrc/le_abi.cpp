@@ -175,6 +175,8 @@ struct ibtk_le_markers_s {
     // names (ibtk_le_markers_rebin swaps them on the device); xcur_set once it is written
     DevBuf sorted_X2, xcur;
     bool xcur_set = false;
+    DevBuf lvl_nbr;                     // ibtk_le_level_fill_interp's neighbour table ...
+    std::vector<int2> lvl_nbr_host;     // ... and what it holds
     DevBuf cand_cnt, cand_off, cand_idx;  // spread candidate lists, built on first use after a bin
     DevBuf last, qdst;                    // interp with duplicate list entries (Params::qdst)
     DevBuf items, nsub, isub, nitems;     // 3-D sweep item table
@@ -538,7 +540,7 @@ extern "C" int ibtk_le_markers_destroy(ibtk_le_markers m) {
     if (!m) return IBTK_LE_OK;
     hipSetDevice(m->ctx->device);
     hipStreamSynchronize(m->ctx->stream);
-    for (DevBuf* b : {&m->sorted_X2, &m->xcur})
+    for (DevBuf* b : {&m->sorted_X2, &m->xcur, &m->lvl_nbr})
         b->release();
     for (DevBuf* b : {&m->sorted_key, &m->sorted_l, &m->sorted_s, &m->sorted_X, &m->sorted_a, &m->plane_start, &m->indices,
                       &m->xshift, &m->cand_cnt, &m->cand_off, &m->cand_idx, &m->last, &m->qdst, &m->items,
@@ -1704,23 +1706,21 @@ extern "C" int ibtk_le_level_zero_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int
 // dims): LDataManager::interp's fill schedule (LDataManager.cpp:748-751).
 // q_dev as for ibtk_le_level_interp.  The device tables live in the context
 // until the next call with another tiling.
-extern "C" int ibtk_le_level_fill_ghosts(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms,
-                                         int centering, double* const* q_dev, int q_depth, const int* periodic) {
-    if (!ctx || !geoms || !q_dev || npatch <= 0) return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: null argument");
-    if (centering != IBTK_LE_SIDE && centering != IBTK_LE_CELL)
-        return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: side or cell data");
-    LevelTiling t;
+// The tiling of a level of equal patches tiling a box (periodic in the flagged dims):
+// cells per patch, tiles per dim, tile of each patch and patch of each tile (-1: none).
+static int level_tiling(int npatch, const ibtk_le_patch_geom* geoms, int centering, const int* periodic,
+                        const char* who, LevelTiling& t, std::vector<int>& tile_of, std::vector<int>& patch_of) {
     std::memset(&t, 0, sizeof(t));
     int lo[3] = {INT_MAX, INT_MAX, INT_MAX}, hi[3] = {INT_MIN, INT_MIN, INT_MIN};
     for (int q = 0; q < npatch; ++q) {
         if (int rc = check_geom(&geoms[q])) return rc;
         if (!packed(&geoms[q])) return fail(IBTK_LE_ERR_ARG, "level calls take packed arrays (pitch {0, 0})");
-        if (geoms[q].ndim != 3) return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: 3-D patches");
+        if (geoms[q].ndim != 3) return fail(IBTK_LE_ERR_ARG, "%s: 3-D patches", who);
         for (int d = 0; d < 3; ++d) {
             const int n = geoms[q].iupper[d] - geoms[q].ilower[d] + 1;
             if (q == 0) t.n[d] = n;
             if (n != t.n[d] || geoms[q].gcw[d] != geoms[0].gcw[0])
-                return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: equal patches and ghost widths only");
+                return fail(IBTK_LE_ERR_ARG, "%s: equal patches and ghost widths only", who);
             lo[d] = std::min(lo[d], geoms[q].ilower[d]);
             hi[d] = std::max(hi[d], geoms[q].iupper[d]);
         }
@@ -1731,23 +1731,57 @@ extern "C" int ibtk_le_level_fill_ghosts(ibtk_le_ctx ctx, int npatch, const ibtk
         t.dom_lo[d] = lo[d];
         t.ntile[d] = (hi[d] - lo[d] + 1) / t.n[d];
         if (t.ntile[d] * t.n[d] != hi[d] - lo[d] + 1 || t.g > t.n[d])
-            return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: the patches must tile a box, ghost width <= patch size");
+            return fail(IBTK_LE_ERR_ARG, "%s: the patches must tile a box, ghost width <= patch size", who);
         t.periodic[d] = periodic ? periodic[d] != 0 : 1;
         ntiles *= t.ntile[d];
     }
-    std::vector<int> tile_of(npatch), patch_of((size_t)ntiles, -1);
+    tile_of.assign(npatch, 0);
+    patch_of.assign((size_t)ntiles, -1);
     for (int q = 0; q < npatch; ++q) {
         int tc[3];
         for (int d = 0; d < 3; ++d) {
             tc[d] = (geoms[q].ilower[d] - lo[d]) / t.n[d];
-            if ((geoms[q].ilower[d] - lo[d]) % t.n[d]) return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: unaligned patch");
+            if ((geoms[q].ilower[d] - lo[d]) % t.n[d]) return fail(IBTK_LE_ERR_ARG, "%s: unaligned patch", who);
         }
         tile_of[q] = tc[0] + t.ntile[0] * (tc[1] + t.ntile[1] * tc[2]);
-        if (patch_of[tile_of[q]] >= 0) return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: overlapping patches");
+        if (patch_of[tile_of[q]] >= 0) return fail(IBTK_LE_ERR_ARG, "%s: overlapping patches", who);
         patch_of[tile_of[q]] = q;
     }
     t.side = centering == IBTK_LE_SIDE;
     t.ncomp = t.side ? 3 : 1;
+    return IBTK_LE_OK;
+}
+
+// the patch supplying patch q's ghost points in direction dir (per dim -1, 0, +1), as
+// k_level_fill finds it: wrapped in the periodic dims, none (-1) across another face
+static int level_neighbour(const LevelTiling& t, const std::vector<int>& tile_of, const std::vector<int>& patch_of,
+                           int q, const int dir[3]) {
+    const int tile = tile_of[q];
+    const int tc[3] = {tile % t.ntile[0], (tile / t.ntile[0]) % t.ntile[1], tile / (t.ntile[0] * t.ntile[1])};
+    int nt[3];
+    for (int d = 0; d < 3; ++d) {
+        nt[d] = tc[d] + dir[d];
+        if (nt[d] < 0 || nt[d] >= t.ntile[d]) {
+            if (!t.periodic[d]) return -1;
+            nt[d] = (nt[d] + t.ntile[d]) % t.ntile[d];
+        }
+    }
+    return patch_of[nt[0] + t.ntile[0] * (nt[1] + t.ntile[1] * nt[2])];
+}
+
+// Ghost fill of a level of equal patches tiling a box (periodic in the flagged
+// dims): LDataManager::interp's fill schedule (LDataManager.cpp:748-751).
+// q_dev as for ibtk_le_level_interp.  The device tables live in the context
+// until the next call with another tiling.
+extern "C" int ibtk_le_level_fill_ghosts(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms,
+                                         int centering, double* const* q_dev, int q_depth, const int* periodic) {
+    if (!ctx || !geoms || !q_dev || npatch <= 0) return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: null argument");
+    if (centering != IBTK_LE_SIDE && centering != IBTK_LE_CELL)
+        return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: side or cell data");
+    LevelTiling t;
+    std::vector<int> tile_of, patch_of;
+    if (int rc = level_tiling(npatch, geoms, centering, periodic, "level_fill_ghosts", t, tile_of, patch_of)) return rc;
+    const long long ntiles = (long long)patch_of.size();
     const size_t narr = (size_t)npatch * t.ncomp;
     for (size_t i = 0; i < narr; ++i)
         if (!q_dev[i]) return fail(IBTK_LE_ERR_ARG, "level_fill_ghosts: null array");
@@ -1770,6 +1804,95 @@ extern "C" int ibtk_le_level_fill_ghosts(ibtk_le_ctx ctx, int npatch, const ibtk
         HIP_TRY(hipMemcpyAsync(base, ctx->lvl_host.data(), host.size(), hipMemcpyHostToDevice, s));
     }
     HIP_TRY(launch_level_fill(t, npatch, tile_d, patch_d, arr_d, t.side ? 1 : q_depth, s));
+    return IBTK_LE_OK;
+}
+
+// ibtk_le_level_fill_ghosts followed by ibtk_le_level_interp, Q bit for bit, in one
+// sweep: a ghost point of a patch is read in the neighbour patch that the fill would
+// copy it from (k_level_fill's rule: the patch owning its wrapped cell, at the same
+// global index), so no ghost layer is written or read twice.  Needs, per component,
+// every patch's array within one 2-GB window (e.g. one allocation per component for the
+// level) and patches of at least (32 + W - 1) x (COLY + W - 1) cells in x and y;
+// otherwise, or for cell data of depth > 1, the two calls.
+extern "C" int ibtk_le_level_fill_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                                         double* const* q_dev, int q_depth, double* Q_dev, int Q_depth,
+                                         const double* X_dev, const int* periodic) {
+    if (!ctx || !m || !q_dev) return fail(IBTK_LE_ERR_ARG, "level_fill_interp: null argument");
+    if (m->npatch <= 0) return fail(IBTK_LE_ERR_ARG, "level_fill_interp: not a level binning (ibtk_le_level_bin)");
+    const int np = m->npatch;
+    auto unfused = [&]() {
+        if (int rc = ibtk_le_level_fill_ghosts(ctx, np, m->geoms.data(), centering, q_dev, q_depth, periodic)) return rc;
+        return ibtk_le_level_interp(ctx, m, kernel, centering, axis, q_dev, q_depth, Q_dev, Q_depth, X_dev);
+    };
+    if ((centering != IBTK_LE_SIDE && centering != IBTK_LE_CELL) || (centering == IBTK_LE_CELL && q_depth != 1))
+        return unfused();
+    LevelTiling t;
+    std::vector<int> tile_of, patch_of;
+    if (int rc = level_tiling(np, m->geoms.data(), centering, periodic, "level_fill_interp", t, tile_of, patch_of))
+        return rc;
+    {  // a staged column region (COLX + HI - LO by COLY + HI - LO points) crosses at most one
+       // face of its patch per dim (le_sweep.hip, the interp's level-fill staging)
+        const KernelInfo ki = kKernelInfo[kernel < 0 || kernel >= K_COUNT ? 0 : kernel];
+        if (t.n[0] < COLX + ki.HI - ki.LO || t.n[1] < COLY + ki.HI - ki.LO) return unfused();
+    }
+    Params p;
+    std::memset(&p, 0, sizeof(p));
+    int nc = 0;
+    if (int rc = level_params(ctx, m, kernel, centering, axis, q_dev, q_depth, Q_depth, X_dev, true, p, nc)) return rc;
+    if (m->n == 0) return IBTK_LE_OK;
+    if (!Q_dev) return fail(IBTK_LE_ERR_ARG, "null Q");
+    // each component's window: its arrays' lowest start to highest end, below 2 GB
+    // (buffer offsets are 32-bit and OFF_NONE is 2^31)
+    const int per = t.side ? 3 : 1;
+    uintptr_t wlo[MAXC], whi[MAXC];
+    for (int c = 0; c < nc; ++c) {
+        wlo[c] = UINTPTR_MAX;
+        whi[c] = 0;
+        for (int q = 0; q < np; ++q) {
+            const CompDesc& cd = m->pdh[q].comp[c];
+            const uintptr_t a = reinterpret_cast<uintptr_t>(cd.u);
+            const uintptr_t b = a + sizeof(double) * (size_t)cd.s2 * (size_t)(cd.hi[2] - cd.lo[2] + 1);
+            wlo[c] = std::min(wlo[c], a);
+            whi[c] = std::max(whi[c], b);
+        }
+        if (whi[c] - wlo[c] >= (uintptr_t(1) << 31)) return unfused();
+    }
+    (void)per;
+    // the 27-direction table, per component and patch
+    std::vector<int2> tab((size_t)nc * np * 27);
+    for (int c = 0; c < nc; ++c)
+        for (int q = 0; q < np; ++q)
+            for (int k = 0; k < 27; ++k) {
+                const int dir[3] = {k % 3 - 1, (k / 3) % 3 - 1, k / 9 - 1};
+                const int sq = k == 13 ? -1 : level_neighbour(t, tile_of, patch_of, q, dir);
+                const CompDesc& src = m->pdh[sq >= 0 ? sq : q].comp[c];
+                tab[((size_t)c * np + q) * 27 + k] =
+                    make_int2((int)(reinterpret_cast<uintptr_t>(src.u) - wlo[c]), sq >= 0 ? 1 : 0);
+            }
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    const size_t bytes = sizeof(int2) * tab.size();
+    if (int rc = m->lvl_nbr.ensure(bytes)) return rc;
+    if (m->lvl_nbr_host.size() != tab.size() || std::memcmp(m->lvl_nbr_host.data(), tab.data(), bytes) != 0) {
+        m->lvl_nbr_host = tab;  // a pageable copy waits for the stream: only when changed
+        HIP_TRY(hipMemcpyAsync(m->lvl_nbr.p, m->lvl_nbr_host.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+    }
+    p.lvl_nbr = m->lvl_nbr.as<int2>();
+    for (int c = 0; c < nc; ++c) {
+        p.lvl_base[c] = reinterpret_cast<const double*>(wlo[c]);
+        p.lvl_span[c] = (unsigned)(whi[c] - wlo[c]);
+    }
+    for (int d = 0; d < 3; ++d) p.lvl_n[d] = t.n[d];
+    if (m->qin_valid) {
+        p.qdst = m->qin.as<int>();
+    } else {
+        if (int rc = build_dedup(ctx, m)) return rc;
+        p.qdst = m->has_dups ? m->qdst.as<int>() : nullptr;
+    }
+    p.Qout = Q_dev;
+    const bool tm = ctx->timing;
+    ctx->ev_valid = false;
+    HIP_TRY(launch_interp_sweep(kernel, p, m->n, ctx->stream, tm ? ctx->ev0 : nullptr, tm ? ctx->ev1 : nullptr));
+    if (tm) ctx->ev_valid = true;
     return IBTK_LE_OK;
 }
 

@@ -185,6 +185,16 @@ struct Params {
     int iper[3] = {0, 0, 0};  // 3-D interp: read the ghost points of the ghost box at their periodic image in
                               // these dims (ibtk_le_fill_interp: the periodic ghost fill fused in)
     int comp0 = 0;       // 3-D spread: a launch's components are comp[comp0 .. comp0 + ncomp)
+    // 3-D level interp with the level's ghost fill fused in (ibtk_le_level_fill_interp): a
+    // ghost point is read where the fill would copy it from -- the neighbour patch owning
+    // its cell (27 directions), at the same global index.  Component c's arrays of every
+    // patch lie in one 32-bit window from lvl_base[c] (lvl_span[c] bytes); lvl_nbr[(c *
+    // npatch + q) * 27 + dir] = {byte offset of the supplying array in that window, 1 if
+    // it is the neighbour in dir (index mapped by -dir n), 0 if none (own array, as is)}.
+    const int2* lvl_nbr = nullptr;
+    const double* lvl_base[MAXC] = {};
+    unsigned lvl_span[MAXC] = {};
+    int lvl_n[3] = {0, 0, 0};  // cells per patch and dim
 };
 
 // Host-side launchers (le_kernels.hip).

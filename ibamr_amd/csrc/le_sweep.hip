@@ -896,12 +896,58 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
         const bool in = gx >= cd.lo[0] && gx <= cd.hi[0] && gy >= cd.lo[1] && gy <= cd.hi[1];
         poff[k] = in ? 8u * (unsigned)((image(gx, 0) - cd.lo[0]) + (image(gy, 1) - cd.lo[1]) * (int)cd.s1) : OFF_NONE;
     }
+    // level fill fused (p.lvl_nbr, LVL only): a staged point outside the patch box is read
+    // in the neighbour patch that supplies it.  The staged region crosses at most one face
+    // per dim (the host asks for patches at least RX x RY cells), toward (sxd, syd): a
+    // point's class is 2 bits (beyond the x face, beyond the y face), and per plane four
+    // uniform offsets, one per class, turn its unmapped offset poff[k] into the supplier's
+    // (the neighbour's window offset, the -dir n index shift, the plane)
+    const bool lfill = LVL && p.lvl_nbr != nullptr;
+    unsigned lsel = 0;  // bits 2k, 2k+1: the class of point k
+    int sxd = 0, syd = 0;
+    if constexpr (LVL) {
+        if (lfill) {
+            sxd = gx0 < cd.ilower[0] ? -1 : (gx0 + RX - 1 >= cd.ilower[0] + p.lvl_n[0] ? 1 : 0);
+            syd = gy0 < cd.ilower[1] ? -1 : (gy0 + S::RY - 1 >= cd.ilower[1] + p.lvl_n[1] ? 1 : 0);
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                const int q = min(lane + SW * k, S::PV - 1);
+                const int gx = gx0 + q % RX, gy = gy0 + q / RX;
+                const bool bx = gx < cd.ilower[0] || gx >= cd.ilower[0] + p.lvl_n[0];
+                const bool by = gy < cd.ilower[1] || gy >= cd.ilower[1] + p.lvl_n[1];
+                lsel |= ((bx ? 1u : 0u) | (by ? 2u : 0u)) << (2 * k);
+            }
+        }
+    }
     const int plast = a1 - 1 + HI;  // last plane the item reads
     const unsigned plane_bytes = (unsigned)(8 * cd.s2);
     // relative plane zr -> registers
     auto plane_load = [&](int zr, double* v) {
         const int z0 = zorg + min(zr, plast);
         const bool zin = z0 >= cd.lo[2] && z0 <= cd.hi[2];
+        if constexpr (LVL) {
+            if (lfill) {  // one resource over the component's level window
+                const int dz = z0 < cd.ilower[2] ? -1 : (z0 >= cd.ilower[2] + p.lvl_n[2] ? 1 : 0);
+                const int2* tab = p.lvl_nbr + ((int64_t)c * p.npatch + si.patch) * 27 + 9 * (dz + 1) + 4;
+                unsigned O[4];
+#pragma unroll
+                for (int cl = 0; cl < 4; ++cl) {  // class -> (dx, dy) = (sxd or 0, syd or 0)
+                    const int ddx = (cl & 1) ? sxd : 0, ddy = (cl & 2) ? syd : 0;
+                    const int2 e = tab[ddx + 3 * ddy];
+                    const int zl = e.y ? z0 - dz * p.lvl_n[2] : z0;  // the supplier's plane
+                    const int64_t shift = e.y ? (int64_t)ddx * p.lvl_n[0] + (int64_t)ddy * p.lvl_n[1] * cd.s1 : 0;
+                    O[cl] = (unsigned)e.x + (unsigned)(8 * ((int64_t)(zl - cd.lo[2]) * cd.s2 - shift));
+                }
+                const auto pb = plane_rsrc(p.lvl_base[c], zin ? p.lvl_span[c] : 0u);
+#pragma unroll
+                for (int k = 0; k < NPT; ++k) {
+                    const unsigned cl = (lsel >> (2 * k)) & 3u;
+                    const unsigned o = (cl & 2u) ? ((cl & 1u) ? O[3] : O[2]) : ((cl & 1u) ? O[1] : O[0]);
+                    v[k] = buf_ld(pb, poff[k] == OFF_NONE ? OFF_NONE : poff[k] + o);
+                }
+                return;
+            }
+        }
         const int z = zin ? image(z0, 2) : z0;
         const int zc = min(max(z, cd.lo[2]), cd.hi[2]);
         const auto pb = plane_rsrc(cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2, zin ? plane_bytes : 0u);

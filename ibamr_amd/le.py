@@ -8,6 +8,7 @@ handed to libibtk_le.so by pointer.  Arrays follow SAMRAI's Fortran layout, so a
 from __future__ import annotations
 
 import ctypes
+import math
 import sys
 from dataclasses import dataclass
 from typing import Optional, Sequence
@@ -540,6 +541,18 @@ class Level:
                                                 CENTERING[centering], axis, self._arrays(arrays), q_depth, _ptr(Q),
                                                 Q_depth, _ptr(X)))
 
+    def fill_interp(self, centering: str, arrays, Q: torch.Tensor, X: torch.Tensor, q_depth: int = 1,
+                    Q_depth: Optional[int] = None, axis: int = 0, periodic=None):
+        """`fill_ghosts` then `interp`, Q bit for bit, in one sweep that reads each ghost point in
+        the neighbour patch the fill would copy it from (ibtk_le_level_fill_interp); the two calls
+        when a component's arrays do not lie within one 2-GB window (see `alloc_level`)."""
+        if Q_depth is None:
+            Q_depth = 3 if centering in ("side", "edge") else q_depth
+        pa = _periodic_arg(periodic, 3)
+        check(self.ctx.lib.ibtk_le_level_fill_interp(self.ctx.h, self.markers.h, kernel_id(self.kernel),
+                                                     CENTERING[centering], axis, self._arrays(arrays), q_depth,
+                                                     _ptr(Q), Q_depth, _ptr(X), pa[0] if pa else None))
+
     def spread(self, centering: str, arrays, Q: torch.Tensor, X: torch.Tensor, q_depth: int = 1,
                Q_depth: Optional[int] = None, axis: int = 0):
         if Q_depth is None:
@@ -557,6 +570,26 @@ class Level:
         check(self.ctx.lib.ibtk_le_level_zero_spread(self.ctx.h, self.markers.h, kernel_id(self.kernel),
                                                      CENTERING[centering], axis, self._arrays(arrays), q_depth,
                                                      _ptr(Q), Q_depth, _ptr(X)))
+
+
+def alloc_level(geoms: Sequence[Geometry], centering: str, depth: int = 1, device="cuda"):
+    """Per-patch arrays of a level (a list per patch, as Geometry.alloc gives), each component's
+    arrays of every patch carved from one allocation: the layout ibtk_le_level_fill_interp reads
+    across patches in one window."""
+    per = [g.array_shape(centering, a, depth) for g in geoms for a in range(3 if centering in ("side", "edge") else 1)]
+    ncomp = 3 if centering in ("side", "edge") else 1
+    out = [[None] * ncomp for _ in geoms]
+    for a in range(ncomp):
+        sizes = [math.prod(per[q * ncomp + a]) for q in range(len(geoms))]
+        # 16-byte aligned slices
+        offs, tot = [], 0
+        for n in sizes:
+            offs.append(tot)
+            tot += (n + 1) // 2 * 2
+        block = torch.zeros(tot, dtype=torch.float64, device=device)
+        for q in range(len(geoms)):
+            out[q][a] = block[offs[q]:offs[q] + sizes[q]].view(per[q * ncomp + a])
+    return out
 
 
 def _periodic_arg(periodic, ndim):

@@ -279,6 +279,17 @@ int ibtk_le_level_zero(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* ge
  * patch's) or CELL (one array of depth q_depth per patch). */
 int ibtk_le_level_fill_ghosts(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms, int centering,
                               double* const* q_dev, int q_depth, const int* periodic);
+/* ibtk_le_level_fill_ghosts(m's patches, periodic) followed by ibtk_le_level_interp,
+ * Q bit for bit, in one sweep: a patch's ghost point is read in the neighbour patch the
+ * fill would copy it from (the patch owning its wrapped index, at the same global
+ * index), so no ghost value is written (across a non-periodic face, where the fill
+ * copies nothing, the patch's own ghost values are read).  Fused when, per component, every patch's array lies within one 2-GB
+ * address window (one allocation per component for the level, e.g.), the patches have
+ * at least 32 + W - 1 cells in x and 16 + W - 1 in y (W: the kernel's stencil width),
+ * and the data are SIDE or CELL of depth 1; otherwise the two calls. */
+int ibtk_le_level_fill_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
+                              double* const* q_dev, int q_depth, double* Q_dev, int Q_depth, const double* X_dev,
+                              const int* periodic);
 
 /* ---- helpers for a single periodic patch (uniform finest level) -----------------
  * Fill the ghost layers of the arrays of `centering` from the periodic interior

@@ -301,3 +301,78 @@ def test_level_zero_spread(le, ctx, kernel, clustered):
     empty.zero_spread("side", f, Fd, Xd)
     ctx.synchronize()
     assert all(not t.cpu().numpy().any() and not np.isnan(t.cpu().numpy()).any() for row in f for t in row)
+
+
+@pytest.mark.parametrize("kernel,P,centering,periodic,window", [
+    ("IB_4", 2, "side", (1, 1, 1), True), ("IB_4", 4, "side", (1, 1, 1), True),
+    ("IB_6", 2, "side", (1, 1, 1), True), ("PIECEWISE_CUBIC", 2, "side", (1, 1, 1), True),
+    ("IB_4", 2, "side", (1, 0, 1), True), ("IB_4", 4, "side", (0, 1, 0), True),
+    ("IB_4", 2, "cell", (1, 1, 1), True), ("BSPLINE_4", 2, "side", (1, 1, 0), True),
+    ("IB_4", 2, "side", (1, 1, 1), "scattered"), ("IB_4", 2, "side", (1, 1, 1), "far"),
+    ("IB_4", 4, "side", (1, 1, 1), "small")])
+def test_level_fill_interp(le, ctx, kernel, P, centering, periodic, window):
+    """ibtk_le_level_fill_interp equals ibtk_le_level_fill_ghosts then ibtk_le_level_interp,
+    Q bit for bit, and writes no array point: the fused sweep reads a ghost point in the
+    neighbour patch the fill copies it from.  Ghost points that have a neighbour are NaN in the
+    fused call's arrays (never read); across non-periodic faces, where the fill copies nothing,
+    both calls read the same values.  window "scattered": an allocation per array (still within
+one 2-GB window: fused, through the offset table); "far": patch 0's arrays more than 2 GB
+from the others (the two calls)."""
+    N = 96 if P == 2 else 192  # patches of 48 cells: the fused form
+    if window == "small":  # 12-cell patches: the two calls
+        N = 48
+    g = ora.min_ghost_width(kernel)
+    geoms = _patches(le, N, P, g)
+    rng = np.random.default_rng(7 + P)
+    M = 30_000
+    X = rng.uniform(0, 1, (M, 3))
+    Xd = torch.from_numpy(X).cuda()
+    lists_i = [(torch.from_numpy(_lists(geom, X, N, g)[0]).cuda(), None) for geom in geoms]
+    lvl = le.Level(ctx, geoms, kernel, Xd, lists_i)
+    ncomp = 3 if centering == "side" else 1
+    spacer = None
+    if window is True or window == "small":
+        a_arr = le.alloc_level(geoms, centering)
+        b_arr = le.alloc_level(geoms, centering)
+    elif window == "scattered":
+        a_arr = [geom.alloc(centering) for geom in geoms]
+        b_arr = [geom.alloc(centering) for geom in geoms]
+    else:
+        a_arr, b_arr = [geoms[0].alloc(centering)], [geoms[0].alloc(centering)]
+        spacer = torch.empty(int(2.2 * 2**30) // 8, dtype=torch.float64, device="cuda")
+        a_arr += [geom.alloc(centering) for geom in geoms[1:]]
+        b_arr += [geom.alloc(centering) for geom in geoms[1:]]
+    n = N // P
+    for q, geom in enumerate(geoms):
+        tile = [(geom.ilower[d] // n) for d in range(3)]
+        for a in range(ncomp):
+            v = rng.uniform(-1, 1, tuple(a_arr[q][a].shape))
+            a_arr[q][a].copy_(torch.from_numpy(v))
+            # the fused call's ghosts: NaN wherever a neighbour patch supplies them
+            w = v.copy()
+            shp = v.shape[-3:]  # (z, y, x) (cell data: a leading depth)
+            idx = [np.arange(shp[2 - d]) + geom.ilower[d] - g for d in range(3)]  # global index per dim (x, y, z)
+            dirs = [np.where(idx[d] < geom.ilower[d], -1, np.where(idx[d] >= geom.ilower[d] + n, 1, 0)) for d in range(3)]
+            ok = [np.where(dirs[d] == 0, True, bool(periodic[d]) |
+                           ((tile[d] + dirs[d] >= 0) & (tile[d] + dirs[d] < P))) for d in range(3)]
+            ghost = (dirs[2][:, None, None] != 0) | (dirs[1][None, :, None] != 0) | (dirs[0][None, None, :] != 0)
+            supplied = ok[2][:, None, None] & ok[1][None, :, None] & ok[0][None, None, :]
+            w[..., ghost & supplied] = np.nan
+            b_arr[q][a].copy_(torch.from_numpy(w))
+    b_before = [[t.clone() for t in per] for per in b_arr]
+    Qd = 3 if centering == "side" else 1
+    Qa = torch.full((M, Qd), np.nan, dtype=torch.float64, device="cuda")
+    Qb = torch.full_like(Qa, np.nan)
+    lvl.fill_ghosts(centering, a_arr, periodic=list(periodic))
+    lvl.interp(centering, a_arr, Qa, Xd, Q_depth=Qd)
+    lvl.fill_interp(centering, b_arr, Qb, Xd, Q_depth=Qd, periodic=list(periodic))
+    ctx.synchronize()
+    qa, qb = Qa.cpu().numpy(), Qb.cpu().numpy()
+    assert not np.isnan(qb).any(), "a NaN ghost (one a neighbour supplies) was read"
+    assert np.array_equal(qa, qb), f"max diff {np.abs(qa - qb).max()}"
+    if window not in ("far", "small"):  # (the two calls' fill writes the ghosts)
+        for per0, per1 in zip(b_before, b_arr):
+            for t0, t1 in zip(per0, per1):
+                assert torch.equal(torch.nan_to_num(t0, nan=7.0), torch.nan_to_num(t1, nan=7.0)), \
+                    "an array point was written"
+    del spacer
