@@ -200,7 +200,7 @@ struct ibtk_le_markers_s {
     DevBuf rb_cin, rb_cout, rb_d, rb_dpre, rb_mstart, rb_ps2, rb_mbits, rb_wcnt, rb_wpre, rb_mlist, rb_scr, rb_big,
         rb_nbig;
     int rb_zeroed_nb = -1;                // rb_cin / rb_cout are zero for this many buckets
-    int items_sig[8] = {-1, 0, 0, 0, 0, 0, 0, 0};  // what the item table was built with (cuts, strip, target, heavy)
+    int items_sig[12] = {-1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // what the item table was built with (cuts, strip, target, heavy)
 };
 
 static int set_device(ibtk_le_ctx ctx) {
@@ -287,6 +287,10 @@ extern "C" int ibtk_le_ctx_tune(ibtk_le_ctx ctx, const char* key, int value) {
     if (k == "seg_items") t.seg_items = value;
     else if (k == "split_target") t.split_target = value;
     else if (k == "heavy") t.heavy = value;
+    else if (k == "min_piece") t.min_piece = value;
+    else if (k == "heavy_target") t.heavy_target = value;
+    else if (k == "heavy_min_piece") t.heavy_min_piece = value;
+    else if (k == "heavy_first") t.heavy_first = value;
     else if (k == "strip") t.strip = value;
     else if (k == "xcd_block") t.xcd_block = value;
     else if (k == "fdirect") t.fdirect = value;
@@ -567,6 +571,7 @@ extern "C" int ibtk_le_markers_order(ibtk_le_markers m, const int** order_dev) {
 #ifndef IBTK_LE_STRIP
 #define IBTK_LE_STRIP 1  // column rows per strip of the sweep item order (job_column)
 #endif
+constexpr int HEAVY_TARGET_HOST = 2048;  // le_sweep.hip HEAVY_TARGET
 #ifndef IBTK_LE_SPLIT_TARGET
 #define IBTK_LE_SPLIT_TARGET 12288  // own markers per item above which it is cut (cfg4 items hold ~6.8K)
 #endif
@@ -587,7 +592,9 @@ static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const int
         for (int i = 0; i < 4; ++i)
             if (c[i] > 0 && c[i] < m->cg.nz && (p.ncut == 0 || p.cut[p.ncut - 1] != c[i])) p.cut[p.ncut++] = c[i];
     }
-    const long long bound = (long long)nj + (long long)m->n / target + 1 + (long long)p.ncut * m->cg.ncol;
+    // pieces per (column, segment) <= 1 + own markers / (the smaller of the two targets)
+    const int tmin = std::min(target, ctx->tune.heavy_target > 0 ? ctx->tune.heavy_target : HEAVY_TARGET_HOST);
+    const long long bound = (long long)nj + (long long)m->n / tmin + 1 + (long long)p.ncut * m->cg.ncol;
     if (bound * 3 >= (1LL << 31)) return fail(IBTK_LE_ERR_RANGE, "too many sweep items");
     m->item_bound = (int)bound;
     int rc;
@@ -600,6 +607,10 @@ static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const int
     p.nseg = m->nseg;
     p.njobs = nj;
     p.strip = ctx->tune.strip > 0 ? ctx->tune.strip : IBTK_LE_STRIP;
+    p.tune.min_piece = ctx->tune.min_piece;
+    p.tune.heavy_target = ctx->tune.heavy_target;
+    p.tune.heavy_min_piece = ctx->tune.heavy_min_piece;
+    p.tune.heavy_first = ctx->tune.heavy_first;
     p.plane_start = m->plane_start.as<int>();
     p.items_skip = skip_if_zero;  // a re-binning where nothing moved: the table stands
     if (m->npatch) {
@@ -617,7 +628,8 @@ static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const int
     if (ctx->tune.heavy > 0) heavy = ctx->tune.heavy;
     else if (ctx->tune.heavy < 0) heavy = INT_MAX / 2;  // off
     // a re-binning may keep the table only if it would be built the same way
-    const int sig[8] = {p.ncut, p.cut[0], p.cut[1], p.cut[2], p.cut[3], p.strip, target, heavy};
+    const int sig[12] = {p.ncut, p.cut[0], p.cut[1], p.cut[2], p.cut[3], p.strip, target, heavy, p.tune.min_piece,
+                         p.tune.heavy_target, p.tune.heavy_min_piece, p.tune.heavy_first};
     if (std::memcmp(sig, m->items_sig, sizeof(sig)) != 0) p.items_skip = nullptr;
     std::memcpy(m->items_sig, sig, sizeof(sig));
     HIP_TRY(launch_item_table(kernel, p, target, heavy, m->nsub.as<int>(), m->isub.as<int>(),
@@ -1858,17 +1870,22 @@ extern "C" int ibtk_le_level_fill_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int
         if (whi[c] - wlo[c] >= (uintptr_t(1) << 31)) return unfused();
     }
     (void)per;
-    // the 27-direction table, per component and patch
-    std::vector<int2> tab((size_t)nc * np * 27);
+    // the record per component and patch (le_sweep.hip LVL_REC): the 27 suppliers, the window
+    constexpr int REC = 32;
+    std::vector<int2> tab((size_t)nc * np * REC, make_int2(0, 0));
     for (int c = 0; c < nc; ++c)
-        for (int q = 0; q < np; ++q)
+        for (int q = 0; q < np; ++q) {
+            int2* r = tab.data() + ((size_t)c * np + q) * REC;
             for (int k = 0; k < 27; ++k) {
                 const int dir[3] = {k % 3 - 1, (k / 3) % 3 - 1, k / 9 - 1};
                 const int sq = k == 13 ? -1 : level_neighbour(t, tile_of, patch_of, q, dir);
                 const CompDesc& src = m->pdh[sq >= 0 ? sq : q].comp[c];
-                tab[((size_t)c * np + q) * 27 + k] =
-                    make_int2((int)(reinterpret_cast<uintptr_t>(src.u) - wlo[c]), sq >= 0 ? 1 : 0);
+                r[k] = make_int2((int)(reinterpret_cast<uintptr_t>(src.u) - wlo[c]), sq >= 0 ? 1 : 0);
             }
+            const uint64_t b = (uint64_t)wlo[c];
+            r[27] = make_int2((int)(unsigned)(b & 0xffffffffu), (int)(unsigned)(b >> 32));
+            r[28] = make_int2((int)(unsigned)(whi[c] - wlo[c]), 0);
+        }
     if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
     const size_t bytes = sizeof(int2) * tab.size();
     if (int rc = m->lvl_nbr.ensure(bytes)) return rc;
@@ -1877,10 +1894,6 @@ extern "C" int ibtk_le_level_fill_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int
         HIP_TRY(hipMemcpyAsync(m->lvl_nbr.p, m->lvl_nbr_host.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
     }
     p.lvl_nbr = m->lvl_nbr.as<int2>();
-    for (int c = 0; c < nc; ++c) {
-        p.lvl_base[c] = reinterpret_cast<const double*>(wlo[c]);
-        p.lvl_span[c] = (unsigned)(whi[c] - wlo[c]);
-    }
     for (int d = 0; d < 3; ++d) p.lvl_n[d] = t.n[d];
     if (m->qin_valid) {
         p.qdst = m->qin.as<int>();

@@ -109,6 +109,10 @@ struct SweepTune {
     int strip = 0;         // column rows per strip of the item order (0: default)
     int xcd_block = 0;     // light sweep items over the XCDs in blocks of this many table entries (1:
                            // round-robin; -1: one contiguous range per XCD; 0: the default, 8)
+    int min_piece = 0;     // planes per sub-segment of a cut item, at least (0: the default, 8)
+    int heavy_target = 0;  // a heavy item's pieces: own markers per piece (0: the default, le_sweep.hip HEAVY_TARGET)
+    int heavy_min_piece = 0;  // ... and planes per piece, at least (0: HEAVY_MIN_PIECE)
+    int heavy_first = 0;   // heavy items head the table (0, the default) or keep their place (-1)
     int fdirect = 0;       // 3-D spread: 1 = the candidates read F through the sorted marker index instead
                            // of the gather pass k_gather_F_col (diagnostic: slower, profiles/r04c)
 };
@@ -188,12 +192,11 @@ struct Params {
     // 3-D level interp with the level's ghost fill fused in (ibtk_le_level_fill_interp): a
     // ghost point is read where the fill would copy it from -- the neighbour patch owning
     // its cell (27 directions), at the same global index.  Component c's arrays of every
-    // patch lie in one 32-bit window from lvl_base[c] (lvl_span[c] bytes); lvl_nbr[(c *
-    // npatch + q) * 27 + dir] = {byte offset of the supplying array in that window, 1 if
-    // it is the neighbour in dir (index mapped by -dir n), 0 if none (own array, as is)}.
+    // patch lie in one window below 2 GB; record (c * npatch + q) of lvl_nbr (32 int2):
+    // [dir] = {byte offset of the supplying array in the window, 1 if it is the neighbour
+    // in dir (index mapped by -dir n), 0 if none (own array, as is)}, [27] = the window's
+    // base (lo, hi), [28].x = its length in bytes.
     const int2* lvl_nbr = nullptr;
-    const double* lvl_base[MAXC] = {};
-    unsigned lvl_span[MAXC] = {};
     int lvl_n[3] = {0, 0, 0};  // cells per patch and dim
 };
 

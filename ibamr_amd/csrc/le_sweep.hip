@@ -840,8 +840,22 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
 // pooled markers.  Points outside the component's array are staged as 0.  One
 // lane per marker sums its W^3 stencil from the ring (Fortran loop order,
 // bitwise the oracle's).
-template <int K, bool LVL>
+// ibtk_le_level_fill_interp's record per (component, patch): 27 suppliers {window offset,
+// mapped}, then the window base (lo, hi 32 bits) and its length in bytes
+constexpr int LVL_REC = 32;
+// the plane-independent part of a staged point's offset for class (dx, dy) at plane
+// direction dz (k_interp_sweep, LF): the supplier's window offset less its index shift
+__device__ __forceinline__ unsigned lvl_class(const int2* tab, int dx, int dy, int dz, int n0, int n1, int n2,
+                                              int64_t s1, int64_t s2) {
+    const int2 e = tab[dx + 3 * dy + 9 * dz];
+    const int64_t shift = e.y ? (int64_t)dx * n0 + (int64_t)dy * n1 * s1 + (int64_t)dz * n2 * s2 : 0;
+    return (unsigned)e.x - (unsigned)(8 * shift);
+}
+// LF: a level with its ghost fill fused in (p.lvl_nbr; a kernel of its own, so that the
+// plain level sweep keeps its registers)
+template <int K, bool LVL, bool LF = false>
 __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
+    static_assert(LVL || !LF, "the fused fill is a level's");
     using S = ISh<K>;
     constexpr int LO = S::LO, HI = S::HI, RX = S::RX, NPT = S::NPT;
     __shared__ double ring[S::NSL * S::PVP];
@@ -902,13 +916,37 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     // point's class is 2 bits (beyond the x face, beyond the y face), and per plane four
     // uniform offsets, one per class, turn its unmapped offset poff[k] into the supplier's
     // (the neighbour's window offset, the -dir n index shift, the plane)
-    const bool lfill = LVL && p.lvl_nbr != nullptr;
+    constexpr bool lfill = LF;
     unsigned lsel = 0;  // bits 2k, 2k+1: the class of point k
+    // per plane direction dz and class: the plane-independent part of the class offset
+    // (the supplier's window offset, its x/y/z index shift), read once per item
+    // (named scalars, not arrays: an array selected by class or plane direction would go to scratch)
+    struct Cls {
+        unsigned o0, o1, o2, o3;
+    };
+    Cls ob_m{}, ob_0{}, ob_p{};
+    const double* lbase = nullptr;  // the component's level window
+    unsigned lspan = 0;
     int sxd = 0, syd = 0;
-    if constexpr (LVL) {
-        if (lfill) {
+    if constexpr (LF) {
+        {
             sxd = gx0 < cd.ilower[0] ? -1 : (gx0 + RX - 1 >= cd.ilower[0] + p.lvl_n[0] ? 1 : 0);
             syd = gy0 < cd.ilower[1] ? -1 : (gy0 + S::RY - 1 >= cd.ilower[1] + p.lvl_n[1] ? 1 : 0);
+            const int2* rec = p.lvl_nbr + ((int64_t)c * p.npatch + si.patch) * LVL_REC;
+            const int2* tab = rec + 13;
+            const int n0 = p.lvl_n[0], n1 = p.lvl_n[1], n2 = p.lvl_n[2];
+            const int64_t s1 = cd.s1, s2 = cd.s2;
+            ob_m = Cls{lvl_class(tab, 0, 0, -1, n0, n1, n2, s1, s2), lvl_class(tab, sxd, 0, -1, n0, n1, n2, s1, s2),
+                       lvl_class(tab, 0, syd, -1, n0, n1, n2, s1, s2), lvl_class(tab, sxd, syd, -1, n0, n1, n2, s1, s2)};
+            ob_0 = Cls{lvl_class(tab, 0, 0, 0, n0, n1, n2, s1, s2), lvl_class(tab, sxd, 0, 0, n0, n1, n2, s1, s2),
+                       lvl_class(tab, 0, syd, 0, n0, n1, n2, s1, s2), lvl_class(tab, sxd, syd, 0, n0, n1, n2, s1, s2)};
+            ob_p = Cls{lvl_class(tab, 0, 0, 1, n0, n1, n2, s1, s2), lvl_class(tab, sxd, 0, 1, n0, n1, n2, s1, s2),
+                       lvl_class(tab, 0, syd, 1, n0, n1, n2, s1, s2), lvl_class(tab, sxd, syd, 1, n0, n1, n2, s1, s2)};
+            // the window from the record (an index by component into the kernel arguments would
+            // copy them to scratch)
+            const int2 wb = rec[27], ws = rec[28];
+            lbase = reinterpret_cast<const double*>(((uint64_t)(unsigned)wb.y << 32) | (unsigned)wb.x);
+            lspan = (unsigned)ws.x;
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
                 const int q = min(lane + SW * k, S::PV - 1);
@@ -922,27 +960,24 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     const int plast = a1 - 1 + HI;  // last plane the item reads
     const unsigned plane_bytes = (unsigned)(8 * cd.s2);
     // relative plane zr -> registers
-    auto plane_load = [&](int zr, double* v) {
+    auto plane_load = [&](int zr, double* v) __attribute__((always_inline)) {  // (inlined: a call would take p's address)
         const int z0 = zorg + min(zr, plast);
         const bool zin = z0 >= cd.lo[2] && z0 <= cd.hi[2];
-        if constexpr (LVL) {
-            if (lfill) {  // one resource over the component's level window
+        if constexpr (LF) {
+            {  // one resource over the component's level window
                 const int dz = z0 < cd.ilower[2] ? -1 : (z0 >= cd.ilower[2] + p.lvl_n[2] ? 1 : 0);
-                const int2* tab = p.lvl_nbr + ((int64_t)c * p.npatch + si.patch) * 27 + 9 * (dz + 1) + 4;
-                unsigned O[4];
-#pragma unroll
-                for (int cl = 0; cl < 4; ++cl) {  // class -> (dx, dy) = (sxd or 0, syd or 0)
-                    const int ddx = (cl & 1) ? sxd : 0, ddy = (cl & 2) ? syd : 0;
-                    const int2 e = tab[ddx + 3 * ddy];
-                    const int zl = e.y ? z0 - dz * p.lvl_n[2] : z0;  // the supplier's plane
-                    const int64_t shift = e.y ? (int64_t)ddx * p.lvl_n[0] + (int64_t)ddy * p.lvl_n[1] * cd.s1 : 0;
-                    O[cl] = (unsigned)e.x + (unsigned)(8 * ((int64_t)(zl - cd.lo[2]) * cd.s2 - shift));
-                }
-                const auto pb = plane_rsrc(p.lvl_base[c], zin ? p.lvl_span[c] : 0u);
+                const unsigned zo = (unsigned)(8 * (int64_t)(z0 - cd.lo[2]) * cd.s2);
+                // the row of dz by masks (a select chain here becomes a table in scratch)
+                const unsigned mm = 0u - (unsigned)(dz < 0), mp = 0u - (unsigned)(dz > 0), m0 = ~(mm | mp);
+                const unsigned O0 = ((ob_m.o0 & mm) | (ob_0.o0 & m0) | (ob_p.o0 & mp)) + zo;
+                const unsigned O1 = ((ob_m.o1 & mm) | (ob_0.o1 & m0) | (ob_p.o1 & mp)) + zo;
+                const unsigned O2 = ((ob_m.o2 & mm) | (ob_0.o2 & m0) | (ob_p.o2 & mp)) + zo;
+                const unsigned O3 = ((ob_m.o3 & mm) | (ob_0.o3 & m0) | (ob_p.o3 & mp)) + zo;
+                const auto pb = plane_rsrc(lbase, zin ? lspan : 0u);
 #pragma unroll
                 for (int k = 0; k < NPT; ++k) {
                     const unsigned cl = (lsel >> (2 * k)) & 3u;
-                    const unsigned o = (cl & 2u) ? ((cl & 1u) ? O[3] : O[2]) : ((cl & 1u) ? O[1] : O[0]);
+                    const unsigned o = (cl & 2u) ? ((cl & 1u) ? O3 : O2) : ((cl & 1u) ? O1 : O0);
                     v[k] = buf_ld(pb, poff[k] == OFF_NONE ? OFF_NONE : poff[k] + o);
                 }
                 return;
@@ -1682,12 +1717,33 @@ __device__ __forceinline__ int job_column(const ColGeom& cg, int i, int strip) {
 // load-based sub-segments of (column col, planes [a0, a1))
 template <int K>
 __device__ __forceinline__ int load_split(const ColGeom& cg, const int* bs, int col, int a0, int a1, int target,
-                                          long& load) {
+                                          int min_piece, long& load) {
     constexpr int NS = KT<K>::HI - KT<K>::LO + 1;
     load = 0;
     for (int a = a0; a < a1; ++a) load += bs[bucket(cg, a, col, NBAND)] - bs[bucket(cg, a, col, 0)];
-    const int maxsub = max((a1 - a0) / max(NS, 8), 1);
+    const int maxsub = max((a1 - a0) / max(NS, min_piece > 0 ? min_piece : 8), 1);
     return (int)min((long)maxsub, max(1L, (load + target - 1) / target));
+}
+// The pieces of (column col, planes [a0, a1)) and whether they are heavy (own markers
+// per piece above `heavy`: scheduled first).  A heavy (column, segment) -- clustered
+// markers: a fibre bundle along the column, a sheet across it -- is cut finer, down to
+// HEAVY_TARGET own markers and one plane per piece: its pieces are the sweeps' tail
+// (cfg5: the spread's longest items were as long as the rest of the launch).  Uniform
+// markers never qualify, so their items are unchanged.
+constexpr int HEAVY_TARGET = 2048, HEAVY_MIN_PIECE = 1;
+template <int K>
+__device__ __forceinline__ int item_pieces(const Params& p, const ColGeom& cg, const int* bs, int col, int a0, int a1,
+                                           int target, int heavy, long& load, bool& hv) {
+    int n = load_split<K>(cg, bs, col, a0, a1, target, p.tune.min_piece, load);
+    hv = load > (long)heavy * n;
+    if (hv) {
+        const int ht = p.tune.heavy_target > 0 ? p.tune.heavy_target : HEAVY_TARGET;
+        const int hm = p.tune.heavy_min_piece > 0 ? p.tune.heavy_min_piece : HEAVY_MIN_PIECE;
+        long l2;
+        n = max(n, load_split<K>(cg, bs, col, a0, a1, ht, hm, l2));
+        if (p.tune.heavy_first < 0) hv = false;  // cut finer, but in table order
+    }
+    return n;
 }
 // the plane cuts (ibtk_le_ctx_set_plane_window: sorted, relative) strictly inside (b0, b1)
 __device__ __forceinline__ int cuts_inside(const Params& p, int b0, int b1) {
@@ -1711,11 +1767,11 @@ __global__ __launch_bounds__(BLOCK) void k_item_counts(Params p, int target, int
     const int seg = jl / cg.ncol, col = job_column(cg, jl - seg * cg.ncol, p.strip);
     const int a0 = seg * S, a1 = min(a0 + S, cg.nz), len = a1 - a0;
     long load;
-    const int n = load_split<K>(cg, bs, col, a0, a1, target, load);
+    bool hv;
+    const int n = item_pieces<K>(p, cg, bs, col, a0, a1, target, heavy, load, hv);
     int pieces = n;
     if (p.ncut)
         for (int k = 0; k < n; ++k) pieces += cuts_inside(p, a0 + (len * k) / n, a0 + (len * (k + 1)) / n);
-    const bool hv = load > (long)heavy * n;
     nsub[j] = hv ? 0 : pieces;
     nsub[p.njobs + j] = hv ? pieces : 0;
 }
@@ -1733,10 +1789,10 @@ __global__ __launch_bounds__(BLOCK) void k_item_write(Params p, int target, int 
     const int seg = jl / cg.ncol, col = job_column(cg, jl - seg * cg.ncol, p.strip);
     const int a0 = seg * S, a1 = min(a0 + S, cg.nz), len = a1 - a0;
     long load;
-    const int n = load_split<K>(cg, bs, col, a0, a1, target, load);
+    bool hv;
+    const int n = item_pieces<K>(p, cg, bs, col, a0, a1, target, heavy, load, hv);
     const int nj = p.njobs;
     const int nheavy = start[2 * nj - 1] + nsub[2 * nj - 1];
-    const bool hv = load > (long)heavy * n;
     int w = hv ? start[nj + j] : nheavy + start[j];
     for (int k = 0; k < n; ++k) {
         int b0 = a0 + (len * k) / n;
@@ -1803,7 +1859,8 @@ hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent
     const long items = (long)p.item_bound * p.ncomp;
     if (items > 0) {
         const dim3 g(sweep_grid(p, items)), b(SW * IWAVES);
-        if (p.pd) hipLaunchKernelGGL((k_interp_sweep<K, true>), g, b, 0, s, p);
+        if (p.pd && p.lvl_nbr) hipLaunchKernelGGL((k_interp_sweep<K, true, true>), g, b, 0, s, p);
+        else if (p.pd) hipLaunchKernelGGL((k_interp_sweep<K, true>), g, b, 0, s, p);
         else hipLaunchKernelGGL((k_interp_sweep<K, false>), g, b, 0, s, p);
     }
     if (ev1) (void)hipEventRecord(ev1, s);

@@ -518,7 +518,9 @@ int ibtk_le_ctx_enable_timing(ibtk_le_ctx ctx, int enable);
  * item is scheduled first; -1 never; default 4x the mean, at least 2048),
  * "seg_items" (target number of (column, segment)
  * items, which sets the segment length), "split_target" (own markers above
- * which a (column, segment) is cut into sub-segments), "strip" (column rows per
+ * which a (column, segment) is cut into sub-segments), "min_piece" (planes per
+ * sub-segment of a cut item, at least; default 8), "heavy_target" and
+ * "heavy_min_piece" (the same for heavy items; defaults 2048 and 1), "strip" (column rows per
  * strip of the item order), "xcd_block" (light items over the XCDs in blocks of
  * this many table entries: 1 round-robin, -1 one range per XCD; default 8).
  * Interp results do not depend on them; spread results are bit-stable for fixed
