@@ -1016,14 +1016,21 @@ hipError_t launch_slab_update_partition(int scheme, long M, double dt, const dou
 // ---------------------------------------------------------------------------
 // a level's interp on its interior lists, from the binned ghost-box lists
 // ---------------------------------------------------------------------------
+// the patch of entry l (off: npatch + 1 offsets); the wave's first entry's patch
+// is searched once (scalar loads) and kept for the lanes in it (a wave's entries are
+// mostly of one patch)
 __device__ __forceinline__ int patch_of_entry(const int* off, int npatch, int l) {
-    int lo = 0, hi = npatch - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (off[mid] <= l) lo = mid;
-        else hi = mid - 1;
-    }
-    return lo;
+    auto search = [&](int v) {
+        int lo = 0, hi = npatch - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (off[mid] <= v) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    };
+    const int q = search(__builtin_amdgcn_readfirstlane(l));
+    return (off[q] <= l && l < off[q + 1]) ? q : search(l);
 }
 __global__ __launch_bounds__(BLOCK) void k_interior_owner(const int* int_off, int npatch, const int* int_idx, int n_int,
                                                           int n_markers, int* owner, int* err) {

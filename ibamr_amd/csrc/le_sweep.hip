@@ -104,15 +104,22 @@ __device__ __forceinline__ bool col_key_cell(const double* xlo, const double* dx
     return in;
 }
 
-// The patch of list entry l of a level (binary search of the entry offsets).
+// The patch of list entry l of a level (binary search of the entry offsets).  A
+// wave's entries are mostly of one patch (the sorted order is patch-major): the
+// search runs once on the first lane's entry, with scalar loads, and a lane outside
+// that patch searches on its own.
 __device__ __forceinline__ int entry_patch(const Params& p, int l) {
-    int lo = 0, hi = p.npatch - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (p.entry_off[mid] <= l) lo = mid;
-        else hi = mid - 1;
-    }
-    return lo;
+    auto search = [&](int v) {
+        int lo = 0, hi = p.npatch - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (p.entry_off[mid] <= v) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    };
+    const int q = search(__builtin_amdgcn_readfirstlane(l));
+    return (p.entry_off[q] <= l && l < p.entry_off[q + 1]) ? q : search(l);
 }
 
 // band of a key cell in its column: xb = 0 if its stencil reaches the x-1
