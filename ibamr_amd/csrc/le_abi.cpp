@@ -572,16 +572,17 @@ extern "C" int ibtk_le_markers_order(ibtk_le_markers m, const int** order_dev) {
 #define IBTK_LE_STRIP 1  // column rows per strip of the sweep item order (job_column)
 #endif
 constexpr int HEAVY_TARGET_HOST = 2048;  // le_sweep.hip HEAVY_TARGET
-constexpr int LEVEL_SPLIT_TARGET = 2048;
+constexpr int LEVEL_SPLIT_TARGET = 1024;
 #ifndef IBTK_LE_SPLIT_TARGET
 #define IBTK_LE_SPLIT_TARGET 12288  // own markers per item above which it is cut (cfg4 items hold ~6.8K)
 #endif
 static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const int* skip_if_zero = nullptr) {
     const int nj = m->npatch ? m->njobs : m->cg.ncol * m->nseg;
     // a level's items (patches of a few 32-plane segments, clustered markers on a few of
-    // them) are cut at 2048 own markers, one plane per piece at least: cfg5 3.9e9 -> 4.06e9
-    // marker-ops/s; a single patch keeps 12288 and 8 planes (cut that fine, cfg4's uniform
-    // items lose 6 %: 7.04e9 -> 6.62e9, profiles/r04q, r04r)
+    // them) are cut at 1024 own markers, one plane per piece at least: cfg5 3.9e9 -> 4.1e9
+    // (2048) -> 4.23e9 (1024; 512 and 256 are slower again, 4096 3.95e9; profiles/r04v, r04w);
+    // a single patch keeps 12288 and 8 planes (cut that fine, cfg4's uniform items lose 6 %:
+    // 7.04e9 -> 6.62e9, profiles/r04q, r04r)
     const int target = ctx->tune.split_target > 0 ? ctx->tune.split_target
                                                   : (m->npatch ? LEVEL_SPLIT_TARGET : IBTK_LE_SPLIT_TARGET);
     Params p;
