@@ -1668,8 +1668,26 @@ extern "C" int ibtk_le_level_select_interior(ibtk_le_ctx ctx, ibtk_le_markers m,
     HIP_TRY(hipMemsetAsync(ctx->counts.p, 0, sizeof(int) * (size_t)nblk, s));
     HIP_TRY(launch_interior_owner(m->int_off.as<int>(), np, interior_indices_dev, n_int, n_markers, m->owner.as<int>(),
                                   ctx->err.as<int>(), s));
+    // An entry of patch q's list whose marker q owns is a periodic image only if the image
+    // (a whole period away) lies in q's ghost box as well: impossible when the level spans
+    // more than any patch's ghost box in every dim (a period is at least the level's extent),
+    // and then the Xshift rows (a 24-byte gather per entry) need not be read
+    bool need_shift = m->has_xshift;
+    if (need_shift) {
+        bool wide = true;
+        for (int d = 0; d < 3 && wide; ++d) {
+            int lo = INT_MAX, hi = INT_MIN, gb = 0;
+            for (const ibtk_le_patch_geom& g : m->geoms) {
+                lo = std::min(lo, g.ilower[d]);
+                hi = std::max(hi, g.iupper[d]);
+                gb = std::max(gb, g.iupper[d] - g.ilower[d] + 2 + 2 * g.gcw[d]);  // ghost box (+ a face)
+            }
+            wide = hi - lo + 1 > gb;
+        }
+        need_shift = !wide;
+    }
     HIP_TRY(launch_interior_targets(m->sorted_l.as<int>(), m->sorted_s.as<int>(), m->entry_off.as<int>(), np,
-                                    m->has_xshift ? m->xshift.as<double>() : nullptr, m->owner.as<int>(), n_markers,
+                                    need_shift ? m->xshift.as<double>() : nullptr, m->owner.as<int>(), n_markers,
                                     m->n, m->qin.as<int>(), ctx->counts.as<int>(), ctx->err.as<int>(), s));
     HIP_TRY(launch_check_count(ctx->counts.as<int>(), m->n > 0 ? nblk : 0, n_int, ctx->err.as<int>(), 4, s));
     m->qin_valid = true;
