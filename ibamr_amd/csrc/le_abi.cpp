@@ -498,6 +498,8 @@ static int make_comps(const ibtk_le_patch_geom* g, int centering, int axis, doub
             }
         }
         cd.zcell = (nd == 3 && !((shift_mask >> 2) & 1)) ? 1 : 0;
+        cd.xcell = !(shift_mask & 1) ? 1 : 0;
+        cd.ycell = (nd >= 2 && !((shift_mask >> 1) & 1)) ? 1 : 0;
         int64_t sd;
         array_strides(g, n, cd.s1, cd.s2, sd);
         cd.u = base + (int64_t)depth_index * sd;

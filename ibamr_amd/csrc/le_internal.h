@@ -58,6 +58,7 @@ struct CompDesc {
     int qcomp;       // which AoS component of Q this array pairs with
     int axis;        // `axis` argument (DISCONTINUOUS_LINEAR)
     int zcell;       // 3-D: the z frame is the cell frame of the bin keys (not shifted by dx/2)
+    int xcell, ycell;  // 3-D: likewise the x and y frames
     int64_t s1, s2;  // strides of dims 1 and 2 (elements)
 };
 

@@ -760,7 +760,9 @@ __device__ __forceinline__ double interp_marker(const Params& p, const CompDesc&
     // ring (FAM 0 reads all W per dim, clipped ones as staged zeros)
     bool ok;
     if constexpr (FAM == 0) {
-        ok = ox >= 0 && ox + W <= RX && oy >= 0 && oy + W <= S::RY && oz >= a + S::LO && oz + W - 1 <= a + S::HI;
+        // (a cell-frame dim's last staged index is not loaded: k_interp_sweep's poff)
+        ok = ox >= 0 && ox + W <= RX - cd.xcell && oy >= 0 && oy + W <= S::RY - cd.ycell && oz >= a + S::LO &&
+             oz + W - 1 <= a + S::HI;
     } else {
         bool empty = false;
 #pragma unroll
@@ -909,12 +911,19 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
         int r = (i - cd.ilower[d]) % n;
         return cd.ilower[d] + (r < 0 ? r + n : r);
     };
+    // The closed-form kernels (FAM 0) read, in a dim where the component's frame is the keys'
+    // (cell) frame, only the staged indices [0, RX - 2] (x) / [0, RY - 2] (y): the stencil of
+    // key k spans k + [LO, HI - 1] there (the spread's ZC ring rests on the same fact in z).
+    // Such a component's last staged column / row is not loaded (staged as 0, never read).
+    const bool xlast = S::FAM == 0 && cd.xcell, ylast = S::FAM == 0 && cd.ycell;
     unsigned poff[NPT];
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
         const int q = min(lane + SW * k, S::PV - 1);
-        const int gx = gx0 + q % RX, gy = gy0 + q / RX;
-        const bool in = gx >= cd.lo[0] && gx <= cd.hi[0] && gy >= cd.lo[1] && gy <= cd.hi[1];
+        const int qx = q % RX, qy = q / RX;
+        const int gx = gx0 + qx, gy = gy0 + qy;
+        const bool in = gx >= cd.lo[0] && gx <= cd.hi[0] && gy >= cd.lo[1] && gy <= cd.hi[1] &&
+                        !(xlast && qx == RX - 1) && !(ylast && qy == S::RY - 1);
         poff[k] = in ? 8u * (unsigned)((image(gx, 0) - cd.lo[0]) + (image(gy, 1) - cd.lo[1]) * (int)cd.s1) : OFF_NONE;
     }
     // level fill fused (p.lvl_nbr, LVL only): a staged point outside the patch box is read
