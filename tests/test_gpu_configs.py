@@ -323,7 +323,19 @@ def _slab_run(le, ctx, N, M, world, rank, kernel="IB_4", move=False, overlap=Fal
         m = le.Markers(ctx).bin(geom, kernel, X)
     f = geom.alloc("side")
     le.zero_ghosts(ctx, geom, "side", f)
-    if mode == "markers" and world > 1:
+    if mode == "zero":
+        # the bench's default: f as LDataManager::spread hands it over (zeroed, ghosts
+        # included) in the spread's own sweep (ibtk_le_zero_spread); f starts as NaN here,
+        # so every point must be written
+        for t in f:
+            t.fill_(float("nan"))
+        zs = lambda: le.zero_spread(ctx, m, kernel, "side", geom, f, F, X)
+        if overlap:
+            SlabExchange(slab, f, ctx).ghost_sum(zs)
+        else:
+            zs()
+            SlabExchange(slab, f, ctx).ghost_sum()
+    elif mode == "markers" and world > 1:
         # the reference's exchange: ghost markers in, the own planes kept, x/y folded
         Xa, Fa, _ = GhostMarkers(slab).exchange(X, F)
         ma = le.Markers(ctx).bin(geom, kernel, Xa)
@@ -350,6 +362,8 @@ def _slab_worker(rank, world, port, N, M, move, out_q, mode="sum"):
         from ibamr_amd import le
         ctx = le.Context(0)
         ids, U, fin, z0, nz = _slab_run(le, ctx, N, M, world, rank, move=move, mode=mode)
+        if mode == "zero":
+            assert not any(np.isnan(t).any() for t in fin), f"rank {rank}: a point of f was not written"
         if mode == "markers":
             # bit-stable on a repeat
             ids2, U2, fin2, _, _ = _slab_run(le, ctx, N, M, world, rank, move=move, mode=mode)
@@ -358,7 +372,7 @@ def _slab_worker(rank, world, port, N, M, move, out_q, mode="sum"):
         elif not move:
             # the overlapped form (cut items, two half-sweeps around each exchange)
             # must give the same bits
-            ids2, U2, fin2, _, _ = _slab_run(le, ctx, N, M, world, rank, move=move, overlap=True)
+            ids2, U2, fin2, _, _ = _slab_run(le, ctx, N, M, world, rank, move=move, overlap=True, mode=mode)
             assert np.array_equal(ids2, ids) and np.array_equal(U2, U), f"rank {rank}: overlapped interp differs"
             for c in range(3):
                 assert np.array_equal(fin2[c], fin[c]), f"rank {rank}: overlapped spread comp {c} differs"
@@ -372,7 +386,7 @@ def _slab_worker(rank, world, port, N, M, move, out_q, mode="sum"):
 
 @pytest.mark.parametrize("world,move,mode", [(2, False, "sum"), (4, False, "sum"), (8, False, "sum"), (2, True, "sum"),
                                              (4, True, "sum"), (2, False, "markers"), (4, False, "markers"),
-                                             (4, True, "markers")])
+                                             (4, True, "markers"), (2, False, "zero"), (4, True, "zero")])
 def test_cfg4_slab_split_matches_one_rank(le, ctx, world, move, mode):
     import torch.multiprocessing as mp
     N, M = 64, 150_000
