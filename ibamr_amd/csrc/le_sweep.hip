@@ -1223,9 +1223,9 @@ struct Cand {
 };
 
 // w[s] <- w[(s + r) & 3] for s < 4 (a two-stage barrel of selects)
-__device__ __forceinline__ void rot4(double* w, int r) {
+template <typename T> __device__ __forceinline__ void rot4(T* w, int r) {
     const bool b0 = r & 1, b1 = r & 2;
-    const double c0 = b0 ? w[1] : w[0], c1 = b0 ? w[2] : w[1], c2 = b0 ? w[3] : w[2], c3 = b0 ? w[0] : w[3];
+    const T c0 = b0 ? w[1] : w[0], c1 = b0 ? w[2] : w[1], c2 = b0 ? w[3] : w[2], c3 = b0 ? w[0] : w[3];
     w[0] = b1 ? c2 : c0;
     w[1] = b1 ? c3 : c1;
     w[2] = b1 ? c0 : c2;
@@ -1239,8 +1239,14 @@ __device__ __forceinline__ void rot4(double* w, int r) {
 // (mod 4) -- a rotation of its stencil's first four columns and rows by
 // (jx - ox) and (jy - oy) mod 4 -- so the 16 lanes of every lane group hit the
 // 16 bank classes once each, in every instruction, wherever the stencils lie
-// (no ranking or dealing of the candidates).  Wider stencils (IB_6, IB_4_W8)
-// take their further columns and rows unrotated; narrower ones unrotated.
+// (no ranking or dealing of the candidates).  IB_6 adds its 6 x 6 plane in 40
+// steps (tiled6): the rotated 4 x 4 first, then a second rotated round in which
+// the step of relative class (cx, cy) takes the point (cx + 4, cy) for cx < 2,
+// (cx, cy + 4) for cx >= 2 > cy, and a weight-0 add for cx, cy >= 2 -- conflict-free
+// as the first, since a stencil column cx + 4 has the bank class of column cx --
+// and last the 8 points of rows 4, 5 and columns {0, 1, 4, 5}, whose classes
+// repeat (so 8 of 40 adds can conflict, against 20 of 36 unrotated).  IB_4_W8
+// takes its further columns and rows unrotated; narrower stencils unrotated.
 // A stencil point that is clipped (outside the ghost box) or not owned (outside
 // the column, or in a neighbour item's planes) is added with weight 0 at its
 // position wrapped into the column (a +0 on an owned point of the same class),
@@ -1292,43 +1298,98 @@ __device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd
         wy[i] = (i >= y0 && i <= y1) ? st[1].w[i] : 0.0;
         wz[i] = st[2].w[i] * inv_h3;  // planes outside [z0, z1] are skipped below
     }
-    int rx = 0, ry = 0;
-    if constexpr (ROT) {
+    // byte offsets in a slot of stencil column / row s: the x and y parts of
+    // ring_wrapped
+    auto xpart = [&](int s) {
+        const int xw = (ox + s) & (COLX - 1);
+        return 8 * (16 * (xw >> 2) + (xw & 3));
+    };
+    auto ypart = [&](int s) {
+        const int yw = (((oy + s) % COLY) + COLY) % COLY;
+        return 8 * (16 * (COLX / 4) * (yw >> 2) + 4 * (yw & 3));
+    };
+    // the plane's adds: products of the x and y weights and the byte offsets of
+    // their points in a slot, in issue order
+    constexpr int NA = W == 6 ? 40 : W * W;
+    int off[NA];
+    double P[NA];
+    if constexpr (W == 6) {  // tiled6 (see above)
         const int lane = lane_id();
-        rx = ((lane & 3) - ox) & 3;
-        ry = (((lane >> 2) & 3) - oy) & 3;
+        const int jx = lane & 3, jy = (lane >> 2) & 3;
+        const int rx = (jx - ox) & 3, ry = (jy - oy) & 3;
+        int bxa[6], bya[6];
+#pragma unroll
+        for (int s = 0; s < 6; ++s) {
+            bxa[s] = xpart(s);
+            bya[s] = ypart(s);
+        }
+        // round 3: columns {0, 1, 4, 5} turned by jx, rows {4, 5} by jy (a partial spread)
+        double x3[4] = {wx[0], wx[1], wx[4], wx[5]};
+        int bx3[4] = {bxa[0], bxa[1], bxa[4], bxa[5]};
+        rot4(x3, jx);
+        rot4(bx3, jx);
+        const bool sy = jy & 1;
+        const double y3[2] = {sy ? wy[5] : wy[4], sy ? wy[4] : wy[5]};
+        const int by3[2] = {sy ? bya[5] : bya[4], sy ? bya[4] : bya[5]};
+        // rounds 1 and 2: entry s of a rotated vector is relative class (s + r) & 3
+        double x4[4] = {wx[4], wx[5], 0.0, 0.0}, y4[4] = {wy[4], wy[5], 0.0, 0.0};
+        int bx4[4] = {bxa[4], bxa[5], bxa[2], bxa[3]}, by4[4] = {bya[4], bya[5], bya[2], bya[3]};
+        int bxr[4] = {bxa[0], bxa[1], bxa[2], bxa[3]}, byr[4] = {bya[0], bya[1], bya[2], bya[3]};
         rot4(wx, rx);
+        rot4(x4, rx);
+        rot4(bx4, rx);
+        rot4(bxr, rx);
         rot4(wy, ry);
-    }
-    // byte offsets in a slot of the points of step (s0, s1): the x and y parts
-    // of ring_wrapped, summed
-    int off[W * W];
-    {
+        rot4(y4, ry);
+        rot4(by4, ry);
+        rot4(byr, ry);
+#pragma unroll
+        for (int s1 = 0; s1 < 4; ++s1)
+#pragma unroll
+            for (int s0 = 0; s0 < 4; ++s0) {
+                const int k = 4 * s1 + s0;
+                P[k] = wx[s0] * wy[s1];
+                off[k] = bxr[s0] + byr[s1];
+                const bool lo = ((s0 + rx) & 3) < 2;  // cx < 2: column cx + 4, row cy
+                P[16 + k] = lo ? x4[s0] * wy[s1] : wx[s0] * y4[s1];
+                off[16 + k] = lo ? bx4[s0] + byr[s1] : bxr[s0] + by4[s1];
+            }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                P[32 + 4 * u + t] = x3[t] * y3[u];
+                off[32 + 4 * u + t] = bx3[t] + by3[u];
+            }
+    } else {
+        int rx = 0, ry = 0;
+        if constexpr (ROT) {
+            const int lane = lane_id();
+            rx = ((lane & 3) - ox) & 3;
+            ry = (((lane >> 2) & 3) - oy) & 3;
+            rot4(wx, rx);
+            rot4(wy, ry);
+        }
         int bx[W], by[W];
 #pragma unroll
         for (int s = 0; s < W; ++s) {
-            const int xw = (ox + ((ROT && s < 4) ? ((s + rx) & 3) : s)) & (COLX - 1);
-            const int yv = oy + ((ROT && s < 4) ? ((s + ry) & 3) : s);
-            const int yw = ((yv % COLY) + COLY) % COLY;
-            bx[s] = 8 * (16 * (xw >> 2) + (xw & 3));
-            by[s] = 8 * (16 * (COLX / 4) * (yw >> 2) + 4 * (yw & 3));
+            bx[s] = xpart((ROT && s < 4) ? ((s + rx) & 3) : s);
+            by[s] = ypart((ROT && s < 4) ? ((s + ry) & 3) : s);
         }
 #pragma unroll
         for (int s1 = 0; s1 < W; ++s1)
 #pragma unroll
-            for (int s0 = 0; s0 < W; ++s0) off[s1 * W + s0] = bx[s0] + by[s1];
+            for (int s0 = 0; s0 < W; ++s0) {
+                off[s1 * W + s0] = bx[s0] + by[s1];
+                P[s1 * W + s0] = wx[s0] * wy[s1];
+            }
     }
-    double P[W * W];
-#pragma unroll
-    for (int s1 = 0; s1 < W; ++s1)
-#pragma unroll
-        for (int s0 = 0; s0 < W; ++s0) P[s1 * W + s0] = wx[s0] * wy[s1];
     if constexpr (CNT) {  // counted launch (ibtk_le_ctx_count_adds): the adds issued below
 #pragma unroll
         for (int i2 = 0; i2 < W; ++i2) {
             const unsigned long long bm = __ballot(i2 >= z0 && i2 <= z1);
-            cnt[0] += bm ? (unsigned long long)(W * W) : 0ull;
-            cnt[1] += (unsigned long long)__popcll(bm) * (unsigned long long)(W * W);
+            cnt[0] += bm ? (unsigned long long)NA : 0ull;
+            cnt[1] += (unsigned long long)__popcll(bm) * (unsigned long long)NA;
         }
     }
     char* const rb = reinterpret_cast<char*>(ring);
@@ -1342,22 +1403,27 @@ __device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd
         // plane: the edge anchors of a short z-piece reach mostly unowned planes)
         if (!(i2 >= z0 && i2 <= z1)) continue;
         const double w2 = wz[i2];
-        // the plane's values and addresses first, each in a register of its own
-        // (the empty asm holds it there), then the adds back to back: otherwise
+        // the values and addresses of a batch first, each in a register of its own
+        // (the empty asm holds it there), then its adds back to back: otherwise
         // the compiler recycles one register pair, so that every ds_add_f64 waits
-        // for its own multiply and the next multiply for the ds_add
-        double v[W * W];
-        char* ad[W * W];
+        // for its own multiply and the next multiply for the ds_add (IB_6: batches
+        // of 8, for the registers)
+        constexpr int BT = W == 6 ? 8 : NA;
 #pragma unroll
-        for (int k = 0; k < W * W; ++k) {
-            v[k] = P[k] * w2;
-            ad[k] = plane + off[k];
-            asm volatile("" ::"v"(v[k]));
+        for (int k0 = 0; k0 < NA; k0 += BT) {
+            double v[BT];
+            char* ad[BT];
+#pragma unroll
+            for (int k = 0; k < BT; ++k) {
+                v[k] = P[k0 + k] * w2;
+                ad[k] = plane + off[k0 + k];
+                asm volatile("" ::"v"(v[k]));
+            }
+#pragma unroll
+            for (int k = 0; k < BT; ++k)
+                __hip_atomic_fetch_add(reinterpret_cast<double*>(ad[k]), v[k], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-#pragma unroll
-        for (int k = 0; k < W * W; ++k)
-            __hip_atomic_fetch_add(reinterpret_cast<double*>(ad[k]), v[k], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     clk.lap(3);
 }
