@@ -1258,11 +1258,22 @@ template <typename T> __device__ __forceinline__ void rot4(T* w, int r) {
 // `before` runs on every lane after the weights are computed and before any add
 // (the anchor step's writeback stores go there: issued after the candidate loads
 // they would otherwise be counted ahead of, and while the previous adds drain).
+// The work is split in two: spread_setup (the stencils, weights and offsets, into
+// a TileAdds) and spread_adds (the ring adds), so that a dense anchor's full
+// chunks can be set up two at a time before either's adds (k_spread_sweep).
+template <int W> struct TileAdds {
+    static constexpr int NA = W == 6 ? 40 : W * W;  // adds per stencil plane
+    double P[NA];  // products of the x and y weights, in issue order
+    int off[NA];   // their points' byte offsets in a slot
+    double wz[W];
+    int z0, z1;    // the stencil planes added (none: z0 > z1)
+    int sl;        // ring slot of stencil plane 0
+};
 template <int K, bool CNT, bool ZC, typename Before>
-__device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
-                                             bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
-                                             int yhi, int plo, int phi, double inv_h3, const double* inv_d, Clk& clk,
-                                             unsigned long long* cnt, Before&& before) {
+__device__ __forceinline__ void spread_setup(const Params& p, const CompDesc& cd, const Cand& cdat, bool act, int a,
+                                             int X0, int Y0, int zorg, int xlo, int xhi, int ylo, int yhi, int plo,
+                                             int phi, double inv_h3, const double* inv_d, unsigned long long* cnt,
+                                             Before&& before, TileAdds<SSh<K, ZC>::W>& T) {
     using S = SSh<K, ZC>;
     constexpr int W = S::W, FAM = S::FAM, NSL = S::NSL;
     constexpr bool ROT = W >= 4;
@@ -1283,15 +1294,17 @@ __device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd
     const bool bad = ox < LO - HI - 1 || ox + W - 1 > COLX - LO + HI || oy < LO - HI - 1 || oy + W - 1 > COLY - LO + HI;
     if (act && bad) atomicOr(p.err, 2);
     before();
-    if (!act || bad) return;  // idle lanes sit the adds out
+    const bool go = act && !bad;  // idle lanes sit the adds out (no planes)
     // owned and clipped-in ranges of the stencil indices
     const int x0 = max(st[0].ist, xlo - ox), x1 = min(st[0].isp, xhi - ox);
     const int y0 = max(st[1].ist, ylo - oy), y1 = min(st[1].isp, yhi - oy);
     // planes within the ring's reach of the lane's anchor, [LO, HIE] (a stencil
     // moved by a NINT tie of the multiply -- a weight of an ulp's order -- is cut there)
-    const int z0 = max(max(st[2].ist, plo - (a + oz)), S::LO - oz);
-    const int z1 = min(min(st[2].isp, phi - (a + oz)), S::HIE - oz);
-    double wx[W], wy[W], wz[W];
+    T.z0 = go ? max(max(st[2].ist, plo - (a + oz)), S::LO - oz) : W;
+    T.z1 = min(min(st[2].isp, phi - (a + oz)), S::HIE - oz);
+    T.sl = (int)((unsigned)(a + oz + 64 * NSL) % (unsigned)NSL);
+    double wx[W], wy[W];
+    double* const wz = T.wz;
 #pragma unroll
     for (int i = 0; i < W; ++i) {
         wx[i] = (i >= x0 && i <= x1) ? st[0].w[i] * cdat.V : 0.0;  // V applied first (f.m4:1512-1513 up to rounding)
@@ -1310,9 +1323,9 @@ __device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd
     };
     // the plane's adds: products of the x and y weights and the byte offsets of
     // their points in a slot, in issue order
-    constexpr int NA = W == 6 ? 40 : W * W;
-    int off[NA];
-    double P[NA];
+    constexpr int NA = TileAdds<W>::NA;
+    int* const off = T.off;
+    double* const P = T.P;
     if constexpr (W == 6) {  // tiled6 (see above)
         const int lane = lane_id();
         const int jx = lane & 3, jy = (lane >> 2) & 3;
@@ -1387,22 +1400,26 @@ __device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd
     if constexpr (CNT) {  // counted launch (ibtk_le_ctx_count_adds): the adds issued below
 #pragma unroll
         for (int i2 = 0; i2 < W; ++i2) {
-            const unsigned long long bm = __ballot(i2 >= z0 && i2 <= z1);
+            const unsigned long long bm = __ballot(i2 >= T.z0 && i2 <= T.z1);
             cnt[0] += bm ? (unsigned long long)NA : 0ull;
             cnt[1] += (unsigned long long)__popcll(bm) * (unsigned long long)NA;
         }
     }
+}
+template <int K, bool ZC>
+__device__ __forceinline__ void spread_adds(double* ring, const TileAdds<SSh<K, ZC>::W>& T) {
+    using S = SSh<K, ZC>;
+    constexpr int W = S::W, NSL = S::NSL, NA = TileAdds<W>::NA;
     char* const rb = reinterpret_cast<char*>(ring);
-    int sl = (int)((unsigned)(a + oz + 64 * NSL) % (unsigned)NSL);  // ring slot of plane i2 = 0
-    clk.lap(2);
+    int sl = T.sl;
 #pragma unroll
     for (int i2 = 0; i2 < W; ++i2) {
         char* const plane = rb + sl * (8 * S::PV);
         sl = sl + 1 == NSL ? 0 : sl + 1;
         // lanes whose plane is clipped or not owned sit it out (one exec mask per
         // plane: the edge anchors of a short z-piece reach mostly unowned planes)
-        if (!(i2 >= z0 && i2 <= z1)) continue;
-        const double w2 = wz[i2];
+        if (!(i2 >= T.z0 && i2 <= T.z1)) continue;
+        const double w2 = T.wz[i2];
         // the values and addresses of a batch first, each in a register of its own
         // (the empty asm holds it there), then its adds back to back: otherwise
         // the compiler recycles one register pair, so that every ds_add_f64 waits
@@ -1415,8 +1432,8 @@ __device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd
             char* ad[BT];
 #pragma unroll
             for (int k = 0; k < BT; ++k) {
-                v[k] = P[k0 + k] * w2;
-                ad[k] = plane + off[k0 + k];
+                v[k] = T.P[k0 + k] * w2;
+                ad[k] = plane + T.off[k0 + k];
                 asm volatile("" ::"v"(v[k]));
             }
 #pragma unroll
@@ -1425,6 +1442,17 @@ __device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
+}
+template <int K, bool CNT, bool ZC, typename Before>
+__device__ __forceinline__ void spread_tiled(const Params& p, const CompDesc& cd, double* ring, const Cand& cdat,
+                                             bool act, int a, int X0, int Y0, int zorg, int xlo, int xhi, int ylo,
+                                             int yhi, int plo, int phi, double inv_h3, const double* inv_d, Clk& clk,
+                                             unsigned long long* cnt, Before&& before) {
+    TileAdds<SSh<K, ZC>::W> T;
+    spread_setup<K, CNT, ZC>(p, cd, cdat, act, a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi, inv_h3, inv_d, cnt,
+                             before, T);
+    clk.lap(2);
+    spread_adds<K, ZC>(ring, T);
     clk.lap(3);
 }
 
@@ -1556,6 +1584,20 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
                              inv_h3, inv_d, clk, cnt, before);
     };
     auto nothing = [] {};
+    // two full chunks of anchor a (a dense plane's middle chunks): both set up, then
+    // the first's adds and the second's -- the adds in the order of two process calls
+    constexpr bool PAIR = S::W <= 4;  // (wider stencils: the registers of two set-ups)
+    auto process2 = [&](int a, const Cand& m0, const Cand& m1) {
+        TileAdds<S::W> T0, T1;
+        spread_setup<K, CNT, ZC>(p, cd, m0, true, a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi, inv_h3, inv_d, cnt,
+                                 nothing, T0);
+        spread_setup<K, CNT, ZC>(p, cd, m1, true, a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi, inv_h3, inv_d, cnt,
+                                 nothing, T1);
+        clk.lap(2);
+        spread_adds<K, ZC>(ring, T0);
+        spread_adds<K, ZC>(ring, T1);
+        clk.lap(3);
+    };
     // plane z -> registers (the lane's NPL points); registers -> ring slot.  A
     // plane the item does not own receives no adds and is not written back: its
     // slot's contents do not matter, so it is not read.
@@ -1658,9 +1700,21 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
             make_ranges_lanes(rowm, rgm);
             // chunk k + 1's candidates load while chunk k is added (a dense plane,
             // e.g. a sheet of markers, is hundreds of chunks of one wave)
-            Cand more;
+            Cand more, more2;
             cand_at(range_pos(rgm, h + lane), more);
-            for (int k = 0; k < nmid; ++k) {
+            int k = 0;
+            if constexpr (PAIR) {
+                // two chunks set up before either's adds (two independent chains of
+                // set-up arithmetic per lane); their adds keep the chunk order
+                if (nmid > 1) cand_at(range_pos(rgm, h + SW + lane), more2);
+                for (; k + 1 < nmid; k += 2) {
+                    const Cand n0 = more, n1 = more2;
+                    if (k + 2 < nmid) cand_at(range_pos(rgm, h + SW * (k + 2) + lane), more);
+                    if (k + 3 < nmid) cand_at(range_pos(rgm, h + SW * (k + 3) + lane), more2);
+                    process2(a, n0, n1);
+                }
+            }
+            for (; k < nmid; ++k) {
                 const Cand now = more;
                 if (k + 1 < nmid) cand_at(range_pos(rgm, h + SW * (k + 1) + lane), more);
                 process(a, 0, SW, now, nothing);
