@@ -1246,7 +1246,8 @@ template <typename T> __device__ __forceinline__ void rot4(T* w, int r) {
 // as the first, since a stencil column cx + 4 has the bank class of column cx --
 // and last the 8 points of rows 4, 5 and columns {0, 1, 4, 5}, whose classes
 // repeat (so 8 of 40 adds can conflict, against 20 of 36 unrotated).  IB_4_W8
-// takes its further columns and rows unrotated; narrower stencils unrotated.
+// turns each of its four 4 x 4 blocks alike (all 64 conflict-free); narrower
+// stencils go unrotated.
 // A stencil point that is clipped (outside the ghost box) or not owned (outside
 // the column, or in a neighbour item's planes) is added with weight 0 at its
 // position wrapped into the column (a +0 on an owned point of the same class),
@@ -1375,19 +1376,25 @@ __device__ __forceinline__ void spread_setup(const Params& p, const CompDesc& cd
                 off[32 + 4 * u + t] = bx3[t] + by3[u];
             }
     } else {
+        static_assert(!ROT || W % 4 == 0, "rotated blocks of 4");
         int rx = 0, ry = 0;
         if constexpr (ROT) {
             const int lane = lane_id();
             rx = ((lane & 3) - ox) & 3;
             ry = (((lane >> 2) & 3) - oy) & 3;
-            rot4(wx, rx);
-            rot4(wy, ry);
+            // every aligned block of 4 columns (rows) turned alike: stencil column
+            // 4 i + c has the bank class of column c (IB_4_W8: 64 steps, all conflict-free)
+#pragma unroll
+            for (int b = 0; b + 4 <= W; b += 4) {
+                rot4(wx + b, rx);
+                rot4(wy + b, ry);
+            }
         }
         int bx[W], by[W];
 #pragma unroll
         for (int s = 0; s < W; ++s) {
-            bx[s] = xpart((ROT && s < 4) ? ((s + rx) & 3) : s);
-            by[s] = ypart((ROT && s < 4) ? ((s + ry) & 3) : s);
+            bx[s] = xpart(ROT ? (s & ~3) + (((s & 3) + rx) & 3) : s);
+            by[s] = ypart(ROT ? (s & ~3) + (((s & 3) + ry) & 3) : s);
         }
 #pragma unroll
         for (int s1 = 0; s1 < W; ++s1)
@@ -1423,9 +1430,9 @@ __device__ __forceinline__ void spread_adds(double* ring, const TileAdds<SSh<K, 
         // the values and addresses of a batch first, each in a register of its own
         // (the empty asm holds it there), then its adds back to back: otherwise
         // the compiler recycles one register pair, so that every ds_add_f64 waits
-        // for its own multiply and the next multiply for the ds_add (IB_6: batches
-        // of 8, for the registers)
-        constexpr int BT = W == 6 ? 8 : NA;
+        // for its own multiply and the next multiply for the ds_add (IB_6, IB_4_W8:
+        // batches of 8, 16, for the registers)
+        constexpr int BT = W == 6 ? 8 : (W == 8 ? 16 : NA);
 #pragma unroll
         for (int k0 = 0; k0 < NA; k0 += BT) {
             double v[BT];
