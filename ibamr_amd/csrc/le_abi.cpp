@@ -194,6 +194,16 @@ struct ibtk_le_markers_s {
     bool dedup_done = false, has_dups = false;
     DevBuf qin, owner, int_off;           // ibtk_le_level_select_interior: per sorted entry, its Q target or -1
     bool qin_valid = false;               // cleared by every bin
+    // the selection's cache: a re-binning in which nothing moved keeps the order, and then
+    // the selection of the same interior lists stands (the lists are the binned lists' own,
+    // fixed between binnings as ibtk_le_markers_rebin takes them to be).  sel_gs = {order
+    // generation (bumped by k_rebin_commit when something moved), the selection's}; a full
+    // binning clears sel_cached
+    DevBuf sel_gs;
+    bool sel_cached = false;
+    std::vector<int> sel_off;
+    const int* sel_idx = nullptr;
+    int sel_nm = -1;
     // ibtk_le_markers_rebin: the last binning's list (n_dev of a fixed-capacity one) and its scratch
     const int* n_dev = nullptr;
     bool binned3 = false;                 // a 3-D column binning (ibtk_le_markers_bin(_count) / level_bin) holds
@@ -787,6 +797,7 @@ extern "C" int ibtk_le_markers_rebin(ibtk_le_ctx ctx, ibtk_le_markers m, const d
     r.xcur = m->xcur.as<double*>();
     r.xa = m->sorted_X.as<double>();
     r.xb = m->sorted_X2.as<double>();
+    r.order_gen = m->sel_gs.p ? m->sel_gs.as<int>() : nullptr;
     HIP_TRY(launch_rekey(m->kernel, p, r, s));
     if ((rc = scan_excl(ctx, r.wcnt, r.wpre, nw + 1))) return rc;  // wpre[nw]: the mover count
     // everything below returns at once on the device when nothing moved
@@ -830,6 +841,7 @@ static int markers_bin_impl(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_pa
     m->cand_valid = false;
     m->dedup_done = false;
     m->qin_valid = false;
+    m->sel_cached = false;
     m->has_dups = false;
     m->n_dev = n_dev;
     m->binned3 = cols;
@@ -1492,6 +1504,7 @@ extern "C" int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch,
     m->cand_valid = false;
     m->dedup_done = false;
     m->qin_valid = false;
+    m->sel_cached = false;
     m->has_dups = false;
     m->n_dev = nullptr;
     m->binned3 = true;
@@ -1662,6 +1675,17 @@ extern "C" int ibtk_le_level_select_interior(ibtk_le_ctx ctx, ibtk_le_markers m,
     int rc;
     if ((rc = m->qin.ensure(sizeof(int) * (size_t)std::max(m->n, 1)))) return rc;
     if ((rc = m->owner.ensure(sizeof(int) * (size_t)std::max(n_markers, 1)))) return rc;
+    // the same lists as the last selection since the last full binning: the kernels below
+    // return at once on the device unless a re-binning moved something (sel_gs)
+    const bool same = m->sel_cached && m->sel_idx == interior_indices_dev && m->sel_nm == n_markers &&
+                      m->sel_off.size() == (size_t)(np + 1) &&
+                      std::equal(m->sel_off.begin(), m->sel_off.end(), interior_offsets);
+    if (!m->sel_gs.p) {
+        if ((rc = m->sel_gs.ensure(2 * sizeof(int)))) return rc;
+        HIP_TRY(hipMemsetAsync(m->sel_gs.p, 0, sizeof(int), s));
+    }
+    if (!same) HIP_TRY(hipMemsetAsync(m->sel_gs.as<int>() + 1, 0xff, sizeof(int), s));  // -1: no selection
+    const int* gs = m->sel_gs.as<int>();
     if ((rc = m->int_off.ensure(sizeof(int) * (size_t)(np + 1)))) return rc;
     const int nblk = CHECK_STRIPES;  // the kept entries' count, striped over CHECK_STRIPES counters
     if ((rc = ctx->counts.ensure(sizeof(int) * (size_t)nblk))) return rc;
@@ -1669,7 +1693,7 @@ extern "C" int ibtk_le_level_select_interior(ibtk_le_ctx ctx, ibtk_le_markers m,
     HIP_TRY(hipMemsetAsync(m->owner.p, 0xff, sizeof(int) * (size_t)std::max(n_markers, 1), s));
     HIP_TRY(hipMemsetAsync(ctx->counts.p, 0, sizeof(int) * (size_t)nblk, s));
     HIP_TRY(launch_interior_owner(m->int_off.as<int>(), np, interior_indices_dev, n_int, n_markers, m->owner.as<int>(),
-                                  ctx->err.as<int>(), s));
+                                  ctx->err.as<int>(), gs, s));
     // An entry of patch q's list whose marker q owns is a periodic image only if the image
     // (a whole period away) lies in q's ghost box as well: impossible when the level spans
     // more than any patch's ghost box in every dim (a period is at least the level's extent),
@@ -1690,9 +1714,14 @@ extern "C" int ibtk_le_level_select_interior(ibtk_le_ctx ctx, ibtk_le_markers m,
     }
     HIP_TRY(launch_interior_targets(m->sorted_l.as<int>(), m->sorted_s.as<int>(), m->entry_off.as<int>(), np,
                                     need_shift ? m->xshift.as<double>() : nullptr, m->owner.as<int>(), n_markers,
-                                    m->n, m->qin.as<int>(), ctx->counts.as<int>(), ctx->err.as<int>(), s));
-    HIP_TRY(launch_check_count(ctx->counts.as<int>(), m->n > 0 ? nblk : 0, n_int, ctx->err.as<int>(), 4, s));
+                                    m->n, m->qin.as<int>(), ctx->counts.as<int>(), ctx->err.as<int>(), gs, s));
+    HIP_TRY(launch_check_count(ctx->counts.as<int>(), m->n > 0 ? nblk : 0, n_int, ctx->err.as<int>(), 4, s, gs));
+    HIP_TRY(launch_sel_mark(m->sel_gs.as<int>(), s));
     m->qin_valid = true;
+    m->sel_cached = true;
+    m->sel_idx = interior_indices_dev;
+    m->sel_nm = n_markers;
+    m->sel_off.assign(interior_offsets, interior_offsets + np + 1);
     return IBTK_LE_OK;
 }
 

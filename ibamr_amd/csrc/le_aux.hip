@@ -1032,8 +1032,12 @@ __device__ __forceinline__ int patch_of_entry(const int* off, int npatch, int l)
     const int q = search(__builtin_amdgcn_readfirstlane(l));
     return (off[q] <= l && l < off[q + 1]) ? q : search(l);
 }
+// gs (ibtk_le_level_select_interior's cache): {the binning's order generation, the one the
+// selection was made at}; equal: the selection stands and these kernels return at once
+__device__ __forceinline__ bool sel_current(const int* gs) { return gs && gs[0] == gs[1]; }
 __global__ __launch_bounds__(BLOCK) void k_interior_owner(const int* int_off, int npatch, const int* int_idx, int n_int,
-                                                          int n_markers, int* owner, int* err) {
+                                                          int n_markers, int* owner, int* err, const int* gs) {
+    if (sel_current(gs)) return;
     const int j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= n_int) return;
     const int s = int_idx[j];
@@ -1044,16 +1048,17 @@ __global__ __launch_bounds__(BLOCK) void k_interior_owner(const int* int_off, in
     atomicMax(owner + s, patch_of_entry(int_off, npatch, j));
 }
 hipError_t launch_interior_owner(const int* int_off, int npatch, const int* int_idx, int n_int, int n_markers,
-                                 int* owner, int* err, hipStream_t s) {
+                                 int* owner, int* err, const int* gs, hipStream_t s) {
     if (n_int <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_interior_owner, dim3((n_int + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, int_off, npatch, int_idx,
-                       n_int, n_markers, owner, err);
+                       n_int, n_markers, owner, err, gs);
     return hipGetLastError();
 }
 __global__ __launch_bounds__(BLOCK) void k_interior_targets(const int* sorted_l, const int* sorted_s,
                                                             const int* entry_off, int npatch, const double* xshift,
                                                             const int* owner, int n_markers, int n, int* qin,
-                                                            int* found, int* err) {
+                                                            int* found, int* err, const int* gs) {
+    if (sel_current(gs)) return;  // (uniform over the block: before its barriers)
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     bool keep = false;
     int s = -1;
@@ -1080,10 +1085,16 @@ __global__ __launch_bounds__(BLOCK) void k_interior_targets(const int* sorted_l,
 }
 hipError_t launch_interior_targets(const int* sorted_l, const int* sorted_s, const int* entry_off, int npatch,
                                    const double* xshift, const int* owner, int n_markers, int n, int* qin, int* found,
-                                   int* err, hipStream_t s) {
+                                   int* err, const int* gs, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_interior_targets, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, sorted_l, sorted_s,
-                       entry_off, npatch, xshift, owner, n_markers, n, qin, found, err);
+                       entry_off, npatch, xshift, owner, n_markers, n, qin, found, err, gs);
+    return hipGetLastError();
+}
+// the selection is of the current order: gs[1] = gs[0]
+__global__ void k_sel_mark(int* gs) { gs[1] = gs[0]; }
+hipError_t launch_sel_mark(int* gs, hipStream_t s) {
+    hipLaunchKernelGGL(k_sel_mark, dim3(1), dim3(1), 0, s, gs);
     return hipGetLastError();
 }
 // fixed-capacity migration: pack the leavers, unpack stayers + arrivals (no host sync)
@@ -1161,7 +1172,9 @@ hipError_t launch_wrap_positions(const WrapBox& w, long long n, double* X, hipSt
     return hipGetLastError();
 }
 
-__global__ __launch_bounds__(BLOCK) void k_check_count(const int* count, int ncount, int expect, int* err, int bit) {
+__global__ __launch_bounds__(BLOCK) void k_check_count(const int* count, int ncount, int expect, int* err, int bit,
+                                                       const int* gs) {
+    if (sel_current(gs)) return;
     __shared__ long long tot;
     if (threadIdx.x == 0) tot = 0;
     __syncthreads();
@@ -1171,8 +1184,9 @@ __global__ __launch_bounds__(BLOCK) void k_check_count(const int* count, int nco
     __syncthreads();
     if (threadIdx.x == 0 && tot != expect) atomicOr(err, bit);
 }
-hipError_t launch_check_count(const int* count, int ncount, int expect, int* err, int bit, hipStream_t s) {
-    hipLaunchKernelGGL(k_check_count, dim3(1), dim3(BLOCK), 0, s, count, ncount, expect, err, bit);
+hipError_t launch_check_count(const int* count, int ncount, int expect, int* err, int bit, hipStream_t s,
+                              const int* gs) {
+    hipLaunchKernelGGL(k_check_count, dim3(1), dim3(BLOCK), 0, s, count, ncount, expect, err, bit, gs);
     return hipGetLastError();
 }
 

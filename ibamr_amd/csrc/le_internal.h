@@ -247,6 +247,7 @@ struct RebinBufs {
     double** xcur;          // the current sorted-position buffer (xa or xb; le_sweep.hip rebin_other)
     double* xa;
     double* xb;
+    int* order_gen;         // bumped when something moved (the order changed; nullable)
 };
 hipError_t launch_set_xcur(double** xcur, double* x, hipStream_t s);
 hipError_t launch_rekey(int kernel, const Params& p, const RebinBufs& r, hipStream_t s);
@@ -370,11 +371,14 @@ hipError_t launch_level_node_keys(const LevelNum& L, const int* tab, const doubl
 // then per sorted entry e of the binned lists: qin[e] = s if owner[s] is the entry's
 // patch and the entry is unshifted, else -1; found[block] counts the block's kept entries.
 // Marker indices outside [0, n_markers) (in either list) are not dereferenced: err bit 4.
+// gs: the selection cache {order generation, generation of the selection} (nullable):
+// equal, and the kernels return at once; launch_sel_mark records the selection's
 hipError_t launch_interior_owner(const int* int_off, int npatch, const int* int_idx, int n_int, int n_markers,
-                                 int* owner, int* err, hipStream_t s);
+                                 int* owner, int* err, const int* gs, hipStream_t s);
 hipError_t launch_interior_targets(const int* sorted_l, const int* sorted_s, const int* entry_off, int npatch,
                                    const double* xshift, const int* owner, int n_markers, int n, int* qin, int* found,
-                                   int* err, hipStream_t s);
+                                   int* err, const int* gs, hipStream_t s);
+hipError_t launch_sel_mark(int* gs, hipStream_t s);
 struct WrapBox {
     double lo[3], hi[3];
     int per[3];
@@ -409,7 +413,8 @@ hipError_t launch_user_contrib(const UserDesc& u, unsigned* keys, int* vals, dou
 hipError_t launch_user_segsum(const UserDesc& u, const unsigned* skeys, const int* svals, const double* contrib,
                               int ncontrib, hipStream_t s);
 constexpr int CHECK_STRIPES = 64;  // counters k_interior_targets adds its block counts into
-hipError_t launch_check_count(const int* count, int ncount, int expect, int* err, int bit, hipStream_t s);
+hipError_t launch_check_count(const int* count, int ncount, int expect, int* err, int bit, hipStream_t s,
+                              const int* gs = nullptr);
 // out[i * depth + k] = in[order[i] * depth + k]
 hipError_t launch_rows_gather(const int* order, int n, const double* in, int depth, double* out, hipStream_t s);
 // flag[i] = entry i of the (lag, ckey)-sorted list is the first of its lag run and not local

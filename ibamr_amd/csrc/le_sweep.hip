@@ -559,11 +559,12 @@ __global__ __launch_bounds__(BLOCK) void k_rebin_scatter(Params p, int n, int nb
 // the new bucket starts in place when something moved; else the other buffer,
 // which holds the new positions in the unchanged order, becomes current
 __global__ __launch_bounds__(BLOCK) void k_rebin_commit(int nb, const int* T, const int* ns, int* plane_start,
-                                                        double** xcur, double* xa, double* xb) {
+                                                        double** xcur, double* xa, double* xb, int* order_gen) {
     if (*T == 0) {
         if (blockIdx.x == 0 && threadIdx.x == 0) *xcur = rebin_other(xcur, xa, xb);
         return;
     }
+    if (order_gen && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(order_gen, 1);  // a new order
     for (int b = blockIdx.x * BLOCK + threadIdx.x; b <= nb; b += gridDim.x * BLOCK) plane_start[b] = ns[b];
 }
 // *xcur := x (a fresh binning gathered the positions into x)
@@ -2176,7 +2177,7 @@ hipError_t launch_rebin_scatter(const Params& p, const RebinBufs& r, hipStream_t
     hipLaunchKernelGGL(k_rebin_scatter, dim3(RB_GRID), dim3(BLOCK), 0, s, p, r.n, r.nb, r.mbits, r.wpre, r.nw, r.knew,
                        r.lold, r.os, r.ns, r.mstart, r.mlist, r.sorted_l, r.sorted_key, r.sorted_s, r.xcur, r.xa, r.xb);
     hipLaunchKernelGGL(k_rebin_commit, dim3(RB_GRID), dim3(BLOCK), 0, s, r.nb, r.wpre + r.nw, r.ns,
-                       const_cast<int*>(r.os), r.xcur, r.xa, r.xb);
+                       const_cast<int*>(r.os), r.xcur, r.xa, r.xb, r.order_gen);
     return hipGetLastError();
 }
 hipError_t launch_gather_col(int kernel, const Params& p, int n, int* sorted_s, double* sorted_X,

@@ -260,7 +260,10 @@ int ibtk_le_level_zero_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, in
  * sub-list of its ghost-box list whose cells lie in the patch box, LIndexSetData.cpp:
  * 111-166), so results equal interp over a binning of the interior lists bit for bit.
  * Cleared by the next bin.  An interior entry missing from its patch's binned list
- * raises device flag 4 (ibtk_le_ctx_synchronize). */
+ * raises device flag 4 (ibtk_le_ctx_synchronize).  After ibtk_le_markers_rebin, a call
+ * with the same offsets, index pointer and n_markers as the last one since the last
+ * full binning is a no-op on the device when no marker changed bucket (the lists are
+ * taken to be unchanged between binnings, as the re-binning takes the binned ones). */
 int ibtk_le_level_select_interior(ibtk_le_ctx ctx, ibtk_le_markers m, int n_markers, const int* interior_offsets,
                                   const int* interior_indices_dev);
 /* Zeroes every patch array of a level, ghosts included, in one launch: the

@@ -376,3 +376,53 @@ from the others (the two calls)."""
                 assert torch.equal(torch.nan_to_num(t0, nan=7.0), torch.nan_to_num(t1, nan=7.0)), \
                     "an array point was written"
     del spacer
+
+
+def test_level_select_interior_cache(le, ctx):
+    """A repeated selection of the same interior lists after a re-binning
+    (ibtk_le_level_select_interior's cache): kept when no marker changed bucket, made
+    again when some did -- the interp equal bit for bit to a fresh level's."""
+    kernel, N, P = "IB_4", 32, 2
+    g = ora.min_ghost_width(kernel)
+    geoms = _patches(le, N, P, g)
+    rng = np.random.default_rng(11)
+    M = 6000
+    X = rng.uniform(0.05, 0.95, (M, 3))
+    G = [rng.uniform(-1, 1, (N, N, N)) for _ in range(3)]
+    u = [[torch.from_numpy(a).cuda() for a in _fill(geom, G, N)] for geom in geoms]
+    lists_i, lists_s = [], []
+    for geom in geoms:
+        interior, idx, xs = _lists(geom, X, N, g)
+        lists_i.append(torch.from_numpy(interior).cuda())
+        lists_s.append((torch.from_numpy(idx).cuda(), torch.from_numpy(xs).cuda()))
+    offs = [0]
+    for l in lists_i:
+        offs.append(offs[-1] + l.numel())
+    ii = torch.cat(lists_i)
+
+    def interp(level, Xq):
+        U = torch.full((M, 3), np.nan, dtype=torch.float64, device="cuda")
+        level.interp("side", u, U, Xq)
+        return U
+
+    Xd = torch.from_numpy(X).cuda()
+    lvl = le.Level(ctx, geoms, kernel, Xd, lists_s)
+    lvl.select_interior(M, ii, offs)
+    U0 = interp(lvl, Xd)
+    assert not torch.isnan(U0).any()
+    lvl.rebin(Xd)  # nothing moved: the selection stands
+    lvl.select_interior(M, ii, offs)
+    assert torch.equal(interp(lvl, Xd), U0)
+    # moved a fraction of a cell (within the lists' ghost slack): many change bucket
+    X1d = torch.from_numpy(X + rng.uniform(-0.3, 0.3, X.shape) / N).cuda()
+    lvl.rebin(X1d)
+    lvl.select_interior(M, ii, offs)
+    U1 = interp(lvl, X1d)
+    ref = le.Level(ctx, geoms, kernel, X1d, lists_s)
+    ref.select_interior(M, ii.clone(), offs)
+    assert torch.equal(U1, interp(ref, X1d))
+    assert not torch.equal(U1, U0)
+    lvl.rebin(X1d)  # and nothing moved again
+    lvl.select_interior(M, ii, offs)
+    assert torch.equal(interp(lvl, X1d), U1)
+    ctx.synchronize()
