@@ -155,6 +155,7 @@ _SIGS = [
     ("ibtk_le_level_zero_spread", c_int,
      [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(c_void_p), c_int, c_void_p, c_int, c_void_p]),
     ("ibtk_le_level_select_interior", c_int, [c_void_p, c_void_p, c_int, ctypes.POINTER(c_int), c_void_p]),
+    ("ibtk_le_level_select_interior_reset", c_int, [c_void_p]),
     ("ibtk_le_level_fill_ghosts", c_int,
      [c_void_p, c_int, ctypes.POINTER(PatchGeom), c_int, ctypes.POINTER(c_void_p), c_int, c_void_p]),
     ("ibtk_le_level_fill_interp", c_int,

@@ -303,7 +303,6 @@ extern "C" int ibtk_le_ctx_tune(ibtk_le_ctx ctx, const char* key, int value) {
     else if (k == "heavy_first") t.heavy_first = value;
     else if (k == "strip") t.strip = value;
     else if (k == "xcd_block") t.xcd_block = value;
-    else if (k == "fdirect") t.fdirect = value;
     else return fail(IBTK_LE_ERR_ARG, "unknown tuning key %s", key);
     return IBTK_LE_OK;
 }
@@ -798,6 +797,9 @@ extern "C" int ibtk_le_markers_rebin(ibtk_le_ctx ctx, ibtk_le_markers m, const d
     r.xa = m->sorted_X.as<double>();
     r.xb = m->sorted_X2.as<double>();
     r.order_gen = m->sel_gs.p ? m->sel_gs.as<int>() : nullptr;
+    // k_rekey raises the per-bucket mover counts and k_rebin_append consumes them back
+    // to zero: until the sequence has been queued whole, the next call must clear them
+    m->rb_zeroed_nb = -1;
     HIP_TRY(launch_rekey(m->kernel, p, r, s));
     if ((rc = scan_excl(ctx, r.wcnt, r.wpre, nw + 1))) return rc;  // wpre[nw]: the mover count
     // everything below returns at once on the device when nothing moved
@@ -805,6 +807,7 @@ extern "C" int ibtk_le_markers_rebin(ibtk_le_ctx ctx, ibtk_le_markers m, const d
     HIP_TRY(launch_rebin_starts(r, s));
     HIP_TRY(launch_rebin_movers(r, s));
     HIP_TRY(launch_rebin_scatter(p, r, s));  // ... and the new starts into plane_start
+    m->rb_zeroed_nb = nb;
     return build_items(ctx, m, m->kernel, r.wpre + nw);
 }
 
@@ -1128,6 +1131,10 @@ extern "C" int ibtk_le_fill_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kerne
             return rc;
         return ibtk_le::interp_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, X_dev, true);
     }
+    // the fill's own argument check (ghost_op), so that the fused form fails where the pair does
+    for (int d = 0; d < 3; ++d)
+        if (per[d] && geom->iupper[d] - geom->ilower[d] + 1 < 2 * geom->gcw[d] + 1)
+            return fail(IBTK_LE_ERR_ARG, "periodic dim %d narrower than 2*ghost+1", d);
     return ibtk_le::interp_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, X_dev, true, per);
 }
 
@@ -1396,7 +1403,7 @@ static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cente
     p.ds = ds_dev;
     p.Q_depth = Q_depth;
     p.nsorted = m->n;
-    if (geom->ndim == 2 || !ctx->tune.fdirect) {  // fdirect: the 3-D sweeps read F through the sorted index
+    {
         if (int rc = ctx->fbuf.ensure(sizeof(double) * (size_t)m->n * (size_t)std::min(nc, MAXC))) return rc;
         p.sorted_F = ctx->fbuf.as<double>();
     }
@@ -1658,6 +1665,15 @@ extern "C" int ibtk_le_level_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kern
 // later level interps write Q from those entries only, and the next bin clears it.
 // An interior entry with no match in its patch's binned list raises device flag 4
 // (reported by ibtk_le_ctx_synchronize; no host sync here).
+// Forget the last selection: the next ibtk_le_level_select_interior recomputes it even if its
+// offsets, index pointer and n_markers are the same (the caller rewrote the lists in place, or
+// a new list was allocated at the old address)
+extern "C" int ibtk_le_level_select_interior_reset(ibtk_le_markers m) {
+    if (!m) return fail(IBTK_LE_ERR_ARG, "select_interior_reset: null markers");
+    m->sel_cached = false;
+    return IBTK_LE_OK;
+}
+
 extern "C" int ibtk_le_level_select_interior(ibtk_le_ctx ctx, ibtk_le_markers m, int n_markers,
                                              const int* interior_offsets, const int* interior_indices_dev) {
     if (!ctx || !m || !interior_offsets) return fail(IBTK_LE_ERR_ARG, "select_interior: null argument");
@@ -1738,7 +1754,7 @@ static int level_spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int
     if (!Q_dev) return fail(IBTK_LE_ERR_ARG, "null Q");
     p.Qin = Q_dev;
     p.zero_first = zero_first ? 1 : 0;
-    if (!ctx->tune.fdirect) {
+    {
         if (int rc = ctx->fbuf.ensure(sizeof(double) * (size_t)m->n * (size_t)nc)) return rc;
         p.sorted_F = ctx->fbuf.as<double>();
     }

@@ -114,8 +114,6 @@ struct SweepTune {
     int heavy_target = 0;  // a heavy item's pieces: own markers per piece (0: the default, le_sweep.hip HEAVY_TARGET)
     int heavy_min_piece = 0;  // ... and planes per piece, at least (0: HEAVY_MIN_PIECE)
     int heavy_first = 0;   // heavy items head the table (0, the default) or keep their place (-1)
-    int fdirect = 0;       // 3-D spread: 1 = the candidates read F through the sorted marker index instead
-                           // of the gather pass k_gather_F_col (diagnostic: slower, profiles/r04c)
 };
 // One 3-D sweep item: a patch, a column and its owned planes [p0, p1) (relative
 // to the patch's cg.org[2]).

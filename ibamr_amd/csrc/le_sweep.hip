@@ -41,6 +41,10 @@
 namespace ibtk_le {
 
 constexpr int SW = 64;  // one wavefront per work item
+#ifndef IBTK_LE_DIAG_SPREAD
+#define IBTK_LE_DIAG_SPREAD 0  // diagnostic builds only (tools/diag_variants.sh): 1 no adds, 2 trivial weights,
+                               // 4 no candidate work, 8 no candidate loads
+#endif
 
 // LDS read of one double that the compiler may not merge with its neighbour into a
 // ds_read2_b64 (half the rate of two ds_read_b64 on gfx950: interp sweep 10.7 ->
@@ -56,6 +60,19 @@ struct D3 {
     double v[3];
 };
 __device__ __forceinline__ D3 ld3(const double* q) { return *reinterpret_cast<const D3*>(q); }
+// Global-memory pointers.  A pointer read from memory (the sorted positions' current
+// buffer, Params::sorted_X_ref) is generic to the compiler: its loads become flat_load,
+// which may return out of order, so every wait on them is vmcnt(0) lgkmcnt(0) -- it
+// waits for every other load and store of the wave as well.  Through an
+// address_space(1) pointer they are global_load, and the waits count.
+using gdouble = __attribute__((address_space(1))) const double;
+__device__ __forceinline__ gdouble* as_global(const double* q) { return (gdouble*)q; }
+__device__ __forceinline__ D3 ld3(gdouble* q) {
+    D3 r;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) r.v[d] = q[d];
+    return r;
+}
 
 // One plane of an Eulerian array as a raw buffer resource (base in SGPRs, a
 // 32-bit byte offset per lane): the sweeps' plane loads and stores take one
@@ -614,8 +631,10 @@ __global__ __launch_bounds__(BLOCK) void k_gather_col(Params p, int n, int* sort
 
 // the current sorted positions of a 3-D binning (Params::sorted_X_ref: xa or xb of
 // the re-binning), read once per kernel
-__device__ __forceinline__ const double* cur_sorted_X(const Params& p) {
-    return p.sorted_X_ref ? *p.sorted_X_ref : p.sorted_X;
+__device__ __forceinline__ gdouble* cur_sorted_X(const Params& p) {
+    typedef const double* dptr;
+    if (!p.sorted_X_ref) return as_global(p.sorted_X);
+    return as_global(*(const __attribute__((address_space(1))) dptr*)p.sorted_X_ref);
 }
 
 // ---------------------------------------------------------------------------
@@ -882,7 +901,7 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     CompDesc cd;
     const int* bs;
     item_patch<LVL>(p, si, c, cg, cd, bs);
-    const double* const sorted_X = cur_sorted_X(p);
+    gdouble* const sorted_X = cur_sorted_X(p);
     if (p.zmode) {  // the planes the item reads: a0 + LO .. a1 - 1 + HI
         const bool inner = cg.org[2] + a0 + LO >= p.zlo && cg.org[2] + a1 - 1 + HI <= p.zhi;
         if (inner != (p.zmode == 1)) return;
@@ -1066,7 +1085,7 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
         am = a + k;
         e = min(e, nlast);
         m.s = p.sorted_s[e];
-        m.q = p.qdst ? p.qdst[e] : m.s;
+        m.q = (p.qdst ? p.qdst : p.sorted_s)[e];  // (not a copy of m.s: a copy waits for its load)
         const D3 xs = ld3(sorted_X + (int64_t)3 * e);
         m.X[0] = xs.v[0];
         m.X[1] = xs.v[1];
@@ -1100,6 +1119,7 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
         const Mk cur = nxt;
         const int acur = anx;
         const GSpan gc = gs;
+
         // prefetch for the next group: its spans (loaded a group ago), its chunk
         // w, the spans of the group after it, plane my+IWAVES+HI
         gspan_get(a + IWAVES, vsp1, gs);
@@ -1284,8 +1304,20 @@ __device__ __forceinline__ void spread_setup(const Params& p, const CompDesc& cd
     for (int d = 0; d < 3; ++d) {
         const double Xraw = (FAM == 2) ? p.X[(int64_t)3 * cdat.s + d] : cdat.X[d];
         // X/dx by a multiply (see stencil1d for ties)
+#if IBTK_LE_DIAG_SPREAD & 2  // diagnostic: trivial weights (results wrong by design)
+        {
+            const double xo = (cdat.X[d] - cd.xlo[d]) * inv_d[d];
+            st[d].icl = (int)__builtin_rint(xo) + cd.ilower[d] - W / 2;
+            st[d].ist = 0;
+            st[d].isp = W - 1;
+#pragma unroll
+            for (int i = 0; i < W; ++i) st[d].w[i] = 0.25 + 0.01 * i;
+            (void)Xraw;
+        }
+#else
         stencil1d<K, true>(cdat.X[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis,
                            p.K6, st[d], inv_d[d]);
+#endif
     }
     const int ox = st[0].icl - X0, oy = st[1].icl - Y0, oz = st[2].icl - (zorg + a);
     // binning invariant: every stencil index lies in [key + LO, key + HI] and the
@@ -1445,9 +1477,14 @@ __device__ __forceinline__ void spread_adds(double* ring, const TileAdds<SSh<K, 
                 asm volatile("" ::"v"(v[k]));
             }
 #pragma unroll
-            for (int k = 0; k < BT; ++k)
+            for (int k = 0; k < BT; ++k) {
+#if IBTK_LE_DIAG_SPREAD & 1  // diagnostic: no LDS adds (results wrong by design)
+                asm volatile("" ::"v"(v[k]), "v"(ad[k]));
+#else
                 __hip_atomic_fetch_add(reinterpret_cast<double*>(ad[k]), v[k], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+            }
         }
     }
 }
@@ -1489,7 +1526,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     CompDesc cd;
     const int* bs;
     item_patch<LVL>(p, si, c, cg, cd, bs);
-    const double* const sorted_X = cur_sorted_X(p);
+    gdouble* const sorted_X = cur_sorted_X(p);
     const int ncx = cg.ncx;
     const int cx = col % ncx, cy = col / ncx;
     if (cx == 0 || cx == ncx - 1 || cy == 0 || cy == cg.ncy - 1) return;  // guard columns own no points
@@ -1564,22 +1601,18 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // candidate data of sorted position e
     auto cand_at = [&](int e, Cand& d) {
         e = min(e, nlast);
+#if IBTK_LE_DIAG_SPREAD & 8  // diagnostic: no candidate loads
+        d.X[0] = d.X[1] = d.X[2] = 0.5 + 1e-9 * e;
+        d.V = 1.0;
+        d.s = 0;
+        return;
+#endif
         const D3 xs = ld3(sorted_X + (int64_t)3 * e);
         d.X[0] = xs.v[0];
         d.X[1] = xs.v[1];
         d.X[2] = xs.v[2];
-        if (p.tune.fdirect) {
-            // F through the sorted marker index, no gather pass: measured slower again in
-            // round 4 (cfg4: spread sweep +2.2 ms against k_gather_F_col's 1.13 ms; cfg5 +1.0
-            // ms, profiles/r04c), a diagnostic only
-            const int s = p.sorted_s[e];
-            const double v = p.Qin[(int64_t)p.Q_depth * s + cd.qcomp];
-            d.V = p.ds ? v * p.ds[s] : v;  // F ds rounded once, as LDataManager.cpp:446-451 forms it
-            d.s = s;
-        } else {
-            d.V = p.sorted_F[(int64_t)c * p.nsorted + e];
-            d.s = FAM == 2 ? p.sorted_s[e] : 0;
-        }
+        d.V = p.sorted_F[(int64_t)c * p.nsorted + e];
+        d.s = FAM == 2 ? p.sorted_s[e] : 0;
     };
     Clk clk;
     unsigned long long cnt[2] = {0ull, 0ull};  // CNT: wave-uniform totals of the item
@@ -1588,14 +1621,24 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // adds of the n <= 64 candidates held one per lane (lane j's anchor plane:
     // a - 1 for j < r, else a); `before` as for spread_tiled
     auto process = [&](int a, int r, int n, const Cand& mine, auto&& before) {
+#if IBTK_LE_DIAG_SPREAD & 4  // diagnostic: no candidate work at all (the skeleton)
+        asm volatile("" ::"v"(mine.X[0]), "v"(mine.X[1]), "v"(mine.X[2]), "v"(mine.V));
+        before();
+#else
         spread_tiled<K, CNT, ZC>(p, cd, ring, mine, lane < n, lane < r ? a - 1 : a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi,
                              inv_h3, inv_d, clk, cnt, before);
+#endif
     };
     auto nothing = [] {};
     // two full chunks of anchor a (a dense plane's middle chunks): both set up, then
     // the first's adds and the second's -- the adds in the order of two process calls
     constexpr bool PAIR = S::W <= 4;  // (wider stencils: the registers of two set-ups)
     auto process2 = [&](int a, const Cand& m0, const Cand& m1) {
+#if IBTK_LE_DIAG_SPREAD & 4
+        asm volatile("" ::"v"(m0.X[0]), "v"(m0.X[1]), "v"(m0.X[2]), "v"(m0.V));
+        asm volatile("" ::"v"(m1.X[0]), "v"(m1.X[1]), "v"(m1.X[2]), "v"(m1.V));
+        return;
+#endif
         TileAdds<S::W> T0, T1;
         spread_setup<K, CNT, ZC>(p, cd, m0, true, a, X0, Y0, zorg, xlo, xhi, ylo, yhi, plo, phi, inv_h3, inv_d, cnt,
                                  nothing, T0);
@@ -1664,7 +1707,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     Ranges rg;  // ranges of the anchor whose chunk 1 is prefetched (wave-uniform)
     make_ranges_lanes(rowv, rg);
     int tA = rg.pre[S::NR];
-    Cand nxt;
+    Cand nxt, nxt2;  // chunk 1 of the anchor of the step, of the next
     cand_at(range_pos(rg, min(lane, max(tA - 1, 0))), nxt);
     int r_prev = 0;        // candidates of anchor a-1 carried into a's chunk 1
     int n1 = min(tA, SW);  // lanes of a's chunk 1
@@ -1673,12 +1716,18 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // One anchor step: plane a+HI from registers into the ring, plane a+HI+1 into
     // registers.  (Two anchors ahead through two register buffers measured the same,
     // 16.1 vs 16.3 ms on cfg4: the streams are not what waits.)
-    auto anchor_step = [&](int a) {
+    auto anchor_step = [&](int a, const Cand& cur, Cand& nxt) __attribute__((always_inline)) {
         const int zw = a - 2 + LO;  // no anchor left reaches it: written back this step
         double wb[NPL];
         wb_read(zw, wb);       // its slot ...
         plane_put(a + HI, pv);  // ... takes plane a+HI
-        const Cand cur = nxt;
+        // The step's inputs loaded at the previous step (chunk 1, the rows of a+1) are
+        // waited for here, before this step issues its own loads and stores.  Left to the
+        // compiler, the wait falls mid-step and is vmcnt(0) (the loop-carried copy of a
+        // pending load): it then waits for this step's prefetch and writeback too.  cfg4
+        // spread sweep 15.0 -> 13.0 ms (round 5).
+        asm volatile("" ::"v"(cur.X[0]), "v"(cur.X[1]), "v"(cur.X[2]), "v"(cur.V), "v"(rowv[0]), "v"(rowv[1]),
+                     "v"(rowv[2]));
         const int cur_r = r_prev, cur_n = n1;
         const int tCur = tA;
         const int h = min(SW - r_prev, tCur);  // a's candidates in chunk 1
@@ -1735,7 +1784,10 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         }
         clk.lap(4);
     };
-    for (int a = afirst; a <= alast; ++a) anchor_step(a);
+    for (int a = afirst; a <= alast; ++a) {
+        anchor_step(a, nxt, nxt2);
+        nxt = nxt2;
+    }
     {
         double wb[NPL];
         wb_read(alast - 1 + LO, wb);
@@ -2036,7 +2088,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather_F_col(Params p, int n, double*
 }
 
 template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-    if (p.nsorted > 0 && !p.tune.fdirect) {
+    if (p.nsorted > 0) {
         const bool rec3 = p.ncomp == 3 && p.Q_depth == 3 && p.comp[0].qcomp == 0 && p.comp[1].qcomp == 1 &&
                           p.comp[2].qcomp == 2;
         const dim3 g((p.nsorted + BLOCK - 1) / BLOCK), b(BLOCK);

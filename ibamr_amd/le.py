@@ -236,6 +236,7 @@ class Markers:
         check(self.ctx.lib.ibtk_le_markers_bin(self.ctx.h, self.h, ctypes.byref(geom.c), kernel_id(kernel), _ptr(X),
                                                _ptr(indices), _ptr(Xshift), int(n)))
         self.kernel, self.geom, self.n = kernel, geom, n
+        self._n_dev = None
         return self
 
     def bin_count(self, geom: Geometry, kernel: str, X: torch.Tensor, n_dev: torch.Tensor):
@@ -248,6 +249,8 @@ class Markers:
         check(self.ctx.lib.ibtk_le_markers_bin_count(self.ctx.h, self.h, ctypes.byref(geom.c), kernel_id(kernel),
                                                      _ptr(X), int(X.shape[0]), _ptr(n_dev)))
         self.kernel, self.geom, self.n = kernel, geom, X.shape[0]
+        # rebin() reads the count again on the device: keep its memory alive until the next bin
+        self._n_dev = n_dev
         return self
 
     def rebin(self, X: torch.Tensor):
@@ -502,6 +505,10 @@ class Level:
         if len(offsets) != len(self.geoms) + 1:
             raise ValueError("one offset per patch, plus the end")
         idx = indices.to(torch.int32).contiguous()
+        if idx is not getattr(self, "_sel", None):
+            # another list object (possibly at the old list's address): the library's kept
+            # selection is keyed on the pointer, so it is dropped here
+            check(self.ctx.lib.ibtk_le_level_select_interior_reset(self.markers.h))
         self._sel = idx  # kept alive until the next bin
         O = (ctypes.c_int * len(offsets))(*[int(o) for o in offsets])
         check(self.ctx.lib.ibtk_le_level_select_interior(self.ctx.h, self.markers.h, int(n_markers), O, _ptr(idx)))

@@ -160,7 +160,9 @@ int ibtk_le_markers_bin_count(ibtk_le_ctx ctx, ibtk_le_markers m, const ibtk_le_
  * bucket did not change keep their relative order and the others are inserted
  * (with nothing moved, one pass over the list).  No host sync.  Replaces the
  * per-step re-binning of LDataManager's LIndexSetData (LDataManager.cpp:1446-1493,
- * IndexUtilities-inl.h:66-89) after a position update. */
+ * IndexUtilities-inl.h:66-89) after a position update.  After ibtk_le_markers_bin_count
+ * the re-binning reads the device count n_dev of that call again: it must stay valid
+ * (and hold the list's length) until the next full binning of `m`. */
 int ibtk_le_markers_rebin(ibtk_le_ctx ctx, ibtk_le_markers m, const double* X_dev);
 /* Number of list entries, and device pointers to the sorted list (entry -> marker
  * index, and entry -> Xshift[NDIM]); valid until the next bin call. */
@@ -266,6 +268,10 @@ int ibtk_le_level_zero_spread(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, in
  * taken to be unchanged between binnings, as the re-binning takes the binned ones). */
 int ibtk_le_level_select_interior(ibtk_le_ctx ctx, ibtk_le_markers m, int n_markers, const int* interior_offsets,
                                   const int* interior_indices_dev);
+/* Forget the selection kept by ibtk_le_level_select_interior: the next call recomputes it
+ * whatever its arguments (a caller that rewrites the interior lists in place, or frees them
+ * and allocates new ones, calls this first). */
+int ibtk_le_level_select_interior_reset(ibtk_le_markers m);
 /* Zeroes every patch array of a level, ghosts included, in one launch: the
  * f := 0 before LDataManager::spread accumulates into the level (its
  * f_data_ops->setToScalar(f_data_idx, 0.0, interior_only = false),
