@@ -229,6 +229,18 @@ def level_lists(X, N, P, g):
     return (interior, None, off_i), (es[o2].to(torch.int32).contiguous(), ex[o2].contiguous(), off_s)
 
 
+def binning_label(counts, full_name):
+    """What the timed steps' binning did: full binnings and re-binnings, counted."""
+    f, r = counts.get("full", 0), counts.get("rebin", 0)
+    parts = []
+    if f:
+        parts.append(f"{f} full binning(s) (device radix sort, {full_name})")
+    if r:
+        parts.append(f"{r} re-binning(s) from the previous order (ibtk_le_markers_rebin: every key recomputed "
+                     "from the current positions, the entries whose bucket changed inserted; equal to a full binning)")
+    return " + ".join(parts) + " over the timed steps" if parts else "none in the timed steps (binned once at setup)"
+
+
 # ds_add_f64 cost, conflict-free (tools/ubench_lds2.hip, DESIGN.md section 4): 10 cycles
 # per wave-instruction per CU at 2.4 GHz (MI355X_MICROARCH.md), 256 CUs
 LDS_ADD_CYCLES, CLOCK_GHZ, NCU = 10.0, 2.4, 256
@@ -352,8 +364,10 @@ def run_level(args, cfg, kernel, dev):
             E[1].record()
         if args.full_bin:
             lvl_s.bin(X)
+            binning["full"] += 1
         else:
             lvl_s.rebin(X)  # the same lists (between regrids): from the previous order
+            binning["rebin"] += 1
         lvl_s.select_interior(M, lists["ii"], lists["oi"])
         if record:
             E[2].record()
@@ -365,10 +379,19 @@ def run_level(args, cfg, kernel, dev):
         if record:
             E[5].record()
 
+    nstep = {"k": 0}
+    binning = {"full": 0, "rebin": 0}
+
     def step_move(record):
         # a moving step on the level: interp at the current positions (the interior lists
-        # binned there), X += dt U, the per-patch lists rebuilt at the new positions
-        # (LIndexSetData's lists after redistribution), re-bin, spread
+        # binned there), X += dt U, spread at the new positions.  At a regrid step (every
+        # --regrid-every k-th; IBHierarchyIntegrator's regrid_interval) the positions are
+        # wrapped and the per-patch lists rebuilt (LIndexSetData's lists after the
+        # redistribution; bench.level_lists, torch ops) and binned afresh; between regrids
+        # the lists stay (the markers drift within the ghost width's slack,
+        # LDataManager.cpp:167) and are re-binned at the new positions (ibtk_le_markers_rebin)
+        at_regrid = nstep["k"] % args.regrid_every == 0
+        nstep["k"] += 1
         if record:
             E[0].record()
         fill()
@@ -378,12 +401,17 @@ def run_level(args, cfg, kernel, dev):
         if record:
             E[2].record()
         le.position_update(ctx, "euler", dt_move, X, U, out=X)
-        X.remainder_(1.0)
-        X.masked_fill_(X >= 1.0, 0.0)  # remainder can round up to L
-        (ii2, _, oi2), (si2, sx2, os2) = level_lists(X, N, P, g)
-        lists.update(ii=ii2, oi=oi2)
-        lvl_s.relist(si2, sx2, os2).bin(X)
-        lvl_s.select_interior(M, ii2, oi2)
+        if at_regrid:
+            X.remainder_(1.0)
+            X.masked_fill_(X >= 1.0, 0.0)  # remainder can round up to L
+            (ii2, _, oi2), (si2, sx2, os2) = level_lists(X, N, P, g)
+            lists.update(ii=ii2, oi=oi2)
+            lvl_s.relist(si2, sx2, os2).bin(X)
+            binning["full"] += 1
+        else:
+            lvl_s.rebin(X)
+            binning["rebin"] += 1
+        lvl_s.select_interior(M, lists["ii"], lists["oi"])
         if record:
             E[3].record()
             E[4].record()
@@ -395,11 +423,13 @@ def run_level(args, cfg, kernel, dev):
         step(False)
     ctx.synchronize()
     torch.cuda.synchronize()
+    binning.update(full=0, rebin=0)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(False)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    timed_binning = dict(binning)
     for _ in range(max(3, min(args.steps, 10))):
         step(True)
         torch.cuda.synchronize()
@@ -439,12 +469,14 @@ def run_level(args, cfg, kernel, dev):
         "config": {"workload": cfg["desc"], "kernel": kernel, "grid": [N, N, N], "markers": M,
                    "parallelism": "one GPU", "patches": [P, P, P], "patch_cells": [n, n, n], "ghost": g,
                    "marker_order": args.marker_order, "move": args.move,
-                   "bin": "full device radix sort every step" if args.full_bin or args.move else
-                          "re-binned every step from the previous order (ibtk_le_level_bin's result, "
-                          "ibtk_le_markers_rebin)",
-                   "step": ("level ghost fill + interp(3 comps) + position update + per-patch lists rebuilt "
-                            "(bench.level_lists, torch ops) + bin(ghost-box lists, interior selected) + zero f and "
-                            "spread(3 comps) in one launch" if args.move else
+                   "regrid_every": args.regrid_every if args.move else None,
+                   "bin": binning_label(timed_binning, "ibtk_le_level_bin"),
+                   "step": ("level ghost fill and interp(3 comps) in one launch + position update + "
+                            + (f"at every {args.regrid_every}-th step (regrid) " if args.regrid_every > 1 else "")
+                            + "positions wrapped and per-patch lists rebuilt (bench.level_lists, torch ops) and binned"
+                            + ("; between regrids the lists kept and re-binned at the new positions"
+                               if args.regrid_every > 1 else "")
+                            + " + interior entries selected + zero f and spread(3 comps) in one launch" if args.move else
                             "bin(ghost-box lists; the interior lists select interp's entries) + "
                             + ("level ghost fill + interp(3 comps)" if args.unfused_fill else
                                "level ghost fill and interp(3 comps) in one launch (ibtk_le_level_fill_interp: ghost points "
@@ -634,9 +666,12 @@ def main():
             bad &= torch.arange(Xc.shape[0], device=Xc.device) < n_rows
         drift_flag.logical_or_(bad.any())
 
+    binning = {"full": 0, "rebin": 0}  # what the binning did (the record's "bin" label)
+
     def bin_step():
         if fixed:
             bins.bin_count(geom, kernel, X, n_dev)
+            binning["full"] += 1
             cur.update(X=X, F=F, U=U)
             return
         if gm is None:
@@ -644,14 +679,17 @@ def main():
             # from the previous order (ibtk_le_markers_rebin, exact); else bin afresh
             if not args.full_bin and binned["rows"] == X.shape[0] and not binned["changed"]:
                 bins.rebin(X)
+                binning["rebin"] += 1
             else:
                 bins.bin(geom, kernel, X)
+                binning["full"] += 1
                 binned["rows"] = X.shape[0]
                 binned["changed"] = False
             cur.update(X=X, F=F, U=U)
             return
         Xa, Fa, _ = gm.exchange(X, F)
         bins.bin(geom, kernel, Xa)
+        binning["full"] += 1
         Ua = cur["U"] if cur["U"].shape == Xa.shape else torch.empty_like(Xa)
         cur.update(X=Xa, F=Fa, U=Ua)
 
@@ -860,10 +898,12 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    binning.update(full=0, rebin=0)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(False)
     torch.cuda.synchronize()
+    timed_binning = dict(binning)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -952,11 +992,7 @@ def main():
         "config": {"workload": cfg["desc"], "kernel": kernel, "grid": [N, N, N], "markers": M_total,
                    "parallelism": f"z-slab x{world}", "ghost": ghost, "marker_order": args.marker_order, "layout": args.layout, "spread_mode": args.spread_mode if world > 1 else "one rank",
                    "solo_slab": args.solo_slab or None,
-                   "bin": ("full device radix sort every step" if args.full_bin or fixed or gm is not None
-                           or (args.move and world > 1) else
-                           "re-binned every step from the previous order (ibtk_le_markers_rebin: every key "
-                           "recomputed from the current positions, the entries whose bucket changed inserted; "
-                           "equal to a full binning)"),
+                   "bin": binning_label(timed_binning, "ibtk_le_markers_bin" + ("_count" if fixed else "")),
                    "move": args.move, "renumber": args.renumber,
                    "spread_into": ("zeroed f (LDataManager::spread, LDataManager.cpp:596)" if args.spread_into == "zero"
                                    else "f += S F, ghosts zeroed"),

@@ -1315,10 +1315,35 @@ __device__ __forceinline__ void spread_setup(const Params& p, const CompDesc& cd
             (void)Xraw;
         }
 #else
-        stencil1d<K, true>(cdat.X[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d], d == cd.axis,
-                           p.K6, st[d], inv_d[d]);
+        if constexpr (K == K_IB_4) {
+            // IB_4 (f.m4:1447-1457) with X/dx by a multiply and the anchor by rint: NINT
+            // differs from it only at a tie, where the stencil one cell over carries the
+            // same weights on the same points (the end weight is 0 at r = 0 or 1).  The
+            // weights keep 0.125 (a -+ q) unscaled here (t[]): the x / z scalings below
+            // fold 0.125 into V / 1 / h^3 -- exact powers of two, the same bits.
+            const double xo = (cdat.X[d] - cd.xlo[d]) * inv_d[d];
+            const double n = __builtin_rint(xo);
+            st[d].icl = (int)n + cd.ilower[d] - 2;
+            const double r = xo - (n - 0.5);
+            const double q = sqrt_1_2(1.0 + 4.0 * r * (1.0 - r));
+            const double ta = 3.0 - 2.0 * r, tb = 1.0 + 2.0 * r;
+            st[d].w[0] = ta - q;
+            st[d].w[1] = ta + q;
+            st[d].w[2] = tb + q;
+            st[d].w[3] = tb - q;
+            st[d].ist = max(cd.lo[d] - st[d].icl, 0);
+            st[d].isp = 3 - max(st[d].icl + 3 - cd.hi[d], 0);
+            (void)Xraw;
+        } else {
+            stencil1d<K, true>(cdat.X[d], Xraw, cd.xlo[d], p.bg.dx[d], cd.ilower[d], cd.lo[d], cd.hi[d],
+                               d == cd.axis, p.K6, st[d], inv_d[d]);
+        }
 #endif
     }
+    // IB_4: the weights above are 8 w; 0.125 goes into the x and z scalings (exact)
+    const double sx = K == K_IB_4 ? 0.125 * cdat.V : cdat.V;
+    const double sy = K == K_IB_4 ? 0.125 : 1.0;
+    const double sz = K == K_IB_4 ? 0.125 * inv_h3 : inv_h3;
     const int ox = st[0].icl - X0, oy = st[1].icl - Y0, oz = st[2].icl - (zorg + a);
     // binning invariant: every stencil index lies in [key + LO, key + HI] and the
     // candidates' key cells lie within HI / -LO of the column (key_band), +-1 for
@@ -1341,9 +1366,9 @@ __device__ __forceinline__ void spread_setup(const Params& p, const CompDesc& cd
     double* const wz = T.wz;
 #pragma unroll
     for (int i = 0; i < W; ++i) {
-        wx[i] = (i >= x0 && i <= x1) ? st[0].w[i] * cdat.V : 0.0;  // V applied first (f.m4:1512-1513 up to rounding)
-        wy[i] = (i >= y0 && i <= y1) ? st[1].w[i] : 0.0;
-        wz[i] = st[2].w[i] * inv_h3;  // planes outside [z0, z1] are skipped below
+        wx[i] = (i >= x0 && i <= x1) ? st[0].w[i] * sx : 0.0;  // V applied first (f.m4:1512-1513 up to rounding)
+        wy[i] = (i >= y0 && i <= y1) ? (K == K_IB_4 ? st[1].w[i] * sy : st[1].w[i]) : 0.0;
+        wz[i] = st[2].w[i] * sz;  // planes outside [z0, z1] are skipped below
     }
     // byte offsets in a slot of stencil column / row s: the x and y parts of
     // ring_wrapped
@@ -1424,10 +1449,30 @@ __device__ __forceinline__ void spread_setup(const Params& p, const CompDesc& cd
             }
         }
         int bx[W], by[W];
+        if constexpr (ROT && COLY == 16) {
+            // Step s of a block of 4 takes the stencil column x = ox + c, c = (s + rx) & 3,
+            // whose x & 3 is cls = (s + lane) & 3 (a lane constant) and whose x >> 2 is
+            // (ox >> 2) + [cls < (ox & 3)]: its offset in a slot, 128 ((x >> 2) & 7) + 8 cls,
+            // needs a compare and a select per step (likewise the rows, 1024 ((y >> 2) & 3) + 32 cls)
+            const int lane = lane_id();
+            const int qx = ox >> 2, rxl = ox & 3, qy = oy >> 2, ryl = oy & 3;
 #pragma unroll
-        for (int s = 0; s < W; ++s) {
-            bx[s] = xpart(ROT ? (s & ~3) + (((s & 3) + rx) & 3) : s);
-            by[s] = ypart(ROT ? (s & ~3) + (((s & 3) + ry) & 3) : s);
+            for (int b = 0; b < W; b += 4) {
+                const int hx0 = 128 * ((qx + b / 4) & 7), hx1 = 128 * ((qx + b / 4 + 1) & 7);
+                const int hy0 = 1024 * ((qy + b / 4) & 3), hy1 = 1024 * ((qy + b / 4 + 1) & 3);
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const int cx = (s + lane) & 3, cy = (s + (lane >> 2)) & 3;
+                    bx[b + s] = (cx < rxl ? hx1 : hx0) | (8 * cx);
+                    by[b + s] = (cy < ryl ? hy1 : hy0) | (32 * cy);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < W; ++s) {
+                bx[s] = xpart(ROT ? (s & ~3) + (((s & 3) + rx) & 3) : s);
+                by[s] = ypart(ROT ? (s & ~3) + (((s & 3) + ry) & 3) : s);
+            }
         }
 #pragma unroll
         for (int s1 = 0; s1 < W; ++s1)
@@ -1726,6 +1771,10 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         // compiler, the wait falls mid-step and is vmcnt(0) (the loop-carried copy of a
         // pending load): it then waits for this step's prefetch and writeback too.  cfg4
         // spread sweep 15.0 -> 13.0 ms (round 5).
+#if IBTK_LE_SPREAD_VM8
+        // vmcnt(8): all but the previous step's 8 writeback stores (issued after its loads)
+        __builtin_amdgcn_s_waitcnt(0x0F78);
+#endif
         asm volatile("" ::"v"(cur.X[0]), "v"(cur.X[1]), "v"(cur.X[2]), "v"(cur.V), "v"(rowv[0]), "v"(rowv[1]),
                      "v"(rowv[2]));
         const int cur_r = r_prev, cur_n = n1;
