@@ -177,3 +177,28 @@ def test_rebin_empty_and_tiny(le):
         m.rebin(X2)
         if M:
             _check_same(le, geom, ctx, m, X2, F, u)
+
+
+def test_rebin_after_bin_count_keeps_its_count(le):
+    """ADVICE r4 (medium): a rebin after bin_count reads the count again on the device;
+    the Python wrapper keeps the count tensor alive, and the rebin equals a fresh
+    count-binning even after the caller dropped its reference and the allocator reused
+    the memory."""
+    import gc
+    N = (48, 48, 64)
+    geom = le.Geometry.periodic_unit(list(N), 3)
+    rng = np.random.default_rng(12)
+    cap, M = 12000, 10000
+    X = torch.zeros((cap, 3), dtype=torch.float64, device="cuda")
+    X[:M] = torch.from_numpy(rng.uniform(0.0, 1.0, (M, 3))).cuda()
+    ctx = le.Context(0)
+    m = le.Markers(ctx).bin_count(geom, "IB_4", X, torch.tensor([M], dtype=torch.int32, device="cuda"))
+    gc.collect()
+    junk = [torch.full((1 << 16,), 7, dtype=torch.int32, device="cuda") for _ in range(8)]  # reuse freed blocks
+    h = 1.0 / max(N)
+    X[:M] = torch.remainder(X[:M] + 0.3 * h * (torch.rand_like(X[:M]) - 0.5), 1.0)
+    m.rebin(X)
+    fresh = le.Markers(ctx).bin_count(geom, "IB_4", X, torch.tensor([M], dtype=torch.int32, device="cuda"))
+    ctx.synchronize()
+    assert torch.equal(m.order(), fresh.order())
+    del junk
