@@ -180,6 +180,12 @@ struct ibtk_le_markers_s {
     DevBuf cand_cnt, cand_off, cand_idx;  // spread candidate lists, built on first use after a bin
     DevBuf last, qdst;                    // interp with duplicate list entries (Params::qdst)
     DevBuf items, nsub, isub, nitems;     // 3-D sweep item table
+    // the 3-D spread's candidate stream (launch_cand_stream), built on the first spread after
+    // a binning: 0 stale, 1 built, 2 stale unless the last re-binning moved nothing (the
+    // build then skips on the device, cs_skip = that re-binning's mover count)
+    DevBuf cs_cnt, cs_off, cs_pos;
+    int cs_state = 0;
+    const int* cs_skip = nullptr;
     int item_bound = 0;
     // a level of patches (ibtk_le_level_bin): 0 = one patch (the fields above)
     int npatch = 0;
@@ -588,6 +594,10 @@ constexpr int LEVEL_SPLIT_TARGET = 1024;
 #define IBTK_LE_SPLIT_TARGET 12288  // own markers per item above which it is cut (cfg4 items hold ~6.8K)
 #endif
 static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const int* skip_if_zero = nullptr) {
+    // the candidate stream follows the bucket starts: kept only across a re-binning that
+    // moved nothing since it was built (decided on the device)
+    m->cs_state = (m->cs_state == 1 && skip_if_zero) ? 2 : 0;
+    m->cs_skip = skip_if_zero;
     const int nj = m->npatch ? m->njobs : m->cg.ncol * m->nseg;
     // a level's items (patches of a few 32-plane segments, clustered markers on a few of
     // them) are cut at 1024 own markers, one plane per piece at least: cfg5 3.9e9 -> 4.1e9
@@ -1387,6 +1397,36 @@ extern "C" int ibtk_le_user_spread(ibtk_le_ctx ctx, int centering, int axis, con
                      indices_dev, Xshift_dev, n);
 }
 
+// The 3-D spread's candidate stream of m's binning (le_sweep.hip, launch_cand_stream):
+// built on the first spread after a binning, kept until the next; p.cs_* set.
+static int cand_stream(ibtk_le_ctx ctx, ibtk_le_markers m, Params& p) {
+    const long long ncl = (long long)m->nbuckets_total / NBAND;
+    // a marker is a candidate of at most four columns (its own, one x- and one y-neighbour,
+    // the corner between them: a stencil never reaches both neighbours in a dim)
+    const long long cap = std::max(4LL * m->n, 1LL);
+    if (cap >= (1LL << 31) || ncl + 1 >= (1LL << 31)) return fail(IBTK_LE_ERR_RANGE, "candidate stream too long");
+    p.cs_off = m->cs_off.as<int>();
+    p.cs_pos = m->cs_pos.as<int>();
+    p.cs_total = (int)cap;
+    if (m->cs_state == 1 && m->cs_pos.p) return IBTK_LE_OK;
+    int rc;
+    if ((rc = m->cs_cnt.ensure(sizeof(int) * (size_t)(ncl + 1)))) return rc;
+    if ((rc = m->cs_off.ensure(sizeof(int) * (size_t)(ncl + 1)))) return rc;
+    if ((rc = m->cs_pos.ensure(sizeof(int) * (size_t)cap))) return rc;
+    p.cs_off = m->cs_off.as<int>();
+    p.cs_pos = m->cs_pos.as<int>();
+    HIP_TRY(hipMemsetAsync(m->cs_cnt.as<int>() + ncl, 0, sizeof(int), ctx->stream));
+    size_t tb = 0;
+    HIP_TRY(launch_scan(nullptr, tb, m->cs_cnt.as<int>(), m->cs_off.as<int>(), (int)(ncl + 1), ctx->stream));
+    if ((rc = ctx->temp.ensure(tb))) return rc;
+    Params q = p;
+    q.items_skip = m->cs_state == 2 ? m->cs_skip : nullptr;
+    HIP_TRY(launch_cand_stream(q, (int)ncl, m->cs_cnt.as<int>(), m->cs_off.as<int>(), m->cs_pos.as<int>(), ctx->temp.p,
+                               ctx->temp.cap, ctx->stream));
+    m->cs_state = 1;
+    return IBTK_LE_OK;
+}
+
 static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                        const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
                        int Q_depth, const double* ds_dev, const double* X_dev, bool zero_ghosts, bool zero_first) {
@@ -1411,6 +1451,8 @@ static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cente
         if (int rc = build_candidates(ctx, m, p)) return rc;
         p.cand_off = m->cand_off.as<int>();
         p.cand_idx = m->cand_idx.as<int>();
+    } else if (int rc = cand_stream(ctx, m, p)) {
+        return rc;
     }
     ctx->ev_valid = false;
     for (int first = 0; first < nc; first += MAXC) {
@@ -1758,6 +1800,7 @@ static int level_spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int
         if (int rc = ctx->fbuf.ensure(sizeof(double) * (size_t)m->n * (size_t)nc)) return rc;
         p.sorted_F = ctx->fbuf.as<double>();
     }
+    if (int rc = cand_stream(ctx, m, p)) return rc;
     const bool t = ctx->timing;
     ctx->ev_valid = false;
     const size_t nst = (size_t)m->item_bound * nc * 8;

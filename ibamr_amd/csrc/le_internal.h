@@ -169,6 +169,9 @@ struct Params {
                                // (brick b's entries are [plane_start[b*B], plane_start[(b+1)*B]))
     const int* cand_off;       // spread: (super-brick, class) candidate lists: offsets, items*NCLS + 1
     const int* cand_idx;       // spread: candidate sorted positions, canonical order per super-brick
+    const int* cs_off;         // 3-D spread: candidate stream offsets per column-anchor (launch_cand_stream)
+    const int* cs_pos;         // 3-D spread: the candidate stream (sorted positions)
+    int cs_total;              // its length
     const int* nentries_dev;   // device copy of the list length
     const double* Qin;         // spread: marker values
     const double* sorted_F;    // spread: Qin gathered in sorted order, [comp][sorted position]
@@ -284,6 +287,10 @@ hipError_t launch_spread_sweep(int kernel, const Params& p, hipStream_t s, hipEv
 void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items, bool level);
 hipError_t launch_item_table(int kernel, const Params& p, int target, int heavy, int* nsub, int* start, SweepItem* tab, int* ntot,
                              void* temp, size_t temp_bytes, hipStream_t s);
+// the spread's candidate stream of a 3-D column binning: cnt[ncl + 1] (cnt[ncl] = 0 on entry),
+// off[ncl + 1] (off[ncl] = the length), pos[length]; p.items_skip as for the item table
+hipError_t launch_cand_stream(const Params& p, int ncl, int* cnt, int* off, int* pos, void* temp, size_t temp_bytes,
+                              hipStream_t s);
 
 // Periodic helpers
 struct GhostDesc {

@@ -1236,6 +1236,109 @@ __device__ __forceinline__ int range_pos(const Ranges& R, int j) {
     return pos;
 }
 
+// ---------------------------------------------------------------------------
+// the spread's candidate stream (built once per binning, on the first spread)
+// ---------------------------------------------------------------------------
+// Per (patch, column, anchor plane) -- "column-anchor" ca, column-major within a
+// patch (ca = bucket_base / NBAND + col * nz + a) -- the sorted positions of the
+// markers whose stencil reaches the column from that anchor plane: the 11 ranges of
+// make_ranges_lanes, in that order.  A column's anchors are consecutive, so chunk 1
+// of an anchor (the previous anchor's leftovers, then its own first) is one piece of
+// the stream, and the sweep needs no range arithmetic per chunk.  k_cand_count: the
+// lengths; an exclusive scan: cs_off; k_cand_write: the positions (a wave per ca).
+__device__ __forceinline__ bool ca_decode(const Params& p, int ca, ColGeom& cg, int& col, int& a, const int*& bs) {
+    int base = 0;
+    if (p.pd) {
+        int lo = 0, hi = p.npatch - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (p.pd[mid].bucket_base / NBAND <= ca) lo = mid;
+            else hi = mid - 1;
+        }
+        const PatchDesc& P = p.pd[lo];
+        cg = P.cg;
+        base = P.bucket_base / NBAND;
+        bs = p.plane_start + P.bucket_base;
+    } else {
+        cg = p.cg;
+        bs = p.plane_start;
+    }
+    const int l = ca - base;
+    col = l / cg.nz;
+    a = l - col * cg.nz;
+    const int cx = col % cg.ncx, cy = col / cg.ncx;
+    return !(cx == 0 || cx == cg.ncx - 1 || cy == 0 || cy == cg.ncy - 1);  // guard columns: no items
+}
+// the 11 candidate ranges of (column col, anchor a): begin / end sorted positions
+__device__ __forceinline__ void ca_range(const ColGeom& cg, const int* bs, int col, int a, int r, int& b, int& e) {
+    constexpr int rr[11] = {0, 0, 0, 0, 0, 1, 2, 2, 2, 2, 2};
+    constexpr int ib[11] = {8, 11, 14, 17, 20, 6, 6, 9, 12, 15, 18};
+    constexpr int ie[11] = {9, 12, 15, 18, 21, 21, 7, 10, 13, 16, 19};
+    const int cx = col % cg.ncx, cy = col / cg.ncx;
+    const int base = bucket(cg, a, (cy - 1 + rr[r]) * cg.ncx + (cx - 1), 0);
+    b = bs[base + ib[r]];
+    e = bs[base + ie[r]];
+}
+// (grid-stride loops over the column-anchors on a bounded grid: with nothing moved
+// the launches return at once, and cfg5's 0.5 M column-anchors, mostly empty, cost
+// no launch of their own)
+constexpr int CS_GRID = 8192;
+__global__ __launch_bounds__(BLOCK) void k_cand_count(Params p, int ncl, int* cnt) {
+    if (p.items_skip && *p.items_skip == 0) return;  // a re-binning that moved nothing: the stream stands
+    for (int ca = blockIdx.x * BLOCK + threadIdx.x; ca < ncl; ca += gridDim.x * BLOCK) {
+        ColGeom cg;
+        int col, a;
+        const int* bs;
+        int t = 0;
+        if (ca_decode(p, ca, cg, col, a, bs)) {
+#pragma unroll
+            for (int r = 0; r < 11; ++r) {
+                int b, e;
+                ca_range(cg, bs, col, a, r, b, e);
+                t += e - b;
+            }
+        }
+        cnt[ca] = t;
+    }
+}
+// a wave per column-anchor: its three rows of bucket starts one entry a lane (three
+// coalesced loads), the ranges made once (make_ranges_lanes), then stream entry j of it
+// by range_pos, 64 a store
+__global__ __launch_bounds__(BLOCK) void k_cand_write(Params p, int ncl, const int* off, int* pos) {
+    if (p.items_skip && *p.items_skip == 0) return;
+    const int lane = threadIdx.x & (SW - 1);
+    const int nw = gridDim.x * (BLOCK / SW);
+    for (int ca = blockIdx.x * (BLOCK / SW) + (int)(threadIdx.x / SW); ca < ncl; ca += nw) {
+        ColGeom cg;
+        int col, a;
+        const int* bs;
+        if (!ca_decode(p, ca, cg, col, a, bs)) continue;
+        const int o = off[ca];
+        if (off[ca + 1] == o) continue;  // no candidate
+        const int cx = col % cg.ncx, cy = col / cg.ncx;
+        const int col0 = (cy - 1) * cg.ncx + (cx - 1);
+        int rowv[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) rowv[r] = bs[bucket(cg, a, col0 + r * cg.ncx, 0) + min(lane, 27)];
+        Ranges R;
+        make_ranges_lanes(rowv, R);
+        const int t = R.pre[SSh<K_IB_4>::NR];
+        for (int j = lane; j < t; j += SW) pos[o + j] = range_pos(R, j);
+    }
+}
+hipError_t launch_cand_stream(const Params& p, int ncl, int* cnt, int* off, int* pos, void* temp, size_t temp_bytes,
+                              hipStream_t s) {
+    if (ncl <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_cand_count, dim3(std::min((ncl + BLOCK - 1) / BLOCK, CS_GRID)), dim3(BLOCK), 0, s, p, ncl,
+                       cnt);
+    hipError_t e = launch_scan(temp, temp_bytes, cnt, off, ncl + 1, s);  // cnt[ncl] = 0: off[ncl] = the total
+    if (e != hipSuccess) return e;
+    const int per = BLOCK / SW;
+    hipLaunchKernelGGL(k_cand_write, dim3(std::min((ncl + per - 1) / per, CS_GRID)), dim3(BLOCK), 0, s, p, ncl, off,
+                       pos);
+    return hipGetLastError();
+}
+
 // candidate data of one lane
 struct Cand {
     double X[3];
@@ -1587,12 +1690,11 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         if (inner != (p.zmode == 1)) return;
     }
     const int afirst = max(plo - HI, 0), alast = min(phi - LO, cg.nz - 1);
-    const int col0 = (cy - 1) * ncx + (cx - 1);  // column (cx-1, cy-1)
-    bool any = false;  // no candidate reaches the item: u unchanged (zero_first: 0; zero_ghosts: ghosts 0)
-    for (int a = afirst + lane; a <= alast; a += SW)
-        for (int r = 0; r < 3; ++r)
-            any = any || bs[bucket(cg, a, col0 + r * ncx, 3 * NBAND)] > bs[bucket(cg, a, col0 + r * ncx, 0)];
-    any = __any(any);
+    // the item's stretch of its column's candidate stream (k_cand_stream, column-major
+    // (patch, column, anchor) order): anchors afirst .. alast are [cs_off[ca0], cs_off[ca0 + nk])
+    const int ca0 = (LVL ? p.pd[si.patch].bucket_base / NBAND : 0) + col * cg.nz + afirst;
+    // no candidate reaches the item: u unchanged (zero_first: 0; zero_ghosts: ghosts 0)
+    const bool any = p.cs_off[ca0 + (alast - afirst + 1)] > p.cs_off[ca0];
     // zero_ghosts (ibtk_le_zero_ghosts_spread): the owned points outside the component's
     // data box start from 0 instead of their values -- ibtk_le_zero_ghosts fused in
     const bool zg = p.zero_ghosts && !p.zero_first;
@@ -1637,15 +1739,9 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         }
         return;
     }
-    // bucket starts of anchor plane a: rows cy-1, cy, cy+1 (28 entries: bands of
-    // columns cx-1 .. cx+1), one entry per lane
-    auto rows_load = [&](int a, int* rowv) {
-#pragma unroll
-        for (int r = 0; r < 3; ++r) rowv[r] = bs[bucket(cg, a, col0 + r * ncx, 0) + min(lane, 27)];
-    };
     // candidate data of sorted position e
     auto cand_at = [&](int e, Cand& d) {
-        e = min(e, nlast);
+        e = min(max(e, 0), nlast);  // (an idle lane's stream entry may lie past the stream's end)
 #if IBTK_LE_DIAG_SPREAD & 8  // diagnostic: no candidate loads
         d.X[0] = d.X[1] = d.X[2] = 0.5 + 1e-9 * e;
         d.V = 1.0;
@@ -1738,99 +1834,121 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     // lanes 0..r-1) and the first 64-r of a; full middle chunks of a follow;
     // a's last partial chunk is carried into a+1's chunk 1.  The ring holds the
     // planes of anchors a-1 and a: [a-1+LO, a+HI].
+    // The candidates come from the column's candidate stream (k_cand_stream): the
+    // sorted positions of the 11 candidate ranges of every anchor plane, anchor after
+    // anchor, so that chunk 1 of an anchor is one contiguous piece of it, and the
+    // anchor boundaries o(k) = cs_off[ca0 + k] (k = a - afirst).  Each step loads the
+    // positions of chunk 1 two anchors ahead and the candidates of chunk 1 one anchor
+    // ahead (from the positions loaded at the step before).
     clk.start(p.stamps != nullptr);
-    // prologue: planes afirst+LO .. afirst+HI-1 into the ring; planes afirst+HI and
-    // afirst+HI+1, the ranges and chunk 1 of afirst into registers
+    const int* const cs_pos = p.cs_pos;
+    const int cs_last = p.cs_total - 1;
+    const int nk = alast - afirst + 1;  // anchors of the item; o(nk) ends its stream
+    auto off_load = [&](int k) { return p.cs_off[ca0 + min(k, nk)]; };
+    auto pos_load = [&](int j) { return cs_pos[min(max(j, 0), cs_last)]; };
+    // prologue: planes afirst+LO .. afirst+HI-1 into the ring; plane afirst+HI, the
+    // anchor boundaries o(0) .. o(3), chunk 1 of afirst and the positions of chunk 1
+    // of afirst + 1 into registers
     double pv[NPL] = {};
     for (int z = afirst + LO; z < afirst + HI; ++z) {
         plane_load(z, pv);
         plane_put(z, pv);
     }
     plane_load(afirst + HI, pv);
-    int rowv[3];
-    rows_load(afirst, rowv);
-    Ranges rg;  // ranges of the anchor whose chunk 1 is prefetched (wave-uniform)
-    make_ranges_lanes(rowv, rg);
-    int tA = rg.pre[S::NR];
-    Cand nxt, nxt2;  // chunk 1 of the anchor of the step, of the next
-    cand_at(range_pos(rg, min(lane, max(tA - 1, 0))), nxt);
-    int r_prev = 0;        // candidates of anchor a-1 carried into a's chunk 1
-    int n1 = min(tA, SW);  // lanes of a's chunk 1
-    if (afirst + 1 <= alast) rows_load(afirst + 1, rowv);
+    int O0 = __builtin_amdgcn_readfirstlane(off_load(0)), O1 = __builtin_amdgcn_readfirstlane(off_load(1));
+    int O2 = __builtin_amdgcn_readfirstlane(off_load(2)), O3 = __builtin_amdgcn_readfirstlane(off_load(3));
+    int O4v = off_load(4);  // o(k + 4), in flight
+    int R0 = 0;                                 // candidates of anchor k-1 carried into chunk 1 of k
+    int N0 = min(O1 - O0, SW);                  // lanes of chunk 1 of k
+    int R1 = (O1 - O0 - N0) % SW;               // carried into chunk 1 of k+1
+    int N1 = R1 + min(SW - R1, O2 - O1);        // lanes of chunk 1 of k+1
+    Cand nxt, nxt2;                             // chunk 1 of k, of k+1
+    {
+        const int e0 = pos_load(O0 + min(lane, max(N0 - 1, 0)));
+        cand_at(e0, nxt);
+    }
+    int I1 = pos_load(O1 - R1 + min(lane, max(N1 - 1, 0)));  // positions of chunk 1 of k+1, in flight
     clk.lap(0);
     // One anchor step: plane a+HI from registers into the ring, plane a+HI+1 into
     // registers.  (Two anchors ahead through two register buffers measured the same,
     // 16.1 vs 16.3 ms on cfg4: the streams are not what waits.)
     auto anchor_step = [&](int a, const Cand& cur, Cand& nxt) __attribute__((always_inline)) {
+        const int k = a - afirst;
         const int zw = a - 2 + LO;  // no anchor left reaches it: written back this step
         double wb[NPL];
         wb_read(zw, wb);       // its slot ...
         plane_put(a + HI, pv);  // ... takes plane a+HI
-        // The step's inputs loaded at the previous step (chunk 1, the rows of a+1) are
-        // waited for here, before this step issues its own loads and stores.  Left to the
-        // compiler, the wait falls mid-step and is vmcnt(0) (the loop-carried copy of a
-        // pending load): it then waits for this step's prefetch and writeback too.  cfg4
-        // spread sweep 15.0 -> 13.0 ms (round 5).
-#if IBTK_LE_SPREAD_VM8
-        // vmcnt(8): all but the previous step's 8 writeback stores (issued after its loads)
-        __builtin_amdgcn_s_waitcnt(0x0F78);
-#endif
-        asm volatile("" ::"v"(cur.X[0]), "v"(cur.X[1]), "v"(cur.X[2]), "v"(cur.V), "v"(rowv[0]), "v"(rowv[1]),
-                     "v"(rowv[2]));
-        const int cur_r = r_prev, cur_n = n1;
-        const int tCur = tA;
-        const int h = min(SW - r_prev, tCur);  // a's candidates in chunk 1
-        const int nmid = (tCur - h) / SW;       // full middle chunks
-        const int r_a = (tCur - h) % SW;        // carried into a+1
+        // The step's inputs loaded at the previous step (chunk 1, the positions of the
+        // next chunk 1, an anchor boundary) are waited for here, before this step issues
+        // its own loads and stores.  Left to the compiler, the wait falls mid-step and is
+        // vmcnt(0) (the loop-carried copy of a pending load): it then waits for this
+        // step's prefetch and writeback too.  cfg4 spread sweep 15.0 -> 13.0 ms (round 5).
+        asm volatile("" ::"v"(cur.X[0]), "v"(cur.X[1]), "v"(cur.X[2]), "v"(cur.V), "v"(I1), "v"(O4v));
+        const int O4 = __builtin_amdgcn_readfirstlane(O4v);
+        const int cur_r = R0, cur_n = N0;
+        const int tCur = O1 - O0;
+        const int h = min(SW - R0, tCur);   // a's candidates in chunk 1
+        const int nmid = (tCur - h) / SW;   // full middle chunks
+        const int r_a = R1;                 // carried into a+1: (tCur - h) % SW
         clk.lap(1);
-        // prefetch for a+1: its ranges, its chunk 1 (a's last r_a, then a+1's
-        // first), the rows of a+2; plane a+HI+1
+        // prefetch: the candidates of chunk 1 of a+1 (positions I1), the positions of
+        // chunk 1 of a+2 (a+1's last r, then a+2's first), the boundary o(k+5); plane a+HI+1
+        int R2 = 0, N2 = 0;
         if (a + 1 <= alast) {
-            const int eA = range_pos(rg, max(tCur - r_a + lane, 0));  // rg: a's ranges
-            make_ranges_lanes(rowv, rg);
-            tA = rg.pre[S::NR];
-            const int eB = range_pos(rg, min(max(lane - r_a, 0), max(tA - 1, 0)));
-            cand_at(lane < r_a ? eA : eB, nxt);
-            n1 = r_a + min(SW - r_a, tA);
-            r_prev = r_a;
+            cand_at(I1, nxt);
+            const int t1 = O2 - O1;
+            R2 = (t1 - min(SW - R1, t1)) % SW;
+            N2 = R2 + min(SW - R2, O3 - O2);
+            I1 = pos_load(O2 - R2 + min(lane, max(N2 - 1, 0)));
+            O4v = off_load(k + 5);
             plane_load(a + HI + 1, pv);
-            if (a + 2 <= alast) rows_load(a + 2, rowv);
         }
         const bool wbon = a >= afirst + 2;
         if (cur_n > 0) process(a, cur_r, cur_n, cur, [&] { wb_store(zw, wbon, wb); });
         else wb_store(zw, wbon, wb);
-        if (nmid > 0) {  // dense planes: the full middle chunks (ranges of a rebuilt)
-            int rowm[3];
-            rows_load(a, rowm);
-            Ranges rgm;
-            make_ranges_lanes(rowm, rgm);
-            // chunk k + 1's candidates load while chunk k is added (a dense plane,
-            // e.g. a sheet of markers, is hundreds of chunks of one wave)
+        if (nmid > 0) {  // dense planes: the full middle chunks, stream positions O0 + h + 64 m
+            // chunk m + 1's candidates load while chunk m is added (a dense plane, e.g. a
+            // sheet of markers, is hundreds of chunks of one wave); their positions a chunk earlier
+            const int mbase = O0 + h + lane;
             Cand more, more2;
-            cand_at(range_pos(rgm, h + lane), more);
-            int k = 0;
+            cand_at(pos_load(mbase), more);
+            int m = 0;
             if constexpr (PAIR) {
                 // two chunks set up before either's adds (two independent chains of
-                // set-up arithmetic per lane); their adds keep the chunk order
-                if (nmid > 1) cand_at(range_pos(rgm, h + SW + lane), more2);
-                for (; k + 1 < nmid; k += 2) {
+                // set-up arithmetic per lane); their adds keep the chunk order.  The
+                // positions of a pair are loaded while the pair before it is added.
+                if (nmid > 1) cand_at(pos_load(mbase + SW), more2);
+                int q2 = pos_load(mbase + SW * 2), q3 = pos_load(mbase + SW * 3);
+                for (; m + 1 < nmid; m += 2) {
                     const Cand n0 = more, n1 = more2;
-                    if (k + 2 < nmid) cand_at(range_pos(rgm, h + SW * (k + 2) + lane), more);
-                    if (k + 3 < nmid) cand_at(range_pos(rgm, h + SW * (k + 3) + lane), more2);
+                    if (m + 2 < nmid) cand_at(q2, more);
+                    if (m + 3 < nmid) cand_at(q3, more2);
+                    q2 = pos_load(mbase + SW * (m + 4));
+                    q3 = pos_load(mbase + SW * (m + 5));
                     process2(a, n0, n1);
                 }
             }
-            for (; k < nmid; ++k) {
+            int q1 = pos_load(mbase + SW * (m + 1));
+            for (; m < nmid; ++m) {
                 const Cand now = more;
-                if (k + 1 < nmid) cand_at(range_pos(rgm, h + SW * (k + 1) + lane), more);
+                if (m + 1 < nmid) cand_at(q1, more);
+                q1 = pos_load(mbase + SW * (m + 2));
                 process(a, 0, SW, now, nothing);
             }
         }
-        if (a == alast && r_a > 0) {  // the last anchor's leftovers (rg: a's ranges)
+        if (a == alast && r_a > 0) {  // the last anchor's leftovers: stream O1 - r_a .. O1 - 1
             Cand last;
-            cand_at(range_pos(rg, tCur - r_a + min(lane, r_a - 1)), last);
+            cand_at(pos_load(O1 - r_a + min(lane, r_a - 1)), last);
             process(a, 0, r_a, last, nothing);
         }
+        R0 = R1;
+        N0 = N1;
+        R1 = R2;
+        N1 = N2;
+        O0 = O1;
+        O1 = O2;
+        O2 = O3;
+        O3 = O4;
         clk.lap(4);
     };
     for (int a = afirst; a <= alast; ++a) {
