@@ -191,7 +191,8 @@ def cpu_baseline(cfg, kernel, seconds_target=15.0):
 
 def level_lists(X, N, P, g):
     """LIndexSetData's per-patch lists on a level of P^3 equal patches tiling a
-    periodic [0,1)^3 (device torch ops): the interior lists (markers whose cell is
+    periodic [0,1)^3 in torch ops -- the check for ibtk_le_level_index_lists, which the
+    bench uses (tests/test_gpu_level_lists.py): the interior lists (markers whose cell is
     in the patch box, for interp) and the ghost-box lists (the markers and their
     periodic images whose cell is in the patch's ghost box, for spread,
     LDataManager.cpp:634-654).  Returns flat (indices, Xshift, offsets) per kind,
@@ -305,7 +306,8 @@ def run_level(args, cfg, kernel, dev):
     gen = torch.Generator(device=dev).manual_seed(4321)
     F = torch.rand((M, 3), dtype=torch.float64, device=dev, generator=gen).mul_(2).sub_(1)
     U = torch.zeros((M, 3), dtype=torch.float64, device=dev)
-    (ii, _, oi), (si, sx, os_) = level_lists(X, N, P, g)
+    # the per-patch lists (LIndexSetData::cacheLocalIndices) built on the device in one call
+    (ii, _, oi), (si, sx, os_) = le.level_index_lists(ctx, geoms, [0, 0, 0], [N - 1] * 3, X, g)
     # one binning serves both sweeps: the ghost-box lists (spread), told which of their
     # entries the interior lists (interp) name (ibtk_le_level_select_interior)
     lvl_s = le.Level.from_flat(ctx, geoms, kernel, X, si, sx, os_)
@@ -387,7 +389,7 @@ def run_level(args, cfg, kernel, dev):
         # binned there), X += dt U, spread at the new positions.  At a regrid step (every
         # --regrid-every k-th; IBHierarchyIntegrator's regrid_interval) the positions are
         # wrapped and the per-patch lists rebuilt (LIndexSetData's lists after the
-        # redistribution; bench.level_lists, torch ops) and binned afresh; between regrids
+        # redistribution; ibtk_le_level_index_lists, one device pass) and binned afresh; between regrids
         # the lists stay (the markers drift within the ghost width's slack,
         # LDataManager.cpp:167) and are re-binned at the new positions (ibtk_le_markers_rebin)
         at_regrid = nstep["k"] % args.regrid_every == 0
@@ -404,7 +406,7 @@ def run_level(args, cfg, kernel, dev):
         if at_regrid:
             X.remainder_(1.0)
             X.masked_fill_(X >= 1.0, 0.0)  # remainder can round up to L
-            (ii2, _, oi2), (si2, sx2, os2) = level_lists(X, N, P, g)
+            (ii2, _, oi2), (si2, sx2, os2) = le.level_index_lists(ctx, geoms, [0, 0, 0], [N - 1] * 3, X, g)
             lists.update(ii=ii2, oi=oi2)
             lvl_s.relist(si2, sx2, os2).bin(X)
             binning["full"] += 1
@@ -473,7 +475,7 @@ def run_level(args, cfg, kernel, dev):
                    "bin": binning_label(timed_binning, "ibtk_le_level_bin"),
                    "step": ("level ghost fill and interp(3 comps) in one launch + position update + "
                             + (f"at every {args.regrid_every}-th step (regrid) " if args.regrid_every > 1 else "")
-                            + "positions wrapped and per-patch lists rebuilt (bench.level_lists, torch ops) and binned"
+                            + "positions wrapped and per-patch lists rebuilt (ibtk_le_level_index_lists, on the device) and binned"
                             + ("; between regrids the lists kept and re-binned at the new positions"
                                if args.regrid_every > 1 else "")
                             + " + interior entries selected + zero f and spread(3 comps) in one launch" if args.move else

@@ -142,6 +142,7 @@ struct ibtk_le_ctx_s {
     DevBuf lst_idx, lst_xs, lst_key, lst_perm;  // index-list / node-distribution scratch
     DevBuf lst_cell, lst2_idx, lst2_xs, lst2_cell, lst_flag;  // index lists: cells, the sorted list, unique flags
     DevBuf num_tab, num_lkey, num_ckey;                        // level numbering: tile table, keys
+    DevBuf ll_cnt, ll_key, ll_key2, ll_id, ll_id2, ll_src, ll_img, ll_off;  // level index lists
     DevBuf lvl_tab;                             // level ghost fill tables
     std::vector<char> lvl_host;                 // what lvl_tab holds
     DevBuf zero_tab;                            // level zero tables
@@ -186,6 +187,14 @@ struct ibtk_le_markers_s {
     DevBuf cs_cnt, cs_off, cs_pos;
     int cs_state = 0;
     const int* cs_skip = nullptr;
+    // closed-form kernels: the stream split by the shifted-z anchor and its boundaries in
+    // that frame (cs_off_z, nclz = Σ ncol (nz + 1) + 1 entries) -- built with the stream
+    // when a spread's components need them (cs_split)
+    DevBuf cs_off_z;
+    bool cs_split = false;
+    long long nclz = 0;
+    // the re-binning's shifted-z anchor parities and their state (RebinBufs::zbits, zst)
+    DevBuf zbits, zst;
     int item_bound = 0;
     // a level of patches (ibtk_le_level_bin): 0 = one patch (the fields above)
     int npatch = 0;
@@ -255,7 +264,8 @@ extern "C" int ibtk_le_ctx_destroy(ibtk_le_ctx ctx) {
                       &ctx->usr_last, &ctx->usr_x0, &ctx->usr_x1, &ctx->temp, &ctx->counts, &ctx->offsets, &ctx->fbuf, &ctx->err, &ctx->sink,
                        &ctx->stamps, &ctx->lst_idx, &ctx->lst_xs, &ctx->lst_key, &ctx->lst_perm, &ctx->lst_cell,
                        &ctx->lst2_idx, &ctx->lst2_xs, &ctx->lst2_cell, &ctx->lst_flag, &ctx->num_tab, &ctx->num_lkey,
-                       &ctx->num_ckey,
+                       &ctx->num_ckey, &ctx->ll_cnt, &ctx->ll_key, &ctx->ll_key2, &ctx->ll_id, &ctx->ll_id2,
+                       &ctx->ll_src, &ctx->ll_img, &ctx->ll_off,
                        &ctx->lvl_tab, &ctx->zero_tab, &ctx->mig_cls, &ctx->mig_cnt, &ctx->adds})
         b->release();
     if (ctx->ev0) hipEventDestroy(ctx->ev0);
@@ -567,7 +577,8 @@ extern "C" int ibtk_le_markers_destroy(ibtk_le_markers m) {
                       &m->xshift, &m->cand_cnt, &m->cand_off, &m->cand_idx, &m->last, &m->qdst, &m->items,
                       &m->nsub, &m->isub, &m->nitems, &m->pd, &m->entry_off, &m->qin, &m->owner, &m->int_off,
                       &m->rb_cin, &m->rb_cout, &m->rb_d, &m->rb_dpre, &m->rb_mstart, &m->rb_ps2, &m->rb_mbits,
-                      &m->rb_wcnt, &m->rb_wpre, &m->rb_mlist, &m->rb_scr, &m->rb_big, &m->rb_nbig})
+                      &m->rb_wcnt, &m->rb_wpre, &m->rb_mlist, &m->rb_scr, &m->rb_big, &m->rb_nbig, &m->cs_cnt,
+                      &m->cs_off, &m->cs_pos, &m->cs_off_z, &m->zbits, &m->zst, &m->sel_gs})
         b->release();
     delete m;
     return IBTK_LE_OK;
@@ -598,6 +609,8 @@ static int build_items(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, const int
     // moved nothing since it was built (decided on the device)
     m->cs_state = (m->cs_state == 1 && skip_if_zero) ? 2 : 0;
     m->cs_skip = skip_if_zero;
+    // a fresh binning's order is not the one the last re-binning's parities follow
+    if (!skip_if_zero && m->zst.p) HIP_TRY(hipMemsetAsync(m->zst.p, 0, sizeof(int), ctx->stream));
     const int nj = m->npatch ? m->njobs : m->cg.ncol * m->nseg;
     // a level's items (patches of a few 32-plane segments, clustered markers on a few of
     // them) are cut at 1024 own markers, one plane per piece at least: cfg5 3.9e9 -> 4.1e9
@@ -746,6 +759,10 @@ extern "C" int ibtk_le_markers_rebin(ibtk_le_ctx ctx, ibtk_le_markers m, const d
     for (DevBuf* b : {&m->rb_mlist, &m->rb_scr})
         if ((rc = b->ensure(sizeof(int) * (size_t)n))) return rc;
     if ((rc = m->rb_nbig.ensure(sizeof(int)))) return rc;
+    if ((rc = m->zbits.ensure(wb))) return rc;
+    const bool znew = !m->zst.p;
+    if ((rc = m->zst.ensure(2 * sizeof(int)))) return rc;
+    HIP_TRY(hipMemsetAsync(m->zst.as<int>() + (znew ? 0 : 1), 0, (znew ? 2 : 1) * sizeof(int), s));
     if ((rc = ctx->keys_in.ensure(sizeof(unsigned) * (size_t)n))) return rc;
     if ((rc = ctx->vals_in.ensure(sizeof(int) * (size_t)n))) return rc;
     if (fresh) {  // the in/out counts start from zero (k_rebin_append leaves them so)
@@ -807,6 +824,8 @@ extern "C" int ibtk_le_markers_rebin(ibtk_le_ctx ctx, ibtk_le_markers m, const d
     r.xa = m->sorted_X.as<double>();
     r.xb = m->sorted_X2.as<double>();
     r.order_gen = m->sel_gs.p ? m->sel_gs.as<int>() : nullptr;
+    r.zbits = m->zbits.as<unsigned>();
+    r.zst = m->zst.as<int>();
     // k_rekey raises the per-bucket mover counts and k_rebin_append consumes them back
     // to zero: until the sequence has been queued whole, the next call must clear them
     m->rb_zeroed_nb = -1;
@@ -1398,32 +1417,51 @@ extern "C" int ibtk_le_user_spread(ibtk_le_ctx ctx, int centering, int axis, con
 }
 
 // The 3-D spread's candidate stream of m's binning (le_sweep.hip, launch_cand_stream):
-// built on the first spread after a binning, kept until the next; p.cs_* set.
+// built on the first spread after a binning, kept until the next; p.cs_* set.  A
+// closed-form kernel's components in a z frame shifted by -dz/2 (p.comp) need it split by
+// their anchor (cs_off_z): a stream built without the split is rebuilt with it, and one
+// built with it stands across a re-binning only if that moved no marker and changed no
+// shifted-z anchor (positions move within their cells).
 static int cand_stream(ibtk_le_ctx ctx, ibtk_le_markers m, Params& p) {
     const long long ncl = (long long)m->nbuckets_total / NBAND;
+    const long long nclz = m->npatch ? m->nclz : (long long)m->cg.ncol * (m->cg.nz + 1);
+    const int k = m->kernel;
+    bool split = false;
+    if (k == K_IB_4 || k == K_BSPLINE_4 || k == K_IB_6 || k == K_IB_4_W8)
+        for (int c = 0; c < p.ncomp; ++c) split = split || !p.comp[c].zcell;
     // a marker is a candidate of at most four columns (its own, one x- and one y-neighbour,
     // the corner between them: a stencil never reaches both neighbours in a dim)
     const long long cap = std::max(4LL * m->n, 1LL);
-    if (cap >= (1LL << 31) || ncl + 1 >= (1LL << 31)) return fail(IBTK_LE_ERR_RANGE, "candidate stream too long");
+    if (cap >= (1LL << 31) || ncl + 1 >= (1LL << 31) || nclz + 1 >= (1LL << 31))
+        return fail(IBTK_LE_ERR_RANGE, "candidate stream too long");
     p.cs_off = m->cs_off.as<int>();
     p.cs_pos = m->cs_pos.as<int>();
     p.cs_total = (int)cap;
-    if (m->cs_state == 1 && m->cs_pos.p) return IBTK_LE_OK;
+    p.cs_off_z = m->cs_split ? m->cs_off_z.as<int>() : nullptr;
+    p.cs_rint = k == K_IB_4 ? 1 : 0;  // the IB_4 spread anchors by rint (spread_setup)
+    if (m->cs_state == 1 && m->cs_pos.p && (m->cs_split || !split)) return IBTK_LE_OK;
     int rc;
     if ((rc = m->cs_cnt.ensure(sizeof(int) * (size_t)(ncl + 1)))) return rc;
     if ((rc = m->cs_off.ensure(sizeof(int) * (size_t)(ncl + 1)))) return rc;
     if ((rc = m->cs_pos.ensure(sizeof(int) * (size_t)cap))) return rc;
+    if (split && (rc = m->cs_off_z.ensure(sizeof(int) * (size_t)(nclz + 1)))) return rc;
     p.cs_off = m->cs_off.as<int>();
     p.cs_pos = m->cs_pos.as<int>();
+    p.cs_off_z = split ? m->cs_off_z.as<int>() : nullptr;
     HIP_TRY(hipMemsetAsync(m->cs_cnt.as<int>() + ncl, 0, sizeof(int), ctx->stream));
     size_t tb = 0;
     HIP_TRY(launch_scan(nullptr, tb, m->cs_cnt.as<int>(), m->cs_off.as<int>(), (int)(ncl + 1), ctx->stream));
     if ((rc = ctx->temp.ensure(tb))) return rc;
     Params q = p;
-    q.items_skip = m->cs_state == 2 ? m->cs_skip : nullptr;
+    // (a split stream stands across a re-binning that moved nothing only if no shifted-z
+    // anchor changed either: RebinBufs::zst[1])
+    const bool keep = m->cs_state == 2 && (!split || (m->cs_split && m->zst.p));
+    q.items_skip = keep ? m->cs_skip : nullptr;
+    q.cs_zflip = m->zst.p ? m->zst.as<int>() + 1 : nullptr;
     HIP_TRY(launch_cand_stream(q, (int)ncl, m->cs_cnt.as<int>(), m->cs_off.as<int>(), m->cs_pos.as<int>(), ctx->temp.p,
                                ctx->temp.cap, ctx->stream));
     m->cs_state = 1;
+    m->cs_split = split;
     return IBTK_LE_OK;
 }
 
@@ -1451,13 +1489,13 @@ static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cente
         if (int rc = build_candidates(ctx, m, p)) return rc;
         p.cand_off = m->cand_off.as<int>();
         p.cand_idx = m->cand_idx.as<int>();
-    } else if (int rc = cand_stream(ctx, m, p)) {
-        return rc;
     }
     ctx->ev_valid = false;
     for (int first = 0; first < nc; first += MAXC) {
         const int cnt = std::min(MAXC, nc - first);
         if (int rc = make_comps(geom, centering, axis, q_dev, q_depth, Q_depth, first, cnt, p)) return rc;
+        if (geom->ndim == 3)
+            if (int rc = cand_stream(ctx, m, p)) return rc;
         const bool t = ctx->timing && first == 0;
         const size_t nst = (size_t)m->item_bound * cnt * 8;
         if (geom->ndim == 3)
@@ -1516,7 +1554,7 @@ extern "C" int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch,
     std::vector<PatchDesc> prev;
     prev.swap(m->pdh);
     m->pdh.assign((size_t)npatch, PatchDesc{});
-    long long nb = 0, nj = 0;
+    long long nb = 0, nj = 0, nz = 0;
     BinGeom bg0{};
     for (int q = 0; q < npatch; ++q) {
         BinGeom bg;
@@ -1527,6 +1565,7 @@ extern "C" int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch,
         std::memset(&P, 0, sizeof(P));
         P.cg = cg;
         P.bucket_base = (int)nb;
+        P.ca_base_z = (int)nz;
         P.jbase = (int)nj;
         sweep_segments(cg, P.S, P.nseg, ctx->tune.seg_items, true);
         for (int d = 0; d < 3; ++d) {
@@ -1535,10 +1574,12 @@ extern "C" int ibtk_le_level_bin(ibtk_le_ctx ctx, ibtk_le_markers m, int npatch,
         }
         if (prev.size() == (size_t)npatch) std::memcpy(P.comp, prev[q].comp, sizeof(P.comp));  // arrays of the last call
         nb += cg.nbuckets;
+        nz += (long long)cg.ncol * (cg.nz + 1);
         nj += (long long)cg.ncol * P.nseg;
         if (nb + 1 >= (1LL << 31) || nj >= (1LL << 30)) return fail(IBTK_LE_ERR_RANGE, "level too large for 31-bit keys");
     }
     m->nbuckets_total = (int)nb;
+    m->nclz = nz;
     m->njobs = (int)nj;
     m->n = n;
     m->kernel = kernel;
@@ -2584,23 +2625,13 @@ static int sort_pairs(ibtk_le_ctx ctx, const unsigned* kin, unsigned* kout, cons
     return IBTK_LE_OK;
 }
 
-// LDataManager::computeNodeDistribution (LDataManager.cpp:2874-2947) over the local
-// patches of a level (geoms[q], q in PatchLevel order): the local nodes patch by
-// patch (data_begin(patch_box): box cells, x fastest; each cell's set by Lagrangian
-// index, uniqued, :1487-1493), then the nonlocal ones -- nodes of the patches' ghost
-// cells whose Lagrangian index no local node has -- each at its first sighting
-// (patches in order, a patch's ghost cells in ghost-box order).  The patches are equal
-// boxes aligned to one tiling of the domain [dom_lo, dom_hi] (periodic images across
-// its periodic sides, the index data's periodic ghost fill).
-extern "C" int ibtk_le_level_node_distribution(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms,
-                                               const int* dom_lo, const int* dom_hi, const int* periodic,
-                                               const double* X_dev, const int* lag_dev, int n_markers, int ghost,
-                                               int* order_dev, int* n_local, int* n_nonlocal) {
-    if (!ctx || !n_local || !n_nonlocal || !geoms || !dom_lo || !dom_hi) return fail(IBTK_LE_ERR_ARG, "null argument");
-    if (npatch < 1 || n_markers < 0 || ghost < 0) return fail(IBTK_LE_ERR_ARG, "bad sizes");
-    *n_local = *n_nonlocal = 0;
+// A level of equal patches aligned to one tiling of the domain [dom_lo, dom_hi]: its
+// numbering frame (LevelNum) and the tile -> patch table (-1: no local patch).
+static int make_level_num(int npatch, const ibtk_le_patch_geom* geoms, const int* dom_lo, const int* dom_hi,
+                          const int* periodic, int ghost, LevelNum& L, std::vector<int>& tab) {
+    if (!geoms || !dom_lo || !dom_hi) return fail(IBTK_LE_ERR_ARG, "null argument");
+    if (npatch < 1 || ghost < 0) return fail(IBTK_LE_ERR_ARG, "bad sizes");
     const int nd = geoms[0].ndim;
-    LevelNum L;
     std::memset(&L, 0, sizeof(L));
     L.ndim = nd;
     L.g = ghost;
@@ -2639,7 +2670,7 @@ extern "C" int ibtk_le_level_node_distribution(ibtk_le_ctx ctx, int npatch, cons
     }
     if ((long long)npatch * pcells >= 0xffffffffLL || (long long)npatch * gcells >= 0xfffffffeLL)
         return fail(IBTK_LE_ERR_RANGE, "level too large for 32-bit node keys");
-    std::vector<int> tab((size_t)ntab, -1);
+    tab.assign((size_t)ntab, -1);
     for (int q = 0; q < npatch; ++q) {
         long long lin = 0, str = 1;
         for (int k = 0; k < nd; ++k) {
@@ -2649,6 +2680,27 @@ extern "C" int ibtk_le_level_node_distribution(ibtk_le_ctx ctx, int npatch, cons
         if (tab[(size_t)lin] >= 0) return fail(IBTK_LE_ERR_ARG, "patches %d and %d overlap", tab[(size_t)lin], q);
         tab[(size_t)lin] = q;
     }
+    return IBTK_LE_OK;
+}
+
+// LDataManager::computeNodeDistribution (LDataManager.cpp:2874-2947) over the local
+// patches of a level (geoms[q], q in PatchLevel order): the local nodes patch by
+// patch (data_begin(patch_box): box cells, x fastest; each cell's set by Lagrangian
+// index, uniqued, :1487-1493), then the nonlocal ones -- nodes of the patches' ghost
+// cells whose Lagrangian index no local node has -- each at its first sighting
+// (patches in order, a patch's ghost cells in ghost-box order).  The patches are equal
+// boxes aligned to one tiling of the domain [dom_lo, dom_hi] (periodic images across
+// its periodic sides, the index data's periodic ghost fill).
+extern "C" int ibtk_le_level_node_distribution(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms,
+                                               const int* dom_lo, const int* dom_hi, const int* periodic,
+                                               const double* X_dev, const int* lag_dev, int n_markers, int ghost,
+                                               int* order_dev, int* n_local, int* n_nonlocal) {
+    if (!ctx || !n_local || !n_nonlocal) return fail(IBTK_LE_ERR_ARG, "null argument");
+    if (n_markers < 0) return fail(IBTK_LE_ERR_ARG, "bad sizes");
+    *n_local = *n_nonlocal = 0;
+    LevelNum L;
+    std::vector<int> tab;
+    if (int rc = make_level_num(npatch, geoms, dom_lo, dom_hi, periodic, ghost, L, tab)) return rc;
     if (n_markers == 0) return IBTK_LE_OK;
     if (!X_dev || !order_dev) return fail(IBTK_LE_ERR_ARG, "null array");
     if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
@@ -2700,6 +2752,97 @@ extern "C" int ibtk_le_level_node_distribution(ibtk_le_ctx ctx, int npatch, cons
     HIP_TRY(hipStreamSynchronize(s));
     *n_local = nl;
     *n_nonlocal = nn;
+    return IBTK_LE_OK;
+}
+
+// LIndexSetData::cacheLocalIndices (LIndexSetData.cpp:83-169) for every local patch of a
+// level in one pass -- the per-patch lists LDataManager::spread / interp hand LEInteractor
+// (LDataManager.cpp:634-654, 763-807): the interior lists (markers whose getCellIndex cell
+// is in the patch box) and the ghost-box lists (markers and their periodic images whose
+// cell is in the patch's ghost box, with their shifts), patch by patch, each patch's
+// entries in its box's (ghost box's) cell order, x fastest, a cell's markers by index --
+// the order ibtk_le_periodic_index_list gives one patch.  Keys per marker, a stable device
+// radix sort by (patch, cell), the patch offsets by binary search in the sorted keys.
+extern "C" int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms,
+                                         const int* dom_lo, const int* dom_hi, const int* periodic,
+                                         const double* X_dev, int n_markers, int ghost, int* interior_dev,
+                                         int interior_cap, int* interior_off, int* ghost_dev, double* Xshift_dev,
+                                         int ghost_cap, int* ghost_off) {
+    if (!ctx || !interior_off || !ghost_off) return fail(IBTK_LE_ERR_ARG, "null argument");
+    if (n_markers < 0 || interior_cap < 0 || ghost_cap < 0) return fail(IBTK_LE_ERR_ARG, "bad sizes");
+    LevelNum L;
+    std::vector<int> tab;
+    if (int rc = make_level_num(npatch, geoms, dom_lo, dom_hi, periodic, ghost, L, tab)) return rc;
+    for (int q = 0; q <= npatch; ++q) interior_off[q] = ghost_off[q] = 0;
+    const int n = n_markers;
+    if (n == 0) return IBTK_LE_OK;
+    if (!X_dev) return fail(IBTK_LE_ERR_ARG, "null X");
+    unsigned pcells = 1, gcells = 1;
+    for (int k = 0; k < L.ndim; ++k) {
+        pcells *= (unsigned)L.n[k];
+        gcells *= (unsigned)(L.n[k] + 2 * ghost);
+    }
+    if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
+    const hipStream_t s = ctx->stream;
+    int rc;
+    if ((rc = ctx->num_tab.ensure(sizeof(int) * tab.size()))) return rc;
+    if ((rc = ctx->ll_cnt.ensure(sizeof(int) * (size_t)(n + 1)))) return rc;
+    if ((rc = ctx->ll_off.ensure(sizeof(int) * (size_t)(n + 1)))) return rc;
+    if ((rc = ctx->ll_key.ensure(sizeof(unsigned) * (size_t)n))) return rc;
+    if ((rc = ctx->ll_key2.ensure(sizeof(unsigned) * (size_t)n))) return rc;
+    if ((rc = ctx->ll_id.ensure(sizeof(int) * (size_t)n))) return rc;
+    if ((rc = ctx->ll_id2.ensure(sizeof(int) * (size_t)n))) return rc;
+    if ((rc = ctx->counts.ensure(sizeof(int) * (size_t)(npatch + 1)))) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->num_tab.p, tab.data(), sizeof(int) * tab.size(), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(ctx->ll_cnt.as<int>() + n, 0, sizeof(int), s));
+    HIP_TRY(launch_level_list_keys(L, ctx->num_tab.as<int>(), X_dev, n, ctx->ll_key.as<unsigned>(),
+                                   ctx->ll_cnt.as<int>(), s));
+    if ((rc = scan_excl(ctx, ctx->ll_cnt.as<int>(), ctx->ll_off.as<int>(), n + 1))) return rc;
+    // interior: markers by (patch, cell), stable
+    HIP_TRY(launch_iota(ctx->ll_id.as<int>(), n, s));
+    if ((rc = sort_pairs(ctx, ctx->ll_key.as<unsigned>(), ctx->ll_key2.as<unsigned>(), ctx->ll_id.as<int>(),
+                         ctx->ll_id2.as<int>(), n, 32)))
+        return rc;
+    HIP_TRY(launch_key_offsets(ctx->ll_key2.as<unsigned>(), n, pcells, npatch, ctx->counts.as<int>(), s));
+    int total = 0;
+    HIP_TRY(hipMemcpyAsync(interior_off, ctx->counts.p, sizeof(int) * (size_t)(npatch + 1), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&total, ctx->ll_off.as<int>() + n, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const int nint = interior_off[npatch];
+    bool short_cap = nint > interior_cap;
+    if (nint > 0 && !short_cap) {
+        if (!interior_dev) return fail(IBTK_LE_ERR_ARG, "null interior list");
+        HIP_TRY(hipMemcpyAsync(interior_dev, ctx->ll_id2.p, sizeof(int) * (size_t)nint, hipMemcpyDeviceToDevice, s));
+    }
+    // ghost boxes: entries per marker in marker order, then by (patch, cell), stable
+    if (total > 0) {
+        for (DevBuf* b : {&ctx->ll_src, &ctx->ll_img})
+            if ((rc = b->ensure(sizeof(int) * (size_t)total))) return rc;
+        if ((size_t)total > (size_t)n) {  // the interior's scratch reused, grown to the entries
+            for (DevBuf* b : {&ctx->ll_key, &ctx->ll_key2, &ctx->ll_id, &ctx->ll_id2})
+                if ((rc = b->ensure(sizeof(int) * (size_t)total))) return rc;
+        }
+        HIP_TRY(launch_level_list_write(L, ctx->num_tab.as<int>(), X_dev, n, ctx->ll_off.as<int>(),
+                                        ctx->ll_key.as<unsigned>(), ctx->ll_id.as<int>(), ctx->ll_src.as<int>(),
+                                        ctx->ll_img.as<int>(), s));
+        if ((rc = sort_pairs(ctx, ctx->ll_key.as<unsigned>(), ctx->ll_key2.as<unsigned>(), ctx->ll_id.as<int>(),
+                             ctx->ll_id2.as<int>(), total, 32)))
+            return rc;
+        HIP_TRY(launch_key_offsets(ctx->ll_key2.as<unsigned>(), total, gcells, npatch, ctx->counts.as<int>(), s));
+        HIP_TRY(hipMemcpyAsync(ghost_off, ctx->counts.p, sizeof(int) * (size_t)(npatch + 1), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (total <= ghost_cap) {
+            if (!ghost_dev) return fail(IBTK_LE_ERR_ARG, "null ghost-box list");
+            HIP_TRY(launch_level_list_out(L, ctx->ll_id2.as<int>(), ctx->ll_src.as<int>(), ctx->ll_img.as<int>(), total,
+                                          ghost_dev, Xshift_dev, s));
+        } else {
+            short_cap = true;
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    if (short_cap)
+        return fail(IBTK_LE_ERR_ARG, "level_index_lists: %d interior / %d ghost-box entries exceed the capacities %d / %d",
+                    nint, total, interior_cap, ghost_cap);
     return IBTK_LE_OK;
 }
 

@@ -691,6 +691,159 @@ hipError_t launch_level_node_keys(const LevelNum& L, const int* tab, const doubl
     hipLaunchKernelGGL(k_level_node_keys, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, L, tab, X, n, lkey, ckey);
     return hipGetLastError();
 }
+// ---------------------------------------------------------------------------
+// a level's index lists in one pass: LIndexSetData::cacheLocalIndices
+// (LIndexSetData.cpp:83-169) over every local patch of the level
+// ---------------------------------------------------------------------------
+// getCellIndex in the domain frame (IndexUtilities-inl.h:66-89), as k_level_node_keys
+__device__ __forceinline__ void level_cell(const LevelNum& L, const double* X, int s, int* c) {
+    for (int k = 0; k < 3; ++k) c[k] = 0;
+    for (int k = 0; k < L.ndim; ++k) {
+        const double x = X[(int64_t)L.ndim * s + k];
+        const double dl = x - L.xlo[k], du = x - L.xup[k];
+        if (fabs(dl) <= fabs(du)) c[k] = L.dom_lo[k] + (int)floor(dl / L.dx[k]);
+        else c[k] = L.dom_hi[k] + (int)floor(du / L.dx[k]) + 1;
+    }
+}
+// f(j, q, key) for every periodic image j (shift (j % 3 - 1, j / 3 % 3 - 1, j / 9 - 1) in
+// domain extents; non-periodic dims unshifted) of cell c and every local patch q whose ghost
+// box holds the image's cell, key = q * (ghost-box cells) + the cell's ghost-box index (x
+// fastest); images and patches in increasing (j, tile) order
+template <typename F>
+__device__ __forceinline__ void level_ghost_visit(const LevelNum& L, const int* tab, const int* c, F&& f) {
+    const int nd = L.ndim;
+    unsigned gcells = 1;
+    for (int k = 0; k < nd; ++k) gcells *= (unsigned)(L.n[k] + 2 * L.g);
+    const int nsh = nd == 3 ? 27 : 9;
+    for (int j = 0; j < nsh; ++j) {
+        const int sh[3] = {j % 3 - 1, (j / 3) % 3 - 1, nd == 3 ? j / 9 - 1 : 0};
+        int ci[3] = {0, 0, 0}, tlo[3] = {0, 0, 0}, thi[3] = {0, 0, 0};
+        bool ok = true;
+        for (int k = 0; k < nd; ++k) {
+            if (sh[k] != 0 && !L.periodic[k]) ok = false;
+            ci[k] = c[k] + sh[k] * (L.dom_hi[k] - L.dom_lo[k] + 1);
+            // tiles t whose ghost box [org + t n - g, org + t n + n - 1 + g] holds ci[k]
+            tlo[k] = max(-floordiv(-(ci[k] - L.org[k] - L.n[k] + 1 - L.g), L.n[k]), 0);
+            thi[k] = min(floordiv(ci[k] - L.org[k] + L.g, L.n[k]), L.nt[k] - 1);
+            if (tlo[k] > thi[k]) ok = false;
+        }
+        if (!ok) continue;
+        for (int tz = tlo[2]; tz <= thi[2]; ++tz)
+            for (int ty = tlo[1]; ty <= thi[1]; ++ty)
+                for (int tx = tlo[0]; tx <= thi[0]; ++tx) {
+                    const int tt[3] = {tx, ty, tz};
+                    int lin = 0, str = 1;
+                    for (int k = 0; k < nd; ++k) {
+                        lin += tt[k] * str;
+                        str *= L.nt[k];
+                    }
+                    const int q = tab[lin];
+                    if (q < 0) continue;
+                    unsigned gk = 0, gs = 1;
+                    for (int k = 0; k < nd; ++k) {
+                        gk += (unsigned)(ci[k] - (L.org[k] + tt[k] * L.n[k] - L.g)) * gs;
+                        gs *= (unsigned)(L.n[k] + 2 * L.g);
+                    }
+                    f(j, q, (unsigned)q * gcells + gk);
+                }
+    }
+}
+// per marker: its interior key (patch q * patch cells + the cell's box index; 0xffffffff
+// in no local patch box) and its number of ghost-box entries
+__global__ __launch_bounds__(BLOCK) void k_level_list_keys(LevelNum L, const int* tab, const double* X, int n,
+                                                           unsigned* ikey, int* gcnt) {
+    const int s = blockIdx.x * BLOCK + threadIdx.x;
+    if (s >= n) return;
+    const int nd = L.ndim;
+    int c[3];
+    level_cell(L, X, s, c);
+    unsigned key = 0xffffffffu, pcells = 1, k0 = 0;
+    int lin = 0, str = 1, t[3] = {0, 0, 0};
+    bool in = true;
+    for (int k = 0; k < nd; ++k) {
+        t[k] = floordiv(c[k] - L.org[k], L.n[k]);
+        in = in && t[k] >= 0 && t[k] < L.nt[k];
+        lin += t[k] * str;
+        str *= L.nt[k];
+        k0 += (unsigned)(c[k] - (L.org[k] + t[k] * L.n[k])) * pcells;
+        pcells *= (unsigned)L.n[k];
+    }
+    if (in && tab[lin] >= 0) key = (unsigned)tab[lin] * pcells + k0;
+    ikey[s] = key;
+    int cnt = 0;
+    level_ghost_visit(L, tab, c, [&](int, int, unsigned) { ++cnt; });
+    gcnt[s] = cnt;
+}
+// the ghost-box entries at goff[s]: key, entry id (the stable sort's value), marker, image
+__global__ __launch_bounds__(BLOCK) void k_level_list_write(LevelNum L, const int* tab, const double* X, int n,
+                                                            const int* goff, unsigned* gkey, int* gid, int* gsrc,
+                                                            int* gimg) {
+    const int s = blockIdx.x * BLOCK + threadIdx.x;
+    if (s >= n) return;
+    int c[3];
+    level_cell(L, X, s, c);
+    int o = goff[s];
+    level_ghost_visit(L, tab, c, [&](int j, int, unsigned key) {
+        gkey[o] = key;
+        gid[o] = o;
+        gsrc[o] = s;
+        gimg[o] = j;
+        ++o;
+    });
+}
+// the sorted entries out: marker index and its periodic shift (sh * domain length per dim)
+__global__ __launch_bounds__(BLOCK) void k_level_list_out(LevelNum L, const int* sid, const int* gsrc,
+                                                          const int* gimg, int total, int* idx, double* xs) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= total) return;
+    const int e = sid[i];
+    idx[i] = gsrc[e];
+    if (xs) {
+        const int j = gimg[e];
+        const int sh[3] = {j % 3 - 1, (j / 3) % 3 - 1, j / 9 - 1};
+        for (int k = 0; k < L.ndim; ++k)
+            xs[(int64_t)L.ndim * i + k] = (double)sh[k] * ((double)(L.dom_hi[k] - L.dom_lo[k] + 1) * L.dx[k]);
+    }
+}
+// off[q] = the first sorted key >= q * per (q = 0 .. npatch; keys of no patch sort last)
+__global__ __launch_bounds__(BLOCK) void k_key_offsets(const unsigned* skeys, int n, unsigned per, int npatch,
+                                                       int* off) {
+    const int q = blockIdx.x * BLOCK + threadIdx.x;
+    if (q > npatch) return;
+    const unsigned long long b = (unsigned long long)q * per;
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((unsigned long long)skeys[mid] < b) lo = mid + 1;
+        else hi = mid;
+    }
+    off[q] = lo;
+}
+hipError_t launch_level_list_keys(const LevelNum& L, const int* tab, const double* X, int n, unsigned* ikey,
+                                  int* gcnt, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_level_list_keys, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, L, tab, X, n, ikey, gcnt);
+    return hipGetLastError();
+}
+hipError_t launch_level_list_write(const LevelNum& L, const int* tab, const double* X, int n, const int* goff,
+                                   unsigned* gkey, int* gid, int* gsrc, int* gimg, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_level_list_write, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, L, tab, X, n, goff, gkey,
+                       gid, gsrc, gimg);
+    return hipGetLastError();
+}
+hipError_t launch_level_list_out(const LevelNum& L, const int* sid, const int* gsrc, const int* gimg, int total,
+                                 int* idx, double* xs, hipStream_t s) {
+    if (total <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_level_list_out, dim3((total + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, L, sid, gsrc, gimg,
+                       total, idx, xs);
+    return hipGetLastError();
+}
+hipError_t launch_key_offsets(const unsigned* skeys, int n, unsigned per, int npatch, int* off, hipStream_t s) {
+    hipLaunchKernelGGL(k_key_offsets, dim3((npatch + 1 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, skeys, n, per, npatch,
+                       off);
+    return hipGetLastError();
+}
 // entry i of the list sorted by (lag, ckey): the first of its lag run, and that run
 // has no local node (ckey 0 sorts first) -- a nonlocal node at its first sighting
 __global__ __launch_bounds__(BLOCK) void k_nonlocal_flags(const unsigned* sckey, const int* sorder, const int* lag,

@@ -125,6 +125,7 @@ struct SweepItem {
 struct PatchDesc {
     ColGeom cg;
     int bucket_base;  // first bucket of the patch in the level's table
+    int ca_base_z;    // first column-anchor of the patch in the shifted-z frame (cs_off_z)
     int jbase;        // first (segment, column) pair of the patch (item table)
     int S, nseg;      // sweep segments
     double xlo[3];    // cell-frame x_lower
@@ -172,6 +173,10 @@ struct Params {
     const int* cs_off;         // 3-D spread: candidate stream offsets per column-anchor (launch_cand_stream)
     const int* cs_pos;         // 3-D spread: the candidate stream (sorted positions)
     int cs_total;              // its length
+    const int* cs_off_z;       // closed-form kernels: the stream's boundaries per anchor of the frame
+                               // shifted by -dz/2 in z (side-z, node, x/y-edge components; k_cand_write)
+    int cs_rint;               // the spread's stencils anchor by rint (IB_4), not NINT
+    const int* cs_zflip;       // with cs_off_z and items_skip: nonzero when a shifted-z anchor changed
     const int* nentries_dev;   // device copy of the list length
     const double* Qin;         // spread: marker values
     const double* sorted_F;    // spread: Qin gathered in sorted order, [comp][sorted position]
@@ -249,6 +254,8 @@ struct RebinBufs {
     double* xa;
     double* xb;
     int* order_gen;         // bumped when something moved (the order changed; nullable)
+    unsigned* zbits;        // shifted-z anchor parities per sorted position (nw + 1 words; k_rekey)
+    int* zst;               // [0] zbits are in the current order, [1] (zeroed before) a parity changed
 };
 hipError_t launch_set_xcur(double** xcur, double* x, hipStream_t s);
 hipError_t launch_rekey(int kernel, const Params& p, const RebinBufs& r, hipStream_t s);
@@ -288,7 +295,9 @@ void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items, bool le
 hipError_t launch_item_table(int kernel, const Params& p, int target, int heavy, int* nsub, int* start, SweepItem* tab, int* ntot,
                              void* temp, size_t temp_bytes, hipStream_t s);
 // the spread's candidate stream of a 3-D column binning: cnt[ncl + 1] (cnt[ncl] = 0 on entry),
-// off[ncl + 1] (off[ncl] = the length), pos[length]; p.items_skip as for the item table
+// off[ncl + 1] (off[ncl] = the length), pos[length]; p.items_skip as for the item table.
+// p.cs_off_z set (closed-form kernels): each anchor's candidates split by their shifted-z
+// anchor and p.cs_off_z[Σ ncol (nz + 1) + 1] written (k_cand_write; no skip)
 hipError_t launch_cand_stream(const Params& p, int ncl, int* cnt, int* off, int* pos, void* temp, size_t temp_bytes,
                               hipStream_t s);
 
@@ -371,6 +380,19 @@ struct LevelNum {
 // key_ghost for cls 1, 0xffffffff for cls 2.
 hipError_t launch_level_node_keys(const LevelNum& L, const int* tab, const double* X, int n, unsigned* lkey,
                                   unsigned* ckey, hipStream_t s);
+// A level's index lists (ibtk_le_level_index_lists): per marker its interior key (patch *
+// patch cells + box index; 0xffffffff outside every local patch box) and ghost-box entry
+// count; then its entries at goff[s] (key = patch * ghost-box cells + ghost-box index of the
+// image's cell, id = the entry's own index, the marker, the image 0 .. 26); the entries taken
+// in sorted order (sid) out as marker indices and periodic shifts; off[q] = first sorted key
+// >= q * per, q = 0 .. npatch.
+hipError_t launch_level_list_keys(const LevelNum& L, const int* tab, const double* X, int n, unsigned* ikey,
+                                  int* gcnt, hipStream_t s);
+hipError_t launch_level_list_write(const LevelNum& L, const int* tab, const double* X, int n, const int* goff,
+                                   unsigned* gkey, int* gid, int* gsrc, int* gimg, hipStream_t s);
+hipError_t launch_level_list_out(const LevelNum& L, const int* sid, const int* gsrc, const int* gimg, int total,
+                                 int* idx, double* xs, hipStream_t s);
+hipError_t launch_key_offsets(const unsigned* skeys, int n, unsigned per, int npatch, int* off, hipStream_t s);
 // A level's interp restricted to its interior lists (ibtk_le_level_select_interior):
 // owner[s] = max patch whose interior list names marker s (owner pre-filled with -1);
 // then per sorted entry e of the binned lists: qin[e] = s if owner[s] is the entry's

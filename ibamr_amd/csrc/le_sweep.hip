@@ -153,12 +153,17 @@ template <int K> __device__ __forceinline__ int key_band(int kx, int ky) {
 // Bucket key of list entry i at shifted position Xs: (anchor plane, column, band)
 // in its patch's bucket range, or nbuckets_total (outside).
 template <int K>
-__device__ __forceinline__ unsigned entry_key(const Params& p, int i, const double* Xs) {
+// (*zpar, when given: the parity of the entry's z anchor in the frame shifted by -dz/2,
+// computed as k_cand_write computes that anchor -- for a stayer, which of the two shifted
+// anchors of its key plane it takes)
+__device__ __forceinline__ unsigned entry_key(const Params& p, int i, const double* Xs, int* zpar = nullptr) {
     if (p.n_dev && i >= *p.n_dev) return (unsigned)p.nbuckets_total;  // a fixed-capacity list's unused rows
     int ka[3];
     unsigned key = (unsigned)p.nbuckets_total;  // outside
+    double zxlo = p.bg.xlo[2];
     if (p.pd) {  // a level: the entry's patch, its frame and its range of buckets
         const PatchDesc& P = p.pd[entry_patch(p, i)];
+        zxlo = P.xlo[2];
         if (col_key_cell<K>(P.xlo, p.bg.dx, P.ilower, P.cg, Xs, ka)) {
             const int col = (ka[1] / COLY) * P.cg.ncx + ka[0] / COLX;
             key = (unsigned)(P.bucket_base + (ka[2] * P.cg.ncol + col) * NBAND + key_band<K>(ka[0], ka[1]));
@@ -166,6 +171,10 @@ __device__ __forceinline__ unsigned entry_key(const Params& p, int i, const doub
     } else if (col_key_cell<K>(p.bg.xlo, p.bg.dx, p.bg.ilower, p.cg, Xs, ka)) {
         const int col = (ka[1] / COLY) * p.cg.ncx + ka[0] / COLX;
         key = (unsigned)((ka[2] * p.cg.ncol + col) * NBAND + key_band<K>(ka[0], ka[1]));
+    }
+    if (zpar) {
+        const double xo = (Xs[2] - (zxlo - 0.5 * p.bg.dx[2])) * (1.0 / p.bg.dx[2]);
+        *zpar = (K == K_IB_4 ? (int)__builtin_rint(xo) : d_nint(xo)) & 1;
     }
     return key;
 }
@@ -210,14 +219,28 @@ __device__ __forceinline__ double* rebin_other(double* const* xcur, double* xa, 
 // R1: new keys in the old order; the shifted positions stored at the old sorted
 // positions in the other buffer; per-bucket mover counts in/out; the mover flags
 // as a bit per entry with per-word counts.
+// zbits (closed-form kernels, nullable): the shifted-z anchor parity per sorted position,
+// 32 per word (entry_key), compared with the last re-binning's when zst[0] says those are in
+// this order (it moved nothing) -- a difference, or none to compare with, sets zst[1]: a
+// split candidate stream (k_cand_write SHZ) must then be rebuilt even if nothing moved.
 template <int K>
 __global__ __launch_bounds__(BLOCK) void k_rekey(Params p, int n, const unsigned* kold, const int* sl,
                                                  double* const* xcur, double* xa, double* xb, unsigned* mbits,
-                                                 int* wcnt, int* cin, int* cout) {
+                                                 int* wcnt, int* cin, int* cout, unsigned* zbits, int* zst) {
     __shared__ double sx[3 * BLOCK];
     const int e0 = blockIdx.x * BLOCK;
     const int e = e0 + threadIdx.x;
     bool mv = false;
+    int zp = 0;
+    // the last parities of the wave's two words and their state, loaded ahead of the
+    // gather (their latency hidden behind it, not added before the block's barrier)
+    unsigned zo0 = 0, zo1 = 0;
+    int zv = 0;
+    if (zbits && (threadIdx.x & 63) == 0 && e < n) {
+        zo0 = zbits[e >> 5];
+        zo1 = zbits[(e >> 5) + 1];
+        zv = zst[0];
+    }
     if (e < n) {
         const int l = sl[e];
         const int s = p.indices ? p.indices[l] : l;
@@ -225,7 +248,7 @@ __global__ __launch_bounds__(BLOCK) void k_rekey(Params p, int n, const unsigned
         double Xs[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) Xs[d] = x.v[d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
-        const unsigned k = entry_key<K>(p, l, Xs);
+        const unsigned k = entry_key<K>(p, l, Xs, zbits ? &zp : nullptr);
         const unsigned ko = kold[e];
         mv = k != ko;
         if (mv) {
@@ -242,6 +265,16 @@ __global__ __launch_bounds__(BLOCK) void k_rekey(Params p, int n, const unsigned
         mbits[w + 1] = (unsigned)(bal >> 32);
         wcnt[w] = __popc((unsigned)bal);
         wcnt[w + 1] = __popc((unsigned)(bal >> 32));
+    }
+    if (zbits) {
+        const unsigned long long zb = __ballot(zp != 0);
+        if ((threadIdx.x & 63) == 0 && e < n) {
+            const int w = e >> 5;
+            const bool same = zv != 0 && zo0 == (unsigned)zb && zo1 == (unsigned)(zb >> 32);
+            zbits[w] = (unsigned)zb;
+            zbits[w + 1] = (unsigned)(zb >> 32);
+            if (!same) zst[1] = 1;
+        }
     }
     __syncthreads();
     const int cnt = 3 * min(BLOCK, n - e0);
@@ -265,7 +298,9 @@ constexpr int RB_GRID = 4096;  // grid-stride kernels of the re-binning's tail
 template <int K>
 __global__ __launch_bounds__(BLOCK) void k_rebin_copy(Params p, int n, const int* T, const unsigned* mbits,
                                                       const unsigned* kold, const int* sl, double* const* xcur,
-                                                      double* xa, double* xb, unsigned* knew, int* lold) {
+                                                      double* xa, double* xb, unsigned* knew, int* lold, int* zst) {
+    // the parities k_rekey wrote are in the new order iff nothing moved
+    if (zst && blockIdx.x == 0 && threadIdx.x == 0) zst[0] = *T == 0 ? 1 : 0;
     if (*T == 0) return;
     const double* xo = rebin_other(xcur, xa, xb);
     for (int e = blockIdx.x * BLOCK + threadIdx.x; e < n; e += gridDim.x * BLOCK) {
@@ -1246,7 +1281,19 @@ __device__ __forceinline__ int range_pos(const Ranges& R, int j) {
 // of an anchor (the previous anchor's leftovers, then its own first) is one piece of
 // the stream, and the sweep needs no range arithmetic per chunk.  k_cand_count: the
 // lengths; an exclusive scan: cs_off; k_cand_write: the positions (a wave per ca).
-__device__ __forceinline__ bool ca_decode(const Params& p, int ca, ColGeom& cg, int& col, int& a, const int*& bs) {
+// The shifted-z frame (closed-form kernels, cs_off_z set).  A component whose z frame is
+// shifted by -dz/2 (side-z, node and x/y-edge data) has its stencil planes at a' + [LO,
+// HI - 1] for its own anchor a' = NINT in that frame (ic_lower = NINT - W/2), and a' is
+// the key anchor a or a + 1.  k_cand_write puts each anchor's candidates with a' = a
+// first (in range order) and those with a' = a + 1 after them (in reverse range order),
+// so the candidates of shifted anchor a' -- the upper ones of a' - 1, then the lower ones
+// of a' -- are again one piece of the stream, [cs_off_z[zb], cs_off_z[zb + 1]) with zb =
+// ca_base_z + col (nz + 1) + a' (a' = 0 .. nz): such a component's ring needs the
+// key-frame components' slots (5 for IB_4), not one more.
+// (zb: the column-anchor's index in the shifted-z frame, patch base ca_base_z + col (nz + 1)
+// + a; zxlo, zilo: the z origin of that frame, x_lower - dz / 2, and the z ilower)
+__device__ __forceinline__ bool ca_decode(const Params& p, int ca, ColGeom& cg, int& col, int& a, const int*& bs,
+                                          int& zb, double& zxlo, int& zilo) {
     int base = 0;
     if (p.pd) {
         int lo = 0, hi = p.npatch - 1;
@@ -1259,13 +1306,20 @@ __device__ __forceinline__ bool ca_decode(const Params& p, int ca, ColGeom& cg, 
         cg = P.cg;
         base = P.bucket_base / NBAND;
         bs = p.plane_start + P.bucket_base;
+        zb = P.ca_base_z;
+        zxlo = P.xlo[2] - 0.5 * p.bg.dx[2];  // (make_comps' frame shift)
+        zilo = P.ilower[2];
     } else {
         cg = p.cg;
         bs = p.plane_start;
+        zb = 0;
+        zxlo = p.bg.xlo[2] - 0.5 * p.bg.dx[2];
+        zilo = p.bg.ilower[2];
     }
     const int l = ca - base;
     col = l / cg.nz;
     a = l - col * cg.nz;
+    zb += col * (cg.nz + 1) + a;
     const int cx = col % cg.ncx, cy = col / cg.ncx;
     return !(cx == 0 || cx == cg.ncx - 1 || cy == 0 || cy == cg.ncy - 1);  // guard columns: no items
 }
@@ -1283,14 +1337,20 @@ __device__ __forceinline__ void ca_range(const ColGeom& cg, const int* bs, int c
 // the launches return at once, and cfg5's 0.5 M column-anchors, mostly empty, cost
 // no launch of their own)
 constexpr int CS_GRID = 8192;
+// a re-binning that moved nothing (and, for a split stream, changed no shifted-z anchor):
+// the stream stands
+__device__ __forceinline__ bool cs_stands(const Params& p) {
+    return p.items_skip && *p.items_skip == 0 && (!p.cs_off_z || *p.cs_zflip == 0);
+}
 __global__ __launch_bounds__(BLOCK) void k_cand_count(Params p, int ncl, int* cnt) {
-    if (p.items_skip && *p.items_skip == 0) return;  // a re-binning that moved nothing: the stream stands
+    if (cs_stands(p)) return;
     for (int ca = blockIdx.x * BLOCK + threadIdx.x; ca < ncl; ca += gridDim.x * BLOCK) {
         ColGeom cg;
-        int col, a;
+        int col, a, zb, zilo;
+        double zxlo;
         const int* bs;
         int t = 0;
-        if (ca_decode(p, ca, cg, col, a, bs)) {
+        if (ca_decode(p, ca, cg, col, a, bs, zb, zxlo, zilo)) {
 #pragma unroll
             for (int r = 0; r < 11; ++r) {
                 int b, e;
@@ -1303,18 +1363,32 @@ __global__ __launch_bounds__(BLOCK) void k_cand_count(Params p, int ncl, int* cn
 }
 // a wave per column-anchor: its three rows of bucket starts one entry a lane (three
 // coalesced loads), the ranges made once (make_ranges_lanes), then stream entry j of it
-// by range_pos, 64 a store
+// by range_pos, 64 a store.  SHZ: split by the shifted anchor (a ballot compaction from
+// each end) and the shifted-z boundary cs_off_z[zb + 1] written; lane 0 of the wave that
+// takes a column's anchor 0 writes its column's first boundary, cs_off_z[zb] = cs_off[ca].
+template <bool SHZ>
 __global__ __launch_bounds__(BLOCK) void k_cand_write(Params p, int ncl, const int* off, int* pos) {
-    if (p.items_skip && *p.items_skip == 0) return;
+    if (cs_stands(p)) return;
     const int lane = threadIdx.x & (SW - 1);
     const int nw = gridDim.x * (BLOCK / SW);
+    gdouble* const sX = cur_sorted_X(p);
+    const double inv_dz = 1.0 / p.bg.dx[2];
+    int* const offz = const_cast<int*>(p.cs_off_z);
     for (int ca = blockIdx.x * (BLOCK / SW) + (int)(threadIdx.x / SW); ca < ncl; ca += nw) {
         ColGeom cg;
-        int col, a;
+        int col, a, zb, zilo;
+        double zxlo;
         const int* bs;
-        if (!ca_decode(p, ca, cg, col, a, bs)) continue;
+        const bool items = ca_decode(p, ca, cg, col, a, bs, zb, zxlo, zilo);
         const int o = off[ca];
-        if (off[ca + 1] == o) continue;  // no candidate
+        if (SHZ && lane == 0) {
+            if (a == 0) offz[zb] = o;
+            if (ca == ncl - 1) offz[zb + 2] = off[ca + 1];  // the stream's end (a' = nz + 1 of the last column)
+        }
+        if (!items || off[ca + 1] == o) {
+            if (SHZ && lane == 0) offz[zb + 1] = o;
+            continue;  // no candidate
+        }
         const int cx = col % cg.ncx, cy = col / cg.ncx;
         const int col0 = (cy - 1) * cg.ncx + (cx - 1);
         int rowv[3];
@@ -1323,7 +1397,31 @@ __global__ __launch_bounds__(BLOCK) void k_cand_write(Params p, int ncl, const i
         Ranges R;
         make_ranges_lanes(rowv, R);
         const int t = R.pre[SSh<K_IB_4>::NR];
-        for (int j = lane; j < t; j += SW) pos[o + j] = range_pos(R, j);
+        if constexpr (!SHZ) {
+            for (int j = lane; j < t; j += SW) pos[o + j] = range_pos(R, j);
+        } else {
+            const int aa = a + cg.org[2] - zilo;  // the key anchor as a shifted-frame NINT
+            int nlo = 0, nup = 0;
+            for (int j0 = 0; j0 < t; j0 += SW) {
+                const int j = j0 + lane;
+                const int e = j < t ? range_pos(R, j) : 0;
+                bool up = false;
+                if (j < t) {
+                    const double xo = (sX[(int64_t)3 * e + 2] - zxlo) * inv_dz;
+                    const int n = p.cs_rint ? (int)__builtin_rint(xo) : d_nint(xo);
+                    up = n > aa;  // n = aa + 1 (the binning invariant: aa or aa + 1)
+                }
+                const unsigned long long bu = __ballot(up), bl = __ballot(j < t && !up);
+                const unsigned long long below = (1ull << lane) - 1ull;
+                if (j < t) {
+                    if (up) pos[o + t - 1 - (nup + __popcll(bu & below))] = e;
+                    else pos[o + nlo + __popcll(bl & below)] = e;
+                }
+                nlo += __popcll(bl);
+                nup += __popcll(bu);
+            }
+            if (lane == 0) offz[zb + 1] = o + nlo;
+        }
     }
 }
 hipError_t launch_cand_stream(const Params& p, int ncl, int* cnt, int* off, int* pos, void* temp, size_t temp_bytes,
@@ -1334,8 +1432,9 @@ hipError_t launch_cand_stream(const Params& p, int ncl, int* cnt, int* off, int*
     hipError_t e = launch_scan(temp, temp_bytes, cnt, off, ncl + 1, s);  // cnt[ncl] = 0: off[ncl] = the total
     if (e != hipSuccess) return e;
     const int per = BLOCK / SW;
-    hipLaunchKernelGGL(k_cand_write, dim3(std::min((ncl + per - 1) / per, CS_GRID)), dim3(BLOCK), 0, s, p, ncl, off,
-                       pos);
+    const dim3 g(std::min((ncl + per - 1) / per, CS_GRID)), b(BLOCK);
+    if (p.cs_off_z) hipLaunchKernelGGL(k_cand_write<true>, g, b, 0, s, p, ncl, off, pos);
+    else hipLaunchKernelGGL(k_cand_write<false>, g, b, 0, s, p, ncl, off, pos);
     return hipGetLastError();
 }
 
@@ -1689,12 +1788,19 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         const bool inner = zorg + plo >= p.zlo && zorg + phi <= p.zhi;
         if (inner != (p.zmode == 1)) return;
     }
-    const int afirst = max(plo - HI, 0), alast = min(phi - LO, cg.nz - 1);
+    // a closed-form kernel's component whose z frame is shifted by -dz/2 takes its
+    // candidates by the anchor of that frame (anchors 0 .. nz, the boundaries cs_off_z;
+    // see k_cand_write), which puts its stencil planes at a + [LO, HI - 1] as a key-frame one's
+    const bool shz = FAM == 0 && !cd.zcell;
+    static_assert(ZC || FAM != 0, "closed-form kernels: every component on the key-frame ring");
+    const int nza = shz ? cg.nz + 1 : cg.nz;  // anchor planes of the component's stream
+    const int afirst = max(plo - HI, 0), alast = min(phi - LO, nza - 1);
     // the item's stretch of its column's candidate stream (k_cand_stream, column-major
     // (patch, column, anchor) order): anchors afirst .. alast are [cs_off[ca0], cs_off[ca0 + nk])
-    const int ca0 = (LVL ? p.pd[si.patch].bucket_base / NBAND : 0) + col * cg.nz + afirst;
+    const int* const cs_offs = shz ? p.cs_off_z : p.cs_off;
+    const int ca0 = (LVL ? (shz ? p.pd[si.patch].ca_base_z : p.pd[si.patch].bucket_base / NBAND) : 0) + col * nza + afirst;
     // no candidate reaches the item: u unchanged (zero_first: 0; zero_ghosts: ghosts 0)
-    const bool any = p.cs_off[ca0 + (alast - afirst + 1)] > p.cs_off[ca0];
+    const bool any = cs_offs[ca0 + (alast - afirst + 1)] > cs_offs[ca0];
     // zero_ghosts (ibtk_le_zero_ghosts_spread): the owned points outside the component's
     // data box start from 0 instead of their values -- ibtk_le_zero_ghosts fused in
     const bool zg = p.zero_ghosts && !p.zero_first;
@@ -1844,7 +1950,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
     const int* const cs_pos = p.cs_pos;
     const int cs_last = p.cs_total - 1;
     const int nk = alast - afirst + 1;  // anchors of the item; o(nk) ends its stream
-    auto off_load = [&](int k) { return p.cs_off[ca0 + min(k, nk)]; };
+    auto off_load = [&](int k) { return cs_offs[ca0 + min(k, nk)]; };
     auto pos_load = [&](int j) { return cs_pos[min(max(j, 0), cs_last)]; };
     // prologue: planes afirst+LO .. afirst+HI-1 into the ring; plane afirst+HI, the
     // anchor boundaries o(0) .. o(3), chunk 1 of afirst and the positions of chunk 1
@@ -2263,44 +2369,25 @@ template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s
         else hipLaunchKernelGGL(k_gather_F_col<false>, g, b, 0, s, p, p.nsorted, const_cast<double*>(p.sorted_F));
     }
     if (ev0) (void)hipEventRecord(ev0, s);  // the events bracket the sweep kernels alone
-    // One launch per run of components alike in z frame: the components whose z
-    // frame is the keys' take the shorter ring (SSh ZC; side data: components 0 and
-    // 1 in one launch, then 2), every other one the full ring.  cfg4 spread sweep
-    // 15.6 -> 15.0 ms (profiles/r03j; all components on 5 slots in one launch would
-    // be 14.2, but the z-side component needs 6; the two launches side by side on
-    // two streams measured 15.4).
-    for (int c0 = 0; c0 < p.ncomp;) {
-        const bool zc = KT<K>::FAM == 0 && p.comp[c0].zcell;
-        int c1 = c0 + 1;
-        while (c1 < p.ncomp && (KT<K>::FAM == 0 && p.comp[c1].zcell) == zc) ++c1;
+    // One launch of every component.  Closed-form kernels run them all on the 5-slot
+    // key-frame ring (ZC): a component whose z frame is shifted by -dz/2 reads its
+    // candidates from the shifted-z stream (k_cand_z), anchored in its own frame, so its
+    // planes sit at a + [LO, HI - 1] as a key-frame one's.  (r03j had the z-side component
+    // on a 6-slot ring in a second launch: cfg4 spread 15.0 ms vs 14.2 all on 5 slots.)
+    // Tabulated kernels keep the general ring.
+    const long items = (long)p.item_bound * p.ncomp;
+    if (items > 0) {
         Params q = p;
-        q.comp0 = c0;
-        q.ncomp = c1 - c0;
-        const long items = (long)q.item_bound * q.ncomp;
-        if (items > 0) {
-            const dim3 g(sweep_grid(q, items)), b(SW);
-            if constexpr (KT<K>::FAM == 0) {
-                if (zc) {
-                    if (q.nadd) {
-                        if (q.pd) hipLaunchKernelGGL((k_spread_sweep<K, true, true, true>), g, b, 0, s, q);
-                        else hipLaunchKernelGGL((k_spread_sweep<K, false, true, true>), g, b, 0, s, q);
-                    } else {
-                        if (q.pd) hipLaunchKernelGGL((k_spread_sweep<K, true, false, true>), g, b, 0, s, q);
-                        else hipLaunchKernelGGL((k_spread_sweep<K, false, false, true>), g, b, 0, s, q);
-                    }
-                    c0 = c1;
-                    continue;
-                }
-            }
-            if (q.nadd) {
-                if (q.pd) hipLaunchKernelGGL((k_spread_sweep<K, true, true, false>), g, b, 0, s, q);
-                else hipLaunchKernelGGL((k_spread_sweep<K, false, true, false>), g, b, 0, s, q);
-            } else {
-                if (q.pd) hipLaunchKernelGGL((k_spread_sweep<K, true, false, false>), g, b, 0, s, q);
-                else hipLaunchKernelGGL((k_spread_sweep<K, false, false, false>), g, b, 0, s, q);
-            }
+        q.comp0 = 0;
+        const dim3 g(sweep_grid(q, items)), b(SW);
+        constexpr bool ZC = KT<K>::FAM == 0;
+        if (q.nadd) {
+            if (q.pd) hipLaunchKernelGGL((k_spread_sweep<K, true, true, ZC>), g, b, 0, s, q);
+            else hipLaunchKernelGGL((k_spread_sweep<K, false, true, ZC>), g, b, 0, s, q);
+        } else {
+            if (q.pd) hipLaunchKernelGGL((k_spread_sweep<K, true, false, ZC>), g, b, 0, s, q);
+            else hipLaunchKernelGGL((k_spread_sweep<K, false, false, ZC>), g, b, 0, s, q);
         }
-        c0 = c1;
     }
     if (ev1) (void)hipEventRecord(ev1, s);
     return hipGetLastError();
@@ -2346,14 +2433,15 @@ template <int K>
 hipError_t launch_rekey_t(const Params& p, const RebinBufs& r, hipStream_t s) {
     if (r.n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_rekey<K>, dim3((r.n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, r.n, r.kold, r.lsorted,
-                       r.xcur, r.xa, r.xb, r.mbits, r.wcnt, r.cin, r.cout);
+                       r.xcur, r.xa, r.xb, r.mbits, r.wcnt, r.cin, r.cout, KT<K>::FAM == 0 ? r.zbits : nullptr,
+                       r.zst);
     return hipGetLastError();
 }
 template <int K>
 hipError_t launch_rebin_copy_t(const Params& p, const RebinBufs& r, hipStream_t s) {
     if (r.n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_rebin_copy<K>, dim3(RB_GRID), dim3(BLOCK), 0, s, p, r.n, r.wpre + r.nw, r.mbits, r.kold,
-                       r.lsorted, r.xcur, r.xa, r.xb, r.knew, r.lold);
+                       r.lsorted, r.xcur, r.xa, r.xb, r.knew, r.lold, KT<K>::FAM == 0 ? r.zst : nullptr);
     return hipGetLastError();
 }
 using RekeyFn = hipError_t (*)(const Params&, const RebinBufs&, hipStream_t);

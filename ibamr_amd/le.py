@@ -855,6 +855,40 @@ def level_node_distribution(ctx: Context, geoms: Sequence[Geometry], dom_lo, dom
     return order[:nl.value + ng.value].contiguous(), nl.value, ng.value
 
 
+def level_index_lists(ctx: Context, geoms: Sequence[Geometry], dom_lo, dom_hi, X: torch.Tensor, ghost: int,
+                      periodic=None):
+    """LIndexSetData::cacheLocalIndices over every local patch of a level in one call
+    (ibtk_le_level_index_lists): ((interior int32, None, offsets), (ghost-box int32, Xshift
+    (n, ndim) float64, offsets)) -- the flat per-patch lists Level.from_flat and
+    Level.select_interior take, offsets as Python lists of npatch + 1."""
+    M = X.shape[0]
+    if M and (X.dtype != torch.float64 or not X.is_cuda or not X.is_contiguous()):
+        raise ValueError("X: contiguous float64 device tensor")
+    nd = geoms[0].ndim
+    lo, hi = _box_arg(dom_lo, dom_hi, nd)
+    pa = _periodic_arg(periodic, nd)
+    P = len(geoms)
+    tab = (PatchGeom * P)(*[g.c for g in geoms])
+    ioff, goff = (ctypes.c_int * (P + 1))(), (ctypes.c_int * (P + 1))()
+    icap, gcap = max(M, 1), max(M + M // 4, 1)
+    for attempt in range(2):
+        ii = torch.empty(icap, dtype=torch.int32, device=X.device)
+        gi = torch.empty(gcap, dtype=torch.int32, device=X.device)
+        gx = torch.empty((gcap, nd), dtype=torch.float64, device=X.device)
+        rc = ctx.lib.ibtk_le_level_index_lists(ctx.h, P, tab, lo.p, hi.p, pa[0] if pa else None,
+                                               _ptr(X) if M else None, M, ghost, _ptr(ii), icap,
+                                               ctypes.cast(ioff, ctypes.c_void_p), _ptr(gi), _ptr(gx), gcap,
+                                               ctypes.cast(goff, ctypes.c_void_p))
+        if rc != 0 and attempt == 0 and (ioff[P] > icap or goff[P] > gcap):
+            icap, gcap = max(icap, ioff[P]), max(gcap, goff[P])  # the sizes it reported
+            continue
+        check(rc)
+        break
+    ni, ng = ioff[P], goff[P]
+    return ((ii[:ni].contiguous(), None, list(ioff)),
+            (gi[:ng].contiguous(), gx[:ng].contiguous(), list(goff)))
+
+
 def wrap_positions(ctx: Context, X: torch.Tensor, x_lower, x_upper, periodic=None):
     """beginDataRedistribution's periodic wrap of X (n, ndim) in place
     (ibtk_le_wrap_positions, LDataManager.cpp:1385-1399)."""

@@ -445,6 +445,26 @@ int ibtk_le_node_distribution(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom, c
 int ibtk_le_level_node_distribution(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms, const int* dom_lo,
                                     const int* dom_hi, const int* periodic, const double* X_dev, const int* lag_dev,
                                     int n_markers, int ghost, int* order_dev, int* n_local, int* n_nonlocal);
+/* LIndexSetData::cacheLocalIndices (LIndexSetData.cpp:83-169) for every local patch of a
+ * level in one call: the lists LDataManager::spread / interp hand LEInteractor per patch
+ * (LDataManager.cpp:634-654, 763-807).  The patches as for ibtk_le_level_node_distribution
+ * (equal boxes on one tiling of [dom_lo, dom_hi], periodic[d] != 0 periodic, NULL = all);
+ * cells by getCellIndex in the domain frame, without Lagrangian indices (every marker is its
+ * own node).
+ *   interior lists: the markers whose cell lies in patch q's box, at interior_dev
+ *     [interior_off[q], interior_off[q + 1]);
+ *   ghost-box lists: the markers and their periodic images whose cell lies in patch q's
+ *     box grown by `ghost`, at ghost_dev / Xshift_dev (NDIM doubles an entry: the image's
+ *     shift, +-(dom_hi - dom_lo + 1) dx per periodic dim) [ghost_off[q], ghost_off[q + 1]).
+ * Within a patch the entries follow its (ghost) box's cells in box order, x fastest, a
+ * cell's markers by index -- ibtk_le_periodic_index_list's order for one patch.
+ * interior_off / ghost_off are host arrays of npatch + 1.  If either list needs more than
+ * its capacity, the offsets are still written (off[npatch] = the size needed), the lists
+ * are not, and IBTK_LE_ERR_ARG is returned.  Synchronises. */
+int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms, const int* dom_lo,
+                              const int* dom_hi, const int* periodic, const double* X_dev, int n_markers, int ghost,
+                              int* interior_dev, int interior_cap, int* interior_off, int* ghost_dev,
+                              double* Xshift_dev, int ghost_cap, int* ghost_off);
 /* beginDataRedistribution's wrap of marker positions into the periodic domain
  * (LDataManager.cpp:1385-1399), in place on n (ndim)-records: per periodic dim
  * (periodic NULL: all) add / subtract the domain length while outside

@@ -202,3 +202,52 @@ def test_rebin_after_bin_count_keeps_its_count(le):
     ctx.synchronize()
     assert torch.equal(m.order(), fresh.order())
     del junk
+
+
+@pytest.mark.parametrize("kernel", ["IB_4", "BSPLINE_4"])
+def test_rebin_within_cells_flips_shifted_anchors(le, kernel):
+    """Markers that move within their cells change no bucket (the re-binning moves
+    nothing) but can change their anchor in the frame shifted by -dz/2, by which the
+    spread's candidate stream is split for the side-z / node components (k_cand_write
+    SHZ): the re-binning's parities (k_rekey zbits) must send that stream to be rebuilt,
+    and a re-binning that changed nothing must keep it."""
+    N = (64, 48, 72)
+    g = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
+    geom = le.Geometry.periodic_unit(list(N), g)
+    rng = np.random.default_rng(17)
+    M = 30000
+    Xn = rng.uniform(0.0, 1.0, (M, 3))
+    k = rng.integers(1, N[2] - 1, M)
+    Xn[:, 2] = (k - rng.uniform(0.15, 0.25, M)) / N[2]      # z / dz in k - [0.15, 0.25]
+    X = torch.from_numpy(Xn).cuda()
+    F = torch.from_numpy(rng.standard_normal((M, 3))).cuda()
+    Fn = torch.from_numpy(rng.standard_normal((M, 1))).cuda()
+    u = _fields(le, geom, rng)
+    ctx = le.Context(0)
+    m = le.Markers(ctx).bin(geom, kernel, X)
+
+    def node_spread(mk, Xc):
+        f = geom.alloc("node", depth=1)
+        le.spread(ctx, mk, kernel, "node", geom, f, Fn, Xc)
+        ctx.synchronize()
+        return f
+
+    _check_same(le, geom, ctx, m, X, F, u, kernel)          # the split stream built
+    m.rebin(X)                                               # nothing changed
+    _check_same(le, geom, ctx, m, X, F, u, kernel)
+    m.rebin(X)                                               # ... again (the parities compared)
+    _check_same(le, geom, ctx, m, X, F, u, kernel)
+    X2 = X.clone()
+    X2[:, 2] += 0.35 / N[2]                                  # z / dz in k + [0.1, 0.2]: the same cells
+    m.rebin(X2)
+    fr = le.Markers(ctx).bin(geom, kernel, X2)
+    assert torch.equal(m.order(), fr.order())
+    _check_same(le, geom, ctx, m, X2, F, u, kernel)
+    for a, b in zip(node_spread(m, X2), node_spread(fr, X2)):
+        assert torch.equal(a, b)
+    m.rebin(X2)                                              # nothing changed: the stream stands
+    _check_same(le, geom, ctx, m, X2, F, u, kernel)
+    m.rebin(X)                                               # and back across
+    _check_same(le, geom, ctx, m, X, F, u, kernel)
+    for a, b in zip(node_spread(m, X), node_spread(le.Markers(ctx).bin(geom, kernel, X), X)):
+        assert torch.equal(a, b)
