@@ -714,38 +714,52 @@ __device__ __forceinline__ void level_ghost_visit(const LevelNum& L, const int* 
     const int nd = L.ndim;
     unsigned gcells = 1;
     for (int k = 0; k < nd; ++k) gcells *= (unsigned)(L.n[k] + 2 * L.g);
-    const int nsh = nd == 3 ? 27 : 9;
-    for (int j = 0; j < nsh; ++j) {
-        const int sh[3] = {j % 3 - 1, (j / 3) % 3 - 1, nd == 3 ? j / 9 - 1 : 0};
-        int ci[3] = {0, 0, 0}, tlo[3] = {0, 0, 0}, thi[3] = {0, 0, 0};
-        bool ok = true;
-        for (int k = 0; k < nd; ++k) {
-            if (sh[k] != 0 && !L.periodic[k]) ok = false;
-            ci[k] = c[k] + sh[k] * (L.dom_hi[k] - L.dom_lo[k] + 1);
-            // tiles t whose ghost box [org + t n - g, org + t n + n - 1 + g] holds ci[k]
-            tlo[k] = max(-floordiv(-(ci[k] - L.org[k] - L.n[k] + 1 - L.g), L.n[k]), 0);
-            thi[k] = min(floordiv(ci[k] - L.org[k] + L.g, L.n[k]), L.nt[k] - 1);
-            if (tlo[k] > thi[k]) ok = false;
+    // per dim and shift s - 1 (s = 0, 1, 2): the image's cell and the tiles whose ghost box
+    // [org + t n - g, org + t n + n - 1 + g] holds it (empty: no such image here) -- a
+    // marker away from the domain's faces has one image, its own
+    int ci[3][3], tlo[3][3], thi[3][3];
+    for (int k = 0; k < 3; ++k)
+        for (int s = 0; s < 3; ++s) {
+            ci[k][s] = 0;
+            tlo[k][s] = 0;
+            thi[k][s] = (k >= nd && s == 1) ? 0 : -1;  // a missing dim: its one unshifted "tile"
         }
-        if (!ok) continue;
-        for (int tz = tlo[2]; tz <= thi[2]; ++tz)
-            for (int ty = tlo[1]; ty <= thi[1]; ++ty)
-                for (int tx = tlo[0]; tx <= thi[0]; ++tx) {
-                    const int tt[3] = {tx, ty, tz};
-                    int lin = 0, str = 1;
-                    for (int k = 0; k < nd; ++k) {
-                        lin += tt[k] * str;
-                        str *= L.nt[k];
-                    }
-                    const int q = tab[lin];
-                    if (q < 0) continue;
-                    unsigned gk = 0, gs = 1;
-                    for (int k = 0; k < nd; ++k) {
-                        gk += (unsigned)(ci[k] - (L.org[k] + tt[k] * L.n[k] - L.g)) * gs;
-                        gs *= (unsigned)(L.n[k] + 2 * L.g);
-                    }
-                    f(j, q, (unsigned)q * gcells + gk);
-                }
+    for (int k = 0; k < nd; ++k)
+        for (int s = 0; s < 3; ++s) {
+            if (s != 1 && !L.periodic[k]) continue;
+            const int x = c[k] + (s - 1) * (L.dom_hi[k] - L.dom_lo[k] + 1);
+            ci[k][s] = x;
+            tlo[k][s] = max(-floordiv(-(x - L.org[k] - L.n[k] + 1 - L.g), L.n[k]), 0);
+            thi[k][s] = min(floordiv(x - L.org[k] + L.g, L.n[k]), L.nt[k] - 1);
+        }
+    for (int sz = 0; sz < 3; ++sz) {
+        if (tlo[2][sz] > thi[2][sz]) continue;
+        for (int sy = 0; sy < 3; ++sy) {
+            if (tlo[1][sy] > thi[1][sy]) continue;
+            for (int sx = 0; sx < 3; ++sx) {
+                if (tlo[0][sx] > thi[0][sx]) continue;
+                const int j = sx + 3 * sy + 9 * sz;
+                const int sv[3] = {sx, sy, sz};
+                for (int tz = tlo[2][sz]; tz <= thi[2][sz]; ++tz)
+                    for (int ty = tlo[1][sy]; ty <= thi[1][sy]; ++ty)
+                        for (int tx = tlo[0][sx]; tx <= thi[0][sx]; ++tx) {
+                            const int tt[3] = {tx, ty, tz};
+                            int lin = 0, str = 1;
+                            for (int k = 0; k < nd; ++k) {
+                                lin += tt[k] * str;
+                                str *= L.nt[k];
+                            }
+                            const int q = tab[lin];
+                            if (q < 0) continue;
+                            unsigned gk = 0, gs = 1;
+                            for (int k = 0; k < nd; ++k) {
+                                gk += (unsigned)(ci[k][sv[k]] - (L.org[k] + tt[k] * L.n[k] - L.g)) * gs;
+                                gs *= (unsigned)(L.n[k] + 2 * L.g);
+                            }
+                            f(j, q, (unsigned)q * gcells + gk);
+                        }
+            }
+        }
     }
 }
 // per marker: its interior key (patch q * patch cells + the cell's box index; 0xffffffff

@@ -1291,15 +1291,17 @@ __device__ __forceinline__ int range_pos(const Ranges& R, int j) {
 // ca_base_z + col (nz + 1) + a' (a' = 0 .. nz): such a component's ring needs the
 // key-frame components' slots (5 for IB_4), not one more.
 // (zb: the column-anchor's index in the shifted-z frame, patch base ca_base_z + col (nz + 1)
-// + a; zxlo, zilo: the z origin of that frame, x_lower - dz / 2, and the z ilower)
+// + a; zxlo, zilo: the z origin of that frame, x_lower - dz / 2, and the z ilower.  ptab:
+// the patches' first column-anchors in LDS (cs_patch_table), else searched in p.pd)
+constexpr int CS_PTAB = 2048;
 __device__ __forceinline__ bool ca_decode(const Params& p, int ca, ColGeom& cg, int& col, int& a, const int*& bs,
-                                          int& zb, double& zxlo, int& zilo) {
+                                          int& zb, double& zxlo, int& zilo, const int* ptab) {
     int base = 0;
     if (p.pd) {
         int lo = 0, hi = p.npatch - 1;
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
-            if (p.pd[mid].bucket_base / NBAND <= ca) lo = mid;
+            if ((ptab ? ptab[mid] : p.pd[mid].bucket_base / NBAND) <= ca) lo = mid;
             else hi = mid - 1;
         }
         const PatchDesc& P = p.pd[lo];
@@ -1342,15 +1344,25 @@ constexpr int CS_GRID = 8192;
 __device__ __forceinline__ bool cs_stands(const Params& p) {
     return p.items_skip && *p.items_skip == 0 && (!p.cs_off_z || *p.cs_zflip == 0);
 }
+// a level's patch search in LDS: the first column-anchor of every patch (a dependent chain
+// of ~9 loads from the patch table per column-anchor otherwise; cfg5 has 0.8 M of them)
+__device__ __forceinline__ const int* cs_patch_table(const Params& p, int* ptab) {
+    if (!p.pd || p.npatch > CS_PTAB) return nullptr;
+    for (int q = threadIdx.x; q < p.npatch; q += BLOCK) ptab[q] = p.pd[q].bucket_base / NBAND;
+    __syncthreads();
+    return ptab;
+}
 __global__ __launch_bounds__(BLOCK) void k_cand_count(Params p, int ncl, int* cnt) {
     if (cs_stands(p)) return;
+    __shared__ int ptab_s[CS_PTAB];
+    const int* const ptab = cs_patch_table(p, ptab_s);
     for (int ca = blockIdx.x * BLOCK + threadIdx.x; ca < ncl; ca += gridDim.x * BLOCK) {
         ColGeom cg;
         int col, a, zb, zilo;
         double zxlo;
         const int* bs;
         int t = 0;
-        if (ca_decode(p, ca, cg, col, a, bs, zb, zxlo, zilo)) {
+        if (ca_decode(p, ca, cg, col, a, bs, zb, zxlo, zilo, ptab)) {
 #pragma unroll
             for (int r = 0; r < 11; ++r) {
                 int b, e;
@@ -1374,12 +1386,14 @@ __global__ __launch_bounds__(BLOCK) void k_cand_write(Params p, int ncl, const i
     gdouble* const sX = cur_sorted_X(p);
     const double inv_dz = 1.0 / p.bg.dx[2];
     int* const offz = const_cast<int*>(p.cs_off_z);
+    __shared__ int ptab_s[CS_PTAB];
+    const int* const ptab = cs_patch_table(p, ptab_s);
     for (int ca = blockIdx.x * (BLOCK / SW) + (int)(threadIdx.x / SW); ca < ncl; ca += nw) {
         ColGeom cg;
         int col, a, zb, zilo;
         double zxlo;
         const int* bs;
-        const bool items = ca_decode(p, ca, cg, col, a, bs, zb, zxlo, zilo);
+        const bool items = ca_decode(p, ca, cg, col, a, bs, zb, zxlo, zilo, ptab);
         const int o = off[ca];
         if (SHZ && lane == 0) {
             if (a == 0) offz[zb] = o;
