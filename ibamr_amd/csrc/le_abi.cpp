@@ -195,6 +195,7 @@ struct ibtk_le_markers_s {
     long long nclz = 0;
     // the re-binning's shifted-z anchor parities and their state (RebinBufs::zbits, zst)
     DevBuf zbits, zst;
+    int rb_epoch = 0;  // re-binnings so far (RebinBufs::epoch)
     int item_bound = 0;
     // a level of patches (ibtk_le_level_bin): 0 = one patch (the fields above)
     int npatch = 0;
@@ -762,7 +763,8 @@ extern "C" int ibtk_le_markers_rebin(ibtk_le_ctx ctx, ibtk_le_markers m, const d
     if ((rc = m->zbits.ensure(wb))) return rc;
     const bool znew = !m->zst.p;
     if ((rc = m->zst.ensure(2 * sizeof(int)))) return rc;
-    HIP_TRY(hipMemsetAsync(m->zst.as<int>() + (znew ? 0 : 1), 0, (znew ? 2 : 1) * sizeof(int), s));
+    if (znew) HIP_TRY(hipMemsetAsync(m->zst.p, 0, 2 * sizeof(int), s));
+    m->rb_epoch = m->rb_epoch == INT_MAX ? 1 : m->rb_epoch + 1;  // zst[1] = 0 never matches
     if ((rc = ctx->keys_in.ensure(sizeof(unsigned) * (size_t)n))) return rc;
     if ((rc = ctx->vals_in.ensure(sizeof(int) * (size_t)n))) return rc;
     if (fresh) {  // the in/out counts start from zero (k_rebin_append leaves them so)
@@ -770,11 +772,7 @@ extern "C" int ibtk_le_markers_rebin(ibtk_le_ctx ctx, ibtk_le_markers m, const d
         HIP_TRY(hipMemsetAsync(m->rb_cout.p, 0, bb, s));
         m->rb_zeroed_nb = nb;
     }
-    // the sentinel word past the last (k_rekey writes words up to nw; word nw only
-    // with zeros) and the movers' long-list queue
-    HIP_TRY(hipMemsetAsync(m->rb_mbits.as<unsigned>() + nw, 0, sizeof(unsigned), s));
-    HIP_TRY(hipMemsetAsync(m->rb_wcnt.as<int>() + nw, 0, sizeof(int), s));
-    HIP_TRY(hipMemsetAsync(m->rb_nbig.p, 0, sizeof(int), s));
+    // (the sentinel word past the last and the movers' long-list queue: cleared by k_rekey)
     Params p;
     std::memset(&p, 0, sizeof(p));
     p.bg = m->bg;
@@ -826,6 +824,7 @@ extern "C" int ibtk_le_markers_rebin(ibtk_le_ctx ctx, ibtk_le_markers m, const d
     r.order_gen = m->sel_gs.p ? m->sel_gs.as<int>() : nullptr;
     r.zbits = m->zbits.as<unsigned>();
     r.zst = m->zst.as<int>();
+    r.epoch = m->rb_epoch;
     // k_rekey raises the per-bucket mover counts and k_rebin_append consumes them back
     // to zero: until the sequence has been queued whole, the next call must clear them
     m->rb_zeroed_nb = -1;
@@ -1458,6 +1457,7 @@ static int cand_stream(ibtk_le_ctx ctx, ibtk_le_markers m, Params& p) {
     const bool keep = m->cs_state == 2 && (!split || (m->cs_split && m->zst.p));
     q.items_skip = keep ? m->cs_skip : nullptr;
     q.cs_zflip = m->zst.p ? m->zst.as<int>() + 1 : nullptr;
+    q.cs_epoch = m->rb_epoch;
     HIP_TRY(launch_cand_stream(q, (int)ncl, m->cs_cnt.as<int>(), m->cs_off.as<int>(), m->cs_pos.as<int>(), ctx->temp.p,
                                ctx->temp.cap, ctx->stream));
     m->cs_state = 1;

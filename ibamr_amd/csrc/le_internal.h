@@ -176,7 +176,8 @@ struct Params {
     const int* cs_off_z;       // closed-form kernels: the stream's boundaries per anchor of the frame
                                // shifted by -dz/2 in z (side-z, node, x/y-edge components; k_cand_write)
     int cs_rint;               // the spread's stencils anchor by rint (IB_4), not NINT
-    const int* cs_zflip;       // with cs_off_z and items_skip: nonzero when a shifted-z anchor changed
+    const int* cs_zflip;       // with cs_off_z and items_skip: == cs_epoch when a shifted-z anchor changed
+    int cs_epoch;              //     in the last re-binning (RebinBufs::zst, epoch)
     const int* nentries_dev;   // device copy of the list length
     const double* Qin;         // spread: marker values
     const double* sorted_F;    // spread: Qin gathered in sorted order, [comp][sorted position]
@@ -255,7 +256,8 @@ struct RebinBufs {
     double* xb;
     int* order_gen;         // bumped when something moved (the order changed; nullable)
     unsigned* zbits;        // shifted-z anchor parities per sorted position (nw + 1 words; k_rekey)
-    int* zst;               // [0] zbits are in the current order, [1] (zeroed before) a parity changed
+    int* zst;               // [0] zbits are in the current order, [1] = epoch: a parity changed
+    int epoch;              // this re-binning's number (nonzero)
 };
 hipError_t launch_set_xcur(double** xcur, double* x, hipStream_t s);
 hipError_t launch_rekey(int kernel, const Params& p, const RebinBufs& r, hipStream_t s);

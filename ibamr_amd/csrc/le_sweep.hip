@@ -221,15 +221,23 @@ __device__ __forceinline__ double* rebin_other(double* const* xcur, double* xa, 
 // as a bit per entry with per-word counts.
 // zbits (closed-form kernels, nullable): the shifted-z anchor parity per sorted position,
 // 32 per word (entry_key), compared with the last re-binning's when zst[0] says those are in
-// this order (it moved nothing) -- a difference, or none to compare with, sets zst[1]: a
-// split candidate stream (k_cand_write SHZ) must then be rebuilt even if nothing moved.
+// this order (it moved nothing) -- a difference, or none to compare with, sets zst[1] to this
+// re-binning's epoch: a split candidate stream (k_cand_write SHZ) must then be rebuilt even
+// if nothing moved.  Block 0 also clears the words past the last (mbits / wcnt[nw]) and the
+// long-list queue (nbig) the later kernels count on.
 template <int K>
 __global__ __launch_bounds__(BLOCK) void k_rekey(Params p, int n, const unsigned* kold, const int* sl,
                                                  double* const* xcur, double* xa, double* xb, unsigned* mbits,
-                                                 int* wcnt, int* cin, int* cout, unsigned* zbits, int* zst) {
+                                                 int* wcnt, int* cin, int* cout, unsigned* zbits, int* zst, int epoch,
+                                                 int nw, int* nbig) {
     __shared__ double sx[3 * BLOCK];
     const int e0 = blockIdx.x * BLOCK;
     const int e = e0 + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // (a wave ending at word nw writes it 0 as well)
+        mbits[nw] = 0u;
+        wcnt[nw] = 0;
+        *nbig = 0;
+    }
     bool mv = false;
     int zp = 0;
     // the last parities of the wave's two words and their state, loaded ahead of the
@@ -273,7 +281,7 @@ __global__ __launch_bounds__(BLOCK) void k_rekey(Params p, int n, const unsigned
             const bool same = zv != 0 && zo0 == (unsigned)zb && zo1 == (unsigned)(zb >> 32);
             zbits[w] = (unsigned)zb;
             zbits[w + 1] = (unsigned)(zb >> 32);
-            if (!same) zst[1] = 1;
+            if (!same) zst[1] = epoch;
         }
     }
     __syncthreads();
@@ -1342,7 +1350,7 @@ constexpr int CS_GRID = 8192;
 // a re-binning that moved nothing (and, for a split stream, changed no shifted-z anchor):
 // the stream stands
 __device__ __forceinline__ bool cs_stands(const Params& p) {
-    return p.items_skip && *p.items_skip == 0 && (!p.cs_off_z || *p.cs_zflip == 0);
+    return p.items_skip && *p.items_skip == 0 && (!p.cs_off_z || *p.cs_zflip != p.cs_epoch);
 }
 // a level's patch search in LDS: the first column-anchor of every patch (a dependent chain
 // of ~9 loads from the patch table per column-anchor otherwise; cfg5 has 0.8 M of them)
@@ -1378,6 +1386,20 @@ __global__ __launch_bounds__(BLOCK) void k_cand_count(Params p, int ncl, int* cn
 // by range_pos, 64 a store.  SHZ: split by the shifted anchor (a ballot compaction from
 // each end) and the shifted-z boundary cs_off_z[zb + 1] written; lane 0 of the wave that
 // takes a column's anchor 0 writes its column's first boundary, cs_off_z[zb] = cs_off[ca].
+// The loads are unconditional (indices clamped), so that no branch waits on them.  (Two
+// column-anchors a pass, their loads issued together, measured 0.1-0.15 ms slower on cfg4
+// and cfg5 --move, profiles/r05x.)
+struct CaJob {
+    ColGeom cg;
+    int col, a, zb, zilo, o, t;
+    double zxlo;
+    bool items;
+    const int* bs;
+    int rowv[3];
+    Ranges R;
+    int e0;     // the lane's first candidate (clamped into the stream piece)
+    double z0;  // its z (SHZ)
+};
 template <bool SHZ>
 __global__ __launch_bounds__(BLOCK) void k_cand_write(Params p, int ncl, const int* off, int* pos) {
     if (cs_stands(p)) return;
@@ -1388,54 +1410,69 @@ __global__ __launch_bounds__(BLOCK) void k_cand_write(Params p, int ncl, const i
     int* const offz = const_cast<int*>(p.cs_off_z);
     __shared__ int ptab_s[CS_PTAB];
     const int* const ptab = cs_patch_table(p, ptab_s);
-    for (int ca = blockIdx.x * (BLOCK / SW) + (int)(threadIdx.x / SW); ca < ncl; ca += nw) {
-        ColGeom cg;
-        int col, a, zb, zilo;
-        double zxlo;
-        const int* bs;
-        const bool items = ca_decode(p, ca, cg, col, a, bs, zb, zxlo, zilo, ptab);
-        const int o = off[ca];
-        if (SHZ && lane == 0) {
-            if (a == 0) offz[zb] = o;
-            if (ca == ncl - 1) offz[zb + 2] = off[ca + 1];  // the stream's end (a' = nz + 1 of the last column)
-        }
-        if (!items || off[ca + 1] == o) {
-            if (SHZ && lane == 0) offz[zb + 1] = o;
-            continue;  // no candidate
-        }
-        const int cx = col % cg.ncx, cy = col / cg.ncx;
-        const int col0 = (cy - 1) * cg.ncx + (cx - 1);
-        int rowv[3];
+    auto load_rows = [&](int ca, CaJob& J) {
+        J.items = ca < ncl && ca_decode(p, ca, J.cg, J.col, J.a, J.bs, J.zb, J.zxlo, J.zilo, ptab);
+        J.o = off[min(ca, ncl - 1)];
+        if (J.items) {
+            const int cx = J.col % J.cg.ncx, cy = J.col / J.cg.ncx;
+            const int col0 = (cy - 1) * J.cg.ncx + (cx - 1);
 #pragma unroll
-        for (int r = 0; r < 3; ++r) rowv[r] = bs[bucket(cg, a, col0 + r * cg.ncx, 0) + min(lane, 27)];
-        Ranges R;
-        make_ranges_lanes(rowv, R);
-        const int t = R.pre[SSh<K_IB_4>::NR];
+            for (int r = 0; r < 3; ++r) J.rowv[r] = J.bs[bucket(J.cg, J.a, col0 + r * J.cg.ncx, 0) + min(lane, 27)];
+        }
+    };
+    auto load_first = [&](CaJob& J) {
+        J.t = 0;
+        J.e0 = 0;
+        J.z0 = 0.0;
+        if (!J.items) return;
+        make_ranges_lanes(J.rowv, J.R);
+        J.t = J.R.pre[SSh<K_IB_4>::NR];
+        J.e0 = range_pos(J.R, min(lane, max(J.t - 1, 0)));
+        if constexpr (SHZ) J.z0 = sX[(int64_t)3 * min(J.e0, p.nsorted - 1) + 2];  // (t = 0: e0 may be n)
+    };
+    auto finish = [&](int ca, CaJob& J) {
+        if (ca >= ncl) return;
+        const int o = J.o;
+        if (SHZ && lane == 0) {
+            if (J.a == 0) offz[J.zb] = o;
+            if (ca == ncl - 1) offz[J.zb + 2] = off[ca + 1];  // the stream's end (a' = nz + 1 of the last column)
+        }
+        const int t = J.t;
         if constexpr (!SHZ) {
-            for (int j = lane; j < t; j += SW) pos[o + j] = range_pos(R, j);
+            if (lane < t) pos[o + lane] = J.e0;
+            for (int j = lane + SW; j < t; j += SW) pos[o + j] = range_pos(J.R, j);
         } else {
-            const int aa = a + cg.org[2] - zilo;  // the key anchor as a shifted-frame NINT
+            const int aa = J.a + J.cg.org[2] - J.zilo;  // the key anchor as a shifted-frame NINT
             int nlo = 0, nup = 0;
             for (int j0 = 0; j0 < t; j0 += SW) {
                 const int j = j0 + lane;
-                const int e = j < t ? range_pos(R, j) : 0;
-                bool up = false;
-                if (j < t) {
-                    const double xo = (sX[(int64_t)3 * e + 2] - zxlo) * inv_dz;
-                    const int n = p.cs_rint ? (int)__builtin_rint(xo) : d_nint(xo);
-                    up = n > aa;  // n = aa + 1 (the binning invariant: aa or aa + 1)
+                int e = J.e0;
+                double z = J.z0;
+                if (j0 > 0) {
+                    e = range_pos(J.R, min(j, t - 1));
+                    z = sX[(int64_t)3 * e + 2];
                 }
-                const unsigned long long bu = __ballot(up), bl = __ballot(j < t && !up);
+                const double xo = (z - J.zxlo) * inv_dz;
+                const int n = p.cs_rint ? (int)__builtin_rint(xo) : d_nint(xo);
+                const bool in = j < t;
+                const bool up = in && n > aa;  // n = aa + 1 (the binning invariant: aa or aa + 1)
+                const unsigned long long bu = __ballot(up), bl = __ballot(in && !up);
                 const unsigned long long below = (1ull << lane) - 1ull;
-                if (j < t) {
+                if (in) {
                     if (up) pos[o + t - 1 - (nup + __popcll(bu & below))] = e;
                     else pos[o + nlo + __popcll(bl & below)] = e;
                 }
                 nlo += __popcll(bl);
                 nup += __popcll(bu);
             }
-            if (lane == 0) offz[zb + 1] = o + nlo;
+            if (lane == 0) offz[J.zb + 1] = o + nlo;
         }
+    };
+    for (int ca = blockIdx.x * (BLOCK / SW) + (int)(threadIdx.x / SW); ca < ncl; ca += nw) {
+        CaJob J;
+        load_rows(ca, J);
+        load_first(J);
+        finish(ca, J);
     }
 }
 hipError_t launch_cand_stream(const Params& p, int ncl, int* cnt, int* off, int* pos, void* temp, size_t temp_bytes,
@@ -2448,7 +2485,7 @@ hipError_t launch_rekey_t(const Params& p, const RebinBufs& r, hipStream_t s) {
     if (r.n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_rekey<K>, dim3((r.n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, p, r.n, r.kold, r.lsorted,
                        r.xcur, r.xa, r.xb, r.mbits, r.wcnt, r.cin, r.cout, KT<K>::FAM == 0 ? r.zbits : nullptr,
-                       r.zst);
+                       r.zst, r.epoch, r.nw, r.nbig);
     return hipGetLastError();
 }
 template <int K>
