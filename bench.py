@@ -264,9 +264,10 @@ def lds_atomic(ctx, spread_call, k_ms):
 
 
 # what kernel_ms times (HIP events around the sweep launches on the context stream)
-KERNEL_NOTE = ("interp = k_interp_sweep<K, LVL>; spread = its component launches summed: "
-               "k_spread_sweep<K, LVL, false, true> (the components whose z frame is the keys', a 5-slot ring) "
-               "then k_spread_sweep<K, LVL, false, false> (side data's z component); rocprofv3 lists them apart")
+KERNEL_NOTE = ("interp = k_interp_sweep<K, LVL>; spread = k_spread_sweep<K, LVL, false, ZC> over all three "
+               "components in one launch (closed-form kernels: ZC, the 5-slot ring, the z-side component through "
+               "the candidate stream's shifted-z split); the candidate stream's build (k_cand_count / k_cand_write, "
+               "skipped on the device when the re-binning changed nothing) is outside these events")
 
 
 def run_level(args, cfg, kernel, dev):

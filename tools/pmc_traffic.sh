@@ -10,8 +10,8 @@
 # profiles/pmc_<cfg>_<kernel>_1gpu.json, which bench.py reads when the hash
 # matches the build it runs.
 # Usage: [BENCH_ARGS="..."] tools/pmc_traffic.sh <outdir> [cfg] [kernel]
-# Per step: the spread is one launch per run of components alike in z frame
-# (launch_spread_sweep_t: side data = 2 launches); their per-launch means are summed.
+# Per step: the spread sweep is one launch over all components (closed-form kernels;
+# launch_spread_sweep_t); per-launch means of each kernel name are summed.
 out=$1; cfg=${2:-cfg4}; kern=${3:-IB_4}
 export TMPDIR=/tmp
 mkdir -p "$out"
