@@ -187,7 +187,7 @@ __global__ __launch_bounds__(BLOCK) void k_bin_col(Params p, int n, unsigned* ke
     if (!(p.n_dev && i >= *p.n_dev)) {
         const int s = p.indices ? p.indices[i] : i;
 #pragma unroll
-        for (int d = 0; d < 3; ++d) Xs[d] = p.X[(int64_t)3 * s + d] + (p.Xshift ? p.Xshift[(int64_t)3 * i + d] : 0.0);
+        for (int d = 0; d < 3; ++d) Xs[d] = p.Xshift ? p.X[(int64_t)3 * s + d] + p.Xshift[(int64_t)3 * i + d] : p.X[(int64_t)3 * s + d];
     }
     keys[i] = entry_key<K>(p, i, Xs);
     vals[i] = i;
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(BLOCK) void k_rekey(Params p, int n, const unsigned
         const D3 x = ld3(p.X + (int64_t)3 * s);  // as k_gather_col (a fixed-capacity list's rows all exist)
         double Xs[3];
 #pragma unroll
-        for (int d = 0; d < 3; ++d) Xs[d] = x.v[d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
+        for (int d = 0; d < 3; ++d) Xs[d] = p.Xshift ? x.v[d] + p.Xshift[(int64_t)3 * l + d] : x.v[d];  // (no + 0.0: X bit for bit)
         const unsigned k = entry_key<K>(p, l, Xs, zbits ? &zp : nullptr);
         const unsigned ko = kold[e];
         mv = k != ko;
@@ -655,7 +655,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather_col(Params p, int n, int* sort
         sorted_s[e] = s;
         const D3 x = ld3(p.X + (int64_t)3 * s);  // one 24-byte record per lane
 #pragma unroll
-        for (int d = 0; d < 3; ++d) sx[3 * threadIdx.x + d] = x.v[d] + (p.Xshift ? p.Xshift[(int64_t)3 * l + d] : 0.0);
+        for (int d = 0; d < 3; ++d) sx[3 * threadIdx.x + d] = p.Xshift ? x.v[d] + p.Xshift[(int64_t)3 * l + d] : x.v[d];
     }
     __syncthreads();
     const int cnt = 3 * min(BLOCK, n - e0);  // doubles this block writes
@@ -1141,6 +1141,11 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
         if (act) acc = interp_marker<K>(p, cd, ring, gx0, gy0, zorg, am, m.X, m.s);
         double* dst = (act && m.q >= 0) ? p.Qout + ((int64_t)p.Q_depth * m.q + cd.qcomp) : p.sink + lane;
         *dst = acc;
+        if (p.upd_X && act && m.q >= 0) {  // ibtk_le_fill_interp_update: X_out = dt U + X, this component's slot
+            const int d = cd.qcomp;
+            const double x = d == 0 ? m.X[0] : (d == 1 ? m.X[1] : m.X[2]);  // (the sorted copy of X: no shifts)
+            p.upd_X[(int64_t)3 * m.q + d] = p.upd_dt * acc + x;
+        }
     };
     double pv[NPT];
     for (int z = a0 + LO + w; z < a0 + HI; z += IWAVES) {
@@ -1187,10 +1192,17 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
 // Entries binned "outside" (no stencil point can reach any array): V = 0.
 __global__ __launch_bounds__(BLOCK) void k_interp_outside_col(Params p, int n) {
     const int first = p.plane_start[p.nbuckets_total];
+    gdouble* const sX = cur_sorted_X(p);
     for (int e = first + blockIdx.x * BLOCK + threadIdx.x; e < n; e += gridDim.x * BLOCK) {
         const int s = p.qdst ? p.qdst[e] : p.sorted_s[e];
         if (s < 0) continue;
-        for (int c = 0; c < p.ncomp; ++c) p.Qout[(int64_t)p.Q_depth * s + p.comp[c].qcomp] = 0.0;
+        for (int c = 0; c < p.ncomp; ++c) {
+            p.Qout[(int64_t)p.Q_depth * s + p.comp[c].qcomp] = 0.0;
+            if (p.upd_X) {  // (X + dt 0)
+                const int d = p.comp[c].qcomp;
+                p.upd_X[(int64_t)3 * s + d] = p.upd_dt * 0.0 + sX[(int64_t)3 * e + d];
+            }
+        }
     }
 }
 
