@@ -541,9 +541,6 @@ def main():
     ap.add_argument("--move", action="store_true",
                     help="a full explicit coupling step: interp, X += dt U (ibtk_le_position_update), "
                          "migrate the slab leavers (N > 1), re-bin, spread")
-    ap.add_argument("--unfused-update", action="store_true",
-                    help="--move on one rank: the position update as its own pass (ibtk_le_position_update) "
-                         "instead of the interp sweep's epilogue (ibtk_le_fill_interp_update)")
     ap.add_argument("--regrid-every", type=int, default=1, metavar="K",
                     help="with --move: migrate (and with --renumber redistribute) every K-th step only, the "
                          "reference's lazy cadence (regrid_interval); between regrids the markers keep their rank "
@@ -793,20 +790,10 @@ def main():
         nstep["k"] += 1
         if record:
             E[0].record()
-        # one rank, own markers, no shifts: X += dt U in the interp's epilogue
-        # (ibtk_le_fill_interp_update), not a pass of its own
-        fuse_upd = (fused_fill and not args.unfused_update and world == 1 and gm is None and not fixed
-                    and lag is None and cur["X"] is X and cur["U"] is U)
-        if fuse_upd:
-            le.fill_interp_update(ctx, bins, kernel, "side", geom, u, U, X, dt_move,
-                                  periodic=[1, 1, 1])
-        else:
-            interp_with_fill()
+        interp_with_fill()
         if record:
             E[1].record()
-        if fuse_upd:
-            pass
-        elif not at_regrid:
+        if not at_regrid:
             le.position_update(ctx, "euler", dt_move, X, U, out=X)
             if world > 1:  # the slab-ownership slack (one rank: the periodic box is the slab)
                 check_drift(X, n_dev if fixed else None)
@@ -1019,10 +1006,7 @@ def main():
                    "migration": ("fixed-capacity, device counts, no host sync" if fixed else
                                  "counts read by the host" if world > 1 and args.move else None), "overlap": world > 1 and not args.no_overlap,
                    "overlap_check": overlap_check,
-                   "step": ("ghost fill + interp(3 comps) + position update" +
-                            (" (in the interp sweep's epilogue, ibtk_le_fill_interp_update)"
-                             if (world == 1 and not fixed and not args.renumber and not args.unfused_update
-                                 and not args.unfused_fill and gm is None) else "") + " + " +
+                   "step": ("ghost fill + interp(3 comps) + position update + " +
                             (f"at every {args.regrid_every}-th step (regrid) " if args.regrid_every > 1 else "") +
                             "migrate + " +
                             ("redistribute (numbering + nonlocal nodes + reorder) + " if args.renumber else "") +

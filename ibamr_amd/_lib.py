@@ -174,9 +174,6 @@ _SIGS = [
     ("ibtk_le_level_node_distribution", c_int,
      [c_void_p, c_int, ctypes.POINTER(PatchGeom), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
       c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
-    ("ibtk_le_fill_interp_update", c_int,
-     [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.POINTER(PatchGeom), c_void_p, c_int, c_void_p, c_int,
-      c_void_p, c_void_p, c_double, c_void_p]),
     ("ibtk_le_level_index_lists", c_int,
      [c_void_p, c_int, ctypes.POINTER(PatchGeom), c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
       c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),

@@ -1100,12 +1100,10 @@ static int stamps_report(ibtk_le_ctx ctx, size_t nst, Params& p) {
 
 int ibtk_le::interp_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis, const void* geomv,
                          const double* const* q_dev, int q_depth, double* Q_dev, int Q_depth, const double* X_dev,
-                         bool check_ghosts, const int* iper, double* upd_X, double upd_dt) {
+                         bool check_ghosts, const int* iper) {
     const ibtk_le_patch_geom* geom = static_cast<const ibtk_le_patch_geom*>(geomv);
     Params p;
     if (int rc = prepare(ctx, m, kernel, geom, X_dev, p)) return rc;
-    p.upd_X = upd_X;
-    p.upd_dt = upd_dt;
     if (iper)
         for (int d = 0; d < 3; ++d) p.iper[d] = iper[d] ? 1 : 0;
     // LEInteractor.cpp:2416-2426: interp needs min(gcw) >= floor(stencil/2)+1
@@ -1166,34 +1164,6 @@ extern "C" int ibtk_le_fill_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kerne
         if (per[d] && geom->iupper[d] - geom->ilower[d] + 1 < 2 * geom->gcw[d] + 1)
             return fail(IBTK_LE_ERR_ARG, "periodic dim %d narrower than 2*ghost+1", d);
     return ibtk_le::interp_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, X_dev, true, per);
-}
-
-// ibtk_le_fill_interp with IBMethod::eulerStep's position update (IBMethod.cpp:619-655:
-// X_new = dt U + X, VecWAXPY) in its epilogue: the lane that sums a marker's component d
-// also writes X_out(d, s) = dt Q(d, s) + X(d, s), X read from the sorted copy the sweep
-// holds (a list without periodic shifts: the copy is X bit for bit).  k_position_update's
-// pass over X and U goes away.
-extern "C" int ibtk_le_fill_interp_update(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
-                                          const ibtk_le_patch_geom* geom, const double* const* q_dev, int q_depth,
-                                          double* Q_dev, int Q_depth, const double* X_dev, const int* periodic,
-                                          double dt, double* X_out_dev) {
-    if (!geom || !m || !X_out_dev) return fail(IBTK_LE_ERR_ARG, "fill_interp_update: null argument");
-    if (geom->ndim != 3 || !m->binned3) return fail(IBTK_LE_ERR_ARG, "fill_interp_update: 3-D column binnings only");
-    if (m->has_xshift) return fail(IBTK_LE_ERR_ARG, "fill_interp_update: a list with periodic shifts");
-    if (Q_depth != 3) return fail(IBTK_LE_ERR_ARG, "fill_interp_update: Q_depth must be NDIM (one slot a coordinate)");
-    const int nc = ncomponents(geom, centering, q_depth, Q_depth);
-    if (nc != 3) return fail(IBTK_LE_ERR_ARG, "fill_interp_update: three components (side / edge data, or depth NDIM)");
-    // PIECEWISE_CUBIC and IB_3 read X itself (the unshifted side test): not in place
-    if ((kernel == K_PIECEWISE_CUBIC || kernel == K_IB_3) && X_out_dev == X_dev)
-        return fail(IBTK_LE_ERR_ARG, "fill_interp_update: kernel %s reads X, X_out must not be X", kNames[kernel]);
-    int per[3] = {1, 1, 1};
-    if (periodic)
-        for (int d = 0; d < 3; ++d) per[d] = periodic[d] ? 1 : 0;
-    for (int d = 0; d < 3; ++d)
-        if (per[d] && geom->iupper[d] - geom->ilower[d] + 1 < 2 * geom->gcw[d] + 1)
-            return fail(IBTK_LE_ERR_ARG, "periodic dim %d narrower than 2*ghost+1", d);
-    return ibtk_le::interp_impl(ctx, m, kernel, centering, axis, geom, q_dev, q_depth, Q_dev, Q_depth, X_dev, true, per,
-                                X_out_dev, dt);
 }
 
 // Super-brick candidate lists (k_cand): count, exclusive scan, write.  Built once

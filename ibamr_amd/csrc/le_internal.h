@@ -176,8 +176,6 @@ struct Params {
     const int* cs_off_z;       // closed-form kernels: the stream's boundaries per anchor of the frame
                                // shifted by -dz/2 in z (side-z, node, x/y-edge components; k_cand_write)
     int cs_rint;               // the spread's stencils anchor by rint (IB_4), not NINT
-    double* upd_X;             // ibtk_le_fill_interp_update: X_out(d, s) = upd_dt Q(d, s) + X(d, s) from the interp
-    double upd_dt;
     const int* cs_zflip;       // with cs_off_z and items_skip: == cs_epoch when a shifted-z anchor changed
     int cs_epoch;              //     in the last re-binning (RebinBufs::zst, epoch)
     const int* nentries_dev;   // device copy of the list length
@@ -495,5 +493,5 @@ struct ibtk_le_patch_geom_s;
 namespace ibtk_le {
 int interp_impl(ibtk_le_ctx_s* ctx, ibtk_le_markers_s* m, int kernel, int centering, int axis, const void* geom,
                 const double* const* q_dev, int q_depth, double* Q_dev, int Q_depth, const double* X_dev,
-                bool check_ghosts, const int* iper = nullptr, double* upd_X = nullptr, double upd_dt = 0.0);
+                bool check_ghosts, const int* iper = nullptr);
 }  // namespace ibtk_le

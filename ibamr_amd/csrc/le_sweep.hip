@@ -1141,11 +1141,6 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
         if (act) acc = interp_marker<K>(p, cd, ring, gx0, gy0, zorg, am, m.X, m.s);
         double* dst = (act && m.q >= 0) ? p.Qout + ((int64_t)p.Q_depth * m.q + cd.qcomp) : p.sink + lane;
         *dst = acc;
-        if (p.upd_X && act && m.q >= 0) {  // ibtk_le_fill_interp_update: X_out = dt U + X, this component's slot
-            const int d = cd.qcomp;
-            const double x = d == 0 ? m.X[0] : (d == 1 ? m.X[1] : m.X[2]);  // (the sorted copy of X: no shifts)
-            p.upd_X[(int64_t)3 * m.q + d] = p.upd_dt * acc + x;
-        }
     };
     double pv[NPT];
     for (int z = a0 + LO + w; z < a0 + HI; z += IWAVES) {
@@ -1192,17 +1187,10 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
 // Entries binned "outside" (no stencil point can reach any array): V = 0.
 __global__ __launch_bounds__(BLOCK) void k_interp_outside_col(Params p, int n) {
     const int first = p.plane_start[p.nbuckets_total];
-    gdouble* const sX = cur_sorted_X(p);
     for (int e = first + blockIdx.x * BLOCK + threadIdx.x; e < n; e += gridDim.x * BLOCK) {
         const int s = p.qdst ? p.qdst[e] : p.sorted_s[e];
         if (s < 0) continue;
-        for (int c = 0; c < p.ncomp; ++c) {
-            p.Qout[(int64_t)p.Q_depth * s + p.comp[c].qcomp] = 0.0;
-            if (p.upd_X) {  // (X + dt 0)
-                const int d = p.comp[c].qcomp;
-                p.upd_X[(int64_t)3 * s + d] = p.upd_dt * 0.0 + sX[(int64_t)3 * e + d];
-            }
-        }
+        for (int c = 0; c < p.ncomp; ++c) p.Qout[(int64_t)p.Q_depth * s + p.comp[c].qcomp] = 0.0;
     }
 }
 

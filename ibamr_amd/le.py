@@ -358,26 +358,6 @@ def fill_interp(ctx: Context, markers: Markers, kernel: str, centering: str, geo
                                       pa[0] if pa else None))
 
 
-def fill_interp_update(ctx: Context, markers: Markers, kernel: str, centering: str, geom: Geometry,
-                       q: Sequence[torch.Tensor], Q: torch.Tensor, X: torch.Tensor, dt: float,
-                       X_out: Optional[torch.Tensor] = None, q_depth: int = 1, Q_depth: Optional[int] = None,
-                       axis: int = 0, periodic=None):
-    """fill_interp, then X_out = dt Q + X (IBMethod::eulerStep; position_update("euler", dt,
-    X, Q)) bit for bit, in the same sweep (ibtk_le_fill_interp_update).  X_out None: in place."""
-    if Q_depth is None:
-        Q_depth = geom.ndim if centering in ("side", "edge") else q_depth
-    if X_out is None:
-        X_out = X
-    if X_out.shape != X.shape or X_out.dtype != torch.float64 or not X_out.is_contiguous():
-        raise ValueError("X_out: a contiguous float64 tensor shaped as X")
-    arr = _ptr_array(q, geom)
-    pa = _periodic_arg(periodic, geom.ndim)
-    check(ctx.lib.ibtk_le_fill_interp_update(ctx.h, markers.h, kernel_id(kernel), CENTERING[centering], axis,
-                                             ctypes.byref(geom.c), arr, q_depth, _ptr(Q), Q_depth, _ptr(X),
-                                             pa[0] if pa else None, float(dt), _ptr(X_out)))
-    return X_out
-
-
 def zero_ghosts_spread(ctx: Context, markers: Markers, kernel: str, centering: str, geom: Geometry,
                        q: Sequence[torch.Tensor], Q: torch.Tensor, X: torch.Tensor, q_depth: int = 1,
                        Q_depth: Optional[int] = None, axis: int = 0):

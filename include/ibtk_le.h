@@ -313,17 +313,6 @@ int ibtk_le_fill_periodic_ghosts(ibtk_le_ctx ctx, const ibtk_le_patch_geom* geom
 int ibtk_le_fill_interp(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                         const ibtk_le_patch_geom* geom, const double* const* q_dev, int q_depth, double* Q_dev,
                         int Q_depth, const double* X_dev, const int* periodic);
-/* ibtk_le_fill_interp followed by the explicit Euler step of the marker positions
- * (IBMethod::eulerStep, IBMethod.cpp:619-655: X_new = dt U + X, VecWAXPY, with U the
- * interpolated Q -- what ibtk_le_position_update(IBTK_LE_EULER, dt, X, Q, ...) gives, bit
- * for bit), in the same sweep: the lane that sums component d of marker s also writes
- * X_out(d, s).  Q_depth must be NDIM with three components (side / edge data, or cell / node
- * data of depth NDIM); a 3-D column binning of a list without periodic shifts.  X_out may be
- * X_dev (in place) except for PIECEWISE_CUBIC and IB_3, which read X itself.  Rows of markers
- * the list does not name are not written. */
-int ibtk_le_fill_interp_update(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
-                               const ibtk_le_patch_geom* geom, const double* const* q_dev, int q_depth, double* Q_dev,
-                               int Q_depth, const double* X_dev, const int* periodic, double dt, double* X_out_dev);
 /* Spreading in ghost-region-sum mode: zero the ghost layers before spreading the
  * interior markers, then fold every ghost value back onto its periodic interior
  * image (dims folded slowest first, one source per destination per pass:
