@@ -405,8 +405,8 @@ def run_level(args, cfg, kernel, dev):
             E[2].record()
         le.position_update(ctx, "euler", dt_move, X, U, out=X)
         if at_regrid:
-            X.remainder_(1.0)
-            X.masked_fill_(X >= 1.0, 0.0)  # remainder can round up to L
+            # beginDataRedistribution's wrap into the periodic domain (LDataManager.cpp:1385-1399)
+            le.wrap_positions(ctx, X, [0.0, 0.0, 0.0], [1.0, 1.0, 1.0])
             (ii2, _, oi2), (si2, sx2, os2) = le.level_index_lists(ctx, geoms, [0, 0, 0], [N - 1] * 3, X, g)
             lists.update(ii=ii2, oi=oi2)
             lvl_s.relist(si2, sx2, os2).bin(X)
