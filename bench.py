@@ -308,7 +308,9 @@ def run_level(args, cfg, kernel, dev):
     F = torch.rand((M, 3), dtype=torch.float64, device=dev, generator=gen).mul_(2).sub_(1)
     U = torch.zeros((M, 3), dtype=torch.float64, device=dev)
     # the per-patch lists (LIndexSetData::cacheLocalIndices) built on the device in one call
-    (ii, _, oi), (si, sx, os_) = le.level_index_lists(ctx, geoms, [0, 0, 0], [N - 1] * 3, X, g)
+    # (marker order within a patch: the same entries as the reference's cell order, one radix
+    # pass by patch instead of four by (patch, cell))
+    (ii, _, oi), (si, sx, os_) = le.level_index_lists(ctx, geoms, [0, 0, 0], [N - 1] * 3, X, g, order="markers")
     # one binning serves both sweeps: the ghost-box lists (spread), told which of their
     # entries the interior lists (interp) name (ibtk_le_level_select_interior)
     lvl_s = le.Level.from_flat(ctx, geoms, kernel, X, si, sx, os_)
@@ -407,7 +409,8 @@ def run_level(args, cfg, kernel, dev):
         if at_regrid:
             # beginDataRedistribution's wrap into the periodic domain (LDataManager.cpp:1385-1399)
             le.wrap_positions(ctx, X, [0.0, 0.0, 0.0], [1.0, 1.0, 1.0])
-            (ii2, _, oi2), (si2, sx2, os2) = le.level_index_lists(ctx, geoms, [0, 0, 0], [N - 1] * 3, X, g)
+            (ii2, _, oi2), (si2, sx2, os2) = le.level_index_lists(ctx, geoms, [0, 0, 0], [N - 1] * 3, X, g,
+                                                                  order="markers")
             lists.update(ii=ii2, oi=oi2)
             lvl_s.relist(si2, sx2, os2).bin(X)
             binning["full"] += 1

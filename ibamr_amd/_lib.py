@@ -175,7 +175,7 @@ _SIGS = [
      [c_void_p, c_int, ctypes.POINTER(PatchGeom), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
       c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     ("ibtk_le_level_index_lists", c_int,
-     [c_void_p, c_int, ctypes.POINTER(PatchGeom), c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+     [c_void_p, c_int, ctypes.POINTER(PatchGeom), c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
       c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     ("ibtk_le_ldata_reorder", c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     ("ibtk_le_node_distribution", c_int,

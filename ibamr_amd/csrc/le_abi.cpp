@@ -2761,14 +2761,16 @@ extern "C" int ibtk_le_level_node_distribution(ibtk_le_ctx ctx, int npatch, cons
 // is in the patch box) and the ghost-box lists (markers and their periodic images whose
 // cell is in the patch's ghost box, with their shifts), patch by patch, each patch's
 // entries in its box's (ghost box's) cell order, x fastest, a cell's markers by index --
-// the order ibtk_le_periodic_index_list gives one patch.  Keys per marker, a stable device
-// radix sort by (patch, cell), the patch offsets by binary search in the sorted keys.
+// the order ibtk_le_periodic_index_list gives one patch -- or (order 1) in marker order.
+// Keys per marker, a stable device radix sort by (patch, cell) or by patch alone (fewer
+// passes), the patch offsets by binary search in the sorted keys.
 extern "C" int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms,
                                          const int* dom_lo, const int* dom_hi, const int* periodic,
-                                         const double* X_dev, int n_markers, int ghost, int* interior_dev,
+                                         const double* X_dev, int n_markers, int ghost, int order, int* interior_dev,
                                          int interior_cap, int* interior_off, int* ghost_dev, double* Xshift_dev,
                                          int ghost_cap, int* ghost_off) {
     if (!ctx || !interior_off || !ghost_off) return fail(IBTK_LE_ERR_ARG, "null argument");
+    if (order != 0 && order != 1) return fail(IBTK_LE_ERR_ARG, "level_index_lists: order 0 (cells) or 1 (markers)");
     if (n_markers < 0 || interior_cap < 0 || ghost_cap < 0) return fail(IBTK_LE_ERR_ARG, "bad sizes");
     LevelNum L;
     std::vector<int> tab;
@@ -2782,6 +2784,11 @@ extern "C" int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk
         pcells *= (unsigned)L.n[k];
         gcells *= (unsigned)(L.n[k] + 2 * ghost);
     }
+    const int bypatch = order;
+    int pbits = 1;  // bits of the patch keys 0 .. npatch
+    while ((1LL << pbits) <= (long long)npatch) ++pbits;
+    const int kbits = bypatch ? pbits : 32;
+    if (bypatch) pcells = gcells = 1;  // (the offsets' key stride)
     if (set_device(ctx)) return IBTK_LE_ERR_DEVICE;
     const hipStream_t s = ctx->stream;
     int rc;
@@ -2796,12 +2803,12 @@ extern "C" int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk
     HIP_TRY(hipMemcpyAsync(ctx->num_tab.p, tab.data(), sizeof(int) * tab.size(), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(ctx->ll_cnt.as<int>() + n, 0, sizeof(int), s));
     HIP_TRY(launch_level_list_keys(L, ctx->num_tab.as<int>(), X_dev, n, ctx->ll_key.as<unsigned>(),
-                                   ctx->ll_cnt.as<int>(), s));
+                                   ctx->ll_cnt.as<int>(), bypatch, npatch, s));
     if ((rc = scan_excl(ctx, ctx->ll_cnt.as<int>(), ctx->ll_off.as<int>(), n + 1))) return rc;
     // interior: markers by (patch, cell), stable
     HIP_TRY(launch_iota(ctx->ll_id.as<int>(), n, s));
     if ((rc = sort_pairs(ctx, ctx->ll_key.as<unsigned>(), ctx->ll_key2.as<unsigned>(), ctx->ll_id.as<int>(),
-                         ctx->ll_id2.as<int>(), n, 32)))
+                         ctx->ll_id2.as<int>(), n, kbits)))
         return rc;
     HIP_TRY(launch_key_offsets(ctx->ll_key2.as<unsigned>(), n, pcells, npatch, ctx->counts.as<int>(), s));
     int total = 0;
@@ -2824,9 +2831,9 @@ extern "C" int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk
         }
         HIP_TRY(launch_level_list_write(L, ctx->num_tab.as<int>(), X_dev, n, ctx->ll_off.as<int>(),
                                         ctx->ll_key.as<unsigned>(), ctx->ll_id.as<int>(), ctx->ll_src.as<int>(),
-                                        ctx->ll_img.as<int>(), s));
+                                        ctx->ll_img.as<int>(), bypatch, s));
         if ((rc = sort_pairs(ctx, ctx->ll_key.as<unsigned>(), ctx->ll_key2.as<unsigned>(), ctx->ll_id.as<int>(),
-                             ctx->ll_id2.as<int>(), total, 32)))
+                             ctx->ll_id2.as<int>(), total, kbits)))
             return rc;
         HIP_TRY(launch_key_offsets(ctx->ll_key2.as<unsigned>(), total, gcells, npatch, ctx->counts.as<int>(), s));
         HIP_TRY(hipMemcpyAsync(ghost_off, ctx->counts.p, sizeof(int) * (size_t)(npatch + 1), hipMemcpyDeviceToHost, s));

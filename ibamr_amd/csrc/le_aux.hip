@@ -763,9 +763,10 @@ __device__ __forceinline__ void level_ghost_visit(const LevelNum& L, const int* 
     }
 }
 // per marker: its interior key (patch q * patch cells + the cell's box index; 0xffffffff
-// in no local patch box) and its number of ghost-box entries
+// in no local patch box) and its number of ghost-box entries.  bypatch: the keys are the
+// patch alone (npatch: none) -- the lists in marker order within a patch
 __global__ __launch_bounds__(BLOCK) void k_level_list_keys(LevelNum L, const int* tab, const double* X, int n,
-                                                           unsigned* ikey, int* gcnt) {
+                                                           unsigned* ikey, int* gcnt, int bypatch, int npatch) {
     const int s = blockIdx.x * BLOCK + threadIdx.x;
     if (s >= n) return;
     const int nd = L.ndim;
@@ -782,7 +783,8 @@ __global__ __launch_bounds__(BLOCK) void k_level_list_keys(LevelNum L, const int
         k0 += (unsigned)(c[k] - (L.org[k] + t[k] * L.n[k])) * pcells;
         pcells *= (unsigned)L.n[k];
     }
-    if (in && tab[lin] >= 0) key = (unsigned)tab[lin] * pcells + k0;
+    if (in && tab[lin] >= 0) key = bypatch ? (unsigned)tab[lin] : (unsigned)tab[lin] * pcells + k0;
+    else if (bypatch) key = (unsigned)npatch;
     ikey[s] = key;
     int cnt = 0;
     level_ghost_visit(L, tab, c, [&](int, int, unsigned) { ++cnt; });
@@ -791,14 +793,14 @@ __global__ __launch_bounds__(BLOCK) void k_level_list_keys(LevelNum L, const int
 // the ghost-box entries at goff[s]: key, entry id (the stable sort's value), marker, image
 __global__ __launch_bounds__(BLOCK) void k_level_list_write(LevelNum L, const int* tab, const double* X, int n,
                                                             const int* goff, unsigned* gkey, int* gid, int* gsrc,
-                                                            int* gimg) {
+                                                            int* gimg, int bypatch) {
     const int s = blockIdx.x * BLOCK + threadIdx.x;
     if (s >= n) return;
     int c[3];
     level_cell(L, X, s, c);
     int o = goff[s];
-    level_ghost_visit(L, tab, c, [&](int j, int, unsigned key) {
-        gkey[o] = key;
+    level_ghost_visit(L, tab, c, [&](int j, int q, unsigned key) {
+        gkey[o] = bypatch ? (unsigned)q : key;
         gid[o] = o;
         gsrc[o] = s;
         gimg[o] = j;
@@ -834,16 +836,17 @@ __global__ __launch_bounds__(BLOCK) void k_key_offsets(const unsigned* skeys, in
     off[q] = lo;
 }
 hipError_t launch_level_list_keys(const LevelNum& L, const int* tab, const double* X, int n, unsigned* ikey,
-                                  int* gcnt, hipStream_t s) {
+                                  int* gcnt, int bypatch, int npatch, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_level_list_keys, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, L, tab, X, n, ikey, gcnt);
+    hipLaunchKernelGGL(k_level_list_keys, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, L, tab, X, n, ikey, gcnt,
+                       bypatch, npatch);
     return hipGetLastError();
 }
 hipError_t launch_level_list_write(const LevelNum& L, const int* tab, const double* X, int n, const int* goff,
-                                   unsigned* gkey, int* gid, int* gsrc, int* gimg, hipStream_t s) {
+                                   unsigned* gkey, int* gid, int* gsrc, int* gimg, int bypatch, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_level_list_write, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, L, tab, X, n, goff, gkey,
-                       gid, gsrc, gimg);
+                       gid, gsrc, gimg, bypatch);
     return hipGetLastError();
 }
 hipError_t launch_level_list_out(const LevelNum& L, const int* sid, const int* gsrc, const int* gimg, int total,

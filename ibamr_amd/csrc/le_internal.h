@@ -388,10 +388,11 @@ hipError_t launch_level_node_keys(const LevelNum& L, const int* tab, const doubl
 // image's cell, id = the entry's own index, the marker, the image 0 .. 26); the entries taken
 // in sorted order (sid) out as marker indices and periodic shifts; off[q] = first sorted key
 // >= q * per, q = 0 .. npatch.
+// (bypatch: the keys are the patch alone, npatch for none -- marker order within a patch)
 hipError_t launch_level_list_keys(const LevelNum& L, const int* tab, const double* X, int n, unsigned* ikey,
-                                  int* gcnt, hipStream_t s);
+                                  int* gcnt, int bypatch, int npatch, hipStream_t s);
 hipError_t launch_level_list_write(const LevelNum& L, const int* tab, const double* X, int n, const int* goff,
-                                   unsigned* gkey, int* gid, int* gsrc, int* gimg, hipStream_t s);
+                                   unsigned* gkey, int* gid, int* gsrc, int* gimg, int bypatch, hipStream_t s);
 hipError_t launch_level_list_out(const LevelNum& L, const int* sid, const int* gsrc, const int* gimg, int total,
                                  int* idx, double* xs, hipStream_t s);
 hipError_t launch_key_offsets(const unsigned* skeys, int n, unsigned per, int npatch, int* off, hipStream_t s);

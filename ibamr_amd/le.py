@@ -856,11 +856,14 @@ def level_node_distribution(ctx: Context, geoms: Sequence[Geometry], dom_lo, dom
 
 
 def level_index_lists(ctx: Context, geoms: Sequence[Geometry], dom_lo, dom_hi, X: torch.Tensor, ghost: int,
-                      periodic=None):
+                      periodic=None, order: str = "cells"):
     """LIndexSetData::cacheLocalIndices over every local patch of a level in one call
     (ibtk_le_level_index_lists): ((interior int32, None, offsets), (ghost-box int32, Xshift
     (n, ndim) float64, offsets)) -- the flat per-patch lists Level.from_flat and
-    Level.select_interior take, offsets as Python lists of npatch + 1."""
+    Level.select_interior take, offsets as Python lists of npatch + 1.  order "cells": a
+    patch's entries in its box's cell order (the reference's); "markers": in marker order."""
+    if order not in ("cells", "markers"):
+        raise ValueError("order: 'cells' or 'markers'")
     M = X.shape[0]
     if M and (X.dtype != torch.float64 or not X.is_cuda or not X.is_contiguous()):
         raise ValueError("X: contiguous float64 device tensor")
@@ -876,7 +879,8 @@ def level_index_lists(ctx: Context, geoms: Sequence[Geometry], dom_lo, dom_hi, X
         gi = torch.empty(gcap, dtype=torch.int32, device=X.device)
         gx = torch.empty((gcap, nd), dtype=torch.float64, device=X.device)
         rc = ctx.lib.ibtk_le_level_index_lists(ctx.h, P, tab, lo.p, hi.p, pa[0] if pa else None,
-                                               _ptr(X) if M else None, M, ghost, _ptr(ii), icap,
+                                               _ptr(X) if M else None, M, ghost, 0 if order == "cells" else 1,
+                                               _ptr(ii), icap,
                                                ctypes.cast(ioff, ctypes.c_void_p), _ptr(gi), _ptr(gx), gcap,
                                                ctypes.cast(goff, ctypes.c_void_p))
         if rc != 0 and attempt == 0 and (ioff[P] > icap or goff[P] > gcap):

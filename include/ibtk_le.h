@@ -456,14 +456,16 @@ int ibtk_le_level_node_distribution(ibtk_le_ctx ctx, int npatch, const ibtk_le_p
  *   ghost-box lists: the markers and their periodic images whose cell lies in patch q's
  *     box grown by `ghost`, at ghost_dev / Xshift_dev (NDIM doubles an entry: the image's
  *     shift, +-(dom_hi - dom_lo + 1) dx per periodic dim) [ghost_off[q], ghost_off[q + 1]).
- * Within a patch the entries follow its (ghost) box's cells in box order, x fastest, a
- * cell's markers by index -- ibtk_le_periodic_index_list's order for one patch.
+ * Within a patch the entries follow (order 0) its (ghost) box's cells in box order, x
+ * fastest, a cell's markers by index -- ibtk_le_periodic_index_list's order for one patch,
+ * the reference's IndexData order -- or (order 1) the markers' order, a marker's images in
+ * image order (the same sets; a sort by patch alone, fewer radix passes).
  * interior_off / ghost_off are host arrays of npatch + 1.  If either list needs more than
  * its capacity, the offsets are still written (off[npatch] = the size needed), the lists
  * are not, and IBTK_LE_ERR_ARG is returned.  Synchronises. */
 int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms, const int* dom_lo,
                               const int* dom_hi, const int* periodic, const double* X_dev, int n_markers, int ghost,
-                              int* interior_dev, int interior_cap, int* interior_off, int* ghost_dev,
+                              int order, int* interior_dev, int interior_cap, int* interior_off, int* ghost_dev,
                               double* Xshift_dev, int ghost_cap, int* ghost_off);
 /* beginDataRedistribution's wrap of marker positions into the periodic domain
  * (LDataManager.cpp:1385-1399), in place on n (ndim)-records: per periodic dim

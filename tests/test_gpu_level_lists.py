@@ -183,3 +183,31 @@ def test_cfg5_lists_match_the_bench_torch_lists(le):
 
     assert torch.equal(canon(ii, None, oi), canon(ti.to(ii.device), None, toi))
     assert torch.equal(canon(gi, gx, og), canon(tg, tgx, tog))
+
+
+def test_marker_order_lists_equal_the_torch_lists(le):
+    """order="markers": each patch's entries in marker order -- exactly bench.level_lists'
+    lists (torch ops), entry for entry and shift for shift, on a reduced cfg5 level."""
+    import bench
+    from ibamr_amd.slab import Slab
+    N, P, g = 128, 4, 3
+    n = N // P
+    ctx = le.Context(0)
+    geoms, _ = _tiles(le, [n] * 3, [P] * 3, g, [1.0 / N] * 3)
+    X = bench.make_markers("clustered", 200000, Slab([N, N, N], 1, 0, g), 5, "cuda")
+    X = torch.remainder(X, 1.0).contiguous()
+    X.masked_fill_(X >= 1.0, 0.0)
+    (ii, _, oi), (gi, gx, og) = le.level_index_lists(ctx, geoms, [0, 0, 0], [N - 1] * 3, X, g, order="markers")
+    (ti, _, toi), (tg, tgx, tog) = bench.level_lists(X, N, P, g)
+    assert list(oi) == [int(v) for v in toi] and list(og) == [int(v) for v in tog]
+    assert torch.equal(ii, ti.to(ii.device))
+    assert torch.equal(gi, tg.to(gi.device))
+    assert torch.equal(gx, tgx)
+    # and the same sets as the cell order
+    (ci, _, coi), (cg, cgx, cog) = le.level_index_lists(ctx, geoms, [0, 0, 0], [N - 1] * 3, X, g)
+    assert list(coi) == list(oi) and list(cog) == list(og)
+    for q in range(len(geoms)):
+        a = torch.sort(ii[oi[q]:oi[q + 1]]).values
+        b = torch.sort(ci[coi[q]:coi[q + 1]]).values
+        assert torch.equal(a, b), q
+
