@@ -1387,7 +1387,7 @@ __global__ __launch_bounds__(BLOCK) void k_cand_count(Params p, int ncl, int* cn
 // each end) and the shifted-z boundary cs_off_z[zb + 1] written; lane 0 of the wave that
 // takes a column's anchor 0 writes its column's first boundary, cs_off_z[zb] = cs_off[ca].
 // The candidates' loads are unconditional (indices clamped), so that no branch waits on
-// them; an empty column-anchor skips its rows (one wait on its two offsets).  (Two
+// them; on a level an empty column-anchor skips its rows (one wait on its two offsets).  (Two
 // column-anchors a pass, their loads issued together, measured 0.1-0.15 ms slower on cfg4
 // and cfg5 --move, profiles/r05x.)
 struct CaJob {
@@ -1414,8 +1414,9 @@ __global__ __launch_bounds__(BLOCK) void k_cand_write(Params p, int ncl, const i
     auto load_rows = [&](int ca, CaJob& J) {
         J.items = ca < ncl && ca_decode(p, ca, J.cg, J.col, J.a, J.bs, J.zb, J.zxlo, J.zilo, ptab);
         J.o = off[min(ca, ncl - 1)];
-        // an empty column-anchor (most of a clustered level's) loads no rows
-        J.items = J.items && off[min(ca + 1, ncl)] != J.o;
+        // on a level an empty column-anchor (most of a clustered level's) loads no rows; one
+        // patch of uniform markers has few, and would only wait for the offsets
+        if (p.pd) J.items = J.items && off[min(ca + 1, ncl)] != J.o;
         if (J.items) {
             const int cx = J.col % J.cg.ncx, cy = J.col / J.cg.ncx;
             const int col0 = (cy - 1) * J.cg.ncx + (cx - 1);
