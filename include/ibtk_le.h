@@ -460,9 +460,9 @@ int ibtk_le_level_node_distribution(ibtk_le_ctx ctx, int npatch, const ibtk_le_p
  * fastest, a cell's markers by index -- ibtk_le_periodic_index_list's order for one patch,
  * the reference's IndexData order -- or (order 1) the markers' order, a marker's images in
  * image order (the same sets; a sort by patch alone, fewer radix passes).
- * interior_off / ghost_off are host arrays of npatch + 1.  If either list needs more than
- * its capacity, the offsets are still written (off[npatch] = the size needed), the lists
- * are not, and IBTK_LE_ERR_ARG is returned.  Synchronises. */
+ * interior_off / ghost_off are host arrays of npatch + 1.  If a list needs more than its
+ * capacity, both offset arrays are still written (off[npatch] = the size needed), that list
+ * is not, and IBTK_LE_ERR_ARG is returned.  Synchronises. */
 int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk_le_patch_geom* geoms, const int* dom_lo,
                               const int* dom_hi, const int* periodic, const double* X_dev, int n_markers, int ghost,
                               int order, int* interior_dev, int interior_cap, int* interior_off, int* ghost_dev,
