@@ -96,20 +96,6 @@ __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, unsigned off, d
     using V2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, v), r, (int)off, 0, 0);
 }
-// The spread's plane writeback with the nontemporal policy (aux 2, `nt`): f is written once
-// and not read back in the sweep, and the lines two x-neighbour columns share (the packed
-// rows end mid-line) keep their L2 residency longer, so more of them leave L2 whole.  cfg4
-// spread sweep 10.77-10.91 -> 10.54-10.61 ms, cfg5 2.12 -> 2.05 ms
-// (profiles/r05/r05zi_nt_writeback_ab.txt); sc0 (aux 1) within noise.  The zeros that items
-// no marker reaches store stay on the default policy: nt there cost cfg5 2.12 -> 2.80 ms
-// (profiles/r05/r05zj_nt_all_ab.txt).
-#ifndef IBTK_LE_WB_NT
-#define IBTK_LE_WB_NT 2
-#endif
-__device__ __forceinline__ void buf_st_nt(__amdgpu_buffer_rsrc_t r, unsigned off, double v) {
-    using V2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, v), r, (int)off, 0, IBTK_LE_WB_NT);
-}
 
 // ---------------------------------------------------------------------------
 // binning
@@ -2001,7 +1987,7 @@ __global__ __launch_bounds__(SW) void k_spread_sweep(Params p) {
         const bool own = on && z >= plo && z <= phi;
         const auto pb = plane_rsrc(cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2, own ? plane_bytes : 0u);
 #pragma unroll
-        for (int k = 0; k < NPL; ++k) buf_st_nt(pb, loff[k], v[k]);  // not-owned points: dropped
+        for (int k = 0; k < NPL; ++k) buf_st(pb, loff[k], v[k]);  // not-owned points: dropped
     };
 
     // The candidates stream through 64-lane chunks across anchor planes.  Anchor
