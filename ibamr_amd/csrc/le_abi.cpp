@@ -1788,11 +1788,16 @@ extern "C" int ibtk_le_level_select_interior(ibtk_le_ctx ctx, ibtk_le_markers m,
     if ((rc = m->int_off.ensure(sizeof(int) * (size_t)(np + 1)))) return rc;
     const int nblk = CHECK_STRIPES;  // the kept entries' count, striped over CHECK_STRIPES counters
     if ((rc = ctx->counts.ensure(sizeof(int) * (size_t)nblk))) return rc;
-    HIP_TRY(hipMemcpyAsync(m->int_off.p, interior_offsets, sizeof(int) * (size_t)(np + 1), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(m->owner.p, 0xff, sizeof(int) * (size_t)std::max(n_markers, 1), s));
     HIP_TRY(hipMemsetAsync(ctx->counts.p, 0, sizeof(int) * (size_t)nblk, s));
-    HIP_TRY(launch_interior_owner(m->int_off.as<int>(), np, interior_indices_dev, n_int, n_markers, m->owner.as<int>(),
-                                  ctx->err.as<int>(), gs, s));
+    // owner[] follows the lists alone: with the same lists (a re-binning between regrids moved
+    // markers, not the lists) the last selection's stands -- only the targets are redone
+    if (!same) {
+        HIP_TRY(hipMemcpyAsync(m->int_off.p, interior_offsets, sizeof(int) * (size_t)(np + 1), hipMemcpyHostToDevice,
+                               s));
+        HIP_TRY(hipMemsetAsync(m->owner.p, 0xff, sizeof(int) * (size_t)std::max(n_markers, 1), s));
+        HIP_TRY(launch_interior_owner(m->int_off.as<int>(), np, interior_indices_dev, n_int, n_markers,
+                                      m->owner.as<int>(), ctx->err.as<int>(), gs, s));
+    }
     // An entry of patch q's list whose marker q owns is a periodic image only if the image
     // (a whole period away) lies in q's ghost box as well: impossible when the level spans
     // more than any patch's ghost box in every dim (a period is at least the level's extent),
