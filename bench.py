@@ -96,20 +96,39 @@ def make_markers(kind, M, slab, seed, device):
     return X[keep].contiguous()
 
 
-def cpu_baseline(cfg, kernel, seconds_target=15.0):
-    """The oracle (the C restatement) timed on a bounded, same-density sample, on 1 thread and
-    on every host thread this process may use, capped by OMP_NUM_THREADS (one replica each;
-    the record states the host's nproc, the affinity set and the cap).
+def physical_cores(cpus):
+    """The physical cores among the logical CPUs `cpus` (SMT siblings counted once), from
+    /sys/devices/system/cpu/cpu*/topology; len(cpus) where the topology is unreadable."""
+    cores = set()
+    for c in cpus:
+        t = Path(f"/sys/devices/system/cpu/cpu{c}/topology")
+        try:
+            cores.add((int((t / "physical_package_id").read_text()), int((t / "core_id").read_text())))
+        except (OSError, ValueError):
+            return len(cpus)
+    return len(cores) or len(cpus)
 
-    Sample: a periodic N_s^3 grid with the workload's marker density (cell-sorted
-    order, as on the GPU), IB_4 side-centred interp + spread (periodic images in the
-    spread list, LIndexSetData semantics), repeated until ~seconds_target of CPU work.
+
+def cpu_baseline(cfg, kernel, seconds_target=15.0):
+    """The oracle (the C restatement) timed on a bounded, same-density sample: on 1 thread, and
+    on one thread per physical core of this process's affinity set (every core
+    of the GPU host), one replica of the sample each, as MPI ranks each holding a patch.  The
+    pool's OMP_NUM_THREADS cap (one GPU's share of a shared host) does not limit it; the record
+    states the cap and also the rate at that many threads (`value_pool_share`).
+
+    Why a sample and not cfg4 itself: the oracle's cost is per marker (a W^3 stencil each way),
+    independent of the grid size, and the full problem (1e8 markers, 52 GB of u and f) would take
+    minutes of CPU time and tens of GB of host memory per replica inside a bench that must
+    finish in a few minutes.  Sample: a periodic N_s^3 grid with the workload's marker density
+    (cell-sorted order, as on the GPU), IB_4 side-centred interp + spread (periodic images in the
+    spread list, LIndexSetData semantics), repeated until ~seconds_target of CPU work.  u is
+    shared read-only by the threads; f and U are per thread.
     """
     import numpy as np
     from oracle import oracle as ora
     N = cfg["N"]
     density = cfg["M"] / float(N ** 3)
-    Ns = min(N, 192)
+    Ns = min(N, 128)
     Ms = max(1000, int(round(density * Ns ** 3)))
     if cfg["markers"] == "sphere":
         Ns, Ms = N, cfg["M"]
@@ -151,42 +170,49 @@ def cpu_baseline(cfg, kernel, seconds_target=15.0):
     # SURVEY.md 8(d)); ctypes releases the GIL inside the C calls
     import threading
     try:
-        ncpu = len(os.sched_getaffinity(0))
+        cpus = sorted(os.sched_getaffinity(0))
     except AttributeError:
-        ncpu = os.cpu_count() or 1
-    # every core this process may use, up to OMP_NUM_THREADS: the GPU pool sets 16, one GPU's
-    # share of its host (os.cpu_count() there counts the whole machine, shared by 8 GPUs)
-    T = max(1, min(ncpu, int(os.environ.get("OMP_NUM_THREADS", str(ncpu)))))
-    reps_t = [0] * T
-    t_multi = 0.6 * seconds_target
-    start = threading.Barrier(T + 1)
+        cpus = list(range(os.cpu_count() or 1))
+    phys = physical_cores(cpus)
+    cap = os.environ.get("OMP_NUM_THREADS")
 
-    def worker(k):
-        uu = [a.copy() for a in u]
-        ff = [np.zeros_like(a) for a in u]
-        UU = np.zeros((Ms, 3))
+    def run_threads(T, t_run):
+        reps_t = [0] * T
+        start = threading.Barrier(T + 1)
+
+        def worker(k):
+            ff = [np.zeros_like(a) for a in u]
+            UU = np.zeros((Ms, 3))
+            start.wait()
+            t0 = time.perf_counter()
+            while time.perf_counter() - t0 < t_run or reps_t[k] < 1:
+                one_pass(u, ff, UU)
+                reps_t[k] += 1
+
+        threads = [threading.Thread(target=worker, args=(k,)) for k in range(T)]
+        for th in threads:
+            th.start()
         start.wait()
         t0 = time.perf_counter()
-        while time.perf_counter() - t0 < t_multi or reps_t[k] < 1:
-            one_pass(uu, ff, UU)
-            reps_t[k] += 1
+        for th in threads:
+            th.join()
+        wall = time.perf_counter() - t0
+        return 2.0 * Ms * sum(reps_t) / wall, sum(reps_t), wall
 
-    threads = [threading.Thread(target=worker, args=(k,)) for k in range(T)]
-    for th in threads:
-        th.start()
-    start.wait()
-    t0 = time.perf_counter()
-    for th in threads:
-        th.join()
-    wall = time.perf_counter() - t0
-    rateT = 2.0 * Ms * sum(reps_t) / wall
-    return {"value": rateT, "unit": "marker-ops/s", "cores": T, "kind": "port", "value_1thread": rate1,
-            "host_nproc": os.cpu_count(), "affinity_cpus": ncpu,
-            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+    rateT, passes, wall = run_threads(phys, 0.45 * seconds_target)
+    # the pool's share of the host (OMP_NUM_THREADS: one GPU's 16 of a host shared by 8), beside it
+    share = None
+    if cap and cap.isdigit() and 0 < int(cap) < phys:
+        share = run_threads(int(cap), 0.25 * seconds_target)[0]
+    return {"value": rateT, "unit": "marker-ops/s", "cores": phys, "kind": "port", "value_1thread": rate1,
+            "value_pool_share": share, "pool_share_threads": int(cap) if share is not None else None,
+            "host_nproc": os.cpu_count(), "affinity_cpus": len(cpus), "physical_cores": phys,
+            "omp_num_threads": cap,
             "sample": f"{Ns}^3 periodic grid, {Ms} uniform markers (same density as the workload), "
-                      f"{kernel} side interp+spread, cell-sorted (oracle C); {T} threads, one replica of the "
-                      f"sample each: {sum(reps_t)} passes in {wall:.1f} s; 1 thread: {reps} passes in "
-                      f"{elapsed:.1f} s"}
+                      f"{kernel} side interp+spread, cell-sorted (oracle C); {phys} threads (one per physical "
+                      f"core of the affinity set, OMP_NUM_THREADS={cap} not applied), one replica of the sample "
+                      f"each: {passes} passes in {wall:.1f} s; 1 thread: {reps} passes in {elapsed:.1f} s; a "
+                      f"sample, not cfg4 itself: the oracle's cost is per marker, independent of the grid"}
 
 
 def level_lists(X, N, P, g):
@@ -240,6 +266,12 @@ def binning_label(counts, full_name):
         parts.append(f"{r} re-binning(s) from the previous order (ibtk_le_markers_rebin: every key recomputed "
                      "from the current positions, the entries whose bucket changed inserted; equal to a full binning)")
     return " + ".join(parts) + " over the timed steps" if parts else "none in the timed steps (binned once at setup)"
+
+
+# the reach of a kernel's stencil beyond its marker's cell (W / 2): the lists' drift slack is
+# the ghost width less it
+KERNEL_HALF_WIDTH = {"PIECEWISE_CONSTANT": 1, "DISCONTINUOUS_LINEAR": 1, "PIECEWISE_LINEAR": 1, "PIECEWISE_CUBIC": 2,
+                     "IB_3": 2, "IB_4": 2, "IB_4_W8": 4, "IB_6": 3, "BSPLINE_4": 2}
 
 
 # ds_add_f64 cost, conflict-free (tools/ubench_lds2.hip): 10 cycles
@@ -386,6 +418,17 @@ def run_level(args, cfg, kernel, dev):
 
     nstep = {"k": 0}
     binning = {"full": 0, "rebin": 0}
+    # Between regrids the per-patch lists are kept (LIndexSetData between regrids): a marker
+    # may drift at most the ghost width's spare cells (g - W/2, LDataManager.cpp:167
+    # CFL_WIDTH) from the cell it was listed in, or a patch would miss its spread or
+    # interpolate outside its ghost box.  Checked on the device after every update between
+    # regrids (no host sync in the step), reported as config.drift_within_slack.
+    slack = g - KERNEL_HALF_WIDTH.get(kernel, 2)
+    cell_at_regrid = torch.floor(X * N)
+    drift_flag = torch.zeros(1, dtype=torch.bool, device=dev)
+
+    def check_drift():
+        drift_flag.logical_or_(((torch.floor(X * N) - cell_at_regrid).abs() > slack).any())
 
     def step_move(record):
         # a moving step on the level: interp at the current positions (the interior lists
@@ -406,12 +449,15 @@ def run_level(args, cfg, kernel, dev):
         if record:
             E[2].record()
         le.position_update(ctx, "euler", dt_move, X, U, out=X)
+        if not at_regrid:
+            check_drift()
         if at_regrid:
             # beginDataRedistribution's wrap into the periodic domain (LDataManager.cpp:1385-1399)
             le.wrap_positions(ctx, X, [0.0, 0.0, 0.0], [1.0, 1.0, 1.0])
             (ii2, _, oi2), (si2, sx2, os2) = le.level_index_lists(ctx, geoms, [0, 0, 0], [N - 1] * 3, X, g,
                                                                   order="markers")
             lists.update(ii=ii2, oi=oi2)
+            cell_at_regrid.copy_(torch.floor(X * N))
             lvl_s.relist(si2, sx2, os2).bin(X)
             binning["full"] += 1
         else:
@@ -476,6 +522,8 @@ def run_level(args, cfg, kernel, dev):
                    "parallelism": "one GPU", "patches": [P, P, P], "patch_cells": [n, n, n], "ghost": g,
                    "marker_order": args.marker_order, "move": args.move,
                    "regrid_every": args.regrid_every if args.move else None,
+                   "drift_within_slack": ((not bool(drift_flag.item())) if args.move and args.regrid_every > 1
+                                          else None),
                    "bin": binning_label(timed_binning, "ibtk_le_level_bin"),
                    "step": ("level ghost fill and interp(3 comps) in one launch + position update + "
                             + (f"at every {args.regrid_every}-th step (regrid) " if args.regrid_every > 1 else "")
@@ -498,6 +546,57 @@ def run_level(args, cfg, kernel, dev):
         "breakdown_ms": {k: mean(v) for k, v in acc.items()},
         "touched_points": S_touched,
     }
+
+
+def rehearsal():
+    """IBTK_BENCH_BACKEND=gloo with IBTK_BENCH_DEVICE set: every rank on that one GPU, the
+    exchanges over gloo staged through the host (a wiring check, not the metric)."""
+    return os.environ.get("IBTK_BENCH_BACKEND") == "gloo" and "IBTK_BENCH_DEVICE" in os.environ
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, visible=None, poll_s=0.2):
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE): one child process per rank,
+    as torch.distributed.run would start them -- RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous
+    at 127.0.0.1 -- each on its own GPU (cuda:LOCAL_RANK), rank 0 printing the line.  Refuses
+    (exit status 2, before any GPU call) when fewer than N GPUs are visible, unless the one-GPU
+    gloo rehearsal is asked for (rehearsal()); never falls back to fewer ranks.  If a rank fails,
+    the others are stopped and its exit status is returned."""
+    import subprocess
+    if visible is None:
+        import torch
+        visible = torch.cuda.device_count()  # counts devices without initialising the GPU
+    if visible < n and not rehearsal():
+        print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {visible} (for a one-GPU rehearsal set "
+              f"IBTK_BENCH_BACKEND=gloo IBTK_BENCH_DEVICE=0)", file=sys.stderr, flush=True)
+        return 2
+    port = os.environ.get("MASTER_PORT") or str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable] + argv, env=env))
+    code = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and code == 0:
+                code = rc if rc > 0 else 1
+                for q in live:  # a failed rank: the others would wait for it forever
+                    q.kill()
+        if live:
+            time.sleep(poll_s)
+    return code
 
 
 def main():
@@ -559,6 +658,10 @@ def main():
     if args.renumber and CONFIGS[args.config].get("patches") and not args.single_patch:
         raise SystemExit("--renumber: slab configurations only (cfg5's level: --single-patch)")
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: start the N ranks here, before anything touches the GPU
+        raise SystemExit(launch_ranks(args.gpus, [str(Path(__file__).resolve())] + sys.argv[1:]))
+
     import torch
     cfg = CONFIGS[args.config]
     kernel = args.kernel or cfg["kernel"]
@@ -566,7 +669,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher and the flag disagree")
     # IBTK_BENCH_DEVICE / IBTK_BENCH_BACKEND=gloo: a multi-rank rehearsal with every
     # rank on one GPU (exchanges staged through the host); the default is one rank
     # per GPU over RCCL

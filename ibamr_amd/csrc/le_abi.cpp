@@ -291,8 +291,8 @@ extern "C" int ibtk_le_ctx_synchronize(ibtk_le_ctx ctx) {
         HIP_TRY(hipMemset(ctx->err.p, 0, sizeof(int)));
         return fail(IBTK_LE_ERR_INVARIANT,
                     "device invariant failed (flag %d): a stencil left its staged region (1) or its bin bounds (2), "
-                    "an interior list entry is not in the level's binned lists (4), or a fixed-capacity "
-                    "migration overflowed (8)",
+                    "an interior list entry is not in the level's binned lists (4), a fixed-capacity "
+                    "migration overflowed (8), or the spread's candidate stream reached 2^31 entries (16)",
                     flag);
     }
     return IBTK_LE_OK;
@@ -1425,13 +1425,18 @@ static int cand_stream(ibtk_le_ctx ctx, ibtk_le_markers m, Params& p) {
     const long long ncl = (long long)m->nbuckets_total / NBAND;
     const long long nclz = m->npatch ? m->nclz : (long long)m->cg.ncol * (m->cg.nz + 1);
     const int k = m->kernel;
-    bool split = false;
-    if (k == K_IB_4 || k == K_BSPLINE_4 || k == K_IB_6 || k == K_IB_4_W8)
-        for (int c = 0; c < p.ncomp; ++c) split = split || !p.comp[c].zcell;
-    // a marker is a candidate of at most four columns (its own, one x- and one y-neighbour,
-    // the corner between them: a stencil never reaches both neighbours in a dim)
-    const long long cap = std::max(4LL * m->n, 1LL);
-    if (cap >= (1LL << 31) || ncl + 1 >= (1LL << 31) || nclz + 1 >= (1LL << 31))
+    // A closed-form kernel's stream is always split by the shifted-z anchor, whichever
+    // components this call spreads: the order of a column-anchor's candidates -- the order in
+    // which they add into a point -- then depends on the binning alone, not on which
+    // centerings were spread since it (advisor, round 5)
+    const bool split = k == K_IB_4 || k == K_BSPLINE_4 || k == K_IB_6 || k == K_IB_4_W8;
+    // A marker is a candidate of at most four columns (its own, one x- and one y-neighbour,
+    // the corner between them: a stencil never reaches both neighbours in a dim), so 4 n
+    // positions always hold the stream (16 bytes a marker; about 1.3 of the 4 are used by
+    // uniform IB_4 markers).  Offsets are 32-bit: a stream of 2^31 entries or more raises
+    // device flag 16 (k_cand_write checks its 64-bit length) instead of being refused here.
+    const long long cap = std::min(std::max(4LL * m->n, 1LL), (1LL << 31) - 1);
+    if (ncl + 1 >= (1LL << 31) || nclz + 1 >= (1LL << 31))
         return fail(IBTK_LE_ERR_RANGE, "candidate stream too long");
     p.cs_off = m->cs_off.as<int>();
     p.cs_pos = m->cs_pos.as<int>();
@@ -1440,7 +1445,9 @@ static int cand_stream(ibtk_le_ctx ctx, ibtk_le_markers m, Params& p) {
     p.cs_rint = k == K_IB_4 ? 1 : 0;  // the IB_4 spread anchors by rint (spread_setup)
     if (m->cs_state == 1 && m->cs_pos.p && (m->cs_split || !split)) return IBTK_LE_OK;
     int rc;
-    if ((rc = m->cs_cnt.ensure(sizeof(int) * (size_t)(ncl + 1)))) return rc;
+    // cs_cnt: ncl + 1 counts, then the stream's 64-bit length (8-byte aligned)
+    const size_t tot_at = (sizeof(int) * (size_t)(ncl + 1) + 7) / 8 * 8;
+    if ((rc = m->cs_cnt.ensure(tot_at + sizeof(unsigned long long)))) return rc;
     if ((rc = m->cs_off.ensure(sizeof(int) * (size_t)(ncl + 1)))) return rc;
     if ((rc = m->cs_pos.ensure(sizeof(int) * (size_t)cap))) return rc;
     if (split && (rc = m->cs_off_z.ensure(sizeof(int) * (size_t)(nclz + 1)))) return rc;
@@ -1459,7 +1466,8 @@ static int cand_stream(ibtk_le_ctx ctx, ibtk_le_markers m, Params& p) {
     q.cs_zflip = m->zst.p ? m->zst.as<int>() + 1 : nullptr;
     q.cs_epoch = m->rb_epoch;
     HIP_TRY(launch_cand_stream(q, (int)ncl, m->cs_cnt.as<int>(), m->cs_off.as<int>(), m->cs_pos.as<int>(), ctx->temp.p,
-                               ctx->temp.cap, ctx->stream));
+                               ctx->temp.cap,
+                               reinterpret_cast<unsigned long long*>(m->cs_cnt.as<char>() + tot_at), ctx->stream));
     m->cs_state = 1;
     m->cs_split = split;
     return IBTK_LE_OK;
@@ -2804,11 +2812,19 @@ extern "C" int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk
     if ((rc = ctx->ll_key2.ensure(sizeof(unsigned) * (size_t)n))) return rc;
     if ((rc = ctx->ll_id.ensure(sizeof(int) * (size_t)n))) return rc;
     if ((rc = ctx->ll_id2.ensure(sizeof(int) * (size_t)n))) return rc;
-    if ((rc = ctx->counts.ensure(sizeof(int) * (size_t)(npatch + 1)))) return rc;
+    // the patch offsets (npatch + 1 ints), then the 64-bit total of the ghost-box entries
+    const size_t sum_at = ((sizeof(int) * (size_t)(npatch + 1)) + 7) / 8 * 8;
+    if ((rc = ctx->counts.ensure(sum_at + sizeof(unsigned long long)))) return rc;
+    unsigned long long* const total64_dev = reinterpret_cast<unsigned long long*>(ctx->counts.as<char>() + sum_at);
     HIP_TRY(hipMemcpyAsync(ctx->num_tab.p, tab.data(), sizeof(int) * tab.size(), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(ctx->ll_cnt.as<int>() + n, 0, sizeof(int), s));
+    HIP_TRY(hipMemsetAsync(total64_dev, 0, sizeof(unsigned long long), s));
     HIP_TRY(launch_level_list_keys(L, ctx->num_tab.as<int>(), X_dev, n, ctx->ll_key.as<unsigned>(),
                                    ctx->ll_cnt.as<int>(), bypatch, npatch, s));
+    // a marker may have many ghost-box entries (up to 27 images, each in several small
+    // patches' ghost boxes): the entries' 32-bit scan below is checked against their sum in
+    // 64 bits, and a level with 2^31 entries or more is refused (advisor, round 5)
+    HIP_TRY(launch_sum64(ctx->ll_cnt.as<int>(), n, total64_dev, s));
     if ((rc = scan_excl(ctx, ctx->ll_cnt.as<int>(), ctx->ll_off.as<int>(), n + 1))) return rc;
     // interior: markers by (patch, cell), stable
     HIP_TRY(launch_iota(ctx->ll_id.as<int>(), n, s));
@@ -2817,9 +2833,13 @@ extern "C" int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk
         return rc;
     HIP_TRY(launch_key_offsets(ctx->ll_key2.as<unsigned>(), n, pcells, npatch, ctx->counts.as<int>(), s));
     int total = 0;
+    unsigned long long total64 = 0;
     HIP_TRY(hipMemcpyAsync(interior_off, ctx->counts.p, sizeof(int) * (size_t)(npatch + 1), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(&total, ctx->ll_off.as<int>() + n, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&total64, total64_dev, sizeof(total64), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    if (total64 >= (1ULL << 31) || (unsigned long long)total != total64)
+        return fail(IBTK_LE_ERR_RANGE, "level_index_lists: %llu ghost-box entries (2^31 or more)", total64);
     const int nint = interior_off[npatch];
     bool short_cap = nint > interior_cap;
     if (nint > 0 && !short_cap) {

@@ -556,6 +556,20 @@ __global__ __launch_bounds__(BLOCK) void k_compact(const int* sorder, const int*
     wave_count(counts, loc);           // one atomic per wave and counter
     wave_count(counts + 1, f && !loc);
 }
+// *out (zeroed by the caller) += the sum of v[0..n) in 64 bits: the range check of a 32-bit
+// scan of per-entry counts (ibtk_le_level_index_lists)
+__global__ __launch_bounds__(BLOCK) void k_sum64(const int* v, int n, unsigned long long* out) {
+    unsigned long long t = 0;
+    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) t += (unsigned)v[i];
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) t += __shfl_xor(t, d);
+    if ((threadIdx.x & 63) == 0 && t) atomicAdd(out, t);
+}
+hipError_t launch_sum64(const int* v, int n, unsigned long long* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sum64, dim3(std::min((n + BLOCK - 1) / BLOCK, 1024)), dim3(BLOCK), 0, s, v, n, out);
+    return hipGetLastError();
+}
 hipError_t launch_iota(int* v, int n, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_iota, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, v, n);

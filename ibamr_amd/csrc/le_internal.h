@@ -300,8 +300,10 @@ hipError_t launch_item_table(int kernel, const Params& p, int target, int heavy,
 // off[ncl + 1] (off[ncl] = the length), pos[length]; p.items_skip as for the item table.
 // p.cs_off_z set (closed-form kernels): each anchor's candidates split by their shifted-z
 // anchor and p.cs_off_z[Σ ncol (nz + 1) + 1] written (k_cand_write; no skip)
+// total: a device u64 for the stream's length in 64 bits (a stream longer than p.cs_total
+// raises device flag 16 and is not written)
 hipError_t launch_cand_stream(const Params& p, int ncl, int* cnt, int* off, int* pos, void* temp, size_t temp_bytes,
-                              hipStream_t s);
+                              unsigned long long* total, hipStream_t s);
 
 // Periodic helpers
 struct GhostDesc {
@@ -342,6 +344,7 @@ hipError_t launch_image_write(const ImageDesc& d, const double* X, int n, const 
                               double* xshift, unsigned* cellkey, int* cells, int capacity, hipStream_t s);
 // small helpers of the reference-ordered lists (le_aux.hip)
 hipError_t launch_iota(int* v, int n, hipStream_t s);
+hipError_t launch_sum64(const int* v, int n, unsigned long long* out, hipStream_t s);
 // out[i] = key_of(src[perm[i]]): mode 0 lag[idx[perm[i]]] (lag null: idx[perm[i]]), mode 1 keys[perm[i]]
 hipError_t launch_perm_keys(int mode, const int* perm, const int* idx, const int* lag, const unsigned* keys, int n,
                             unsigned* out, hipStream_t s);

@@ -1402,8 +1402,15 @@ struct CaJob {
     double z0;  // its z (SHZ)
 };
 template <bool SHZ>
-__global__ __launch_bounds__(BLOCK) void k_cand_write(Params p, int ncl, const int* off, int* pos) {
+__global__ __launch_bounds__(BLOCK) void k_cand_write(Params p, int ncl, const int* off, int* pos,
+                                                      const unsigned long long* total) {
     if (cs_stands(p)) return;
+    // a stream of 2^31 entries or more: its 32-bit offsets wrapped; nothing is written and
+    // device flag 16 says so at the next synchronize (the sweeps' reads stay clamped)
+    if (*total >= (unsigned long long)p.cs_total + 1ull) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(p.err, 16);
+        return;
+    }
     const int lane = threadIdx.x & (SW - 1);
     const int nw = gridDim.x * (BLOCK / SW);
     gdouble* const sX = cur_sorted_X(p);
@@ -1480,16 +1487,20 @@ __global__ __launch_bounds__(BLOCK) void k_cand_write(Params p, int ncl, const i
     }
 }
 hipError_t launch_cand_stream(const Params& p, int ncl, int* cnt, int* off, int* pos, void* temp, size_t temp_bytes,
-                              hipStream_t s) {
+                              unsigned long long* total, hipStream_t s) {
     if (ncl <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_cand_count, dim3(std::min((ncl + BLOCK - 1) / BLOCK, CS_GRID)), dim3(BLOCK), 0, s, p, ncl,
                        cnt);
-    hipError_t e = launch_scan(temp, temp_bytes, cnt, off, ncl + 1, s);  // cnt[ncl] = 0: off[ncl] = the total
+    // the stream's length in 64 bits beside the 32-bit scan (k_cand_write checks it)
+    hipError_t e = hipMemsetAsync(total, 0, sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    if ((e = launch_sum64(cnt, ncl, total, s)) != hipSuccess) return e;
+    e = launch_scan(temp, temp_bytes, cnt, off, ncl + 1, s);  // cnt[ncl] = 0: off[ncl] = the total
     if (e != hipSuccess) return e;
     const int per = BLOCK / SW;
     const dim3 g(std::min((ncl + per - 1) / per, CS_GRID)), b(BLOCK);
-    if (p.cs_off_z) hipLaunchKernelGGL(k_cand_write<true>, g, b, 0, s, p, ncl, off, pos);
-    else hipLaunchKernelGGL(k_cand_write<false>, g, b, 0, s, p, ncl, off, pos);
+    if (p.cs_off_z) hipLaunchKernelGGL(k_cand_write<true>, g, b, 0, s, p, ncl, off, pos, total);
+    else hipLaunchKernelGGL(k_cand_write<false>, g, b, 0, s, p, ncl, off, pos, total);
     return hipGetLastError();
 }
 

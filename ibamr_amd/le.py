@@ -498,20 +498,33 @@ class Level:
         check(self.ctx.lib.ibtk_le_markers_rebin(self.ctx.h, self.markers.h, _ptr(X)))
         return self
 
-    def select_interior(self, n_markers: int, indices: torch.Tensor, offsets: Sequence[int]):
+    def select_interior(self, n_markers: int, indices: torch.Tensor, offsets: Sequence[int],
+                        lists_changed: bool = False):
         """After a bin on the ghost-box lists: later interps write Q only from the entries
         the interior lists (patch q: indices[offsets[q]:offsets[q+1]]) name
-        (ibtk_le_level_select_interior); one binning serves both sweeps."""
+        (ibtk_le_level_select_interior); one binning serves both sweeps.
+
+        The library keeps the selection while the same list (pointer, offsets, n_markers)
+        comes back and no re-binning moved a marker.  A new tensor object drops it here; an
+        int32 list rewritten IN PLACE and passed again is the same object, so say so with
+        `lists_changed=True` (or call reset_selection() first)."""
         if len(offsets) != len(self.geoms) + 1:
             raise ValueError("one offset per patch, plus the end")
         idx = indices.to(torch.int32).contiguous()
-        if idx is not getattr(self, "_sel", None):
+        if lists_changed or idx is not getattr(self, "_sel", None):
             # another list object (possibly at the old list's address): the library's kept
             # selection is keyed on the pointer, so it is dropped here
             check(self.ctx.lib.ibtk_le_level_select_interior_reset(self.markers.h))
         self._sel = idx  # kept alive until the next bin
         O = (ctypes.c_int * len(offsets))(*[int(o) for o in offsets])
         check(self.ctx.lib.ibtk_le_level_select_interior(self.ctx.h, self.markers.h, int(n_markers), O, _ptr(idx)))
+        return self
+
+    def reset_selection(self):
+        """Drop the kept interior selection (ibtk_le_level_select_interior_reset): the next
+        select_interior recomputes it, e.g. after its interior list was edited in place."""
+        check(self.ctx.lib.ibtk_le_level_select_interior_reset(self.markers.h))
+        self._sel = None
         return self
 
     def fill_ghosts(self, centering: str, arrays, q_depth: int = 1, periodic=None):

@@ -131,7 +131,11 @@ int ibtk_le_ctx_set_stream(ibtk_le_ctx ctx, void* stream);
  * reference overlaps nothing (RefineSchedule::fillData, LDataManager.cpp:748). */
 int ibtk_le_ctx_set_plane_window(ibtk_le_ctx ctx, int mode, int zlo, int zhi);
 /* Waits for the context stream and reports device-side invariant failures
- * latched by earlier calls (IBTK_LE_ERR_INVARIANT), then clears them. */
+ * latched by earlier calls (IBTK_LE_ERR_INVARIANT), then clears them: flag 1 / 2 a
+ * stencil left its staged region / bin bounds, 4 an interior list entry missing from a
+ * level's binned lists, 8 a fixed-capacity migration overflowed, 16 a 3-D spread's
+ * candidate stream reached 2^31 entries (it holds up to 4 sorted positions a marker,
+ * 16 bytes of device memory a marker, kept with the binning). */
 int ibtk_le_ctx_synchronize(ibtk_le_ctx ctx);
 
 /* ---- marker binning (device LIndexSetData / LDataManager re-binning) --------------
