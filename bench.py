@@ -581,7 +581,8 @@ def launch_ranks(n, argv, visible=None, poll_s=0.2):
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable] + argv, env=env))
+        # rank 0's stdout is the line; the other ranks' goes to stderr
+        procs.append(subprocess.Popen([sys.executable] + argv, env=env, stdout=None if r == 0 else 2))
     code = 0
     live = list(procs)
     while live:

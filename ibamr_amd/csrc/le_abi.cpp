@@ -320,6 +320,7 @@ extern "C" int ibtk_le_ctx_tune(ibtk_le_ctx ctx, const char* key, int value) {
     else if (k == "heavy_first") t.heavy_first = value;
     else if (k == "strip") t.strip = value;
     else if (k == "xcd_block") t.xcd_block = value;
+    else if (k == "interp3") t.interp3 = value;
     else return fail(IBTK_LE_ERR_ARG, "unknown tuning key %s", key);
     return IBTK_LE_OK;
 }

@@ -1184,6 +1184,200 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     }
 }
 
+// The three components of an interp item in one workgroup (k_interp3): IWAVES waves per
+// component stage its ring exactly as k_interp_sweep's waves do (wave w: component
+// w / IWAVES, the group's plane w % IWAVES), so the workgroup holds three rings (3 x 47 KB
+// for IB_4: one workgroup of 12 waves per CU, the occupancy of three 4-wave items).  The
+// markers are the workgroup's, not a component's: lane L of the group takes component
+// L mod 3 of pool marker L / 3 (256 markers a round), so a marker's position and index
+// are read once for its three sums -- not once per component item -- and the three lanes
+// of a marker store its three Q values next to each other: the Q record is written whole,
+// not 8 bytes at a time by three items at three different times.  Each sum is
+// interp_marker's, in the Fortran order: bitwise the per-component kernel's (and the
+// oracle's).  Closed-form kernels, one patch, three components.
+constexpr int I3C = 3;                // components of a k_interp3 item
+constexpr int I3W = I3C * IWAVES;     // its waves
+constexpr int I3M = I3W * SW / I3C;   // pool markers a round
+template <int K> struct I3Sh {
+    using S = ISh<K>;
+    static constexpr size_t lds = sizeof(double) * I3C * S::NSL * S::PVP;
+    static constexpr bool fits = S::FAM == 0 && lds <= 160 * 1024;
+};
+template <int K>
+__global__ __launch_bounds__(SW * I3W) void k_interp3(Params p) {
+    using S = ISh<K>;
+    static_assert(I3Sh<K>::fits, "k_interp3: closed-form kernels whose three rings fit the LDS");
+    constexpr int LO = S::LO, HI = S::HI, RX = S::RX, NPT = S::NPT, NSL = S::NSL, PVP = S::PVP;
+    __shared__ double ring[I3C * NSL * PVP];
+    const int it = sweep_item(p, 1);
+    if (it < 0) return;
+    const SweepItem si = p.items[it];
+    const int col = si.col;
+    const int a0 = si.p0, a1 = si.p1;  // the item's anchor planes
+    const int lane = lane_id();
+    const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int cw = w / IWAVES, jw = w - cw * IWAVES;  // the wave's staging: component cw, plane jw of a group
+    const ColGeom& cg = p.cg;
+    const int* const bs = p.plane_start;
+    gdouble* const sorted_X = cur_sorted_X(p);
+    if (p.zmode) {  // the planes the item reads: a0 + LO .. a1 - 1 + HI
+        const bool inner = cg.org[2] + a0 + LO >= p.zlo && cg.org[2] + a1 - 1 + HI <= p.zhi;
+        if (inner != (p.zmode == 1)) return;
+    }
+    {
+        bool any = false;  // the same answer in every wave
+        for (int a = a0 + lane; a < a1; a += SW) any = any || bs[bucket(cg, a, col, NBAND)] > bs[bucket(cg, a, col, 0)];
+        if (!__any(any)) return;
+    }
+    const int cx = col % cg.ncx, cy = col / cg.ncx;
+    const int gx0 = cg.org[0] + cx * COLX + LO, gy0 = cg.org[1] + cy * COLY + LO;
+    const int zorg = cg.org[2];
+    const int nlast = p.nsorted - 1;
+    // ---- staging: the wave's component cw (wave-uniform), as k_interp_sweep stages one
+    const CompDesc cd = cw == 0 ? p.comp[0] : (cw == 1 ? p.comp[1] : p.comp[2]);
+    auto image = [&](int i, int d) {
+        if (!p.iper[d] || (i >= cd.ilower[d] && i <= cd.iupper[d])) return i;
+        const int n = cd.iupper[d] - cd.ilower[d] + 1;
+        int r = (i - cd.ilower[d]) % n;
+        return cd.ilower[d] + (r < 0 ? r + n : r);
+    };
+    const bool xlast = cd.xcell, ylast = cd.ycell;  // (FAM 0: the unread last staged column / row)
+    unsigned poff[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+        const int q = min(lane + SW * k, S::PV - 1);
+        const int qx = q % RX, qy = q / RX;
+        const int gx = gx0 + qx, gy = gy0 + qy;
+        const bool in = gx >= cd.lo[0] && gx <= cd.hi[0] && gy >= cd.lo[1] && gy <= cd.hi[1] &&
+                        !(xlast && qx == RX - 1) && !(ylast && qy == S::RY - 1);
+        poff[k] = in ? 8u * (unsigned)((image(gx, 0) - cd.lo[0]) + (image(gy, 1) - cd.lo[1]) * (int)cd.s1) : OFF_NONE;
+    }
+    const int plast = a1 - 1 + HI;  // last plane the item reads
+    const unsigned plane_bytes = (unsigned)(8 * cd.s2);
+    auto plane_load = [&](int zr, double* v) __attribute__((always_inline)) {
+        const int z0 = zorg + min(zr, plast);
+        const bool zin = z0 >= cd.lo[2] && z0 <= cd.hi[2];
+        const int z = zin ? image(z0, 2) : z0;
+        const int zc = min(max(z, cd.lo[2]), cd.hi[2]);
+        const auto pb = plane_rsrc(cd.u + (int64_t)(zc - cd.lo[2]) * cd.s2, zin ? plane_bytes : 0u);
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) v[k] = buf_ld(pb, poff[k]);
+    };
+    double* const ring_w = ring + cw * (NSL * PVP);  // the staged component's ring
+    auto plane_put = [&](int zr, const double* v) {
+        double* sl = ring_w + islot<K>(zr) * PVP;
+#pragma unroll
+        for (int k = 0; k < NPT; ++k)
+            if (S::PV % SW == 0 || k < NPT - 1 || lane + SW * k < S::PV) sl[lane + SW * k] = v[k];
+    };
+    // ---- the lane's component cl (fixed: 3 I3M lanes a round) and its marker slot
+    const int cl = (int)threadIdx.x % I3C, ml = (int)threadIdx.x / I3C;
+    CompDesc cdl;
+#define I3SEL(f) cdl.f = cl == 0 ? p.comp[0].f : (cl == 1 ? p.comp[1].f : p.comp[2].f)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        I3SEL(xlo[d]);
+        I3SEL(ilower[d]);
+        I3SEL(lo[d]);
+        I3SEL(hi[d]);
+    }
+    I3SEL(axis);
+    I3SEL(xcell);
+    I3SEL(ycell);
+    I3SEL(qcomp);
+#undef I3SEL
+    const double* const ring_l = ring + cl * (NSL * PVP);
+    struct Mk {
+        int q;  // the marker whose Q this entry writes (-1: a later duplicate entry does)
+        double X[3];
+    };
+    auto lds_barrier = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    struct GSpan {
+        int beg[IWAVES];
+        int pre[IWAVES + 1];
+    };
+    auto gspan_load = [&](int a) {
+        const int k = lane < IWAVES ? lane : min(lane - IWAVES, IWAVES - 1);
+        const int ac = min(a + k, cg.nz - 1);
+        return bs[bucket(cg, ac, col, lane >= IWAVES && lane < 2 * IWAVES ? NBAND : 0)];
+    };
+    auto gspan_get = [&](int a, int v, GSpan& gsp) {
+        int acc = 0;
+#pragma unroll
+        for (int k = 0; k < IWAVES; ++k) {
+            const int b = __builtin_amdgcn_readlane(v, k);
+            const int e = a + k < a1 ? __builtin_amdgcn_readlane(v, IWAVES + k) : b;
+            gsp.beg[k] = b;
+            gsp.pre[k] = acc;
+            acc += e - b;
+        }
+        gsp.pre[IWAVES] = acc;
+    };
+    // round r of a group: pool marker I3M r + ml (clamped), with its anchor plane
+    auto mk_load = [&](const GSpan& gsp, int a, int r, Mk& m, int& am) {
+        const int tot = gsp.pre[IWAVES];
+        const int j = min(I3M * r + ml, max(tot - 1, 0));
+        int e = gsp.beg[0] + j, k = 0;
+#pragma unroll
+        for (int q = 1; q < IWAVES; ++q)
+            if (j >= gsp.pre[q]) {
+                e = gsp.beg[q] + (j - gsp.pre[q]);
+                k = q;
+            }
+        am = a + k;
+        e = min(e, nlast);
+        m.q = (p.qdst ? p.qdst : p.sorted_s)[e];
+        const D3 xs = ld3(sorted_X + (int64_t)3 * e);
+        m.X[0] = xs.v[0];
+        m.X[1] = xs.v[1];
+        m.X[2] = xs.v[2];
+    };
+    auto process = [&](int n, const Mk& m, int am) {  // round of n <= I3M markers
+        const bool act = ml < n;
+        double acc = 0.0;
+        if (act) acc = interp_marker<K>(p, cdl, ring_l, gx0, gy0, zorg, am, m.X, 0);
+        double* dst = (act && m.q >= 0) ? p.Qout + ((int64_t)p.Q_depth * m.q + cdl.qcomp) : p.sink + lane;
+        *dst = acc;
+    };
+    double pv[NPT];
+    for (int z = a0 + LO + jw; z < a0 + HI; z += IWAVES) {
+        plane_load(z, pv);
+        plane_put(z, pv);
+    }
+    plane_load(a0 + jw + HI, pv);
+    GSpan gs;
+    gspan_get(a0, gspan_load(a0), gs);
+    Mk nxt;
+    int anx;
+    mk_load(gs, a0, 0, nxt, anx);
+    int vsp1 = gspan_load(a0 + IWAVES);
+    for (int a = a0; a < a1; a += IWAVES) {
+        lds_barrier();  // the previous group's reads are done
+        plane_put(a + jw + HI, pv);
+        lds_barrier();  // planes a+LO .. a+IWAVES-1+HI of every component are in the rings
+        const Mk cur = nxt;
+        const int acur = anx;
+        const GSpan gc = gs;
+        gspan_get(a + IWAVES, vsp1, gs);
+        mk_load(gs, a + IWAVES, 0, nxt, anx);
+        vsp1 = gspan_load(a + 2 * IWAVES);
+        plane_load(a + jw + IWAVES + HI, pv);
+        const int tot = gc.pre[IWAVES];
+        Mk m = cur;
+        int am = acur;
+        for (int r = 0; I3M * r < tot; ++r) {  // (dense groups: the next round loads while this one sums)
+            const Mk now = m;
+            const int anow = am;
+            if (I3M * (r + 1) < tot) mk_load(gc, a, r + 1, m, am);
+            process(min(tot - I3M * r, I3M), now, anow);
+        }
+    }
+}
+
 // Entries binned "outside" (no stencil point can reach any array): V = 0.
 __global__ __launch_bounds__(BLOCK) void k_interp_outside_col(Params p, int n) {
     const int first = p.plane_start[p.nbuckets_total];
@@ -2392,7 +2586,15 @@ template <int K>
 hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     if (ev0) (void)hipEventRecord(ev0, s);
     const long items = (long)p.item_bound * p.ncomp;
-    if (items > 0) {
+    bool done = false;
+    if constexpr (I3Sh<K>::fits) {
+        // the three components of an item in one workgroup (k_interp3)
+        if (items > 0 && !p.pd && p.ncomp == I3C && p.tune.interp3 >= 0) {
+            hipLaunchKernelGGL(k_interp3<K>, dim3(sweep_grid(p, p.item_bound)), dim3(SW * I3W), 0, s, p);
+            done = true;
+        }
+    }
+    if (items > 0 && !done) {
         const dim3 g(sweep_grid(p, items)), b(SW * IWAVES);
         if (p.pd && p.lvl_nbr) hipLaunchKernelGGL((k_interp_sweep<K, true, true>), g, b, 0, s, p);
         else if (p.pd) hipLaunchKernelGGL((k_interp_sweep<K, true>), g, b, 0, s, p);

@@ -97,7 +97,8 @@ def test_bench_gpus2_rehearsal_launches_two_ranks():
                         "--steps", "2", "--warmup", "1", "--no-cpu-baseline"],
                        env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    # (gloo itself prints a connection note on stdout; the record is the one JSON line)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2

@@ -87,12 +87,18 @@ def test_select_interior_lists_changed_in_place(le):
     U0 = torch.zeros((M, 3), dtype=torch.float64, device="cuda")
     lvl.fill_ghosts("side", u)
     lvl.interp("side", u, U0, X)
-    # rewrite the interior list in place: the second half of patch 0's entries now repeat
-    # its first marker, so the markers they named drop out of the selection and their Q rows
-    # must no longer be written (a kept, stale selection would still write them)
-    half = oi[0] + (oi[1] - oi[0]) // 2
-    assert oi[1] - half > 10
-    ii32[half:oi[1]].fill_(int(ii32[oi[0]].item()))
+    # rewrite the interior list in place: swap a marker A of patch 0 near its +x face with a
+    # marker B of patch 1 near the same face (each lies in the other patch's ghost box, so
+    # the lists stay valid): A's Q now comes from patch 1's arrays and B's from patch 0's,
+    # where a kept, stale selection would still take them from their old patches
+    cellx = torch.floor(X[:, 0] * N).long()
+    e0 = torch.arange(oi[0], oi[1], device="cuda")
+    e1 = torch.arange(oi[1], oi[2], device="cuda")
+    ea = e0[cellx[ii32[e0].long()] == n - 1][0]
+    eb = e1[cellx[ii32[e1].long()] == n][0]
+    A, B = int(ii32[ea].item()), int(ii32[eb].item())
+    ii32[ea] = B
+    ii32[eb] = A
     oi2 = list(oi)
     for fresh_sel in (False, True):
         lvl2 = le.Level.from_flat(ctx, geoms, "IB_4", X, si, sx, os_)
@@ -108,4 +114,3 @@ def test_select_interior_lists_changed_in_place(le):
         lvl.interp("side", u, U1, X)
         ctx.synchronize()
         assert torch.equal(U1, U_ref)
-        assert (U1 == 7.0).all(dim=1).sum() >= oi[1] - half - 1  # the dropped rows were not written

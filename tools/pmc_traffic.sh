@@ -41,7 +41,7 @@ res = {"build": source_hash(), "counters_kb": {}, "per_launch_bytes": {}, "read_
 for k, d in vals.items():
     # the counted-add launch (..., true, ...>: CNT) is not the product sweep
     cnt = "k_spread_sweep" in k and k.split("<")[1].split(",")[2].strip() == "true"
-    name = "spread" if "k_spread_sweep" in k and not cnt else "interp" if "k_interp_sweep" in k else None
+    name = "spread" if "k_spread_sweep" in k and not cnt else "interp" if ("k_interp_sweep" in k or "k_interp3" in k) else None
     if name is None or not d.get("FETCH_SIZE") or not d.get("WRITE_SIZE"):
         continue
     f = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"])
