@@ -1184,31 +1184,51 @@ __global__ __launch_bounds__(SW * IWAVES) void k_interp_sweep(Params p) {
     }
 }
 
-// The three components of an interp item in one workgroup (k_interp3): IWAVES waves per
-// component stage its ring exactly as k_interp_sweep's waves do (wave w: component
-// w / IWAVES, the group's plane w % IWAVES), so the workgroup holds three rings (3 x 47 KB
-// for IB_4: one workgroup of 12 waves per CU, the occupancy of three 4-wave items).  The
-// markers are the workgroup's, not a component's: lane L of the group takes component
-// L mod 3 of pool marker L / 3 (256 markers a round), so a marker's position and index
-// are read once for its three sums -- not once per component item -- and the three lanes
-// of a marker store its three Q values next to each other: the Q record is written whole,
-// not 8 bytes at a time by three items at three different times.  Each sum is
-// interp_marker's, in the Fortran order: bitwise the per-component kernel's (and the
-// oracle's).  Closed-form kernels, one patch, three components.
-constexpr int I3C = 3;                // components of a k_interp3 item
-constexpr int I3W = I3C * IWAVES;     // its waves
-constexpr int I3M = I3W * SW / I3C;   // pool markers a round
+// The three components of an interp item in one workgroup (k_interp3): WPC waves per
+// component stage its ring (wave w: component w / WPC; the group's new planes jw, jw + WPC,
+// ... of it, jw = w mod WPC), so the workgroup holds three rings (3 x 47 KB for IB_4: one
+// workgroup per CU).  The markers are the workgroup's, not a component's: lane L of the
+// group takes component L mod 3 of pool marker L / 3 (64 WPC markers a round), so a
+// marker's position and index are read once for its three sums -- not once per component
+// item -- and the three lanes of a marker store its three Q values next to each other: the
+// Q record is written whole, not 8 bytes at a time by three items at three different times.
+// Each sum is interp_marker's, in the Fortran order: bitwise the per-component kernel's (and
+// the oracle's).  PF groups of planes are in flight per wave in registers (a group's planes
+// are loaded PF groups before they are put).  Closed-form kernels, one patch, three
+// components.
+constexpr int I3C = 3;  // components of a k_interp3 item
+// The rings lie RSTR = NSL PVP + I3PAD doubles apart: the three lanes of a marker read the
+// same stencil offsets in the three rings, and with rings a multiple of 32 doubles apart
+// those reads hit one bank pair (ds_read_b64: a double's banks are its index mod 32) --
+// a 3-way conflict on every read (SQ: LDS waits 2.3x the per-component kernel's).  11 and
+// 22 doubles apart mod 32 they do not.
+constexpr int I3PAD = 11;
+#ifndef IBTK_LE_I3WPC
+#define IBTK_LE_I3WPC 4
+#endif
+#ifndef IBTK_LE_I3PF
+#define IBTK_LE_I3PF 1
+#endif
+#ifndef IBTK_LE_I3MAJOR
+#define IBTK_LE_I3MAJOR 0
+#endif
+constexpr int I3WPC = IBTK_LE_I3WPC, I3PF = IBTK_LE_I3PF;
 template <int K> struct I3Sh {
     using S = ISh<K>;
-    static constexpr size_t lds = sizeof(double) * I3C * S::NSL * S::PVP;
+    static constexpr int RSTR = S::NSL * S::PVP + I3PAD;
+    static constexpr size_t lds = sizeof(double) * I3C * RSTR;
     static constexpr bool fits = S::FAM == 0 && lds <= 160 * 1024;
 };
-template <int K>
-__global__ __launch_bounds__(SW * I3W) void k_interp3(Params p) {
+template <int K, int WPC, int PF>
+__global__ __launch_bounds__(SW * I3C * WPC) void k_interp3(Params p) {
     using S = ISh<K>;
     static_assert(I3Sh<K>::fits, "k_interp3: closed-form kernels whose three rings fit the LDS");
-    constexpr int LO = S::LO, HI = S::HI, RX = S::RX, NPT = S::NPT, NSL = S::NSL, PVP = S::PVP;
-    __shared__ double ring[I3C * NSL * PVP];
+    static_assert(IWAVES % WPC == 0, "a component's new planes of a group split evenly over its waves");
+    constexpr int LO = S::LO, HI = S::HI, RX = S::RX, NPT = S::NPT, PVP = S::PVP;
+    constexpr int PPW = IWAVES / WPC;    // planes a wave stages per group
+    constexpr int I3M = WPC * SW;        // pool markers a round
+    constexpr int RSTR = I3Sh<K>::RSTR;  // ring stride (doubles)
+    __shared__ double ring[I3C * RSTR];
     const int it = sweep_item(p, 1);
     if (it < 0) return;
     const SweepItem si = p.items[it];
@@ -1216,7 +1236,7 @@ __global__ __launch_bounds__(SW * I3W) void k_interp3(Params p) {
     const int a0 = si.p0, a1 = si.p1;  // the item's anchor planes
     const int lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const int cw = w / IWAVES, jw = w - cw * IWAVES;  // the wave's staging: component cw, plane jw of a group
+    const int cw = w / WPC, jw = w - cw * WPC;  // the wave's staging: component cw, planes jw + WPC t of a group
     const ColGeom& cg = p.cg;
     const int* const bs = p.plane_start;
     gdouble* const sorted_X = cur_sorted_X(p);
@@ -1263,7 +1283,7 @@ __global__ __launch_bounds__(SW * I3W) void k_interp3(Params p) {
 #pragma unroll
         for (int k = 0; k < NPT; ++k) v[k] = buf_ld(pb, poff[k]);
     };
-    double* const ring_w = ring + cw * (NSL * PVP);  // the staged component's ring
+    double* const ring_w = ring + cw * RSTR;  // the staged component's ring
     auto plane_put = [&](int zr, const double* v) {
         double* sl = ring_w + islot<K>(zr) * PVP;
 #pragma unroll
@@ -1271,7 +1291,11 @@ __global__ __launch_bounds__(SW * I3W) void k_interp3(Params p) {
             if (S::PV % SW == 0 || k < NPT - 1 || lane + SW * k < S::PV) sl[lane + SW * k] = v[k];
     };
     // ---- the lane's component cl (fixed: 3 I3M lanes a round) and its marker slot
+#if IBTK_LE_I3MAJOR  // (variant: wave w takes component w mod 3 of pool markers 64 (w / 3) + lane)
+    const int cl = w % I3C, ml = (w / I3C) * SW + lane;
+#else
     const int cl = (int)threadIdx.x % I3C, ml = (int)threadIdx.x / I3C;
+#endif
     CompDesc cdl;
 #define I3SEL(f) cdl.f = cl == 0 ? p.comp[0].f : (cl == 1 ? p.comp[1].f : p.comp[2].f)
 #pragma unroll
@@ -1286,7 +1310,7 @@ __global__ __launch_bounds__(SW * I3W) void k_interp3(Params p) {
     I3SEL(ycell);
     I3SEL(qcomp);
 #undef I3SEL
-    const double* const ring_l = ring + cl * (NSL * PVP);
+    const double* const ring_l = ring + cl * RSTR;
     struct Mk {
         int q;  // the marker whose Q this entry writes (-1: a later duplicate entry does)
         double X[3];
@@ -1343,21 +1367,29 @@ __global__ __launch_bounds__(SW * I3W) void k_interp3(Params p) {
         double* dst = (act && m.q >= 0) ? p.Qout + ((int64_t)p.Q_depth * m.q + cdl.qcomp) : p.sink + lane;
         *dst = acc;
     };
-    double pv[NPT];
-    for (int z = a0 + LO + jw; z < a0 + HI; z += IWAVES) {
-        plane_load(z, pv);
-        plane_put(z, pv);
+    {  // prologue: planes a0 + LO .. a0 + HI - 1 into the rings
+        double pv[NPT];
+        for (int z = a0 + LO + jw; z < a0 + HI; z += WPC) {
+            plane_load(z, pv);
+            plane_put(z, pv);
+        }
     }
-    plane_load(a0 + jw + HI, pv);
+    // pv[b][t]: the group's new plane jw + WPC t, in register buffer b (b = group index mod PF)
+    double pv[PF][PPW][NPT];
+#pragma unroll
+    for (int b = 0; b < PF; ++b)
+#pragma unroll
+        for (int t = 0; t < PPW; ++t) plane_load(a0 + b * IWAVES + jw + WPC * t + HI, pv[b][t]);
     GSpan gs;
     gspan_get(a0, gspan_load(a0), gs);
     Mk nxt;
     int anx;
     mk_load(gs, a0, 0, nxt, anx);
     int vsp1 = gspan_load(a0 + IWAVES);
-    for (int a = a0; a < a1; a += IWAVES) {
+    auto group = [&](int a, double (*pvb)[NPT]) __attribute__((always_inline)) {
         lds_barrier();  // the previous group's reads are done
-        plane_put(a + jw + HI, pv);
+#pragma unroll
+        for (int t = 0; t < PPW; ++t) plane_put(a + jw + WPC * t + HI, pvb[t]);
         lds_barrier();  // planes a+LO .. a+IWAVES-1+HI of every component are in the rings
         const Mk cur = nxt;
         const int acur = anx;
@@ -1365,7 +1397,8 @@ __global__ __launch_bounds__(SW * I3W) void k_interp3(Params p) {
         gspan_get(a + IWAVES, vsp1, gs);
         mk_load(gs, a + IWAVES, 0, nxt, anx);
         vsp1 = gspan_load(a + 2 * IWAVES);
-        plane_load(a + jw + IWAVES + HI, pv);
+#pragma unroll
+        for (int t = 0; t < PPW; ++t) plane_load(a + PF * IWAVES + jw + WPC * t + HI, pvb[t]);
         const int tot = gc.pre[IWAVES];
         Mk m = cur;
         int am = acur;
@@ -1375,6 +1408,11 @@ __global__ __launch_bounds__(SW * I3W) void k_interp3(Params p) {
             if (I3M * (r + 1) < tot) mk_load(gc, a, r + 1, m, am);
             process(min(tot - I3M * r, I3M), now, anow);
         }
+    };
+    for (int a = a0; a < a1; a += PF * IWAVES) {
+#pragma unroll
+        for (int b = 0; b < PF; ++b)
+            if (b == 0 || a + b * IWAVES < a1) group(a + b * IWAVES, pv[b]);
     }
 }
 
@@ -2590,7 +2628,8 @@ hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent
     if constexpr (I3Sh<K>::fits) {
         // the three components of an item in one workgroup (k_interp3)
         if (items > 0 && !p.pd && p.ncomp == I3C && p.tune.interp3 >= 0) {
-            hipLaunchKernelGGL(k_interp3<K>, dim3(sweep_grid(p, p.item_bound)), dim3(SW * I3W), 0, s, p);
+            hipLaunchKernelGGL((k_interp3<K, I3WPC, I3PF>), dim3(sweep_grid(p, p.item_bound)), dim3(SW * I3C * I3WPC), 0,
+                               s, p);
             done = true;
         }
     }
