@@ -114,8 +114,8 @@ struct SweepTune {
     int heavy_target = 0;  // a heavy item's pieces: own markers per piece (0: the default, le_sweep.hip HEAVY_TARGET)
     int heavy_min_piece = 0;  // ... and planes per piece, at least (0: HEAVY_MIN_PIECE)
     int heavy_first = 0;   // heavy items head the table (0, the default) or keep their place (-1)
-    int interp3 = 0;       // 3-D interp of three components: one workgroup per item for all three
-                           // (k_interp3; 0: the default where it applies, -1: a workgroup per component)
+    int interp3 = 0;       // 3-D interp of three components on one patch: 1 = one workgroup per item for
+                           // all three (k_interp3: fewer bytes, measured slower); 0 = a workgroup per component
 };
 // One 3-D sweep item: a patch, a column and its owned planes [p0, p1) (relative
 // to the patch's cg.org[2]).

@@ -1203,16 +1203,16 @@ constexpr int I3C = 3;  // components of a k_interp3 item
 // a 3-way conflict on every read (SQ: LDS waits 2.3x the per-component kernel's).  11 and
 // 22 doubles apart mod 32 they do not.
 constexpr int I3PAD = 11;
-#ifndef IBTK_LE_I3WPC
-#define IBTK_LE_I3WPC 4
-#endif
-#ifndef IBTK_LE_I3PF
-#define IBTK_LE_I3PF 1
-#endif
-#ifndef IBTK_LE_I3MAJOR
-#define IBTK_LE_I3MAJOR 0
-#endif
-constexpr int I3WPC = IBTK_LE_I3WPC, I3PF = IBTK_LE_I3PF;
+// Measured on cfg4 (round 6, profiles/r06): 4 waves a component and one group of planes in
+// flight (12 waves, 146 VGPRs) is the fastest form -- 2 waves a component with one or two
+// groups in flight 11.7-12.1 ms, 1 wave with two 15.4 ms, components dealt by wave instead
+// of by lane 10.4-10.6 ms, against 10.1-10.3 ms -- and still 3-6 % slower than the
+// per-component kernel (9.7 ms) although it moves 20 % fewer bytes (44.6 against 55.4 GB
+// per launch): one 141-KB workgroup per CU waits at each group's barrier for the slowest
+// of its 12 plane loads with nothing else to run, where three independent 4-wave
+// workgroups cover each other's waits.  So k_interp_sweep stays the default and this one
+// runs on request (ctx_tune interp3 = 1).
+constexpr int I3WPC = 4, I3PF = 1;
 template <int K> struct I3Sh {
     using S = ISh<K>;
     static constexpr int RSTR = S::NSL * S::PVP + I3PAD;
@@ -1291,11 +1291,7 @@ __global__ __launch_bounds__(SW * I3C * WPC) void k_interp3(Params p) {
             if (S::PV % SW == 0 || k < NPT - 1 || lane + SW * k < S::PV) sl[lane + SW * k] = v[k];
     };
     // ---- the lane's component cl (fixed: 3 I3M lanes a round) and its marker slot
-#if IBTK_LE_I3MAJOR  // (variant: wave w takes component w mod 3 of pool markers 64 (w / 3) + lane)
-    const int cl = w % I3C, ml = (w / I3C) * SW + lane;
-#else
     const int cl = (int)threadIdx.x % I3C, ml = (int)threadIdx.x / I3C;
-#endif
     CompDesc cdl;
 #define I3SEL(f) cdl.f = cl == 0 ? p.comp[0].f : (cl == 1 ? p.comp[1].f : p.comp[2].f)
 #pragma unroll
@@ -2626,8 +2622,8 @@ hipError_t launch_interp_sweep_t(const Params& p, int n, hipStream_t s, hipEvent
     const long items = (long)p.item_bound * p.ncomp;
     bool done = false;
     if constexpr (I3Sh<K>::fits) {
-        // the three components of an item in one workgroup (k_interp3)
-        if (items > 0 && !p.pd && p.ncomp == I3C && p.tune.interp3 >= 0) {
+        // the three components of an item in one workgroup (k_interp3), on request
+        if (items > 0 && !p.pd && p.ncomp == I3C && p.tune.interp3 > 0) {
             hipLaunchKernelGGL((k_interp3<K, I3WPC, I3PF>), dim3(sweep_grid(p, p.item_bound)), dim3(SW * I3C * I3WPC), 0,
                                s, p);
             done = true;

@@ -557,7 +557,10 @@ int ibtk_le_ctx_enable_timing(ibtk_le_ctx ctx, int enable);
  * sub-segment of a cut item, at least; default 8), "heavy_target" and
  * "heavy_min_piece" (the same for heavy items; defaults 2048 and 1), "strip" (column rows per
  * strip of the item order), "xcd_block" (light items over the XCDs in blocks of
- * this many table entries: 1 round-robin, -1 one range per XCD; default 8).
+ * this many table entries: 1 round-robin, -1 one range per XCD; default 8), and,
+ * taking effect at the next interp, "interp3" (1: the three components of a one-patch
+ * closed-form interp item in one workgroup -- each marker read once, each Q record written
+ * whole; bitwise the same result; 0, the default: a workgroup per component).
  * Interp results do not depend on them; spread results are bit-stable for fixed
  * settings and may differ in the last bits between settings (same-point adds
  * within one 64-candidate chunk follow its step and lane order, and the chunk
