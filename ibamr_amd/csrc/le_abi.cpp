@@ -2820,12 +2820,12 @@ extern "C" int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk
     HIP_TRY(hipMemcpyAsync(ctx->num_tab.p, tab.data(), sizeof(int) * tab.size(), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(ctx->ll_cnt.as<int>() + n, 0, sizeof(int), s));
     HIP_TRY(hipMemsetAsync(total64_dev, 0, sizeof(unsigned long long), s));
-    HIP_TRY(launch_level_list_keys(L, ctx->num_tab.as<int>(), X_dev, n, ctx->ll_key.as<unsigned>(),
-                                   ctx->ll_cnt.as<int>(), bypatch, npatch, s));
     // a marker may have many ghost-box entries (up to 27 images, each in several small
     // patches' ghost boxes): the entries' 32-bit scan below is checked against their sum in
-    // 64 bits, and a level with 2^31 entries or more is refused (advisor, round 5)
-    HIP_TRY(launch_sum64(ctx->ll_cnt.as<int>(), n, total64_dev, s));
+    // 64 bits (formed by the key kernel), and a level with 2^31 entries or more is refused
+    // (advisor, round 5)
+    HIP_TRY(launch_level_list_keys(L, ctx->num_tab.as<int>(), X_dev, n, ctx->ll_key.as<unsigned>(),
+                                   ctx->ll_cnt.as<int>(), bypatch, npatch, total64_dev, s));
     if ((rc = scan_excl(ctx, ctx->ll_cnt.as<int>(), ctx->ll_off.as<int>(), n + 1))) return rc;
     // interior: markers by (patch, cell), stable
     HIP_TRY(launch_iota(ctx->ll_id.as<int>(), n, s));

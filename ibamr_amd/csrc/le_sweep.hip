@@ -1588,10 +1588,13 @@ __device__ __forceinline__ const int* cs_patch_table(const Params& p, int* ptab)
     __syncthreads();
     return ptab;
 }
-__global__ __launch_bounds__(BLOCK) void k_cand_count(Params p, int ncl, int* cnt) {
+// (total, zeroed by the caller: += the stream's length in 64 bits, one atomic a block)
+__global__ __launch_bounds__(BLOCK) void k_cand_count(Params p, int ncl, int* cnt, unsigned long long* total) {
     if (cs_stands(p)) return;
     __shared__ int ptab_s[CS_PTAB];
+    __shared__ unsigned long long ws[BLOCK / 64];
     const int* const ptab = cs_patch_table(p, ptab_s);
+    unsigned long long tsum = 0;
     for (int ca = blockIdx.x * BLOCK + threadIdx.x; ca < ncl; ca += gridDim.x * BLOCK) {
         ColGeom cg;
         int col, a, zb, zilo;
@@ -1607,6 +1610,16 @@ __global__ __launch_bounds__(BLOCK) void k_cand_count(Params p, int ncl, int* cn
             }
         }
         cnt[ca] = t;
+        tsum += (unsigned)t;
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) tsum += __shfl_xor(tsum, d);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = tsum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long b = 0;
+        for (int w = 0; w < BLOCK / 64; ++w) b += ws[w];
+        if (b) atomicAdd(total, b);
     }
 }
 // a wave per column-anchor: its three rows of bucket starts one entry a lane (three
@@ -1707,26 +1720,64 @@ __global__ __launch_bounds__(BLOCK) void k_cand_write(Params p, int ncl, const i
             if (lane == 0) offz[J.zb + 1] = o + nlo;
         }
     };
-    for (int ca = blockIdx.x * (BLOCK / SW) + (int)(threadIdx.x / SW); ca < ncl; ca += nw) {
-        CaJob J;
-        load_rows(ca, J);
-        load_first(J);
-        finish(ca, J);
+    if (!p.pd) {  // one patch: (almost) every column-anchor has candidates
+        for (int ca = blockIdx.x * (BLOCK / SW) + (int)(threadIdx.x / SW); ca < ncl; ca += nw) {
+            CaJob J;
+            load_rows(ca, J);
+            load_first(J);
+            finish(ca, J);
+        }
+        return;
+    }
+    // A level (cfg5: 0.8 M column-anchors, most of them empty): a wave takes 64 column-anchors
+    // at a time, one a lane, nw apart (consecutive ones would hand a sheet's dense stretch
+    // to one wave); the empty ones (and guard columns) write their shifted-z boundaries
+    // lane-parallel, the others are taken one after another by the whole wave.
+    const int wid = blockIdx.x * (BLOCK / SW) + (int)(threadIdx.x / SW);
+    for (int base = wid; base < ncl; base += nw * SW) {
+        const long long cal = (long long)base + (long long)nw * lane;
+        const int cai = cal < ncl ? (int)cal : ncl;
+        bool full = false;
+        if (cai < ncl) {
+            ColGeom cg;
+            int col, a, zb, zilo;
+            double zxlo;
+            const int* bsq;
+            const bool items = ca_decode(p, cai, cg, col, a, bsq, zb, zxlo, zilo, ptab);
+            const int o = off[cai], o1 = off[cai + 1];
+            full = items && o1 != o;
+            if (SHZ && !full) {  // finish() of an empty column-anchor
+                if (a == 0) offz[zb] = o;
+                if (cai == ncl - 1) offz[zb + 2] = o1;
+                offz[zb + 1] = o;
+            }
+        }
+        unsigned long long m = __ballot(full);
+        while (m) {
+            const int k = __builtin_ctzll(m);
+            m &= m - 1;
+            CaJob J;
+            const int ca = base + nw * k;  // (< ncl: a full lane's)
+            load_rows(ca, J);
+            load_first(J);
+            finish(ca, J);
+        }
     }
 }
 hipError_t launch_cand_stream(const Params& p, int ncl, int* cnt, int* off, int* pos, void* temp, size_t temp_bytes,
                               unsigned long long* total, hipStream_t s) {
     if (ncl <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_cand_count, dim3(std::min((ncl + BLOCK - 1) / BLOCK, CS_GRID)), dim3(BLOCK), 0, s, p, ncl,
-                       cnt);
     // the stream's length in 64 bits beside the 32-bit scan (k_cand_write checks it)
     hipError_t e = hipMemsetAsync(total, 0, sizeof(unsigned long long), s);
     if (e != hipSuccess) return e;
-    if ((e = launch_sum64(cnt, ncl, total, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_cand_count, dim3(std::min((ncl + BLOCK - 1) / BLOCK, CS_GRID)), dim3(BLOCK), 0, s, p, ncl,
+                       cnt, total);
     e = launch_scan(temp, temp_bytes, cnt, off, ncl + 1, s);  // cnt[ncl] = 0: off[ncl] = the total
     if (e != hipSuccess) return e;
     const int per = BLOCK / SW;
-    const dim3 g(std::min((ncl + per - 1) / per, CS_GRID)), b(BLOCK);
+    // (a level's waves take 64 column-anchors at a time)
+    const int waves = p.pd ? (ncl + SW - 1) / SW : ncl;
+    const dim3 g(std::min((waves + per - 1) / per, CS_GRID)), b(BLOCK);
     if (p.cs_off_z) hipLaunchKernelGGL(k_cand_write<true>, g, b, 0, s, p, ncl, off, pos, total);
     else hipLaunchKernelGGL(k_cand_write<false>, g, b, 0, s, p, ncl, off, pos, total);
     return hipGetLastError();
