@@ -442,11 +442,23 @@ def run_level(args, cfg, kernel, dev):
     if args.move and args.regrid_every > 1 and (args.regrid_every - 1) * 0.05 > slack:
         raise SystemExit(f"--regrid-every {args.regrid_every}: {args.regrid_every - 1} updates of up to 0.05 "
                          f"cells exceed the lists' drift slack of {slack} cell(s)")
-    cell_at_regrid = torch.floor(X * N)
+    # (scratch allocated once: at a regrid in the timed steps fresh 240-MB temporaries cost a
+    # 30-140 ms allocation stall, profiles/r06/cfg5_move_trace.txt)
+    lazy = args.move and args.regrid_every > 1
+    cell_at_regrid = torch.floor(X * N) if lazy else None
+    drift_tmp = torch.empty_like(X) if lazy else None
+    drift_bad = torch.empty(X.shape, dtype=torch.bool, device=dev) if lazy else None
     drift_flag = torch.zeros(1, dtype=torch.bool, device=dev)
 
+    def cells_of(out):
+        torch.mul(X, N, out=out)
+        out.floor_()
+
     def check_drift():
-        drift_flag.logical_or_(((torch.floor(X * N) - cell_at_regrid).abs() > slack).any())
+        cells_of(drift_tmp)
+        drift_tmp.sub_(cell_at_regrid).abs_()
+        torch.gt(drift_tmp, slack, out=drift_bad)
+        drift_flag.logical_or_(drift_bad.any())
 
     def step_move(record):
         # a moving step on the level: interp at the current positions (the interior lists
@@ -475,8 +487,8 @@ def run_level(args, cfg, kernel, dev):
             (ii2, _, oi2), (si2, sx2, os2) = le.level_index_lists(ctx, geoms, [0, 0, 0], [N - 1] * 3, X, g,
                                                                   order="markers")
             lists.update(ii=ii2, oi=oi2)
-            if args.regrid_every > 1:  # the drift check's reference cells (lazy cadence only)
-                cell_at_regrid.copy_(torch.floor(X * N))
+            if lazy:  # the drift check's reference cells
+                cells_of(cell_at_regrid)
             lvl_s.relist(si2, sx2, os2).bin(X)
             binning["full"] += 1
         else:

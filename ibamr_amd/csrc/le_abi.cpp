@@ -2820,12 +2820,16 @@ extern "C" int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk
     HIP_TRY(hipMemcpyAsync(ctx->num_tab.p, tab.data(), sizeof(int) * tab.size(), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(ctx->ll_cnt.as<int>() + n, 0, sizeof(int), s));
     HIP_TRY(hipMemsetAsync(total64_dev, 0, sizeof(unsigned long long), s));
-    // a marker may have many ghost-box entries (up to 27 images, each in several small
-    // patches' ghost boxes): the entries' 32-bit scan below is checked against their sum in
-    // 64 bits (formed by the key kernel), and a level with 2^31 entries or more is refused
-    // (advisor, round 5)
     HIP_TRY(launch_level_list_keys(L, ctx->num_tab.as<int>(), X_dev, n, ctx->ll_key.as<unsigned>(),
-                                   ctx->ll_cnt.as<int>(), bypatch, npatch, total64_dev, s));
+                                   ctx->ll_cnt.as<int>(), bypatch, npatch, s));
+    // A marker may have many ghost-box entries (its images near the domain's faces, each in
+    // the ghost boxes of several small patches): where n times the most a marker can have
+    // reaches 2^31, the entries' 32-bit scan below is checked against their sum in 64 bits,
+    // and a level with 2^31 entries or more is refused (advisor, round 5)
+    long long per_max = 1;  // per dim: 3 images, each in the ghost boxes of at most 2 g / n + 2 tiles
+    for (int k = 0; k < L.ndim; ++k) per_max *= 3LL * (2LL * ghost / std::max(1, L.n[k]) + 2);
+    const bool check64 = (long long)n * per_max >= (1LL << 31);
+    if (check64) HIP_TRY(launch_sum64(ctx->ll_cnt.as<int>(), n, total64_dev, s));
     if ((rc = scan_excl(ctx, ctx->ll_cnt.as<int>(), ctx->ll_off.as<int>(), n + 1))) return rc;
     // interior: markers by (patch, cell), stable
     HIP_TRY(launch_iota(ctx->ll_id.as<int>(), n, s));
@@ -2839,6 +2843,7 @@ extern "C" int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk
     HIP_TRY(hipMemcpyAsync(&total, ctx->ll_off.as<int>() + n, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(&total64, total64_dev, sizeof(total64), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    if (!check64) total64 = (unsigned long long)(unsigned)total;
     if (total64 >= (1ULL << 31) || (unsigned long long)total != total64)
         return fail(IBTK_LE_ERR_RANGE, "level_index_lists: %llu ghost-box entries (2^31 or more)", total64);
     const int nint = interior_off[npatch];

@@ -556,6 +556,29 @@ __global__ __launch_bounds__(BLOCK) void k_compact(const int* sorder, const int*
     wave_count(counts, loc);           // one atomic per wave and counter
     wave_count(counts + 1, f && !loc);
 }
+// *out (zeroed by the caller) += the sum of v[0..n) in 64 bits: the range check of a 32-bit
+// scan of per-entry counts, run only where the counts could reach 2^31.  A block's waves
+// sum in LDS and one atomic leaves each of at most 256 blocks (per-wave atomics on one
+// address serialise: 0.1 ms for 1e7 counts; one a block of 256 threads, 0.27 ms).
+__global__ __launch_bounds__(BLOCK) void k_sum64(const int* v, int n, unsigned long long* out) {
+    __shared__ unsigned long long ws[BLOCK / 64];
+    unsigned long long t = 0;
+    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) t += (unsigned)v[i];
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) t += __shfl_xor(t, d);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long b = 0;
+        for (int w = 0; w < BLOCK / 64; ++w) b += ws[w];
+        if (b) atomicAdd(out, b);
+    }
+}
+hipError_t launch_sum64(const int* v, int n, unsigned long long* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sum64, dim3(std::min((n + BLOCK - 1) / BLOCK, 256)), dim3(BLOCK), 0, s, v, n, out);
+    return hipGetLastError();
+}
 hipError_t launch_iota(int* v, int n, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_iota, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, v, n);
@@ -789,26 +812,10 @@ __device__ __forceinline__ int level_list_key(LevelNum L, const int* tab, const 
     level_ghost_visit(L, tab, c, [&](int, int, unsigned) { ++cnt; });
     return cnt;
 }
-// (total64, zeroed by the caller: += the ghost-box entry counts in 64 bits, one atomic a
-// block -- the range check of their 32-bit scan)
 __global__ __launch_bounds__(BLOCK) void k_level_list_keys(LevelNum L, const int* tab, const double* X, int n,
-                                                           unsigned* ikey, int* gcnt, int bypatch, int npatch,
-                                                           unsigned long long* total64) {
+                                                           unsigned* ikey, int* gcnt, int bypatch, int npatch) {
     const int s = blockIdx.x * BLOCK + threadIdx.x;
-    int cnt = 0;
-    if (s < n) cnt = level_list_key(L, tab, X, s, ikey, bypatch, npatch);
-    __shared__ unsigned long long ws[BLOCK / 64];
-    unsigned long long t = (unsigned)cnt;
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) t += __shfl_xor(t, d);
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = t;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long b = 0;
-        for (int w = 0; w < BLOCK / 64; ++w) b += ws[w];
-        if (b) atomicAdd(total64, b);
-    }
-    if (s < n) gcnt[s] = cnt;
+    if (s < n) gcnt[s] = level_list_key(L, tab, X, s, ikey, bypatch, npatch);
 }
 // the ghost-box entries at goff[s]: key, entry id (the stable sort's value), marker, image
 __global__ __launch_bounds__(BLOCK) void k_level_list_write(LevelNum L, const int* tab, const double* X, int n,
@@ -856,10 +863,10 @@ __global__ __launch_bounds__(BLOCK) void k_key_offsets(const unsigned* skeys, in
     off[q] = lo;
 }
 hipError_t launch_level_list_keys(const LevelNum& L, const int* tab, const double* X, int n, unsigned* ikey,
-                                  int* gcnt, int bypatch, int npatch, unsigned long long* total64, hipStream_t s) {
+                                  int* gcnt, int bypatch, int npatch, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_level_list_keys, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, L, tab, X, n, ikey, gcnt,
-                       bypatch, npatch, total64);
+                       bypatch, npatch);
     return hipGetLastError();
 }
 hipError_t launch_level_list_write(const LevelNum& L, const int* tab, const double* X, int n, const int* goff,

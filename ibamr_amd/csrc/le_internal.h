@@ -346,6 +346,7 @@ hipError_t launch_image_write(const ImageDesc& d, const double* X, int n, const 
                               double* xshift, unsigned* cellkey, int* cells, int capacity, hipStream_t s);
 // small helpers of the reference-ordered lists (le_aux.hip)
 hipError_t launch_iota(int* v, int n, hipStream_t s);
+hipError_t launch_sum64(const int* v, int n, unsigned long long* out, hipStream_t s);
 // out[i] = key_of(src[perm[i]]): mode 0 lag[idx[perm[i]]] (lag null: idx[perm[i]]), mode 1 keys[perm[i]]
 hipError_t launch_perm_keys(int mode, const int* perm, const int* idx, const int* lag, const unsigned* keys, int n,
                             unsigned* out, hipStream_t s);
@@ -393,9 +394,8 @@ hipError_t launch_level_node_keys(const LevelNum& L, const int* tab, const doubl
 // in sorted order (sid) out as marker indices and periodic shifts; off[q] = first sorted key
 // >= q * per, q = 0 .. npatch.
 // (bypatch: the keys are the patch alone, npatch for none -- marker order within a patch)
-// (total64: a zeroed device u64 that receives the ghost-box entry count in 64 bits)
 hipError_t launch_level_list_keys(const LevelNum& L, const int* tab, const double* X, int n, unsigned* ikey,
-                                  int* gcnt, int bypatch, int npatch, unsigned long long* total64, hipStream_t s);
+                                  int* gcnt, int bypatch, int npatch, hipStream_t s);
 hipError_t launch_level_list_write(const LevelNum& L, const int* tab, const double* X, int n, const int* goff,
                                    unsigned* gkey, int* gid, int* gsrc, int* gimg, int bypatch, hipStream_t s);
 hipError_t launch_level_list_out(const LevelNum& L, const int* sid, const int* gsrc, const int* gimg, int total,

@@ -1588,13 +1588,10 @@ __device__ __forceinline__ const int* cs_patch_table(const Params& p, int* ptab)
     __syncthreads();
     return ptab;
 }
-// (total, zeroed by the caller: += the stream's length in 64 bits, one atomic a block)
-__global__ __launch_bounds__(BLOCK) void k_cand_count(Params p, int ncl, int* cnt, unsigned long long* total) {
+__global__ __launch_bounds__(BLOCK) void k_cand_count(Params p, int ncl, int* cnt) {
     if (cs_stands(p)) return;
     __shared__ int ptab_s[CS_PTAB];
-    __shared__ unsigned long long ws[BLOCK / 64];
     const int* const ptab = cs_patch_table(p, ptab_s);
-    unsigned long long tsum = 0;
     for (int ca = blockIdx.x * BLOCK + threadIdx.x; ca < ncl; ca += gridDim.x * BLOCK) {
         ColGeom cg;
         int col, a, zb, zilo;
@@ -1610,16 +1607,6 @@ __global__ __launch_bounds__(BLOCK) void k_cand_count(Params p, int ncl, int* cn
             }
         }
         cnt[ca] = t;
-        tsum += (unsigned)t;
-    }
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) tsum += __shfl_xor(tsum, d);
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = tsum;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long b = 0;
-        for (int w = 0; w < BLOCK / 64; ++w) b += ws[w];
-        if (b) atomicAdd(total, b);
     }
 }
 // a wave per column-anchor: its three rows of bucket starts one entry a lane (three
@@ -1767,11 +1754,13 @@ __global__ __launch_bounds__(BLOCK) void k_cand_write(Params p, int ncl, const i
 hipError_t launch_cand_stream(const Params& p, int ncl, int* cnt, int* off, int* pos, void* temp, size_t temp_bytes,
                               unsigned long long* total, hipStream_t s) {
     if (ncl <= 0) return hipSuccess;
-    // the stream's length in 64 bits beside the 32-bit scan (k_cand_write checks it)
+    hipLaunchKernelGGL(k_cand_count, dim3(std::min((ncl + BLOCK - 1) / BLOCK, CS_GRID)), dim3(BLOCK), 0, s, p, ncl,
+                       cnt);
+    // the stream's length in 64 bits beside the 32-bit scan (k_cand_write checks it), where
+    // it could reach 2^31 (the 4-a-marker bound, p.cs_total, is 2^31 - 1); else 0
     hipError_t e = hipMemsetAsync(total, 0, sizeof(unsigned long long), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_cand_count, dim3(std::min((ncl + BLOCK - 1) / BLOCK, CS_GRID)), dim3(BLOCK), 0, s, p, ncl,
-                       cnt, total);
+    if (p.cs_total >= 0x7fffffff && (e = launch_sum64(cnt, ncl, total, s)) != hipSuccess) return e;
     e = launch_scan(temp, temp_bytes, cnt, off, ncl + 1, s);  // cnt[ncl] = 0: off[ncl] = the total
     if (e != hipSuccess) return e;
     const int per = BLOCK / SW;
