@@ -2826,8 +2826,13 @@ extern "C" int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk
     // the ghost boxes of several small patches): where n times the most a marker can have
     // reaches 2^31, the entries' 32-bit scan below is checked against their sum in 64 bits,
     // and a level with 2^31 entries or more is refused (advisor, round 5)
-    long long per_max = 1;  // per dim: 3 images, each in the ghost boxes of at most 2 g / n + 2 tiles
-    for (int k = 0; k < L.ndim; ++k) per_max *= 3LL * (2LL * ghost / std::max(1, L.n[k]) + 2);
+    // per dim: 2 images (3 in a domain no wider than 2 g), each in the ghost boxes of at most
+    // 2 g / n + 2 tiles
+    long long per_max = 1;
+    for (int k = 0; k < L.ndim; ++k) {
+        const long long images = (L.dom_hi[k] - L.dom_lo[k] + 1 > 2LL * ghost) ? 2 : 3;
+        per_max *= images * (2LL * ghost / std::max(1, L.n[k]) + 2);
+    }
     const bool check64 = (long long)n * per_max >= (1LL << 31);
     if (check64) HIP_TRY(launch_sum64(ctx->ll_cnt.as<int>(), n, total64_dev, s));
     if ((rc = scan_excl(ctx, ctx->ll_cnt.as<int>(), ctx->ll_off.as<int>(), n + 1))) return rc;

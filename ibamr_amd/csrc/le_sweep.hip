@@ -1707,48 +1707,11 @@ __global__ __launch_bounds__(BLOCK) void k_cand_write(Params p, int ncl, const i
             if (lane == 0) offz[J.zb + 1] = o + nlo;
         }
     };
-    if (!p.pd) {  // one patch: (almost) every column-anchor has candidates
-        for (int ca = blockIdx.x * (BLOCK / SW) + (int)(threadIdx.x / SW); ca < ncl; ca += nw) {
-            CaJob J;
-            load_rows(ca, J);
-            load_first(J);
-            finish(ca, J);
-        }
-        return;
-    }
-    // A level (cfg5: 0.8 M column-anchors, most of them empty): a wave takes 64 column-anchors
-    // at a time, one a lane, nw apart (consecutive ones would hand a sheet's dense stretch
-    // to one wave); the empty ones (and guard columns) write their shifted-z boundaries
-    // lane-parallel, the others are taken one after another by the whole wave.
-    const int wid = blockIdx.x * (BLOCK / SW) + (int)(threadIdx.x / SW);
-    for (int base = wid; base < ncl; base += nw * SW) {
-        const long long cal = (long long)base + (long long)nw * lane;
-        const int cai = cal < ncl ? (int)cal : ncl;
-        bool full = false;
-        if (cai < ncl) {
-            ColGeom cg;
-            int col, a, zb, zilo;
-            double zxlo;
-            const int* bsq;
-            const bool items = ca_decode(p, cai, cg, col, a, bsq, zb, zxlo, zilo, ptab);
-            const int o = off[cai], o1 = off[cai + 1];
-            full = items && o1 != o;
-            if (SHZ && !full) {  // finish() of an empty column-anchor
-                if (a == 0) offz[zb] = o;
-                if (cai == ncl - 1) offz[zb + 2] = o1;
-                offz[zb + 1] = o;
-            }
-        }
-        unsigned long long m = __ballot(full);
-        while (m) {
-            const int k = __builtin_ctzll(m);
-            m &= m - 1;
-            CaJob J;
-            const int ca = base + nw * k;  // (< ncl: a full lane's)
-            load_rows(ca, J);
-            load_first(J);
-            finish(ca, J);
-        }
+    for (int ca = blockIdx.x * (BLOCK / SW) + (int)(threadIdx.x / SW); ca < ncl; ca += nw) {
+        CaJob J;
+        load_rows(ca, J);
+        load_first(J);
+        finish(ca, J);
     }
 }
 hipError_t launch_cand_stream(const Params& p, int ncl, int* cnt, int* off, int* pos, void* temp, size_t temp_bytes,
@@ -1764,9 +1727,7 @@ hipError_t launch_cand_stream(const Params& p, int ncl, int* cnt, int* off, int*
     e = launch_scan(temp, temp_bytes, cnt, off, ncl + 1, s);  // cnt[ncl] = 0: off[ncl] = the total
     if (e != hipSuccess) return e;
     const int per = BLOCK / SW;
-    // (a level's waves take 64 column-anchors at a time)
-    const int waves = p.pd ? (ncl + SW - 1) / SW : ncl;
-    const dim3 g(std::min((waves + per - 1) / per, CS_GRID)), b(BLOCK);
+    const dim3 g(std::min((ncl + per - 1) / per, CS_GRID)), b(BLOCK);
     if (p.cs_off_z) hipLaunchKernelGGL(k_cand_write<true>, g, b, 0, s, p, ncl, off, pos, total);
     else hipLaunchKernelGGL(k_cand_write<false>, g, b, 0, s, p, ncl, off, pos, total);
     return hipGetLastError();
