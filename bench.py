@@ -109,6 +109,26 @@ def physical_cores(cpus):
     return len(cores) or len(cpus)
 
 
+def cpu_quota():
+    """The CPUs' worth of time this process's cgroup may use (cpu.max / cfs_quota), or None if
+    unlimited or unreadable: on the GPU pool the affinity set shows the whole host (256 CPUs)
+    while the quota is one GPU's share."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, -(-q // per))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def cpu_baseline(cfg, kernel, seconds_target=15.0):
     """The oracle (the C restatement) timed on a bounded, same-density sample: on 1 thread, and
     on one thread per physical core of this process's affinity set (every core
@@ -173,7 +193,11 @@ def cpu_baseline(cfg, kernel, seconds_target=15.0):
         cpus = sorted(os.sched_getaffinity(0))
     except AttributeError:
         cpus = list(range(os.cpu_count() or 1))
-    phys = physical_cores(cpus)
+    phys_aff = physical_cores(cpus)
+    quota = cpu_quota()
+    # one thread per physical core the process can run on: the affinity set's, unless the cgroup's
+    # CPU quota allows fewer (then more threads only time-slice the same quota)
+    phys = min(phys_aff, quota) if quota else phys_aff
     cap = os.environ.get("OMP_NUM_THREADS")
 
     def run_threads(T, t_run):
@@ -205,10 +229,10 @@ def cpu_baseline(cfg, kernel, seconds_target=15.0):
     # replicas' f arrays contend for memory bandwidth, and fewer threads may do more
     by_threads = {phys: rateT}
     share = None
-    tries = {16, 32, 64}
-    if cap and cap.isdigit() and 0 < int(cap) < phys:
+    tries = {16, 32, 64, phys_aff}
+    if cap and cap.isdigit() and 0 < int(cap) < phys_aff:
         tries.add(int(cap))
-    for T in sorted(t for t in tries if 1 < t < phys):
+    for T in sorted(t for t in tries if 1 < t <= phys_aff and t != phys):
         by_threads[T] = run_threads(T, 0.1 * seconds_target)[0]
     if cap and cap.isdigit():
         share = by_threads.get(int(cap))
@@ -217,11 +241,12 @@ def cpu_baseline(cfg, kernel, seconds_target=15.0):
             "value_pool_share": share, "pool_share_threads": int(cap) if share is not None else None,
             "value_by_threads": {str(k): v for k, v in sorted(by_threads.items())},
             "value_best": by_threads[best_t], "best_threads": best_t,
-            "host_nproc": os.cpu_count(), "affinity_cpus": len(cpus), "physical_cores": phys,
-            "omp_num_threads": cap,
+            "host_nproc": os.cpu_count(), "affinity_cpus": len(cpus), "physical_cores_affinity": phys_aff,
+            "cgroup_cpu_quota": quota, "physical_cores": phys, "omp_num_threads": cap,
             "sample": f"{Ns}^3 periodic grid, {Ms} uniform markers (same density as the workload), "
                       f"{kernel} side interp+spread, cell-sorted (oracle C); {phys} threads (one per physical "
-                      f"core of the affinity set, OMP_NUM_THREADS={cap} not applied), one replica of the sample "
+                      f"core of the affinity set ({phys_aff}) within the cgroup CPU quota ({quota}), "
+                      f"OMP_NUM_THREADS={cap} not applied), one replica of the sample "
                       f"each: {passes} passes in {wall:.1f} s; 1 thread: {reps} passes in {elapsed:.1f} s; a "
                       f"sample, not cfg4 itself: the oracle's cost is per marker, independent of the grid"}
 
@@ -459,6 +484,12 @@ def run_level(args, cfg, kernel, dev):
         drift_tmp.sub_(cell_at_regrid).abs_()
         torch.gt(drift_tmp, slack, out=drift_bad)
         drift_flag.logical_or_(drift_bad.any())
+
+    if lazy:
+        # once outside the timed steps: the first launch of each torch kernel loads its code
+        # object (a 113-ms hipLaunchKernel at the first regrid in the timed steps otherwise,
+        # profiles/r06/cfg5_r10_stall.txt); the warm-up's regrid skips the check
+        check_drift()
 
     def step_move(record):
         # a moving step on the level: interp at the current positions (the interior lists
