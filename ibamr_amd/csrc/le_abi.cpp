@@ -160,6 +160,10 @@ struct ibtk_le_ctx_s {
     bool timing = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool ev_valid = false;
+    // the 3-D spread's F gather runs on a side stream, concurrent with the candidate-stream
+    // rebuild on `stream` (gather_fork / gather_join), created on first use
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 struct ibtk_le_markers_s {
@@ -271,6 +275,12 @@ extern "C" int ibtk_le_ctx_destroy(ibtk_le_ctx ctx) {
         b->release();
     if (ctx->ev0) hipEventDestroy(ctx->ev0);
     if (ctx->ev1) hipEventDestroy(ctx->ev1);
+    if (ctx->side) {
+        hipStreamSynchronize(ctx->side);
+        hipStreamDestroy(ctx->side);
+    }
+    if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_join) hipEventDestroy(ctx->ev_join);
     delete ctx;
     return IBTK_LE_OK;
 }
@@ -321,6 +331,7 @@ extern "C" int ibtk_le_ctx_tune(ibtk_le_ctx ctx, const char* key, int value) {
     else if (k == "strip") t.strip = value;
     else if (k == "xcd_block") t.xcd_block = value;
     else if (k == "interp3") t.interp3 = value;
+    else if (k == "side_gather") t.side_gather = value;
     else return fail(IBTK_LE_ERR_ARG, "unknown tuning key %s", key);
     return IBTK_LE_OK;
 }
@@ -1189,6 +1200,36 @@ static int build_candidates(ibtk_le_ctx ctx, ibtk_le_markers m, const Params& p)
     return IBTK_LE_OK;
 }
 
+// The 3-D spread's F gather (sorted_F from Q and sorted_s, both ready on `stream`) does not
+// depend on the candidate stream, whose rebuild after a re-binning (k_cand_count, the scan,
+// k_cand_write: about 1 ms at cfg4) leaves CUs idle: when the stream is rebuilt, the
+// gather runs beside it on the side stream (cfg4 moving: spread 14.6 -> 14.4 ms a step,
+// profiles/r06/side_gather_ab.txt); a standing stream keeps the gather in line.  The fork orders the gather after everything on `stream` so far (the
+// binning, the previous sweep still reading sorted_F); the join orders the sweep after it.
+// Worth its cross-stream hops (about 0.05 ms a step) only on a large gather: cfg4 (1e8
+// markers) gains 0.2 ms, cfg5 (1e7, a level) loses 0.04 ms; the gain scales with n, even
+// at about 2.5e7.  side_gather: 0 auto (n >= 2^25), 1 always, -1 never.
+static bool side_gather(ibtk_le_ctx ctx, ibtk_le_markers m) {
+    const int t = ctx->tune.side_gather;
+    return t > 0 || (t == 0 && m->n >= (1 << 25));
+}
+static int gather_fork(ibtk_le_ctx ctx, const Params& p) {
+    if (!ctx->side) {
+        HIP_TRY(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+    }
+    HIP_TRY(hipEventRecord(ctx->ev_fork, ctx->stream));
+    HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    HIP_TRY(launch_gather_F(p, ctx->side));
+    HIP_TRY(hipEventRecord(ctx->ev_join, ctx->side));
+    return IBTK_LE_OK;
+}
+static int gather_join(ibtk_le_ctx ctx) {
+    HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+    return IBTK_LE_OK;
+}
+
 static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int centering, int axis,
                        const ibtk_le_patch_geom* geom, double* const* q_dev, int q_depth, const double* Q_dev,
                        int Q_depth, const double* ds_dev, const double* X_dev, bool zero_ghosts = false,
@@ -1422,15 +1463,20 @@ extern "C" int ibtk_le_user_spread(ibtk_le_ctx ctx, int centering, int axis, con
 // their anchor (cs_off_z): a stream built without the split is rebuilt with it, and one
 // built with it stands across a re-binning only if that moved no marker and changed no
 // shifted-z anchor (positions move within their cells).
+// A closed-form kernel's stream is always split by the shifted-z anchor, whichever
+// components a call spreads: the order of a column-anchor's candidates -- the order in
+// which they add into a point -- then depends on the binning alone, not on which
+// centerings were spread since it (advisor, round 5)
+static bool cand_split(int k) { return k == K_IB_4 || k == K_BSPLINE_4 || k == K_IB_6 || k == K_IB_4_W8; }
+// the stream stands as built: cand_stream launches nothing
+static bool cand_stream_built(ibtk_le_markers m) {
+    return m->cs_state == 1 && m->cs_pos.p && (m->cs_split || !cand_split(m->kernel));
+}
 static int cand_stream(ibtk_le_ctx ctx, ibtk_le_markers m, Params& p) {
     const long long ncl = (long long)m->nbuckets_total / NBAND;
     const long long nclz = m->npatch ? m->nclz : (long long)m->cg.ncol * (m->cg.nz + 1);
     const int k = m->kernel;
-    // A closed-form kernel's stream is always split by the shifted-z anchor, whichever
-    // components this call spreads: the order of a column-anchor's candidates -- the order in
-    // which they add into a point -- then depends on the binning alone, not on which
-    // centerings were spread since it (advisor, round 5)
-    const bool split = k == K_IB_4 || k == K_BSPLINE_4 || k == K_IB_6 || k == K_IB_4_W8;
+    const bool split = cand_split(k);
     // A marker is a candidate of at most four columns (its own, one x- and one y-neighbour,
     // the corner between them: a stencil never reaches both neighbours in a dim), so 4 n
     // positions always hold the stream (16 bytes a marker; about 1.3 of the 4 are used by
@@ -1444,7 +1490,7 @@ static int cand_stream(ibtk_le_ctx ctx, ibtk_le_markers m, Params& p) {
     p.cs_total = (int)cap;
     p.cs_off_z = m->cs_split ? m->cs_off_z.as<int>() : nullptr;
     p.cs_rint = k == K_IB_4 ? 1 : 0;  // the IB_4 spread anchors by rint (spread_setup)
-    if (m->cs_state == 1 && m->cs_pos.p && (m->cs_split || !split)) return IBTK_LE_OK;
+    if (cand_stream_built(m)) return IBTK_LE_OK;
     int rc;
     // cs_cnt: ncl + 1 counts, then the stream's 64-bit length (8-byte aligned)
     const size_t tot_at = (sizeof(int) * (size_t)(ncl + 1) + 7) / 8 * 8;
@@ -1503,15 +1549,21 @@ static int spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int cente
     for (int first = 0; first < nc; first += MAXC) {
         const int cnt = std::min(MAXC, nc - first);
         if (int rc = make_comps(geom, centering, axis, q_dev, q_depth, Q_depth, first, cnt, p)) return rc;
+        const bool side = geom->ndim == 3 && side_gather(ctx, m) && !cand_stream_built(m);
+        if (side)
+            if (int rc = gather_fork(ctx, p)) return rc;
         if (geom->ndim == 3)
             if (int rc = cand_stream(ctx, m, p)) return rc;
+        if (side)
+            if (int rc = gather_join(ctx)) return rc;
         const bool t = ctx->timing && first == 0;
         const size_t nst = (size_t)m->item_bound * cnt * 8;
         if (geom->ndim == 3)
             if (int rc = stamps_begin(ctx, nst, p)) return rc;
         if (geom->ndim == 3) {
             if (int rc = adds_begin(ctx, p, first == 0)) return rc;
-            HIP_TRY(launch_spread_sweep(kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
+            HIP_TRY(launch_spread_sweep(kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr,
+                                        !side));
             if (int rc = adds_end(ctx, p)) return rc;
         } else {
             HIP_TRY(launch_spread(geom->ndim, kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
@@ -1855,13 +1907,18 @@ static int level_spread_impl(ibtk_le_ctx ctx, ibtk_le_markers m, int kernel, int
         if (int rc = ctx->fbuf.ensure(sizeof(double) * (size_t)m->n * (size_t)nc)) return rc;
         p.sorted_F = ctx->fbuf.as<double>();
     }
+    const bool side = side_gather(ctx, m) && !cand_stream_built(m);
+    if (side)
+        if (int rc = gather_fork(ctx, p)) return rc;
     if (int rc = cand_stream(ctx, m, p)) return rc;
+    if (side)
+        if (int rc = gather_join(ctx)) return rc;
     const bool t = ctx->timing;
     ctx->ev_valid = false;
     const size_t nst = (size_t)m->item_bound * nc * 8;
     if (int rc = stamps_begin(ctx, nst, p)) return rc;
     if (int rc = adds_begin(ctx, p, true)) return rc;
-    HIP_TRY(launch_spread_sweep(kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr));
+    HIP_TRY(launch_spread_sweep(kernel, p, ctx->stream, t ? ctx->ev0 : nullptr, t ? ctx->ev1 : nullptr, !side));
     if (int rc = adds_end(ctx, p)) return rc;
     if (int rc = stamps_report(ctx, nst, p)) return rc;
     if (t) ctx->ev_valid = true;

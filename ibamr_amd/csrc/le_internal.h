@@ -116,6 +116,9 @@ struct SweepTune {
     int heavy_first = 0;   // heavy items head the table (0, the default) or keep their place (-1)
     int interp3 = 0;       // 3-D interp of three components on one patch: 1 = one workgroup per item for
                            // all three (k_interp3: fewer bytes, measured slower); 0 = a workgroup per component
+    int side_gather = 0;   // 3-D spread: the F gather on the side stream beside the candidate-stream
+                           // rebuild (1), in line before the sweep (-1), or 0 (the default): on
+                           // the side stream from 2^25 markers
 };
 // One 3-D sweep item: a patch, a column and its owned planes [p0, p1) (relative
 // to the patch's cg.org[2]).
@@ -294,7 +297,11 @@ hipError_t launch_position_update(int scheme, long n, double dt, const double* X
 hipError_t launch_gather_col(int kernel, const Params& p, int n, int* sorted_s, double* sorted_X,
                              const unsigned* sorted_key, int nbuckets, int* bucket_start, hipStream_t s);
 hipError_t launch_interp_sweep(int kernel, const Params& p, int n, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
-hipError_t launch_spread_sweep(int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
+// gather = false: the spread values (sorted_F) were gathered already (launch_gather_F, on
+// the context's side stream while the candidate stream was rebuilt)
+hipError_t launch_spread_sweep(int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
+                               bool gather = true);
+hipError_t launch_gather_F(const Params& p, hipStream_t s);
 void sweep_segments(const ColGeom& cg, int& S, int& nseg, int seg_items, bool level);
 hipError_t launch_item_table(int kernel, const Params& p, int target, int heavy, int* nsub, int* start, SweepItem* tab, int* ntot,
                              void* temp, size_t temp_bytes, hipStream_t s);

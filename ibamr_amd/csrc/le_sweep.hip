@@ -2664,7 +2664,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather_F_col(Params p, int n, double*
     }
 }
 
-template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+hipError_t launch_gather_F(const Params& p, hipStream_t s) {
     if (p.nsorted > 0) {
         const bool rec3 = p.ncomp == 3 && p.Q_depth == 3 && p.comp[0].qcomp == 0 && p.comp[1].qcomp == 1 &&
                           p.comp[2].qcomp == 2;
@@ -2672,6 +2672,12 @@ template <int K> hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s
         if (rec3) hipLaunchKernelGGL(k_gather_F_col<true>, g, b, 0, s, p, p.nsorted, const_cast<double*>(p.sorted_F));
         else hipLaunchKernelGGL(k_gather_F_col<false>, g, b, 0, s, p, p.nsorted, const_cast<double*>(p.sorted_F));
     }
+    return hipGetLastError();
+}
+template <int K>
+hipError_t launch_spread_sweep_t(const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, bool gather) {
+    if (gather)
+        if (hipError_t e = launch_gather_F(p, s); e != hipSuccess) return e;
     if (ev0) (void)hipEventRecord(ev0, s);  // the events bracket the sweep kernels alone
     // One launch of every component.  Closed-form kernels run them all on the 5-slot
     // key-frame ring (ZC): a component whose z frame is shifted by -dz/2 reads its
@@ -2721,7 +2727,7 @@ hipError_t launch_item_table(int kernel, const Params& p, int target, int heavy,
 using BinColFn = hipError_t (*)(const Params&, int, unsigned*, int*, hipStream_t);
 using GatherColFn = hipError_t (*)(const Params&, int, int*, double*, const unsigned*, int, int*, hipStream_t);
 using InterpSwFn = hipError_t (*)(const Params&, int, hipStream_t, hipEvent_t, hipEvent_t);
-using SpreadSwFn = hipError_t (*)(const Params&, hipStream_t, hipEvent_t, hipEvent_t);
+using SpreadSwFn = hipError_t (*)(const Params&, hipStream_t, hipEvent_t, hipEvent_t, bool);
 static BinColFn pick_bin_col(int k) { IBTK_LE_DISPATCH_K(k, launch_bin_col_t) }
 static GatherColFn pick_gather_col(int k) { IBTK_LE_DISPATCH_K(k, launch_gather_col_t) }
 static InterpSwFn pick_interp_sweep(int k) { IBTK_LE_DISPATCH_K(k, launch_interp_sweep_t) }
@@ -2800,9 +2806,10 @@ hipError_t launch_interp_sweep(int kernel, const Params& p, int n, hipStream_t s
     InterpSwFn f = pick_interp_sweep(kernel);
     return f ? f(p, n, s, ev0, ev1) : hipErrorInvalidValue;
 }
-hipError_t launch_spread_sweep(int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+hipError_t launch_spread_sweep(int kernel, const Params& p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
+                               bool gather) {
     SpreadSwFn f = pick_spread_sweep(kernel);
-    return f ? f(p, s, ev0, ev1) : hipErrorInvalidValue;
+    return f ? f(p, s, ev0, ev1, gather) : hipErrorInvalidValue;
 }
 
 }  // namespace ibtk_le

@@ -560,7 +560,10 @@ int ibtk_le_ctx_enable_timing(ibtk_le_ctx ctx, int enable);
  * this many table entries: 1 round-robin, -1 one range per XCD; default 8), and,
  * taking effect at the next interp, "interp3" (1: the three components of a one-patch
  * closed-form interp item in one workgroup -- each marker read once, each Q record written
- * whole; bitwise the same result; 0, the default: a workgroup per component).
+ * whole; bitwise the same result; 0, the default: a workgroup per component), and,
+ * taking effect at the next spread, "side_gather" (1: the 3-D spread's F gather on the
+ * context's side stream, beside a candidate-stream rebuild; -1: in line before the sweep;
+ * 0, the default: the side stream from 2^25 markers; bitwise the same result).
  * Interp results do not depend on them; spread results are bit-stable for fixed
  * settings and may differ in the last bits between settings (same-point adds
  * within one 64-candidate chunk follow its step and lane order, and the chunk

@@ -114,3 +114,38 @@ def test_select_interior_lists_changed_in_place(le):
         lvl.interp("side", u, U1, X)
         ctx.synchronize()
         assert torch.equal(U1, U_ref)
+
+
+@pytest.mark.parametrize("kernel", ["IB_4", "IB_6"])
+def test_side_stream_gather_matches_in_line(le, kernel):
+    """The spread's F gather runs on the context's side stream while the candidate stream
+    is rebuilt (ibtk_le_ctx_tune "side_gather" 1; by default from 2^25 markers); it sees F as the caller's
+    stream left it just before the call (here rewritten in place between spreads) and the
+    result equals the in-line gather's (-1) bit for bit, on the first spread after a
+    binning, after a re-binning that moved markers, and on a standing stream."""
+    g = le._lib.load().ibtk_le_min_ghost_width(le.kernel_id(kernel))
+    geom = le.Geometry.periodic_unit([64, 48, 40], g)
+    rng = np.random.default_rng(5)
+    M = 40000
+    X = torch.from_numpy(rng.uniform(0.0, 1.0, (M, 3))).cuda()
+    F0 = torch.from_numpy(rng.standard_normal((M, 3))).cuda()
+    h = 1.0 / 64
+    X2 = torch.remainder(X + 0.4 * h * (torch.rand_like(X) - 0.5), 1.0)
+    outs = {}
+    for mode in (-1, 1):
+        ctx = le.Context(0)
+        ctx.tune("side_gather", mode)
+        F = F0.clone()
+        m = le.Markers(ctx).bin(geom, kernel, X)
+        res = [_spread(le, ctx, m, kernel, "side", geom, F, X, 1)]
+        F.mul_(-0.75).add_(0.125)          # F changes every step
+        m.rebin(X2)
+        res.append(_spread(le, ctx, m, kernel, "side", geom, F, X2, 1))
+        F.mul_(1.5)
+        res.append(_spread(le, ctx, m, kernel, "side", geom, F, X2, 1))  # standing stream
+        outs[mode] = res
+    for a, b in zip(outs[-1], outs[1]):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+    # and the second spread is not the first one's F: the gather saw the rewrite
+    assert not torch.equal(outs[1][1][0], outs[1][0][0])
