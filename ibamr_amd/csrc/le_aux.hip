@@ -1049,35 +1049,53 @@ hipError_t launch_dedup(const int* indices, const int* sorted_l, const int* sort
 // IBMethod.cpp:619-681): PETSc VecWAXPY w = alpha x + y and VecAXPY y += alpha x,
 // each a rounded multiply then a rounded add (built with -ffp-contract=off, so
 // no fma), elementwise over the n doubles of the (M, NDIM) arrays.  HBM-bound:
-// 16-byte accesses, pairs of doubles per lane when every array is 16-byte aligned.
+// 16-byte accesses, pairs of doubles per lane when every array is 16-byte aligned,
+// PU_UNROLL items a lane with every load issued before the first store (X may be Xn:
+// each element is read and written by one lane, read first).  Round 6: 1.57 ms for
+// cfg4's 1e8 markers (7.2 GB, 4.6 TB/s) with one item a lane in a grid-stride loop.
 // ---------------------------------------------------------------------------
+constexpr int PU_UNROLL = 4;
 template <bool TRAP, typename V>
-__global__ __launch_bounds__(BLOCK) void k_position_update(long n, double dt, const V* X,
-                                                           const V* U0, const V* U1,
-                                                           V* Xn) {
-    const long stride = (long)gridDim.x * BLOCK;
-    for (long i = (long)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
-        if constexpr (sizeof(V) == 16) {
-            const V x = X[i], u = U0[i];
-            V w;
-            if constexpr (TRAP) {
-                const double h = 0.5 * dt;
-                const V v = U1[i];
-                w.x = (h * u.x + x.x) + h * v.x;
-                w.y = (h * u.y + x.y) + h * v.y;
-            } else {
-                w.x = dt * u.x + x.x;
-                w.y = dt * u.y + x.y;
-            }
-            Xn[i] = w;
+__device__ __forceinline__ V pu_step(double dt, const V& x, const V& u, const V& v) {
+    if constexpr (sizeof(V) == 16) {
+        V w;
+        if constexpr (TRAP) {
+            const double h = 0.5 * dt;
+            w.x = (h * u.x + x.x) + h * v.x;
+            w.y = (h * u.y + x.y) + h * v.y;
         } else {
-            if constexpr (TRAP) {
-                const double h = 0.5 * dt;
-                Xn[i] = (h * U0[i] + X[i]) + h * U1[i];
-            } else {
-                Xn[i] = dt * U0[i] + X[i];
-            }
+            w.x = dt * u.x + x.x;
+            w.y = dt * u.y + x.y;
         }
+        return w;
+    } else {
+        if constexpr (TRAP) {
+            const double h = 0.5 * dt;
+            return (h * u + x) + h * v;
+        } else {
+            return dt * u + x;
+        }
+    }
+}
+template <bool TRAP, typename V>
+__global__ __launch_bounds__(BLOCK) void k_position_update(long n, double dt, const V* X, const V* U0, const V* U1,
+                                                           V* Xn) {
+    const long i0 = (long)blockIdx.x * (BLOCK * PU_UNROLL) + threadIdx.x;
+    V x[PU_UNROLL], u[PU_UNROLL], v[PU_UNROLL];
+#pragma unroll
+    for (int k = 0; k < PU_UNROLL; ++k) {
+        const long i = i0 + (long)k * BLOCK;
+        if (i < n) {
+            x[k] = X[i];
+            u[k] = U0[i];
+            if constexpr (TRAP) v[k] = U1[i];
+            else v[k] = u[k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < PU_UNROLL; ++k) {
+        const long i = i0 + (long)k * BLOCK;
+        if (i < n) Xn[i] = pu_step<TRAP, V>(dt, x[k], u[k], v[k]);
     }
 }
 
@@ -1088,19 +1106,19 @@ hipError_t launch_position_update(int scheme, long n, double dt, const double* X
     auto al = [](const void* q) { return q == nullptr || ((uintptr_t)q & 15u) == 0; };
     const bool vec = (n % 2 == 0) && al(X) && al(U0) && al(U1) && al(Xn);
     const long items = vec ? n / 2 : n;
-    const long want = (items + BLOCK - 1) / BLOCK;
-    const int grid = (int)(want < 65536 ? want : 65536);
+    const long grid = (items + BLOCK * PU_UNROLL - 1) / (BLOCK * PU_UNROLL);
+    if (grid > 0x7fffffffL) return hipErrorInvalidValue;
     if (vec) {
         using V = double2;
         auto x = (const V*)X;
         auto u0 = (const V*)U0;
         auto u1 = (const V*)U1;
         auto xn = (V*)Xn;
-        if (trap) hipLaunchKernelGGL((k_position_update<true, V>), dim3(grid), dim3(BLOCK), 0, s, items, dt, x, u0, u1, xn);
-        else hipLaunchKernelGGL((k_position_update<false, V>), dim3(grid), dim3(BLOCK), 0, s, items, dt, x, u0, u1, xn);
+        if (trap) hipLaunchKernelGGL((k_position_update<true, V>), dim3((unsigned)grid), dim3(BLOCK), 0, s, items, dt, x, u0, u1, xn);
+        else hipLaunchKernelGGL((k_position_update<false, V>), dim3((unsigned)grid), dim3(BLOCK), 0, s, items, dt, x, u0, u1, xn);
     } else {
-        if (trap) hipLaunchKernelGGL((k_position_update<true, double>), dim3(grid), dim3(BLOCK), 0, s, items, dt, X, U0, U1, Xn);
-        else hipLaunchKernelGGL((k_position_update<false, double>), dim3(grid), dim3(BLOCK), 0, s, items, dt, X, U0, U1, Xn);
+        if (trap) hipLaunchKernelGGL((k_position_update<true, double>), dim3((unsigned)grid), dim3(BLOCK), 0, s, items, dt, X, U0, U1, Xn);
+        else hipLaunchKernelGGL((k_position_update<false, double>), dim3((unsigned)grid), dim3(BLOCK), 0, s, items, dt, X, U0, U1, Xn);
     }
     return hipGetLastError();
 }
