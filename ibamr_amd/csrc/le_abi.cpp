@@ -164,6 +164,10 @@ struct ibtk_le_ctx_s {
     // rebuild on `stream` (gather_fork / gather_join), created on first use
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // pinned host staging of small read-backs (d2h_sync): a copy into pageable memory is a
+    // staged, blocking copy of its own
+    void* hstage = nullptr;
+    size_t hstage_cap = 0;
 };
 
 struct ibtk_le_markers_s {
@@ -281,6 +285,7 @@ extern "C" int ibtk_le_ctx_destroy(ibtk_le_ctx ctx) {
     }
     if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) hipEventDestroy(ctx->ev_join);
+    if (ctx->hstage) hipHostFree(ctx->hstage);
     delete ctx;
     return IBTK_LE_OK;
 }
@@ -2696,6 +2701,23 @@ static int sort_pairs(ibtk_le_ctx ctx, const unsigned* kin, unsigned* kout, cons
     return IBTK_LE_OK;
 }
 
+// bytes of device memory to host memory after the stream's work so far: one copy through the
+// context's pinned staging, then a wait on the stream
+static int d2h_sync(ibtk_le_ctx ctx, void* host, const void* dev, size_t bytes) {
+    if (ctx->hstage_cap < bytes) {
+        if (ctx->hstage) HIP_TRY(hipHostFree(ctx->hstage));
+        ctx->hstage = nullptr;
+        ctx->hstage_cap = 0;
+        const size_t cap = std::max<size_t>(bytes, 4096);
+        HIP_TRY(hipHostMalloc(&ctx->hstage, cap, hipHostMallocDefault));
+        ctx->hstage_cap = cap;
+    }
+    HIP_TRY(hipMemcpyAsync(ctx->hstage, dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    std::memcpy(host, ctx->hstage, bytes);
+    return IBTK_LE_OK;
+}
+
 // A level of equal patches aligned to one tiling of the domain [dom_lo, dom_hi]: its
 // numbering frame (LevelNum) and the tile -> patch table (-1: no local patch).
 static int make_level_num(int npatch, const ibtk_le_patch_geom* geoms, const int* dom_lo, const int* dom_hi,
@@ -2870,8 +2892,9 @@ extern "C" int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk
     if ((rc = ctx->ll_key2.ensure(sizeof(unsigned) * (size_t)n))) return rc;
     if ((rc = ctx->ll_id.ensure(sizeof(int) * (size_t)n))) return rc;
     if ((rc = ctx->ll_id2.ensure(sizeof(int) * (size_t)n))) return rc;
-    // the patch offsets (npatch + 1 ints), then the 64-bit total of the ghost-box entries
-    const size_t sum_at = ((sizeof(int) * (size_t)(npatch + 1)) + 7) / 8 * 8;
+    // the patch offsets (npatch + 1 ints), the ghost-box entries' 32-bit total, then their
+    // 64-bit total: read back in one copy
+    const size_t sum_at = ((sizeof(int) * (size_t)(npatch + 2)) + 7) / 8 * 8;
     if ((rc = ctx->counts.ensure(sum_at + sizeof(unsigned long long)))) return rc;
     unsigned long long* const total64_dev = reinterpret_cast<unsigned long long*>(ctx->counts.as<char>() + sum_at);
     HIP_TRY(hipMemcpyAsync(ctx->num_tab.p, tab.data(), sizeof(int) * tab.size(), hipMemcpyHostToDevice, s));
@@ -2899,12 +2922,15 @@ extern "C" int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk
                          ctx->ll_id2.as<int>(), n, kbits)))
         return rc;
     HIP_TRY(launch_key_offsets(ctx->ll_key2.as<unsigned>(), n, pcells, npatch, ctx->counts.as<int>(), s));
+    HIP_TRY(hipMemcpyAsync(ctx->counts.as<int>() + npatch + 1, ctx->ll_off.as<int>() + n, sizeof(int),
+                           hipMemcpyDeviceToDevice, s));
+    std::vector<char> back(sum_at + sizeof(unsigned long long));
+    if ((rc = d2h_sync(ctx, back.data(), ctx->counts.p, back.size()))) return rc;
+    std::memcpy(interior_off, back.data(), sizeof(int) * (size_t)(npatch + 1));
     int total = 0;
     unsigned long long total64 = 0;
-    HIP_TRY(hipMemcpyAsync(interior_off, ctx->counts.p, sizeof(int) * (size_t)(npatch + 1), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(&total, ctx->ll_off.as<int>() + n, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(&total64, total64_dev, sizeof(total64), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    std::memcpy(&total, back.data() + sizeof(int) * (size_t)(npatch + 1), sizeof(int));
+    std::memcpy(&total64, back.data() + sum_at, sizeof(total64));
     if (!check64) total64 = (unsigned long long)(unsigned)total;
     if (total64 >= (1ULL << 31) || (unsigned long long)total != total64)
         return fail(IBTK_LE_ERR_RANGE, "level_index_lists: %llu ghost-box entries (2^31 or more)", total64);
@@ -2929,8 +2955,7 @@ extern "C" int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk
                              ctx->ll_id2.as<int>(), total, kbits)))
             return rc;
         HIP_TRY(launch_key_offsets(ctx->ll_key2.as<unsigned>(), total, gcells, npatch, ctx->counts.as<int>(), s));
-        HIP_TRY(hipMemcpyAsync(ghost_off, ctx->counts.p, sizeof(int) * (size_t)(npatch + 1), hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
+        if ((rc = d2h_sync(ctx, ghost_off, ctx->counts.p, sizeof(int) * (size_t)(npatch + 1)))) return rc;
         if (total <= ghost_cap) {
             if (!ghost_dev) return fail(IBTK_LE_ERR_ARG, "null ghost-box list");
             HIP_TRY(launch_level_list_out(L, ctx->ll_id2.as<int>(), ctx->ll_src.as<int>(), ctx->ll_img.as<int>(), total,
@@ -2939,7 +2964,8 @@ extern "C" int ibtk_le_level_index_lists(ibtk_le_ctx ctx, int npatch, const ibtk
             short_cap = true;
         }
     }
-    HIP_TRY(hipStreamSynchronize(s));
+    // (no wait for the lists' write: the offsets are on the host already, the lists follow
+    // on the stream, and the caller's next launches queue behind them)
     if (short_cap)
         return fail(IBTK_LE_ERR_ARG, "level_index_lists: %d interior / %d ghost-box entries exceed the capacities %d / %d",
                     nint, total, interior_cap, ghost_cap);
