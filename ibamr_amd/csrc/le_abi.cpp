@@ -2735,6 +2735,7 @@ static int make_level_num(int npatch, const ibtk_le_patch_geom* geoms, const int
             const int nk = geoms[q].iupper[k] - geoms[q].ilower[k] + 1;
             if (q == 0) {
                 L.n[k] = nk;
+                L.rn[k] = 1.0f / (float)nk;
                 L.org[k] = geoms[0].ilower[k];
                 L.dx[k] = geoms[0].dx[k];
             }

@@ -627,6 +627,17 @@ hipError_t launch_node_keys(const ImageDesc& d, const double* X, int n, unsigned
 // 2874-2947) over the local patches of a level
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+// floor(a / L.n[k]) from a float estimate corrected by one step (exact: |a| < 2^22 keeps the
+// estimate within one of the quotient; larger |a| divide): the level kernels' tile searches
+// take ~20 of these a marker, each a ~30-instruction integer division otherwise
+__device__ __forceinline__ int lfloordiv(const LevelNum& L, int a, int k) {
+    const int b = L.n[k];
+    if (a >= (1 << 22) || a <= -(1 << 22)) return floordiv(a, b);
+    int q = (int)floorf((float)a * L.rn[k]);
+    const int r = a - q * b;
+    q += r < 0 ? -1 : (r >= b ? 1 : 0);
+    return q;
+}
 
 __global__ __launch_bounds__(BLOCK) void k_level_node_keys(LevelNum L, const int* tab, const double* X, int n,
                                                            unsigned* lkey, unsigned* ckey) {
@@ -647,7 +658,7 @@ __global__ __launch_bounds__(BLOCK) void k_level_node_keys(LevelNum L, const int
     auto patch_of = [&](const int* cc, int* t) {
         int lin = 0, str = 1;
         for (int k = 0; k < nd; ++k) {
-            t[k] = floordiv(cc[k] - L.org[k], L.n[k]);
+            t[k] = lfloordiv(L, cc[k] - L.org[k], k);
             if (t[k] < 0 || t[k] >= L.nt[k]) return -1;
             lin += t[k] * str;
             str *= L.nt[k];
@@ -684,7 +695,7 @@ __global__ __launch_bounds__(BLOCK) void k_level_node_keys(LevelNum L, const int
             int tt[3] = {0, 0, 0}, lin = 0, str = 1;
             bool in = true;
             for (int k = 0; k < nd; ++k) {
-                tt[k] = floordiv(ci[k] - L.org[k], L.n[k]) + o[k];
+                tt[k] = lfloordiv(L, ci[k] - L.org[k], k) + o[k];
                 in = in && tt[k] >= 0 && tt[k] < L.nt[k];
                 lin += tt[k] * str;
                 str *= L.nt[k];
@@ -752,8 +763,8 @@ __device__ __forceinline__ void level_ghost_visit(const LevelNum& L, const int* 
             if (s != 1 && !L.periodic[k]) continue;
             const int x = c[k] + (s - 1) * (L.dom_hi[k] - L.dom_lo[k] + 1);
             ci[k][s] = x;
-            tlo[k][s] = max(-floordiv(-(x - L.org[k] - L.n[k] + 1 - L.g), L.n[k]), 0);
-            thi[k][s] = min(floordiv(x - L.org[k] + L.g, L.n[k]), L.nt[k] - 1);
+            tlo[k][s] = max(-lfloordiv(L, -(x - L.org[k] - L.n[k] + 1 - L.g), k), 0);
+            thi[k][s] = min(lfloordiv(L, x - L.org[k] + L.g, k), L.nt[k] - 1);
         }
     for (int sz = 0; sz < 3; ++sz) {
         if (tlo[2][sz] > thi[2][sz]) continue;
@@ -798,7 +809,7 @@ __device__ __forceinline__ int level_list_key(LevelNum L, const int* tab, const 
     int lin = 0, str = 1, t[3] = {0, 0, 0};
     bool in = true;
     for (int k = 0; k < nd; ++k) {
-        t[k] = floordiv(c[k] - L.org[k], L.n[k]);
+        t[k] = lfloordiv(L, c[k] - L.org[k], k);
         in = in && t[k] >= 0 && t[k] < L.nt[k];
         lin += t[k] * str;
         str *= L.nt[k];

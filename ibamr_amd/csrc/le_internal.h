@@ -386,6 +386,7 @@ struct LevelNum {
     int org[3];                    // lower cell of tile (0, 0, 0)
     int nt[3];                     // tiles per dim of the table
     int g;                         // ghost width of the patches' index data
+    float rn[3];                   // 1 / n[k] (le_aux.hip lfloordiv: the quotient's estimate)
 };
 // cls[s]: 0 the marker lies in a local patch (key_local = patch rank * cells per
 // patch + its cell's box index), 1 only in ghost cells (key_ghost = the first
