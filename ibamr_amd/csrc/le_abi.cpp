@@ -1219,10 +1219,12 @@ static bool side_gather(ibtk_le_ctx ctx, ibtk_le_markers m) {
     return t > 0 || (t == 0 && m->n >= (1 << 25));
 }
 static int gather_fork(ibtk_le_ctx ctx, const Params& p) {
-    if (!ctx->side) {
-        HIP_TRY(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+    if (!ctx->side) {  // created together, or not at all
+        if (!ctx->ev_fork) HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+        if (!ctx->ev_join) HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+        hipStream_t st = nullptr;
+        HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        ctx->side = st;
     }
     HIP_TRY(hipEventRecord(ctx->ev_fork, ctx->stream));
     HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
